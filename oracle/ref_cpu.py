@@ -1,0 +1,206 @@
+"""CPU oracle for the attention-agent unroll.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / the timed CPU baseline.  The product
+path (the HIP library behind the drop-in ``attention`` module) never calls it.
+
+What it is: a functional plain-PyTorch (fp32, CPU) restatement of the
+reference hot path, op for op, so its numbers are the reference's numbers:
+
+  * vision encoder + ConvLSTM step ........ attention.py:110-126, 152-181
+  * spatial basis ......................... attention.py:201-232
+  * query MLP on the (always zero) prev_output  attention.py:184-198, 325-331
+  * logits / spatial softmax / readout .... attention.py:235-254, 336-340
+  * answer assembly, answer MLP, LSTMCell,
+    heads ................................. attention.py:343-368
+  * REINFORCE loss (finish_episode) ........ main_mp.py:62-77
+
+Behavioural quirks Q1-Q6 of SURVEY.md §3 are reproduced: zero peepholes
+(c*0 terms kept), zero-state LSTMCell every step, constant query from a zero
+input, transposed image orientation (X.transpose(1,3)), 4 chunks of the answer
+generalised to ``nq`` queries (identical at nq=4).
+
+Parity pinning: tests/test_oracle_golden.py checks this restatement against
+fixtures produced by importing the reference itself (tests/golden/gen_golden.py).
+
+``conv_mode='bf16'`` is the bf16-emulated oracle (SURVEY.md §8c G7 analogue):
+every convolution rounds its GEMM operands to bf16 exactly where the HIP
+kernels do (forward: activation and weight; dgrad: output-gradient and weight;
+wgrad: activation and output-gradient) and accumulates in fp32.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+__all__ = ["spatial_basis", "unroll", "reinforce_loss", "grid_of", "tensor_params"]
+
+
+def grid_of(H: int, W: int):
+    """Spatial grid (h, w) after conv 8/4/1 then conv 4/2/2 (attention.py:155-170)."""
+    def out(n, k, s, p):
+        return (n + 2 * p - k) // s + 1
+    return out(out(H, 8, 4, 1), 4, 2, 2), out(out(W, 8, 4, 1), 4, 2, 2)
+
+
+def spatial_basis(h: int, w: int, channels: int = 64) -> torch.Tensor:
+    """(h, w, channels) cosine basis, attention.py:208-226, same fp32 ops."""
+    nb = int(round(math.sqrt(channels)))
+    iy = torch.arange(1, h + 1).unsqueeze(1).float().mul(torch.ones(1, w)).mul(math.pi / h)
+    ix = torch.ones(h, 1).mul(torch.arange(1, w + 1).unsqueeze(0).float()).mul(math.pi / w)
+    freq = torch.arange(1, nb + 1).unsqueeze(0).float()
+    cy = torch.cos(iy.unsqueeze(2) * freq)          # (h, w, nb)
+    cx = torch.cos(ix.unsqueeze(2) * freq)
+    return (cy.unsqueeze(3) * cx.unsqueeze(2)).reshape(h, w, nb * nb)
+
+
+def tensor_params(params: dict, requires_grad: bool = True, dtype=torch.float32):
+    out = {}
+    for k, v in params.items():
+        t = torch.as_tensor(np.ascontiguousarray(v)).to(dtype).clone()
+        t.requires_grad_(requires_grad)
+        out[k] = t
+    return out
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad):
+        xr, wr = _bf(x), _bf(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.conf = (stride, pad, x.shape, w.shape, b is not None)
+        return F.conv2d(xr, wr, b, stride=stride, padding=pad)
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        stride, pad, xs, ws, hasb = ctx.conf
+        gr = _bf(g)
+        dx = torch.nn.grad.conv2d_input(xs, wr, gr, stride=stride, padding=pad)
+        dw = torch.nn.grad.conv2d_weight(xr, ws, gr, stride=stride, padding=pad)
+        db = g.sum((0, 2, 3)) if hasb else None
+        return dx, dw, db, None, None
+
+
+def _conv(mode, x, w, b, stride, pad):
+    if mode == "bf16":
+        return _Bf16Conv.apply(x, w, b, stride, pad)
+    return F.conv2d(x, w, b, stride=stride, padding=pad)
+
+
+def _vision_step(P, X_t, state, mode, peep):
+    """Encoder + one ConvLSTM step in the reference's transposed orientation."""
+    x = X_t.transpose(1, 3)                                            # attention.py:179
+    y = _conv(mode, x, P["vision.vision_cnn.0.weight"], P["vision.vision_cnn.0.bias"], 4, 1)
+    y = _conv(mode, y, P["vision.vision_cnn.1.weight"], P["vision.vision_cnn.1.bias"], 2, 2)
+    if state is None:
+        B, _, a, b = y.shape
+        h = torch.zeros(B, 128, a, b, dtype=y.dtype)
+        c = torch.zeros(B, 128, a, b, dtype=y.dtype)
+    else:
+        h, c = state
+    if peep is None:                                                     # Q2: zero, lazily sized
+        peep = torch.zeros(1, 128, y.shape[2], y.shape[3], dtype=y.dtype)
+
+    def gate(g):
+        L = "vision.vision_lstm."
+        return (_conv(mode, y, P[L + f"Wx{g}.weight"], P[L + f"Wx{g}.bias"], 1, 1)
+                + _conv(mode, h, P[L + f"Wh{g}.weight"], None, 1, 1))
+
+    gi = torch.sigmoid(gate("i") + c * peep)                            # attention.py:119
+    gf = torch.sigmoid(gate("f") + c * peep)                            # :120
+    c_new = gf * c + gi * torch.tanh(gate("c"))                         # :121
+    go = torch.sigmoid(gate("o") + c_new * peep)                        # :122
+    h_new = go * torch.tanh(c_new)                                      # :123
+    return h_new, c_new, peep
+
+
+def _query(P, B, nq, hidden=256):
+    """QueryNetwork on the zero prev_output (Q1), attention.py:184-198,325-331."""
+    z = torch.zeros(B, hidden)
+    q = F.relu(F.linear(z, P["query.model.0.weight"], P["query.model.0.bias"]))
+    q = F.relu(F.linear(q, P["query.model.2.weight"], P["query.model.2.bias"]))
+    q = F.linear(q, P["query.model.4.weight"], P["query.model.4.bias"])
+    return q.reshape(-1, nq, 72)
+
+
+def _head(P, O, S, nq, prev_reward, prev_action):
+    """Attention readout + answer MLP + zero-state LSTMCell + heads (one frame batch)."""
+    B, h, w, _ = O.shape
+    K, V = O.split([8, 120], dim=3)                                     # attention.py:319
+    Sb = torch.stack([S] * B)
+    K, V = torch.cat([K, Sb], dim=3), torch.cat([V, Sb], dim=3)         # :231-232
+    Q = _query(P, B, nq)
+    A = torch.matmul(K, Q.transpose(2, 1).unsqueeze(1))                  # :336
+    A = F.softmax(A.reshape(B, h * w, nq), dim=1).reshape(B, h, w, nq)  # :235-243
+    a = torch.matmul(A.reshape(B, h * w, nq).transpose(1, 2),
+                     V.reshape(B, h * w, V.shape[3]))                   # :246-254
+    if prev_reward is None:
+        r = torch.zeros(B, 1, 1)
+    else:
+        r = prev_reward.float().reshape(B, 1, 1)
+    if prev_action is None:
+        act = torch.zeros(B, 1, 1)
+    else:
+        act = prev_action.float().reshape(B, 1, 1)
+    answer = torch.cat(torch.chunk(a, nq, dim=1) + torch.chunk(Q, nq, dim=1) + (r, act),
+                       dim=2).squeeze(1)                                 # :343-348
+    x = F.relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]))
+    x = F.linear(x, P["answer_processor.2.weight"], P["answer_processor.2.bias"])
+    zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1])
+    hc, _ = torch._VF.lstm_cell(x, (zeros, zeros), P["policy_core.weight_ih"],
+                                P["policy_core.weight_hh"], P["policy_core.bias_ih"],
+                                P["policy_core.bias_hh"])               # :354-355 (Q1)
+    logits = F.linear(hc, P["policy_head.0.weight"], P["policy_head.0.bias"])
+    values = F.linear(hc, P["values_head.0.weight"], P["values_head.0.bias"])
+    return logits, values, A
+
+
+def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=None,
+           state=None, S=None, conv_mode: str = "fp32", return_state: bool = False):
+    """T-step unroll from ``reset()``: X is (T, B, H, W, 3) fp32 raw pixels.
+
+    Returns logits (T,B,A), values (T,B,A), attention maps (T,B,h,w,nq)
+    [, (h_T, c_T) in the reference's (B,128,w,h) layout].
+    """
+    T = X.shape[0]
+    if S is None:
+        S = spatial_basis(*grid_of(X.shape[2], X.shape[3]))
+    peep = None
+    L, Vv, Am = [], [], []
+    for t in range(T):
+        hN, cN, peep = _vision_step(P, X[t], state, conv_mode, peep)
+        state = (hN, cN)
+        O = hN.transpose(1, 3)                                          # attention.py:181
+        r = None if prev_reward is None else prev_reward[t]
+        a = None if prev_action is None else prev_action[t]
+        lg, vl, A = _head(P, O, S, nq, r, a)
+        L.append(lg), Vv.append(vl), Am.append(A)
+    out = (torch.stack(L), torch.stack(Vv), torch.stack(Am))
+    if return_state:
+        return out + (state,)
+    return out
+
+
+def reinforce_loss(logits: torch.Tensor, actions, rewards, gamma: float = 0.99):
+    """finish_episode's loss (main_mp.py:62-77) given per-step logits (T,1,A)."""
+    eps = np.finfo(np.float32).eps.item()
+    R, returns = 0, []
+    for r in list(rewards)[::-1]:
+        R = r + gamma * R
+        returns.insert(0, R)
+    returns = torch.tensor(returns)
+    returns = (returns - returns.mean()) / (returns.std() + eps)
+    terms = []
+    for t, (a, Rt) in enumerate(zip(actions, returns)):
+        probs = F.softmax(logits[t], dim=-1)
+        lp = torch.distributions.Categorical(probs).log_prob(torch.tensor([int(a)]))
+        terms.append(-lp * Rt)
+    return torch.cat(terms).sum()

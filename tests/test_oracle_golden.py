@@ -1,0 +1,132 @@
+"""Pin the CPU oracle (oracle/ref_cpu.py) to fixtures made by the reference itself.
+
+The fixtures (tests/golden/G*.npz) were produced by gen_golden.py importing
+/root/reference/attention.py and main_mp.py.  The oracle restates the same
+ATen op sequence, so agreement is expected to ~1e-6 (thread-count dependent
+reduction order in oneDNN convolutions is the only source of difference).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import assert_close, check_fp, detinit
+from oracle import ref_cpu
+
+RTOL = 1e-5
+
+
+def _params():
+    return ref_cpu.tensor_params(detinit.deterministic_params(0, 18))
+
+
+def _frames(T, B, H=84, W=84):
+    return torch.from_numpy(detinit.frames_u8(1234, (T, B, H, W, 3)).astype(np.float32))
+
+
+def _loss_backward(P, lg, vl):
+    Gl = torch.from_numpy(detinit.cotangent(2, tuple(lg.shape)))
+    Gv = torch.from_numpy(detinit.cotangent(3, tuple(vl.shape)))
+    ((lg * Gl).sum() + (vl * Gv).sum()).backward()
+
+
+def _check_grads(P, g, rtol):
+    worst = 0.0
+    for name, p in P.items():
+        grad = p.grad if p.grad is not None else torch.zeros_like(p)
+        e = check_fp(g, "g_", name, grad.numpy(), rtol)
+        worst = max(worst, e)
+        assert e <= rtol, f"grad {name}: fingerprint error {e:.3e}"
+    return worst
+
+
+def test_g1_spatial_basis(golden):
+    g = golden("G1")
+    for (h, w) in [(11, 11), (21, 21), (27, 20)]:
+        S = ref_cpu.spatial_basis(h, w).numpy()
+        np.testing.assert_array_equal(S, g[f"S_{h}x{w}"])
+
+
+def test_grid_of():
+    assert ref_cpu.grid_of(84, 84) == (11, 11)
+    assert ref_cpu.grid_of(168, 168) == (21, 21)
+    assert ref_cpu.grid_of(210, 160) == (27, 20)
+
+
+def test_g2_one_step_intermediates(golden):
+    g = golden("G2")
+    P = _params()
+    with torch.no_grad():
+        lg, vl, A = ref_cpu.unroll(P, _frames(1, 2))
+    assert_close(lg.numpy(), g["logits"], RTOL, "logits")
+    assert_close(vl.numpy(), g["values"], RTOL, "values")
+    assert_close(A[0].numpy(), g["attn"], RTOL, "attn")
+
+
+@pytest.mark.parametrize("name,scale", [("G3", 1.0), ("G3n", 1 / 255.0)])
+def test_g3_unroll_fwd_bwd(golden, name, scale):
+    g = golden(name)
+    P = _params()
+    lg, vl, A = ref_cpu.unroll(P, _frames(20, 1) * scale)
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    assert_close(vl.detach().numpy(), g["values"], RTOL, "values")
+    assert_close(A.detach().numpy(), g["attn"], RTOL, "attn")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, RTOL)
+
+
+def test_g4_prev_reward_action(golden):
+    g = golden("G4")
+    P = _params()
+    T, B = 4, 4
+    pr = torch.from_numpy(detinit.cotangent(77, (T, B)))
+    pa = torch.from_numpy((detinit.frames_u8(78, (T, B)) % 18).astype(np.float32))
+    lg, vl, A = ref_cpu.unroll(P, _frames(T, B), prev_reward=pr, prev_action=pa)
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, RTOL)
+
+
+def test_g5_reinforce(golden):
+    g = golden("G5")
+    P = _params()
+    T = int(g["T"])
+    X = torch.from_numpy(detinit.frames_u8(1234, (T, 84, 84, 3)).astype(np.float32)).unsqueeze(1)
+    lg, vl, A = ref_cpu.unroll(P, X)
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    loss = ref_cpu.reinforce_loss(lg, g["actions"].tolist(), g["rewards"].tolist())
+    loss.backward()
+    _check_grads(P, g, RTOL)
+
+
+def test_g6_default_basis_210x160(golden):
+    g = golden("G6")
+    P = _params()
+    with torch.no_grad():
+        lg, vl, A = ref_cpu.unroll(P, _frames(2, 1, 210, 160))
+    assert A.shape[2:4] == (27, 20)
+    assert_close(lg.numpy(), g["logits"], RTOL, "logits")
+    assert_close(A.numpy(), g["attn"], RTOL, "attn")
+
+
+def test_g7_bf16_emulation(golden):
+    g = golden("G7")
+    P = _params()
+    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16")
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, 1e-4)
+
+
+def test_quirks_q1_zero_grads(golden):
+    """Q1: query.model.0.weight and policy_core.weight_hh get exactly zero grads."""
+    g = golden("G3")
+    for name in ("query.model.0.weight", "policy_core.weight_hh"):
+        assert float(g[f"g_norm__{name}"]) == 0.0
+
+
+def test_nq8_generalisation_shapes():
+    """nq=8 (config 5) is an extension: the generalised oracle runs and is finite."""
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, 18, num_queries=8))
+    with torch.no_grad():
+        lg, vl, A = ref_cpu.unroll(P, _frames(1, 1), nq=8)
+    assert A.shape == (1, 1, 11, 11, 8) and torch.isfinite(lg).all()
