@@ -1,0 +1,165 @@
+/*
+ * aaa.h -- C ABI of the MI355X (gfx950) attention-augmented-agent learner.
+ *
+ * One shared library (libaaa.so, built by hipcc --offload-arch=gfx950) that
+ * replaces the ATen op sequence of the reference's batched unroll: the
+ * forward of Agent (reference attention.py:298-368, including
+ * VisionNetwork.forward :178-181, ConvLSTMCell.forward :110-126,
+ * QueryNetwork :184-198, SpatialBasis.__call__ :228-232, spatial_softmax
+ * :235-243, apply_alpha :246-254) over T steps from reset() (:293-296), and
+ * the backward that autograd runs for it when main_mp.py:77 calls
+ * policy_loss.backward().
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers on the caller's current HIP device,
+ *    except the cfg/io structs themselves (host memory).
+ *  - Ownership: the caller owns every buffer (params, packed weights,
+ *    workspace, outputs).  The library never allocates or frees device
+ *    memory and keeps no device state.
+ *  - Streams: all work is enqueued on ``stream``; nothing synchronises.
+ *  - Errors: functions return 0 on success, a negative AAA_E* code
+ *    otherwise; aaa_last_error() returns a thread-local message.
+ *  - Threading: re-entrant; each call only touches the buffers it is given.
+ *
+ * Layouts
+ *  - params / grads: the 34 reference state_dict tensors, fp32, concatenated
+ *    in state_dict order (reference attention.py:257-291),
+ *    each tensor in its PyTorch (contiguous) layout.  aaa_param_layout()
+ *    returns the offsets.  nq != 4 uses the generalised query / answer widths
+ *    (query 256->128->72nq->72nq, answer 256nq+2).
+ *  - frames: (T, B, H, W, 3) fp32 NHWC raw pixels (main_mp.py:53 casts the
+ *    uint8 observation to float without normalisation).
+ *  - basis: (h, w, 64) fp32 spatial basis (SpatialBasis.S, attention.py:226).
+ *  - logits, values: (T, B, A) fp32; attn: (T, B, h, w, nq) fp32 softmax maps.
+ *  - prev_reward / prev_action: (T, B) fp32 or NULL (zeros, :303-312).
+ *  - ConvLSTM state h0, c0, hT, cT, dh0, dc0, dhT, dcT: (B, h, w, 128) fp32
+ *    NHWC (the reference keeps (B,128,w,h)), NULL = zero /
+ *    not requested.
+ */
+#ifndef AAA_H
+#define AAA_H
+
+#include <stddef.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AAA_ABI_VERSION 1
+
+enum aaa_status {
+  AAA_OK = 0,
+  AAA_E_ARG = -1,      /* bad shape / NULL / unsupported configuration */
+  AAA_E_ALIGN = -2,    /* a buffer is not 16-byte aligned */
+  AAA_E_LAUNCH = -3,   /* a HIP launch or runtime call failed */
+  AAA_E_DEVICE = -4    /* current device is not gfx950 */
+};
+
+enum aaa_dtype {
+  AAA_F32 = 0,   /* conv/ConvLSTM GEMM operands fp32 (exact v_mfma_f32_32x32x2_f32) */
+  AAA_BF16 = 1   /* conv/ConvLSTM GEMM operands bf16, fp32 accumulate + gate math */
+};
+
+typedef struct aaa_cfg {
+  int B;        /* sequences (batch rows)                                    */
+  int T;        /* unroll length (steps since reset())                        */
+  int H, W;     /* frame size, e.g. 84x84, 168x168, 210x160                    */
+  int nq;       /* attention queries (reference: 4, attention.py:265)          */
+  int A;        /* actions (Seaquest: 18, main_mp.py:179)                       */
+  int dtype;    /* enum aaa_dtype                                             */
+  int reserved;
+} aaa_cfg;
+
+typedef struct aaa_io {
+  /* inputs */
+  const float* params;       /* flat fp32 params (state_dict order)            */
+  const void* packed;        /* aaa_pack_weights output                        */
+  const float* basis;        /* (h, w, 64)                                     */
+  const float* frames;       /* (T, B, H, W, 3)                                */
+  const float* prev_reward;  /* (T, B) or NULL                                 */
+  const float* prev_action;  /* (T, B) or NULL                                 */
+  const float* h0;           /* (B, h, w, 128) or NULL                         */
+  const float* c0;           /* (B, h, w, 128) or NULL                         */
+  /* forward outputs */
+  float* logits;             /* (T, B, A)                                      */
+  float* values;             /* (T, B, A)                                      */
+  float* attn;               /* (T, B, h, w, nq) or NULL                       */
+  float* hT;                 /* (B, h, w, 128) or NULL                         */
+  float* cT;                 /* (B, h, w, 128) or NULL                         */
+  /* backward inputs */
+  const float* dlogits;      /* (T, B, A)                                      */
+  const float* dvalues;      /* (T, B, A) or NULL                              */
+  const float* dhT;          /* (B, h, w, 128) or NULL                         */
+  const float* dcT;          /* (B, h, w, 128) or NULL                         */
+  /* backward outputs */
+  float* grads;              /* flat fp32 grads, same layout as params         */
+  float* dh0;                /* (B, h, w, 128) or NULL                         */
+  float* dc0;                /* (B, h, w, 128) or NULL                         */
+  /* scratch */
+  void* workspace;           /* aaa_workspace_bytes(); activations saved by
+                                aaa_forward for aaa_backward live here        */
+} aaa_io;
+
+/* Backward phases, in execution order (DP bucket boundaries). */
+enum aaa_bwd_phase {
+  AAA_BWD_HEAD = 1,    /* heads, LSTMCell, answer MLP, attention, query MLP */
+  AAA_BWD_CORE = 2,    /* ConvLSTM BPTT + ConvLSTM weight/bias grads         */
+  AAA_BWD_VISION = 4,  /* conv2 / conv1 weight & bias grads                  */
+  AAA_BWD_ALL = 7
+};
+
+int aaa_abi_version(void);
+const char* aaa_last_error(void);
+
+/* Spatial grid (h, w) the encoder produces for an H x W frame. */
+int aaa_grid(int H, int W, int* h, int* w);
+
+/* Number of fp32 params and the offset/size of each of the 34 tensors
+ * (state_dict order).  offsets/sizes may be NULL. */
+int aaa_param_layout(const aaa_cfg* cfg, size_t* total, size_t* offsets, size_t* sizes);
+
+size_t aaa_packed_bytes(const aaa_cfg* cfg);
+size_t aaa_workspace_bytes(const aaa_cfg* cfg);
+
+/* Re-lay the params into the kernels' operand layouts (gate-interleaved
+ * ConvLSTM / LSTMCell rows, NHWC tap-major conv weights with the
+ * reference's transposed kernel orientation, bf16 when cfg->dtype says so).
+ * Must run after every parameter update. */
+int aaa_pack_weights(const aaa_cfg* cfg, const float* params, void* packed, hipStream_t stream);
+
+/* T-step forward from reset(); replaces T calls of Agent.forward. */
+int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream);
+
+/* Backward of the loss sum(logits*dlogits)+sum(values*dvalues) (+ state
+ * cotangents) through the saved activations of the matching aaa_forward.
+ * ``phases`` is a mask of aaa_bwd_phase; phases must run in order. grads
+ * are overwritten (not accumulated) by the phases that own them. */
+int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
+
+/* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
+
+/* NHWC convolution y[n,oy,ox,co] = b[co] + sum w[co,ky,kx,ci] x[n,iy,ix,ci]
+ * (weights in [Cout][KH][KW][Cin] order, i.e. torch weight.permute(0,2,3,1)).
+ * dtype selects the MFMA operand type.  bias may be NULL. */
+typedef struct aaa_conv_desc {
+  int N, Hin, Win, Cin, Hout, Wout, Cout, KH, KW, stride, pad, dtype;
+} aaa_conv_desc;
+
+int aaa_conv2d_nhwc(const aaa_conv_desc* d, const float* x, const float* w, const float* bias,
+                    float* y, hipStream_t stream);
+/* dx = conv2d_input(dy, w) (NHWC) */
+int aaa_conv2d_nhwc_dgrad(const aaa_conv_desc* d, const float* dy, const float* w, float* dx,
+                          hipStream_t stream);
+/* dw[co][ky][kx][ci] = conv2d_weight(x, dy), overwritten */
+int aaa_conv2d_nhwc_wgrad(const aaa_conv_desc* d, const float* x, const float* dy, float* dw,
+                          hipStream_t stream);
+
+/* C[m][n] = sum_k A[m][k] * Bw[n][k] (+ bias[n]) -- torch.nn.functional.linear */
+int aaa_linear(int M, int N, int K, const float* x, const float* w, const float* bias, float* y,
+               hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AAA_H */

@@ -1,0 +1,196 @@
+"""End-to-end parity of the HIP learner path against the CPU oracle and the
+reference-generated golden fixtures (fp32: 1e-4 relative, SURVEY.md §8c;
+bf16: 2e-2 against the bf16-emulated oracle).
+
+Every test goes through the drop-in ``attention.Agent`` (-> libaaa.so C ABI).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import assert_close, check_fp, detinit, rel_err
+from oracle import ref_cpu
+
+import attention
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def _agent(dev, A=18, nq=4, grid=(11, 11), conv_dtype="fp32"):
+    ag = attention.Agent(A, num_queries=nq, grid=grid, conv_dtype=conv_dtype)
+    detinit.load_into(ag, detinit.deterministic_params(0, A, nq))
+    return ag.to(dev)
+
+
+def _frames(T, B, H=84, W=84, scale=1.0):
+    return torch.from_numpy(detinit.frames_u8(1234, (T, B, H, W, 3)).astype(np.float32)) * scale
+
+
+def _cot(T, B, A=18):
+    return (torch.from_numpy(detinit.cotangent(2, (T, B, A))), torch.from_numpy(detinit.cotangent(3, (T, B, A))))
+
+
+def _grads(agent):
+    return {n: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().cpu()
+            for n, p in agent.named_parameters()}
+
+
+def _oracle(T, B, nq=4, scale=1.0, conv_mode="fp32", A=18, H=84, W=84, **kw):
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A, nq))
+    X = _frames(T, B, H, W, scale)
+    lg, vl, at = ref_cpu.unroll(P, X, nq=nq, conv_mode=conv_mode, **kw)
+    Gl, Gv = _cot(T, B, A)
+    ((lg * Gl).sum() + (vl * Gv).sum()).backward()
+    g = {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}
+    return lg.detach(), vl.detach(), at.detach(), g
+
+
+def _run_unroll(agent, T, B, dev, scale=1.0, A=18, H=84, W=84, **kw):
+    X = _frames(T, B, H, W, scale).to(dev)
+    agent.reset()
+    lg, vl, at = agent.unroll(X, **kw)
+    Gl, Gv = _cot(T, B, A)
+    ((lg * Gl.to(dev)).sum() + (vl * Gv.to(dev)).sum()).backward()
+    torch.cuda.synchronize()
+    return lg.detach().cpu(), vl.detach().cpu(), at.detach().cpu(), _grads(agent)
+
+
+def _compare(out, ref, rtol, what=""):
+    lg, vl, at, g = out
+    rl, rv, ra, rg = ref
+    assert_close(lg.numpy(), rl.numpy(), rtol, what + "logits")
+    assert_close(vl.numpy(), rv.numpy(), rtol, what + "values")
+    assert_close(at.numpy(), ra.numpy(), rtol, what + "attn")
+    for n in rg:
+        if float(rg[n].norm()) == 0.0:
+            assert float(g[n].abs().max()) == 0.0, f"{n}: reference grad is exactly zero (Q1)"
+        else:
+            assert_close(g[n].numpy(), rg[n].numpy(), rtol, what + "grad " + n)
+
+
+@pytest.mark.parametrize("T,B", [(1, 1), (4, 2), (3, 5)])
+def test_unroll_vs_oracle_fp32(cuda, T, B):
+    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL)
+
+
+def test_c1_against_reference_fixture(cuda, golden):
+    """Config 1 (B=1, T=20) against the fixture made by the reference itself."""
+    g = golden("G3")
+    lg, vl, at, grads = _run_unroll(_agent(cuda), 20, 1, cuda)
+    assert_close(lg.numpy(), g["logits"], RTOL, "logits")
+    assert_close(vl.numpy(), g["values"], RTOL, "values")
+    assert_close(at.numpy(), g["attn"], RTOL, "attn")
+    for n, v in grads.items():
+        e = check_fp(g, "g_", n, v.numpy(), RTOL)
+        assert e <= RTOL, f"grad {n}: fingerprint error {e:.2e}"
+
+
+def test_normalised_frames_fixture(cuda, golden):
+    g = golden("G3n")
+    lg, vl, at, grads = _run_unroll(_agent(cuda), 20, 1, cuda, scale=1 / 255.0)
+    assert_close(lg.numpy(), g["logits"], RTOL, "logits")
+    for n, v in grads.items():
+        assert check_fp(g, "g_", n, v.numpy(), RTOL) <= RTOL, n
+
+
+def test_prev_reward_action_fixture(cuda, golden):
+    g = golden("G4")
+    T, B = 4, 4
+    pr = torch.from_numpy(detinit.cotangent(77, (T, B))).to(cuda)
+    pa = torch.from_numpy((detinit.frames_u8(78, (T, B)) % 18).astype(np.float32)).to(cuda)
+    lg, vl, at, grads = _run_unroll(_agent(cuda), T, B, cuda, prev_reward=pr, prev_action=pa)
+    assert_close(lg.numpy(), g["logits"], RTOL, "logits")
+    for n, v in grads.items():
+        assert check_fp(g, "g_", n, v.numpy(), RTOL) <= RTOL, n
+
+
+def test_per_step_forward_chains_bptt(cuda):
+    """Reference usage: T calls of agent(X_t) then one backward (main_mp.py:54,77)."""
+    T, B = 5, 2
+    agent = _agent(cuda)
+    X = _frames(T, B).to(cuda)
+    Gl, Gv = _cot(T, B)
+    agent.reset()
+    loss = 0
+    for t in range(T):
+        lg, vl = agent(X[t])
+        loss = loss + (lg * Gl[t].to(cuda)).sum() + (vl * Gv[t].to(cuda)).sum()
+    loss.backward()
+    ref = _oracle(T, B)
+    g = _grads(agent)
+    for n in ref[3]:
+        if float(ref[3][n].norm()) > 0:
+            assert_close(g[n].numpy(), ref[3][n].numpy(), RTOL, "grad " + n)
+
+
+def test_reinforce_episode_fixture(cuda, golden):
+    """main_mp.finish_episode's REINFORCE loss over a 12-step episode (G5)."""
+    g = golden("G5")
+    T = int(g["T"])
+    agent = _agent(cuda)
+    obs = detinit.frames_u8(1234, (T, 84, 84, 3))
+    agent.reset()
+    logits = []
+    for t in range(T):
+        state = torch.from_numpy(obs[t]).float().unsqueeze(0).to(cuda)   # main_mp.py:53
+        lg, _ = agent(state, ts=t)
+        logits.append(lg)
+    lg = torch.stack(logits)
+    assert_close(lg.detach().cpu().numpy(), g["logits"], RTOL, "logits")
+    loss = ref_cpu.reinforce_loss(lg.cpu(), g["actions"].tolist(), g["rewards"].tolist())
+    loss.backward()
+    for n, v in _grads(agent).items():
+        assert check_fp(g, "g_", n, v.numpy(), RTOL) <= RTOL, n
+
+
+def test_default_basis_210x160_fixture(cuda, golden):
+    g = golden("G6")
+    agent = _agent(cuda, grid=None)
+    X = _frames(2, 1, 210, 160).to(cuda)
+    agent.reset()
+    with torch.no_grad():
+        lg, vl, at = agent.unroll(X)
+    assert_close(lg.cpu().numpy(), g["logits"], RTOL, "logits")
+    assert_close(at.cpu().numpy(), g["attn"], RTOL, "attn")
+
+
+def test_mismatched_basis_raises_like_reference(cuda):
+    agent = _agent(cuda, grid=None)   # default SpatialBasis(27, 20)
+    with pytest.raises(RuntimeError, match="Sizes of tensors must match"):
+        agent(_frames(1, 1)[0].to(cuda))
+
+
+def test_nq8_generalised(cuda):
+    T, B = 2, 2
+    out = _run_unroll(_agent(cuda, nq=8), T, B, cuda)
+    _compare(out, _oracle(T, B, nq=8), RTOL, "nq8 ")
+
+
+def test_168_grid(cuda):
+    T, B = 2, 2
+    out = _run_unroll(_agent(cuda, grid=(21, 21)), T, B, cuda, H=168, W=168)
+    _compare(out, _oracle(T, B, H=168, W=168), RTOL, "168 ")
+
+
+def test_bf16_vs_emulated_oracle(cuda):
+    T, B = 4, 2
+    out = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
+    ref = _oracle(T, B, conv_mode="bf16")
+    _compare(out, ref, 2e-2, "bf16 ")
+
+
+def test_c2_full_size_vs_oracle(cuda):
+    """Config 2 (B=32, T=20, fp32) in full against the oracle on the host CPU."""
+    T, B = 20, 32
+    torch.set_num_threads(16)
+    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, "C2 ")
+
+
+def test_repeat_is_deterministic_enough(cuda):
+    """Two identical runs agree (atomics may reorder fp32 sums: ~1e-6)."""
+    a = _run_unroll(_agent(cuda), 3, 4, cuda)
+    b = _run_unroll(_agent(cuda), 3, 4, cuda)
+    assert torch.equal(a[0], b[0])
+    for n in a[3]:
+        assert rel_err(a[3][n].numpy(), b[3][n].numpy()) < 1e-5, n

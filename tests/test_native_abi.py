@@ -1,0 +1,80 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol
+include/aaa.h declares, and its layout queries agree with the reference's
+state_dict (no GPU compute is issued here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from helpers import ROOT, detinit
+
+import attention  # noqa: F401
+from aaa_amd import _native as N
+
+HEADER = os.path.join(ROOT, "include", "aaa.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(aaa_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_list():
+    assert _declared() == sorted(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version():
+    assert N.load().aaa_abi_version() == 1
+
+
+@pytest.mark.parametrize("H,W,hw", [(84, 84, (11, 11)), (168, 168, (21, 21)), (210, 160, (27, 20))])
+def test_grid(H, W, hw):
+    assert N.grid(H, W) == hw
+
+
+@pytest.mark.parametrize("nq,total", [(4, 2270276), (8, 3080836)])
+def test_param_layout_matches_state_dict(nq, total):
+    cfg = N.Cfg(2, 3, 84, 84, nq, 18, N.F32, 0)
+    n, offs, sizes = N.param_layout(cfg)
+    assert n == total
+    shapes = detinit.param_shapes(18, nq)
+    assert sizes == [int(np.prod(s)) for _, s in shapes]
+    assert offs == list(np.cumsum([0] + sizes[:-1]))
+
+
+def test_layout_sizes_and_errors():
+    lib = N.load()
+    ok = N.Cfg(32, 20, 84, 84, 4, 18, N.F32, 0)
+    ws = lib.aaa_workspace_bytes(ctypes.byref(ok))
+    pk = lib.aaa_packed_bytes(ctypes.byref(ok))
+    assert ws > 32 * 20 * 121 * 128 * 4 and pk > 512 * 1728 * 4
+    bf = N.Cfg(32, 20, 84, 84, 4, 18, N.BF16, 0)
+    assert lib.aaa_packed_bytes(ctypes.byref(bf)) < pk
+    bad = N.Cfg(32, 20, 84, 84, 5, 18, N.F32, 0)
+    assert lib.aaa_workspace_bytes(ctypes.byref(bad)) == 0
+    assert b"nq" in lib.aaa_last_error()
+    bad_rc = lib.aaa_forward(ctypes.byref(bad), None, None)
+    assert bad_rc == -1
+
+
+def test_agent_refuses_cpu_tensors():
+    import torch
+    agent = attention.Agent(18, grid=(11, 11))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        agent(torch.zeros(1, 84, 84, 3))
+
+
+def test_state_dict_keys_match_reference_order():
+    agent = attention.Agent(18)
+    keys = list(agent.state_dict().keys())
+    assert keys == [n for n, _ in detinit.param_shapes(18, 4)]
+    assert len(list(agent.buffers())) == 0

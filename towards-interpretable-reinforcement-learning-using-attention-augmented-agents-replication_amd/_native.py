@@ -1,0 +1,113 @@
+"""ctypes binding of libaaa.so (C ABI in include/aaa.h).
+
+There is no fallback: if the library is missing or the device is not gfx950,
+every entry point raises.  Build with ``python -c "import __graft_entry__ as g; g.build()"``
+(or ``make -C <pkg>/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaaa.so")
+
+F32, BF16 = 0, 1
+BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
+
+# Every symbol include/aaa.h declares (checked by tests/test_native_abi.py).
+EXPORTS = (
+    "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
+    "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
+    "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear",
+)
+
+
+class Cfg(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("T", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("nq", ctypes.c_int), ("A", ctypes.c_int), ("dtype", ctypes.c_int), ("reserved", ctypes.c_int)]
+
+
+IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action", "h0", "c0",
+             "logits", "values", "attn", "hT", "cT", "dlogits", "dvalues", "dhT", "dcT",
+             "grads", "dh0", "dc0", "workspace")
+
+
+class IO(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in IO_FIELDS]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("N", "Hin", "Win", "Cin", "Hout", "Wout", "Cout", "KH", "KW", "stride", "pad", "dtype")]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load libaaa.so (raises if absent).  Safe to call without a GPU."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.isfile(path):
+            raise RuntimeError(f"aaa: native library {path} is missing; build it with "
+                               f"`make -C {os.path.join(_HERE, 'csrc')}` -- there is no CPU fallback")
+        lib = ctypes.CDLL(path)
+        P, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        CP = ctypes.POINTER(Cfg)
+        sig = {
+            "aaa_abi_version": (I, []),
+            "aaa_last_error": (ctypes.c_char_p, []),
+            "aaa_grid": (I, [I, I, ctypes.POINTER(I), ctypes.POINTER(I)]),
+            "aaa_param_layout": (I, [CP, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)]),
+            "aaa_packed_bytes": (S, [CP]),
+            "aaa_workspace_bytes": (S, [CP]),
+            "aaa_pack_weights": (I, [CP, P, P, P]),
+            "aaa_forward": (I, [CP, ctypes.POINTER(IO), P]),
+            "aaa_backward": (I, [CP, ctypes.POINTER(IO), I, P]),
+            "aaa_conv2d_nhwc": (I, [ctypes.POINTER(ConvDesc), P, P, P, P, P]),
+            "aaa_conv2d_nhwc_dgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),
+            "aaa_conv2d_nhwc_wgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),
+            "aaa_linear": (I, [I, I, I, P, P, P, P, P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().aaa_last_error().decode(errors="replace")
+        raise RuntimeError(f"aaa{(' ' + what) if what else ''}: {msg} (status {rc})")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def grid(H: int, W: int):
+    h, w = ctypes.c_int(), ctypes.c_int()
+    check(load().aaa_grid(H, W, ctypes.byref(h), ctypes.byref(w)), "grid")
+    return h.value, w.value
+
+
+def param_layout(cfg: Cfg):
+    total = ctypes.c_size_t()
+    offs = (ctypes.c_size_t * 34)()
+    sizes = (ctypes.c_size_t * 34)()
+    check(load().aaa_param_layout(ctypes.byref(cfg), ctypes.byref(total), offs, sizes), "param_layout")
+    return total.value, list(offs), list(sizes)

@@ -1,1 +1,276 @@
-__all__ = []
+"""Drop-in ``attention`` module: the reference's nn.Module API on the HIP path.
+
+Same class names, constructor signatures, attributes and state_dict keys as
+the reference ``attention.py``, so ``main_mp.py`` /
+``test_model.py`` and saved checkpoints work unchanged:
+
+  ConvLSTMCell   attention.py:7-149      (parameter container; fused into Agent)
+  VisionNetwork  attention.py:152-181    (parameter container; fused into Agent)
+  QueryNetwork   attention.py:184-198
+  SpatialBasis   attention.py:201-232
+  spatial_softmax / apply_alpha  attention.py:235-254
+  Agent          attention.py:257-368
+
+``Agent.forward`` (one step, state carried in ``vision.vision_lstm.prev_hidden``)
+and the added ``Agent.unroll`` (T steps in one call) run entirely in the gfx950
+kernels of libaaa.so through one ``torch.autograd.Function`` per call; the
+Function's backward is the hand-written BPTT, and consecutive per-step calls
+chain through the ConvLSTM state so ``loss.backward()`` after an episode
+(main_mp.py:77) back-propagates through every step exactly like the reference.
+There is no CPU fallback: calling the Agent with CPU tensors raises.
+
+Added (optional) surface: ``Agent(..., grid=None | (h, w) | "auto",
+conv_dtype="fp32" | "bf16")`` and ``Agent.unroll``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .runtime import UnrollRunner
+
+__all__ = ["ConvLSTMCell", "VisionNetwork", "QueryNetwork", "SpatialBasis", "spatial_softmax",
+           "apply_alpha", "Agent"]
+
+
+class ConvLSTMCell(nn.Module):
+    """Zero-peephole ConvLSTM cell parameters (attention.py:7-149).
+
+    The cell math runs fused inside Agent's HIP kernels; ``prev_hidden`` holds
+    the carried (h, c) state as (B, h, w, hidden) NHWC device tensors.
+    """
+
+    def __init__(self, input_channels, hidden_channels, kernel_size):
+        super().__init__()
+        assert hidden_channels % 2 == 0
+        self.input_channels = input_channels
+        self.hidden_channels = hidden_channels
+        self.kernel_size = kernel_size
+        self.num_features = 4
+        self.padding = int((kernel_size - 1) / 2)
+        k, p = kernel_size, self.padding
+        # registration order == reference state_dict order
+        for g in "ifco":
+            setattr(self, f"Wx{g}", nn.Conv2d(input_channels, hidden_channels, k, 1, p, bias=True))
+            setattr(self, f"Wh{g}", nn.Conv2d(hidden_channels, hidden_channels, k, 1, p, bias=False))
+        self.Wci = None
+        self.Wcf = None
+        self.Wco = None
+        self.prev_hidden = None
+
+    def forward(self, x):
+        raise NotImplementedError(
+            "ConvLSTMCell runs fused inside Agent.forward / Agent.unroll on the MI355X HIP path")
+
+    def reset(self):
+        self.prev_hidden = None
+
+    def init_hidden(self, batch_size, hidden, height, width, device):
+        z = torch.zeros(batch_size, height, width, hidden, device=device)
+        return z, z.clone()
+
+
+class VisionNetwork(nn.Module):
+    """conv 8/4/1 -> conv 4/2/2 (no activation) -> ConvLSTM (attention.py:152-181)."""
+
+    def __init__(self):
+        super().__init__()
+        self.vision_cnn = nn.Sequential(
+            nn.Conv2d(in_channels=3, out_channels=32, kernel_size=(8, 8), stride=4, padding=1),
+            nn.Conv2d(in_channels=32, out_channels=64, kernel_size=(4, 4), stride=2, padding=2),
+        )
+        self.vision_lstm = ConvLSTMCell(input_channels=64, hidden_channels=128, kernel_size=3)
+
+    def reset(self):
+        self.vision_lstm.reset()
+
+    def forward(self, X):
+        raise NotImplementedError(
+            "VisionNetwork runs fused inside Agent.forward / Agent.unroll on the MI355X HIP path")
+
+
+class QueryNetwork(nn.Module):
+    """256 -> 128 -> 72*nq -> 72*nq MLP (attention.py:184-198; nq=4 in the reference)."""
+
+    def __init__(self, num_queries: int = 4):
+        super().__init__()
+        self.num_queries = num_queries
+        qd = 72 * num_queries
+        self.model = nn.Sequential(nn.Linear(256, 128), nn.ReLU(), nn.Linear(128, qd), nn.ReLU(),
+                                   nn.Linear(qd, qd))
+
+    def forward(self, query):
+        return self.model(query).reshape(-1, self.num_queries, 72)
+
+
+class SpatialBasis:
+    """Constant (h, w, channels) cosine basis (attention.py:201-232).
+
+    S[i, j, 8u + v] = cos((i+1)*pi/h * (u+1)) * cos((j+1)*pi/w * (v+1)), built
+    with the same fp32 ops as the reference so it is bit-identical.
+    """
+
+    def __init__(self, height=27, width=20, channels=64):
+        nb = int(round(math.sqrt(channels)))
+        rows = torch.arange(1, height + 1).unsqueeze(1).float().mul(torch.ones(1, width)).mul(math.pi / height)
+        cols = torch.ones(height, 1).mul(torch.arange(1, width + 1).unsqueeze(0).float()).mul(math.pi / width)
+        freq = torch.arange(1, nb + 1).unsqueeze(0).float()
+        cy = torch.cos(rows.unsqueeze(2) * freq)
+        cx = torch.cos(cols.unsqueeze(2) * freq)
+        self.S = (cy.unsqueeze(3) * cx.unsqueeze(2)).reshape(height, width, nb * nb)
+
+    def __call__(self, X):
+        S = self.S.to(X.device).unsqueeze(0).expand(X.shape[0], -1, -1, -1)
+        return torch.cat([X, S], dim=3)
+
+
+def spatial_softmax(A):
+    """Softmax over the h*w grid for each query (attention.py:235-243)."""
+    b, h, w, d = A.size()
+    return F.softmax(A.reshape(b, h * w, d), dim=1).reshape(b, h, w, d)
+
+
+def apply_alpha(A, V):
+    """Attention-weighted readout sum_p A[p, q] V[p] (attention.py:246-254)."""
+    b, h, w, c = A.size()
+    return torch.matmul(A.reshape(b, h * w, c).transpose(1, 2), V.reshape(b, h * w, V.size(3)))
+
+
+class _UnrollFn(torch.autograd.Function):
+    """One library forward over T steps; its backward is the hand-written BPTT."""
+
+    @staticmethod
+    def forward(ctx, runner, S, X, pr, pa, h0, c0, *params):
+        flat = torch.cat([p.detach().reshape(-1) for p in params])
+        packed = runner.new_packed()
+        runner.pack(flat, packed)
+        ws = runner.new_workspace()
+        logits, values, attn, hT, cT = runner.forward(flat, packed, S, X, ws, pr, pa, h0, c0,
+                                                      want_attn=True, want_state=True)
+        ctx.runner, ctx.flat, ctx.packed, ctx.ws, ctx.S, ctx.X = runner, flat, packed, ws, S, X
+        ctx.shapes = [p.shape for p in params]
+        ctx.mark_non_differentiable(attn)
+        return logits, values, attn, hT, cT
+
+    @staticmethod
+    def backward(ctx, dl, dv, _dattn, dhT, dcT):
+        r = ctx.runner
+        want_state = bool(ctx.needs_input_grad[5] or ctx.needs_input_grad[6])
+        grads, dh0, dc0 = r.backward(ctx.flat, ctx.packed, ctx.S, ctx.X, ctx.ws, dl, dv, dhT, dcT,
+                                     want_state_grads=want_state)
+        ctx.ws = None
+        views = [g.view(s) for g, s in zip(grads.split(r.sizes), ctx.shapes)]
+        return (None, None, None, None, None, dh0, dc0, *views)
+
+
+class Agent(nn.Module):
+    """Attention-augmented agent (attention.py:257-368) on the gfx950 HIP path."""
+
+    def __init__(self, num_actions, hidden_size: int = 256, c_v: int = 120, c_k: int = 8, c_s: int = 64,
+                 num_queries: int = 4, *, grid=None, conv_dtype: str = "fp32"):
+        super().__init__()
+        if (hidden_size, c_v, c_k, c_s) != (256, 120, 8, 64):
+            raise ValueError("hidden_size/c_v/c_k/c_s are hard-coded elsewhere in the reference "
+                             "(attention.py:171-198, SURVEY.md Q6); only the defaults are supported")
+        if num_queries not in (4, 8):
+            raise ValueError("num_queries must be 4 (reference) or 8 (generalised, SURVEY.md Q5)")
+        if conv_dtype not in ("fp32", "bf16"):
+            raise ValueError("conv_dtype must be 'fp32' or 'bf16'")
+        self.hidden_size = hidden_size
+        self.c_v, self.c_k, self.c_s, self.num_queries = c_v, c_k, c_s, num_queries
+        self.num_actions = num_actions
+        self.conv_dtype = conv_dtype
+        self.vision = VisionNetwork()
+        self.query = QueryNetwork(num_queries)
+        self._auto_grid = grid == "auto"
+        self.spatial = SpatialBasis(*grid) if isinstance(grid, (tuple, list)) else SpatialBasis()
+        self.answer_processor = nn.Sequential(
+            nn.Linear((c_v + c_s) * num_queries + (c_k + c_s) * num_queries + 1 + 1, 512),
+            nn.ReLU(),
+            nn.Linear(512, hidden_size),
+        )
+        self.policy_core = nn.LSTMCell(hidden_size, hidden_size)
+        self.prev_output = None
+        self.prev_hidden = None
+        self.policy_head = nn.Sequential(nn.Linear(hidden_size, num_actions))
+        self.values_head = nn.Sequential(nn.Linear(hidden_size, num_actions))
+        self._runners = {}
+        self._basis = None
+        self.last_attention = None
+
+    # -- reference API --------------------------------------------------------
+    def reset(self):
+        self.vision.reset()
+        self.prev_output = None
+        self.prev_hidden = None
+
+    def forward(self, X, prev_reward=None, prev_action=None, ts=0):
+        """One step (attention.py:298-368): X (B, H, W, 3) -> logits, values (B, A)."""
+        pr = None if prev_reward is None else prev_reward.reshape(1, -1)
+        pa = None if prev_action is None else prev_action.reshape(1, -1)
+        logits, values, attn = self._step(X.unsqueeze(0), pr, pa)
+        self.last_attention = attn[0]
+        return logits[0], values[0]
+
+    # -- added API ----------------------------------------------------------
+    def unroll(self, X, prev_reward=None, prev_action=None):
+        """T steps in one call: X (T, B, H, W, 3) -> logits, values (T, B, A), attn (T, B, h, w, nq).
+
+        Continues from the current ConvLSTM state (zero after ``reset()``) and
+        leaves the final state in ``vision.vision_lstm.prev_hidden``.
+        """
+        logits, values, attn = self._step(X, prev_reward, prev_action)
+        self.last_attention = attn
+        return logits, values, attn
+
+    # -- internals ----------------------------------------------------------
+    def _step(self, X, pr, pa):
+        if not X.is_cuda:
+            raise RuntimeError("aaa: Agent runs only on the MI355X HIP path; move the agent and its "
+                               "inputs to a ROCm GPU (there is no CPU fallback)")
+        T, B, H, W, C = X.shape
+        if C != 3:
+            raise ValueError(f"frames must be (..., H, W, 3), got {tuple(X.shape)}")
+        params = list(self.parameters())
+        for p in params:
+            if p.device != X.device:
+                raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
+                                   f"call agent.to({X.device})")
+        runner = self._runner(B, T, H, W, X.device)
+        S = self._basis_for(runner.h, runner.w, H, W, X.device)
+        cell = self.vision.vision_lstm
+        h0, c0 = cell.prev_hidden if cell.prev_hidden is not None else (None, None)
+        if h0 is not None and tuple(h0.shape) != runner.state_shape():
+            raise RuntimeError(f"carried ConvLSTM state {tuple(h0.shape)} does not match this batch "
+                               f"{runner.state_shape()}; call agent.reset()")
+        Xf = X.float().contiguous()
+        logits, values, attn, hT, cT = _UnrollFn.apply(runner, S, Xf, pr, pa, h0, c0, *params)
+        cell.prev_hidden = (hT, cT)
+        if self.prev_output is None:   # Q1: the query input is created once and never updated
+            self.prev_output = torch.zeros(B, self.hidden_size, device=X.device)
+        return logits, values, attn
+
+    def _runner(self, B, T, H, W, device):
+        key = (B, T, H, W, str(device), self.conv_dtype)
+        r = self._runners.get(key)
+        if r is None:
+            r = UnrollRunner(B, T, H, W, self.num_queries, self.num_actions, self.conv_dtype, device)
+            self._runners[key] = r
+        return r
+
+    def _basis_for(self, h, w, H, W, device):
+        if self._auto_grid and tuple(self.spatial.S.shape[:2]) != (h, w):
+            self.spatial = SpatialBasis(h, w)
+        S = self.spatial.S
+        if tuple(S.shape) != (h, w, 64):
+            raise RuntimeError(
+                f"Sizes of tensors must match: the spatial basis is {tuple(S.shape[:2])} but {H}x{W} frames "
+                f"give a {h}x{w} grid; set agent.spatial = SpatialBasis({h}, {w}) (the reference hard-codes "
+                f"27x20 at attention.py:208,275)")
+        cached = self._basis
+        if cached is None or cached[0] is not S or cached[1] != str(device):
+            self._basis = (S, str(device), S.to(device=device, dtype=torch.float32).contiguous())
+        return self._basis[2]

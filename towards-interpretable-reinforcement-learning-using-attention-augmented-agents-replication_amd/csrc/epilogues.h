@@ -1,0 +1,215 @@
+// GEMM epilogues.  Each is called once per (4 consecutive rows i..i+3, column j)
+// of the D tile with the fp32 accumulators; it owns its bounds checks.
+#pragma once
+#include "common.h"
+
+namespace aaa {
+
+// out[j*ld + i + e] = v[e] (+ bias[i+e]) (relu?)  -- D stored transposed, e.g.
+// a conv output [pixel][channel] or a linear output [row][feature].
+template <typename OT>
+struct EpiStoreT {
+  OT* out;
+  int ld, Mi, Nj;
+  const float* bias;
+  int relu;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    float v[4] = {v0, v1, v2, v3};
+    OT* o = out + (size_t)j * ld + i;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (i + e < Mi) {
+        float x = v[e] + (bias ? bias[i + e] : 0.f);
+        if (relu) x = fmaxf(x, 0.f);
+        o[e] = (OT)x;
+      }
+    }
+  }
+};
+
+// dx[j*ld + i] = v * (mask[j*ldm + i] > 0)   (ReLU backward through a saved output)
+struct EpiReluBwdT {
+  float* out;
+  const float* mask;
+  int ld, ldm, Mi, Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    float v[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i + e < Mi) out[(size_t)j * ld + i + e] = mask[(size_t)j * ldm + i + e] > 0.f ? v[e] : 0.f;
+  }
+};
+
+// Row-major D: out[(i+e)*ld + j] (+)= v[e].  ATOMIC for split-K weight grads.
+template <bool ATOMIC>
+struct EpiStore {
+  float* out;
+  int ld, Mi, Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    float v[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (i + e < Mi) {
+        if constexpr (ATOMIC) atomicAdd(out + (size_t)(i + e) * ld + j, v[e]);
+        else out[(size_t)(i + e) * ld + j] = v[e];
+      }
+    }
+  }
+};
+
+// Policy / value heads: rows o < A -> logits, A <= o < 2A -> values (+bias).
+struct EpiHeads {
+  float* logits;
+  float* values;
+  const float* bias;  // [2A]
+  int A, Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj) return;
+    float v[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int o = i + e;
+      if (o < A) logits[(size_t)j * A + o] = v[e] + bias[o];
+      else if (o < 2 * A) values[(size_t)j * A + o - A] = v[e] + bias[o];
+    }
+  }
+};
+
+// ---------------------------------------------------------------- LSTMs ---
+// Gate-interleaved rows: row 4*u + g, g = (i, f, c~, o).  Zero-peephole
+// ConvLSTM cell (attention.py:119-123) / zero-state LSTMCell (Q1).
+struct GateFwd {
+  __device__ static __forceinline__ void run(float zi, float zf, float zc, float zo, float cprev,
+                                             float& gi, float& gf, float& gc, float& go,
+                                             float& c, float& h) {
+    gi = sigm_acc(zi);
+    gf = sigm_acc(zf);
+    gc = tanhf(zc);
+    c = gf * cprev + gi * gc;
+    go = sigm_acc(zo);
+    h = go * tanhf(c);
+  }
+};
+
+// Backward of one cell given the incoming dh and the carried dc (from t+1).
+// Returns dz (i,f,c~,o) and updates dc to the carry for t-1 (= dc_t * f_t).
+__device__ __forceinline__ void gate_bwd(float dh, const f32x4& g, float cprev, float ccur, float& dc,
+                                         float& di, float& df, float& dcg, float& dout) {
+  const float gi = g[0], gf = g[1], gc = g[2], go = g[3];
+  const float tc = tanhf(ccur);
+  const float dcc = dc + dh * go * (1.f - tc * tc);
+  dout = dh * tc * (1.f - go) * go;
+  di = dcc * gc * (1.f - gi) * gi;
+  df = dcc * cprev * (1.f - gf) * gf;
+  dcg = dcc * gi * (1.f - gc * gc);
+  dc = dcc * gf;
+}
+
+// ConvLSTM forward step epilogue: D[n = 4ch+g][m] = Wx*x_t + Wh*h_{t-1}.
+template <typename T>
+struct EpiConvLstmFwd {
+  const float* bias;   // [512] gate-interleaved
+  const float* cprev;  // [M][128]  c_{t-1}
+  float* cnext;        // [M][128]  c_t
+  float* hout;         // [M][128]  h_t (fp32, attention input)
+  T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
+  float* gates;        // [M][512]  post-activation (i,f,c~,o)
+  int Nj;              // M = B*P
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 512) return;
+    const int ch = i >> 2;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + i);
+    float gi, gf, gc, go, c, h;
+    GateFwd::run(v0 + b[0], v1 + b[1], v2 + b[2], v3 + b[3], cprev[(size_t)j * 128 + ch], gi, gf, gc, go, c, h);
+    cnext[(size_t)j * 128 + ch] = c;
+    hout[(size_t)j * 128 + ch] = h;
+    xhnext[(size_t)j * 192 + 64 + ch] = (T)h;
+    *reinterpret_cast<f32x4*>(gates + (size_t)j * 512 + i) = f32x4{gi, gf, gc, go};
+  }
+};
+
+// ConvLSTM backward step epilogue on D[c'][m] = dgrad of dz_t into [x_t | h_{t-1}]:
+// rows c' < 64 -> dx_t (conv2 output grad); rows >= 64 -> dh_{t-1}, fused with
+// the gate backward of step t-1 (writes dz_{t-1} and the dc carry), or dh0.
+struct EpiConvLstmBwd {
+  float* dx;            // [M][64]  dY2 slot t
+  const float* gates;   // [M][512] slot t-1
+  const float* cprev;   // [M][128] c_{t-2}
+  const float* ccur;    // [M][128] c_{t-1}
+  const float* dO;      // [M][128] attention-path grad of h_{t-1}
+  float* dC;            // [M][128] dc carry (in/out)
+  float* dz;            // [M][512] slot t-1
+  float* dh0;           // [M][128] or null (only when t == 0)
+  int has_prev, Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 192) return;
+    if (i < 64) {
+      *reinterpret_cast<f32x4*>(dx + (size_t)j * 64 + i) = f32x4{v0, v1, v2, v3};
+      return;
+    }
+    const int ch = i - 64;
+    if (!has_prev) {
+      if (dh0) *reinterpret_cast<f32x4*>(dh0 + (size_t)j * 128 + ch) = f32x4{v0, v1, v2, v3};
+      return;
+    }
+    const float v[4] = {v0, v1, v2, v3};
+    const f32x4 dov = *reinterpret_cast<const f32x4*>(dO + (size_t)j * 128 + ch);
+    const f32x4 cp = *reinterpret_cast<const f32x4*>(cprev + (size_t)j * 128 + ch);
+    const f32x4 cc = *reinterpret_cast<const f32x4*>(ccur + (size_t)j * 128 + ch);
+    f32x4 dcv = *reinterpret_cast<const f32x4*>(dC + (size_t)j * 128 + ch);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + 4 * (ch + e));
+      float dc = dcv[e], di, df, dcg, dout;
+      gate_bwd(v[e] + dov[e], g, cp[e], cc[e], dc, di, df, dcg, dout);
+      dcv[e] = dc;
+      *reinterpret_cast<f32x4*>(dz + (size_t)j * 512 + 4 * (ch + e)) = f32x4{di, df, dcg, dout};
+    }
+    *reinterpret_cast<f32x4*>(dC + (size_t)j * 128 + ch) = dcv;
+  }
+};
+
+// LSTMCell(256,256) with zero state (attention.py:355, Q1), rows 4u+g.
+struct EpiLstmCellFwd {
+  const float* bias;  // [1024] interleaved b_ih + b_hh
+  float* gates;       // [F][1024]
+  float* cout;        // [F][256]
+  float* hout;        // [F][256]
+  int Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 1024) return;
+    const int u = i >> 2;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + i);
+    const float gi = sigm_acc(v0 + b[0]), gf = sigm_acc(v1 + b[1]);
+    const float gc = tanhf(v2 + b[2]), go = sigm_acc(v3 + b[3]);
+    const float c = gf * 0.f + gi * gc;
+    cout[(size_t)j * 256 + u] = c;
+    hout[(size_t)j * 256 + u] = go * tanhf(c);
+    *reinterpret_cast<f32x4*>(gates + (size_t)j * 1024 + i) = f32x4{gi, gf, gc, go};
+  }
+};
+
+// dh from the heads' dgrad (rows = units u..u+3) -> d(gates) of the zero-state cell.
+struct EpiLstmCellBwd {
+  const float* gates;  // [F][1024]
+  const float* cst;    // [F][256]
+  float* dgates;       // [F][1024]
+  int Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 256) return;
+    const float v[4] = {v0, v1, v2, v3};
+    const f32x4 cv = *reinterpret_cast<const f32x4*>(cst + (size_t)j * 256 + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 1024 + 4 * (i + e));
+      float dc = 0.f, di, df, dcg, dout;
+      gate_bwd(v[e], g, 0.f, cv[e], dc, di, df, dcg, dout);
+      *reinterpret_cast<f32x4*>(dgates + (size_t)j * 1024 + 4 * (i + e)) = f32x4{di, df, dcg, dout};
+    }
+  }
+};
+
+}  // namespace aaa

@@ -1,0 +1,440 @@
+// Generic MFMA tiled GEMM / implicit-GEMM convolution for gfx950.
+//
+//   D[i][j] = sum_k A(i,k) * B(j,k)          i in [0,Mi), j in [0,Nj), k in [0,K)
+//
+// A and B are produced by "loaders" that stage a BI x BK (resp. BJ x BK) tile
+// into LDS, either k-contiguous (KC: rows of k) or row-contiguous (RC: rows of
+// i/j for a fixed k).  The loaders are where the convolution lives: LdIm2col
+// gathers NHWC pixels for a (tap, channel) k index (forward conv, or the
+// transposed-conv gather used for dgrad), LdIm2colT does the same with the
+// roles of rows and k swapped (weight gradients, where k runs over pixels).
+//
+// Fragment mapping (32x32 MFMA, both dtypes): lane l = r + 32h holds, for one
+// 16-deep k step, the 8 consecutive k values [8h, 8h+8) of row r of A (and of
+// row r of B).  f32: eight v_mfma_f32_32x32x2_f32 (kk = 0..7 feeds k pair
+// {kk, 8+kk}); bf16: one v_mfma_f32_32x32x16_bf16.  D layout: column j =
+// lane&31, rows 8g+4h+e in registers 4g+e, so every lane owns FOUR consecutive
+// rows of one column -- with gate-interleaved row packing (row = 4*ch + gate)
+// that is exactly the four LSTM gates of one (pixel, channel), which is what
+// lets the gate math run in the GEMM epilogue.
+#pragma once
+#include "common.h"
+
+namespace aaa {
+
+template <typename T, int R, int BK, bool KC>
+struct Tile {
+  static constexpr int PAD = 16 / (int)sizeof(T);
+  static constexpr int LD = KC ? (BK + PAD) : (R + PAD);
+  static constexpr int ELEMS = (KC ? R : BK) * LD;
+  __device__ static __forceinline__ int off(int r, int k) { return KC ? r * LD + k : k * LD + r; }
+};
+
+// ---------------------------------------------------------------- loaders --
+// Plain rows: element (row, k) at src[row*ld + k].  K % VG == 0, ld % VG == 0.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdRows {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPR = BK / VG;
+  static constexpr int NCH = R * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  struct Params { const G* src; int ld; int nrows; };
+  const G* rowp[PER];
+  int kc[PER], lr[PER];
+  bool ok[PER], act[PER];
+  u32x4 buf[PER];
+  __device__ __forceinline__ LdRows(const Params& p, int row0) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      lr[c] = ch / CPR;
+      kc[c] = (ch % CPR) * VG;
+      int row = row0 + lr[c];
+      ok[c] = act[c] && row < p.nrows;
+      rowp[c] = p.src + (size_t)(ok[c] ? row : 0) * p.ld;
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int kend) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int k = k0 + kc[c];
+      if (ok[c] && k < kend) buf[c] = *reinterpret_cast<const u32x4*>(rowp[c] + k);
+      else buf[c] = u32x4{0, 0, 0, 0};
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
+  }
+};
+
+// Transposed rows: element (row, k) at src[k*ld + row]; staged row-contiguous.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdRowsT {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPK = R / VG;
+  static constexpr int NCH = BK * CPK;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  struct Params { const G* src; int ld; int nrows; };
+  const G* src;
+  int ld, nrows;
+  int kr[PER], rc[PER], row[PER];
+  bool act[PER];
+  u32x4 buf[PER];
+  __device__ __forceinline__ LdRowsT(const Params& p, int row0) : src(p.src), ld(p.ld), nrows(p.nrows) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      kr[c] = ch / CPK;
+      rc[c] = (ch % CPK) * VG;
+      row[c] = row0 + rc[c];
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int kend) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int k = k0 + kr[c];
+      u32x4 v = u32x4{0, 0, 0, 0};
+      if (act[c] && k < kend) {
+        const G* p = src + (size_t)k * ld + row[c];
+        if (row[c] + VG <= nrows) {
+          v = *reinterpret_cast<const u32x4*>(p);
+        } else {
+          G tmp[VG];
+#pragma unroll
+          for (int e = 0; e < VG; ++e) tmp[e] = (row[c] + e < nrows) ? p[e] : (G)0.0f;
+          v = __builtin_bit_cast(u32x4, tmp);
+        }
+      }
+      buf[c] = v;
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
+  }
+};
+
+// Convolution geometry shared by the im2col loaders.  NHWC input with pixel
+// stride ``cs`` elements and channel offset ``coff``; k = (ky*KW + kx)*Cin + ci.
+struct ConvGeo {
+  int Cin, cs, coff;
+  int Hin, Win, Hout, Wout;
+  int KW, stride, pad;
+  int transposed;  // 0: forward gather, 1: dgrad (transposed-conv) gather
+};
+
+__device__ __forceinline__ bool conv_src(const ConvGeo& g, int oy, int ox, int ky, int kx, int& iy, int& ix) {
+  if (!g.transposed) {
+    iy = oy * g.stride + ky - g.pad;
+    ix = ox * g.stride + kx - g.pad;
+    return iy >= 0 && iy < g.Hin && ix >= 0 && ix < g.Win;
+  }
+  int ty = oy + g.pad - ky, tx = ox + g.pad - kx;
+  if (ty < 0 || tx < 0) return false;
+  if (g.stride == 1) { iy = ty; ix = tx; }
+  else {
+    if ((ty % g.stride) | (tx % g.stride)) return false;
+    iy = ty / g.stride; ix = tx / g.stride;
+  }
+  return iy < g.Hin && ix < g.Win;
+}
+
+// Rows = output pixels (frame-major), k = (tap, ci).  VEC requires Cin % VG == 0.
+template <typename G, typename T, int R, int BK, int NT, bool VEC>
+struct LdIm2col {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPR = BK / VG;
+  static constexpr int NCH = R * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  struct Params { const G* src; ConvGeo g; int nrows; };
+  ConvGeo g;
+  const G* fbase[PER];
+  int oy[PER], ox[PER], kc[PER], lr[PER];
+  bool ok[PER], act[PER];
+  u32x4 buf[PER];
+  __device__ __forceinline__ LdIm2col(const Params& p, int row0) : g(p.g) {
+    const int hw = g.Hout * g.Wout;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      lr[c] = ch / CPR;
+      kc[c] = (ch % CPR) * VG;
+      int m = row0 + lr[c];
+      ok[c] = act[c] && m < p.nrows;
+      int mm = ok[c] ? m : 0;
+      int f = mm / hw, pix = mm - f * hw;
+      oy[c] = pix / g.Wout;
+      ox[c] = pix - oy[c] * g.Wout;
+      fbase[c] = p.src + (size_t)f * g.Hin * g.Win * g.cs + g.coff;
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int kend) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      u32x4 v = u32x4{0, 0, 0, 0};
+      int k = k0 + kc[c];
+      if constexpr (VEC) {
+        if (ok[c] && k < kend) {
+          int tap = k / g.Cin, ci = k - tap * g.Cin;
+          int ky = tap / g.KW, kx = tap - ky * g.KW, iy, ix;
+          if (conv_src(g, oy[c], ox[c], ky, kx, iy, ix))
+            v = *reinterpret_cast<const u32x4*>(fbase[c] + (size_t)(iy * g.Win + ix) * g.cs + ci);
+        }
+      } else {
+        static_assert(sizeof(G) == 4, "scalar im2col path expects fp32 global data");
+        float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ok[c]) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int ke = k + e;
+            if (ke < kend) {
+              int tap = ke / g.Cin, ci = ke - tap * g.Cin;
+              int ky = tap / g.KW, kx = tap - ky * g.KW, iy, ix;
+              if (conv_src(g, oy[c], ox[c], ky, kx, iy, ix))
+                tmp[e] = (float)fbase[c][(size_t)(iy * g.Win + ix) * g.cs + ci];
+            }
+          }
+        }
+        v = __builtin_bit_cast(u32x4, tmp);
+      }
+      buf[c] = v;
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
+  }
+};
+
+// Rows = k' = (tap, ci) of a convolution, k = output pixel m (weight gradient).
+// Staged row-contiguous.  VEC requires Cin % VG == 0 (a chunk never crosses a tap).
+template <typename G, typename T, int R, int BK, int NT, bool VEC>
+struct LdIm2colT {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPK = R / VG;
+  static constexpr int NCH = BK * CPK;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  struct Params { const G* src; ConvGeo g; int nrows; };  // nrows = KH*KW*Cin
+  ConvGeo g;
+  const G* src;
+  int kr[PER], rc[PER];
+  int ky[PER][VEC ? 1 : 4], kx[PER][VEC ? 1 : 4], ci[PER][VEC ? 1 : 4];
+  bool act[PER], rok[PER][VEC ? 1 : 4];
+  u32x4 buf[PER];
+  __device__ __forceinline__ LdIm2colT(const Params& p, int row0) : g(p.g), src(p.src) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      kr[c] = ch / CPK;
+      rc[c] = (ch % CPK) * VG;
+      constexpr int NE = VEC ? 1 : 4;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        int kp = row0 + rc[c] + e;
+        rok[c][e] = act[c] && kp < p.nrows;
+        int kq = rok[c][e] ? kp : 0;
+        int tap = kq / g.Cin;
+        ci[c][e] = kq - tap * g.Cin;
+        ky[c][e] = tap / g.KW;
+        kx[c][e] = tap - ky[c][e] * g.KW;
+      }
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int kend) {
+    const int hw = g.Hout * g.Wout;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      u32x4 v = u32x4{0, 0, 0, 0};
+      int m = k0 + kr[c];
+      if (act[c] && m < kend) {
+        int f = m / hw, pix = m - f * hw;
+        int oy = pix / g.Wout, ox = pix - oy * g.Wout;
+        const G* fb = src + (size_t)f * g.Hin * g.Win * g.cs + g.coff;
+        if constexpr (VEC) {
+          int iy, ix;
+          if (rok[c][0] && conv_src(g, oy, ox, ky[c][0], kx[c][0], iy, ix))
+            v = *reinterpret_cast<const u32x4*>(fb + (size_t)(iy * g.Win + ix) * g.cs + ci[c][0]);
+        } else {
+          static_assert(sizeof(G) == 4, "scalar im2col path expects fp32 global data");
+          float tmp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int iy, ix;
+            if (rok[c][e] && conv_src(g, oy, ox, ky[c][e], kx[c][e], iy, ix))
+              tmp[e] = (float)fb[(size_t)(iy * g.Win + ix) * g.cs + ci[c][e]];
+          }
+          v = __builtin_bit_cast(u32x4, tmp);
+        }
+      }
+      buf[c] = v;
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
+  }
+};
+
+// ----------------------------------------------------------- fragments ----
+template <typename TL>
+__device__ __forceinline__ void frag_f32(const float* t, int r, int k, float (&a)[8]) {
+  if constexpr (TL::KC_) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(t + r * TL::LD + k);
+    f32x4 x = p[0], y = p[1];
+    a[0] = x[0]; a[1] = x[1]; a[2] = x[2]; a[3] = x[3];
+    a[4] = y[0]; a[5] = y[1]; a[6] = y[2]; a[7] = y[3];
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) a[kk] = t[(k + kk) * TL::LD + r];
+  }
+}
+
+template <typename TL>
+__device__ __forceinline__ bf16x8 frag_bf16(const __bf16* t, int r, int k) {
+  if constexpr (TL::KC_) {
+    return *reinterpret_cast<const bf16x8*>(t + r * TL::LD + k);
+  } else {
+    bf16x8 a;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) a[kk] = t[(k + kk) * TL::LD + r];
+    return a;
+  }
+}
+
+template <typename T, int R, int BK, bool KC>
+struct TileK : Tile<T, R, BK, KC> { static constexpr bool KC_ = KC; };
+
+// ------------------------------------------------------------- kernel -----
+template <typename T, int BI_, int BJ_, int BK_, int WI_, int WJ_>
+struct GemmCfg {
+  using type = T;
+  static constexpr int BI = BI_, BJ = BJ_, BK = BK_, WI = WI_, WJ = WJ_;
+  static constexpr int NT = WI * WJ * 64;
+};
+
+template <class C, class LA, class LB, class EP>
+__global__ void __launch_bounds__(C::NT)
+gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk) {
+  using T = typename C::type;
+  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ;
+  constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
+  static_assert(MI >= 1 && MJ >= 1 && BK % 16 == 0, "tile shape");
+  using TA = TileK<T, BI, BK, LA::KC>;
+  using TB = TileK<T, BJ, BK, LB::KC>;
+  __shared__ __attribute__((aligned(16))) T smem[2 * (TA::ELEMS + TB::ELEMS)];
+  T* const As0 = smem;
+  T* const As1 = smem + TA::ELEMS;
+  T* const Bs0 = smem + 2 * TA::ELEMS;
+  T* const Bs1 = Bs0 + TB::ELEMS;
+
+  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+
+  LA la(pa, i0);
+  LB lb(pb, j0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wi = wave / WJ, wj = wave - (wave / WJ) * WJ;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[MI][MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nk = (ke - kb + BK - 1) / BK;
+  la.fetch(kb, ke);
+  lb.fetch(kb, ke);
+  la.commit(As0);
+  lb.commit(Bs0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool odd = kt & 1;
+    const T* Ac = odd ? As1 : As0;
+    const T* Bc = odd ? Bs1 : Bs0;
+    if (kt + 1 < nk) {
+      la.fetch(kb + (kt + 1) * BK, ke);
+      lb.fetch(kb + (kt + 1) * BK, ke);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int kofs = 16 * s + 8 * h;
+      if constexpr (is_f32<T>::value) {
+        float af[MI][8], bfr[MJ][8];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) frag_f32<TA>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) frag_f32<TB>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+          for (int a = 0; a < MI; ++a)
+#pragma unroll
+            for (int b = 0; b < MJ; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+      } else {
+        bf16x8 af[MI], bfr[MJ];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) af[a] = frag_bf16<TA>(Ac, wi * WTI + a * 32 + r32, kofs);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) bfr[b] = frag_bf16<TB>(Bc, wj * WTJ + b * 32 + r32, kofs);
+#pragma unroll
+        for (int a = 0; a < MI; ++a)
+#pragma unroll
+          for (int b = 0; b < MJ; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) {
+      la.commit(odd ? As0 : As1);
+      lb.commit(odd ? Bs0 : Bs1);
+    }
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = i0 + wi * WTI + a * 32 + 8 * g + 4 * h;
+        const int j = j0 + wj * WTJ + b * 32 + r32;
+        ep(i, j, acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+      }
+}
+
+// Host-side launcher.  Mi/Nj are the D extents, K the reduction length,
+// nsplit the number of K slices (epilogue must accumulate when nsplit > 1).
+template <class C, class LA, class LB, class EP>
+inline hipError_t launch_gemm(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep,
+                              int Mi, int Nj, int K, int nsplit, hipStream_t st) {
+  if (Mi <= 0 || Nj <= 0 || K <= 0) return hipSuccess;
+  if (nsplit < 1) nsplit = 1;
+  int kchunk = (K + nsplit - 1) / nsplit;
+  kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
+  hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk);
+  return hipGetLastError();
+}
+
+}  // namespace aaa

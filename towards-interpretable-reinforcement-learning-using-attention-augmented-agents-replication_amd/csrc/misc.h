@@ -1,0 +1,50 @@
+#pragma once
+#include "common.h"
+#include "epilogues.h"
+
+namespace aaa {
+
+struct LstmPtrs {
+  const float* wx[4];  // Wx{i,f,c,o}.weight (128,64,3,3)
+  const float* bx[4];  // Wx{i,f,c,o}.bias   (128)
+  const float* wh[4];  // Wh{i,f,c,o}.weight (128,128,3,3)
+};
+struct LstmGrads {
+  float* wx[4];
+  float* bx[4];
+  float* wh[4];
+};
+struct F32Pack {
+  const float *a0w, *wih, *bih, *bhh, *pw, *vw, *pb, *vb;
+  float *W1p, *Wihp, *blc, *Whd, *bhd;
+  int ans_in, ans_ld, A, ldy;
+};
+struct F32Unpack {
+  const float *gW1p, *gWihp, *gblc, *gWhd, *gbhd;
+  float *a0w, *wih, *bih, *bhh, *pw, *vw, *pb, *vb;
+  int ans_in, ans_ld, A;
+};
+
+hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
+                     const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st);
+hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
+                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st);
+hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
+                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st);
+hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
+                     const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
+                     float* gb2, float* gb0, hipStream_t st);
+hipError_t colsum(const float* X, int ld, int M, int N, float* out, hipStream_t st);
+hipError_t gate_bwd_last(int M, const float* dO, const float* dhT, const float* gates, const float* cprev,
+                         const float* ccur, float* dC, float* dz, hipStream_t st);
+hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
+template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
+template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);
+template <typename T> hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st);
+template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* Wp, float* bl, hipStream_t st);
+hipError_t pack_f32(const F32Pack& p, hipStream_t st);
+hipError_t unpack_conv(const float* g, int Cout, int Cin, int K, float* dst, hipStream_t st);
+hipError_t unpack_lstm(const float* gW, const float* gb, const LstmGrads& L, hipStream_t st);
+hipError_t unpack_f32(const F32Unpack& p, hipStream_t st);
+
+}  // namespace aaa

@@ -1,0 +1,562 @@
+// Non-GEMM kernels of the attention-agent path: constant query MLP, fused
+// spatial-softmax attention readout (fwd/bwd), column reductions, the last
+// BPTT gate step, and parameter (un)packing.
+#include "misc.h"
+
+namespace aaa {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// QueryNetwork on the always-zero prev_output (attention.py:184-198, 325-331;
+// Q1): q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4.  Also the basis
+// half of the attention logits, SQ[p][q] = sum_c S[p][c] * Q[q][8 + c].
+__global__ void k_query_fwd(const float* __restrict__ b0, const float* __restrict__ W2,
+                            const float* __restrict__ b2, const float* __restrict__ W4,
+                            const float* __restrict__ b4, const float* __restrict__ S, int P, int nq,
+                            float* q1, float* q2, float* Q, float* SQ) {
+  __shared__ float s1[128], s2[576], sq[576];
+  const int qd = 72 * nq, tid = threadIdx.x;
+  for (int o = tid; o < 128; o += blockDim.x) { float v = fmaxf(b0[o], 0.f); s1[o] = v; q1[o] = v; }
+  __syncthreads();
+  for (int o = tid; o < qd; o += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < 128; ++k) acc += W2[o * 128 + k] * s1[k];
+    float v = fmaxf(acc + b2[o], 0.f);
+    s2[o] = v; q2[o] = v;
+  }
+  __syncthreads();
+  for (int o = tid; o < qd; o += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < qd; ++k) acc += W4[o * qd + k] * s2[k];
+    float v = acc + b4[o];
+    sq[o] = v; Q[o] = v;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < P * nq; idx += blockDim.x) {
+    int p = idx / nq, q = idx - p * nq;
+    float acc = 0.f;
+    for (int c = 0; c < 64; ++c) acc += S[p * 64 + c] * sq[q * 72 + 8 + c];
+    SQ[idx] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused attention readout, one workgroup per frame (attention.py:319-348):
+// logits A[p][q] = K[p]·Q[q] with K = [O[:8] | S], softmax over the P grid
+// positions (spatial_softmax), readout a[q] = sum_p A[p][q] [O[8:] | S][p],
+// and the answer row [a_0..a_nq-1 | Q_0..Q_nq-1 | r | a_prev | 0-pad].
+template <int NQ>
+__global__ void __launch_bounds__(256)
+k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q,
+           const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
+           int P, float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* L = sm;               // P*NQ
+  float* Qs = sm + P * NQ;     // NQ*72
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* O = Hs + (size_t)f * P * 128;
+  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Q[i];
+  __syncthreads();
+  for (int idx = tid; idx < P * NQ; idx += 256) {
+    const int p = idx / NQ, q = idx - (idx / NQ) * NQ;
+    const f32x4 k0 = *reinterpret_cast<const f32x4*>(O + p * 128);
+    const f32x4 k1 = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
+    const float* qq = Qs + q * 72;
+    float s = k0[0] * qq[0] + k0[1] * qq[1] + k0[2] * qq[2] + k0[3] * qq[3] +
+              k1[0] * qq[4] + k1[1] * qq[5] + k1[2] * qq[6] + k1[3] * qq[7];
+    L[idx] = s + SQ[idx];
+  }
+  __syncthreads();
+  for (int q = wave; q < NQ; q += 4) {
+    float m = -INFINITY;
+    for (int p = lane; p < P; p += 64) m = fmaxf(m, L[p * NQ + q]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int p = lane; p < P; p += 64) { float e = expf(L[p * NQ + q] - m); L[p * NQ + q] = e; s += e; }
+    s = wave_sum(s);
+    const float inv = 1.f / s;
+    for (int p = lane; p < P; p += 64) {
+      const float a = L[p * NQ + q] * inv;
+      L[p * NQ + q] = a;
+      Am[((size_t)f * P + p) * NQ + q] = a;
+    }
+  }
+  __syncthreads();
+  float* arow = ans + (size_t)f * ans_ld;
+  for (int c = tid; c < 184; c += 256) {
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    if (c < 120) {
+      for (int p = 0; p < P; ++p) {
+        const float v = O[p * 128 + 8 + c];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += L[p * NQ + q] * v;
+      }
+    } else {
+      for (int p = 0; p < P; ++p) {
+        const float v = S[p * 64 + c - 120];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += L[p * NQ + q] * v;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) arow[q * 184 + c] = acc[q];
+  }
+  for (int i = tid; i < NQ * 72; i += 256) arow[NQ * 184 + i] = Qs[i];
+  for (int i = NQ * 256 + tid; i < ans_ld; i += 256) {
+    float v = 0.f;
+    if (i == NQ * 256) v = pr ? pr[f] : 0.f;
+    else if (i == NQ * 256 + 1) v = pa ? pa[f] : 0.f;
+    arow[i] = v;
+  }
+}
+
+// Backward of the readout / softmax / logits for one frame: from da (the
+// answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
+// this frame's contribution to dQ.
+template <int NQ>
+__global__ void __launch_bounds__(256)
+k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q,
+           const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int P,
+           float* __restrict__ dO, float* __restrict__ dQp) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* A = sm;                 // P*NQ
+  float* dA = A + P * NQ;        // P*NQ  (becomes dlogits)
+  float* da = dA + P * NQ;       // NQ*184
+  float* Qs = da + NQ * 184;     // NQ*72
+  float* ss = Qs + NQ * 72;      // NQ
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* O = Hs + (size_t)f * P * 128;
+  for (int i = tid; i < P * NQ; i += 256) A[i] = Am[(size_t)f * P * NQ + i];
+  for (int i = tid; i < NQ * 184; i += 256) da[i] = dAns[(size_t)f * da_ld + i];
+  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Q[i];
+  __syncthreads();
+  // dA[p][q] = sum_c da[q][c] * V[p][c], V = [O[8:128] | S]; one wave per p.
+  for (int p = wave; p < P; p += 4) {
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    for (int c = lane; c < 184; c += 64) {
+      const float v = c < 120 ? O[p * 128 + 8 + c] : S[p * 64 + c - 120];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] += da[q * 184 + c] * v;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float s = wave_sum(acc[q]);
+      if (lane == 0) dA[p * NQ + q] = s;
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < NQ; q += 4) {
+    float s = 0.f;
+    for (int p = lane; p < P; p += 64) s += A[p * NQ + q] * dA[p * NQ + q];
+    s = wave_sum(s);
+    if (lane == 0) ss[q] = s;
+  }
+  __syncthreads();
+  for (int i = tid; i < P * NQ; i += 256) {
+    const int q = i - (i / NQ) * NQ;
+    dA[i] = A[i] * (dA[i] - ss[q]);
+  }
+  __syncthreads();
+  float* dOf = dO + (size_t)f * P * 128;
+  for (int i = tid; i < P * 128; i += 256) {
+    const int p = i >> 7, c = i & 127;
+    float acc = 0.f;
+    if (c < 8) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc += dA[p * NQ + q] * Qs[q * 72 + c];
+    } else {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc += A[p * NQ + q] * da[q * 184 + c - 8];
+    }
+    dOf[i] = acc;
+  }
+  for (int i = tid; i < NQ * 72; i += 256) {
+    const int q = i / 72, c = i - q * 72;
+    float acc = 0.f;
+    if (c < 8) for (int p = 0; p < P; ++p) acc += dA[p * NQ + q] * O[p * 128 + c];
+    else for (int p = 0; p < P; ++p) acc += dA[p * NQ + q] * S[p * 64 + c - 8];
+    dQp[(size_t)f * NQ * 72 + i] = acc;
+  }
+}
+
+// Backward of the query MLP (one workgroup).  dQ = sum over frames of the
+// logits-path grads + the answer-path grad, which summed over rows is
+// W1[:, Q-cols]^T · db1.
+__global__ void k_query_bwd(const float* __restrict__ dQs, const float* __restrict__ gb1,
+                            const float* __restrict__ W1, int ans_in, int nq,
+                            const float* __restrict__ W2, const float* __restrict__ W4,
+                            const float* __restrict__ q1, const float* __restrict__ q2,
+                            float* gW4, float* gb4, float* gW2, float* gb2, float* gb0) {
+  __shared__ float dQ[576], dq2[576], s2[576], s1[128];
+  const int qd = 72 * nq, tid = threadIdx.x, off = nq * 184;
+  for (int i = tid; i < qd; i += blockDim.x) s2[i] = q2[i];
+  for (int i = tid; i < 128; i += blockDim.x) s1[i] = q1[i];
+  for (int o = tid; o < qd; o += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < 512; ++r) acc += gb1[r] * W1[(size_t)r * ans_in + off + o];
+    dQ[o] = dQs[o] + acc;
+  }
+  __syncthreads();
+  for (int o = tid; o < qd; o += blockDim.x) {
+    gb4[o] = dQ[o];
+    for (int k = 0; k < qd; ++k) gW4[o * qd + k] = dQ[o] * s2[k];
+  }
+  for (int k = tid; k < qd; k += blockDim.x) {
+    float acc = 0.f;
+    for (int o = 0; o < qd; ++o) acc += W4[o * qd + k] * dQ[o];
+    dq2[k] = s2[k] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+  for (int k = tid; k < qd; k += blockDim.x) {
+    gb2[k] = dq2[k];
+    for (int j = 0; j < 128; ++j) gW2[k * 128 + j] = dq2[k] * s1[j];
+  }
+  for (int j = tid; j < 128; j += blockDim.x) {
+    float acc = 0.f;
+    for (int k = 0; k < qd; ++k) acc += W2[k * 128 + j] * dq2[k];
+    gb0[j] = s1[j] > 0.f ? acc : 0.f;
+  }
+}
+
+// out[n] += sum_{m} X[m*ld + n]; grid (ceil(N/64), nsplit), 256 threads.
+__global__ void k_colsum(const float* __restrict__ X, int ld, int M, int N, int rows_per, float* out) {
+  __shared__ float red[256];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float s = 0.f;
+  if (col < N)
+    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += X[(size_t)r * ld + col];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && col < N) {
+    float t = red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192];
+    atomicAdd(out + col, t);
+  }
+}
+
+// Gate backward of the LAST step (t = T-1): dh = dO + dhT, dc = carry (dcT).
+__global__ void k_gate_bwd_last(int n, const float* __restrict__ dO, const float* __restrict__ dhT,
+                                const float* __restrict__ gates, const float* __restrict__ cprev,
+                                const float* __restrict__ ccur, float* dC, float* dz) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int m = idx >> 7, ch = idx & 127;
+    const float dh = dO[idx] + (dhT ? dhT[idx] : 0.f);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
+    float dc = dC[idx], di, df, dcg, dout;
+    gate_bwd(dh, g, cprev[idx], ccur[idx], dc, di, df, dcg, dout);
+    dC[idx] = dc;
+    *reinterpret_cast<f32x4*>(dz + (size_t)m * 512 + 4 * ch) = f32x4{di, df, dcg, dout};
+  }
+}
+
+// dY[m][o] = [dlogits | dvalues | 0-pad], ld = ldy
+__global__ void k_concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY) {
+  const int n = F * ldy;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int m = idx / ldy, o = idx - m * ldy;
+    float v = 0.f;
+    if (o < A) v = dl[(size_t)m * A + o];
+    else if (o < 2 * A) v = dv ? dv[(size_t)m * A + o - A] : 0.f;
+    dY[idx] = v;
+  }
+}
+
+// XH slot 0 channels 64..191 <- h0 (or zero)
+template <typename T>
+__global__ void k_state_to_xh(int M, const float* h0, T* xh) {
+  const int n = M * 128;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int m = idx >> 7, ch = idx & 127;
+    xh[(size_t)m * 192 + 64 + ch] = (T)(h0 ? h0[idx] : 0.f);
+  }
+}
+
+// ------------------------------------------------------------- packing ----
+// Conv weight in the reference's (Cout, Cin, kx, ky) orientation (Q3) ->
+// [Cout][(ky*K + kx)*Cin + ci].
+template <typename T>
+__global__ void k_pack_conv(const float* __restrict__ w, int Cout, int Cin, int K, T* dst) {
+  const int n = Cout * K * K * Cin;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int o = idx / (K * K * Cin), r = idx - o * (K * K * Cin);
+    const int tap = r / Cin, ci = r - tap * Cin, ky = tap / K, kx = tap - ky * K;
+    dst[idx] = (T)w[((size_t)(o * Cin + ci) * K + kx) * K + ky];
+  }
+}
+
+// WdT[ci][tap*Cout + co] = Wp[co][tap*Cin + ci]
+template <typename T>
+__global__ void k_pack_dgradT(const T* __restrict__ Wp, int Cout, int taps, int Cin, T* WdT) {
+  const int n = Cin * taps * Cout;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int ci = idx / (taps * Cout), r = idx - ci * (taps * Cout);
+    const int tap = r / Cout, co = r - tap * Cout;
+    WdT[idx] = Wp[(size_t)co * taps * Cin + tap * Cin + ci];
+  }
+}
+
+// ConvLSTM: 8 convs -> one [512][9*192] operand, row n = 4*ch + gate, input
+// channels [x (64) | h (128)]; biases interleaved the same way.
+template <typename T>
+__global__ void k_pack_lstm(LstmPtrs L, T* Wp, float* bl) {
+  const int n = 512 * 1728;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int row = idx / 1728, k = idx - row * 1728;
+    const int ch = row >> 2, g = row & 3;
+    const int tap = k / 192, ci = k - tap * 192, ky = tap / 3, kx = tap - ky * 3;
+    float v;
+    if (ci < 64) v = L.wx[g][((size_t)(ch * 64 + ci) * 3 + kx) * 3 + ky];
+    else v = L.wh[g][((size_t)(ch * 128 + ci - 64) * 3 + kx) * 3 + ky];
+    Wp[idx] = (T)v;
+    if (k == 0) bl[row] = L.bx[g][ch];
+  }
+}
+
+__global__ void k_pack_f32(F32Pack p) {
+  const int n1 = 512 * p.ans_ld, n2 = 1024 * 256, n3 = 1024, n4 = p.ldy * 256, n5 = p.ldy;
+  const int tot = n1 + n2 + n3 + n4 + n5;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+    int i = idx;
+    if (i < n1) {
+      const int o = i / p.ans_ld, k = i - o * p.ans_ld;
+      p.W1p[i] = k < p.ans_in ? p.a0w[(size_t)o * p.ans_in + k] : 0.f;
+      continue;
+    }
+    i -= n1;
+    if (i < n2) {
+      const int row = i >> 8, k = i & 255, u = row >> 2, g = row & 3;
+      p.Wihp[i] = p.wih[(size_t)(g * 256 + u) * 256 + k];
+      continue;
+    }
+    i -= n2;
+    if (i < n3) {
+      const int u = i >> 2, g = i & 3;
+      p.blc[i] = p.bih[g * 256 + u] + p.bhh[g * 256 + u];
+      continue;
+    }
+    i -= n3;
+    if (i < n4) {
+      const int o = i >> 8, k = i & 255;
+      float v = 0.f;
+      if (o < p.A) v = p.pw[o * 256 + k];
+      else if (o < 2 * p.A) v = p.vw[(o - p.A) * 256 + k];
+      p.Whd[i] = v;
+      continue;
+    }
+    i -= n4;
+    {
+      float v = 0.f;
+      if (i < p.A) v = p.pb[i];
+      else if (i < 2 * p.A) v = p.vb[i - p.A];
+      p.bhd[i] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------ unpacking ---
+__global__ void k_unpack_conv(const float* __restrict__ g, int Cout, int Cin, int K, float* dst) {
+  const int n = Cout * Cin * K * K;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    int r = idx;
+    const int ky = r % K; r /= K;
+    const int kx = r % K; r /= K;
+    const int ci = r % Cin, o = r / Cin;
+    dst[idx] = g[(size_t)o * K * K * Cin + (ky * K + kx) * Cin + ci];
+  }
+}
+
+__global__ void k_unpack_lstm(const float* __restrict__ gW, const float* __restrict__ gb, LstmGrads L) {
+  const int nx = 128 * 64 * 9, nh = 128 * 128 * 9;
+  const int tot = 4 * (nx + nh + 128);
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+    const int per = nx + nh + 128;
+    const int g = idx / per;
+    int i = idx - g * per;
+    if (i < nx) {
+      int r = i;
+      const int ky = r % 3; r /= 3;
+      const int kx = r % 3; r /= 3;
+      const int ci = r % 64, ch = r / 64;
+      L.wx[g][i] = gW[(size_t)(4 * ch + g) * 1728 + (ky * 3 + kx) * 192 + ci];
+    } else if ((i -= nx) < nh) {
+      int r = i;
+      const int ky = r % 3; r /= 3;
+      const int kx = r % 3; r /= 3;
+      const int ci = r % 128, ch = r / 128;
+      L.wh[g][i] = gW[(size_t)(4 * ch + g) * 1728 + (ky * 3 + kx) * 192 + 64 + ci];
+    } else {
+      i -= nh;
+      L.bx[g][i] = gb[4 * i + g];
+    }
+  }
+}
+
+__global__ void k_unpack_f32(F32Unpack p) {
+  const int n1 = 512 * p.ans_in, n2 = 1024 * 256, n3 = 1024, n4 = 2 * p.A * 256, n5 = 2 * p.A;
+  const int tot = n1 + n2 + n3 + n4 + n5;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+    int i = idx;
+    if (i < n1) {
+      const int o = i / p.ans_in, k = i - o * p.ans_in;
+      p.a0w[i] = p.gW1p[(size_t)o * p.ans_ld + k];
+      continue;
+    }
+    i -= n1;
+    if (i < n2) {
+      const int row = i >> 8, k = i & 255, g = row >> 8, u = row & 255;
+      p.wih[i] = p.gWihp[(size_t)(4 * u + g) * 256 + k];
+      continue;
+    }
+    i -= n2;
+    if (i < n3) {
+      const int g = i >> 8, u = i & 255;
+      const float v = p.gblc[4 * u + g];
+      p.bih[i] = v;
+      p.bhh[i] = v;
+      continue;
+    }
+    i -= n3;
+    if (i < n4) {
+      const int o = i >> 8, k = i & 255;
+      if (o < p.A) p.pw[o * 256 + k] = p.gWhd[i];
+      else p.vw[(o - p.A) * 256 + k] = p.gWhd[i];
+      continue;
+    }
+    i -= n4;
+    if (i < p.A) p.pb[i] = p.gbhd[i];
+    else p.vb[i - p.A] = p.gbhd[i];
+  }
+}
+
+// ---------------------------------------------------------- launchers -----
+static inline int nblk(long n, int bs = 256) {
+  long b = (n + bs - 1) / bs;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
+                     const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st) {
+  hipLaunchKernelGGL(k_query_fwd, dim3(1), dim3(256), 0, st, b0, W2, b2, W4, b4, S, P, nq, q1, q2, Q, SQ);
+  return hipGetLastError();
+}
+
+hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
+                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st) {
+  const size_t sh = (size_t)(P * nq + nq * 72) * sizeof(float);
+  if (nq == 4) hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, SQ, pr, pa, P, Am, ans, ans_ld);
+  else if (nq == 8) hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, SQ, pr, pa, P, Am, ans, ans_ld);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
+                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st) {
+  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8) * sizeof(float);
+  if (nq == 4) hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
+  else if (nq == 8) hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
+                     const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
+                     float* gb2, float* gb0, hipStream_t st) {
+  hipLaunchKernelGGL(k_query_bwd, dim3(1), dim3(256), 0, st, dQs, gb1, W1, ans_in, nq, W2, W4, q1, q2, gW4, gb4,
+                     gW2, gb2, gb0);
+  return hipGetLastError();
+}
+
+hipError_t colsum(const float* X, int ld, int M, int N, float* out, hipStream_t st) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const int cols = (N + 63) / 64;
+  int split = (1024 + cols - 1) / cols;
+  int rows_per = (M + split - 1) / split;
+  if (rows_per < 64) rows_per = 64;
+  split = (M + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(k_colsum, dim3(cols, split), dim3(256), 0, st, X, ld, M, N, rows_per, out);
+  return hipGetLastError();
+}
+
+hipError_t gate_bwd_last(int M, const float* dO, const float* dhT, const float* gates, const float* cprev,
+                         const float* ccur, float* dC, float* dz, hipStream_t st) {
+  hipLaunchKernelGGL(k_gate_bwd_last, dim3(nblk((long)M * 128)), dim3(256), 0, st, M * 128, dO, dhT, gates,
+                     cprev, ccur, dC, dz);
+  return hipGetLastError();
+}
+
+hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st) {
+  hipLaunchKernelGGL(k_concat_dy, dim3(nblk((long)F * ldy)), dim3(256), 0, st, F, A, ldy, dl, dv, dY);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st) {
+  hipLaunchKernelGGL(k_state_to_xh<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, h0, xh);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_conv<T>, dim3(nblk((long)Cout * Cin * K * K)), dim3(256), 0, st, w, Cout, Cin, K, dst);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_dgradT<T>, dim3(nblk((long)Cout * taps * Cin)), dim3(256), 0, st, Wp, Cout, taps, Cin, WdT);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t pack_lstm(const LstmPtrs& L, T* Wp, float* bl, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lstm<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, Wp, bl);
+  return hipGetLastError();
+}
+
+hipError_t pack_f32(const F32Pack& p, hipStream_t st) {
+  long n = 512L * p.ans_ld + 1024L * 256 + 1024 + (long)p.ldy * 256 + p.ldy;
+  hipLaunchKernelGGL(k_pack_f32, dim3(nblk(n)), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t unpack_conv(const float* g, int Cout, int Cin, int K, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack_conv, dim3(nblk((long)Cout * Cin * K * K)), dim3(256), 0, st, g, Cout, Cin, K, dst);
+  return hipGetLastError();
+}
+
+hipError_t unpack_lstm(const float* gW, const float* gb, const LstmGrads& L, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack_lstm, dim3(nblk(4L * (128 * 64 * 9 + 128 * 128 * 9 + 128))), dim3(256), 0, st, gW,
+                     gb, L);
+  return hipGetLastError();
+}
+
+hipError_t unpack_f32(const F32Unpack& p, hipStream_t st) {
+  long n = 512L * p.ans_in + 1024L * 256 + 1024 + 2L * p.A * 256 + 2 * p.A;
+  hipLaunchKernelGGL(k_unpack_f32, dim3(nblk(n)), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+template hipError_t state_to_xh<float>(int, const float*, float*, hipStream_t);
+template hipError_t state_to_xh<__bf16>(int, const float*, __bf16*, hipStream_t);
+template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStream_t);
+template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);
+template hipError_t pack_dgradT<float>(const float*, int, int, int, float*, hipStream_t);
+template hipError_t pack_dgradT<__bf16>(const __bf16*, int, int, int, __bf16*, hipStream_t);
+template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, hipStream_t);
+template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, float*, hipStream_t);
+
+}  // namespace aaa

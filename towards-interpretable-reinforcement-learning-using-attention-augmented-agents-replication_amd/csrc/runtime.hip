@@ -1,0 +1,648 @@
+// Host runtime + C ABI (include/aaa.h): buffer layout, weight packing and the
+// launch sequence of the batched unroll forward / hand-written BPTT backward.
+//
+// Forward (reference attention.py:298-368 over T steps from reset()):
+//   conv1, conv2 over all T*B frames at once (no recurrence there), then one
+//   fused ConvLSTM kernel per step (x- and h-convs as ONE implicit GEMM over
+//   [x_t | h_{t-1}], gate math in the epilogue), then -- because the policy
+//   core never carries state (Q1) -- the whole attention / answer / LSTMCell /
+//   heads tail batched over all T*B frames.
+// Backward (what autograd does for main_mp.py:77): the tail batched over T*B,
+// then the only sequential part, the ConvLSTM BPTT (one dgrad GEMM per step
+// with the previous step's gate backward fused in its epilogue), then all
+// weight gradients as long-K GEMMs over every frame.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <type_traits>
+
+#include "aaa.h"
+#include "epilogues.h"
+#include "gemm.h"
+#include "misc.h"
+
+namespace aaa {
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(AAA_E_LAUNCH, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+static inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline int conv_out(int n, int k, int s, int p) { return (n + 2 * p - k) / s + 1; }
+
+enum PIdx {
+  C0W = 0, C0B, C1W, C1B,
+  XI_W, XI_B, HI_W, XF_W, XF_B, HF_W, XC_W, XC_B, HC_W, XO_W, XO_B, HO_W,
+  Q0W, Q0B, Q2W, Q2B, Q4W, Q4B, A0W, A0B, A2W, A2B, WIH, WHH, BIH, BHH, PW, PB, VW, VB, NPARAM
+};
+
+struct Layout {
+  int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
+  int qd, da, ans_in, ans_ld, ldy;
+  size_t poff[NPARAM], psz[NPARAM], ptotal;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_Wpl, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dY2, dY1;
+  size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
+};
+
+static int build_layout(const aaa_cfg* c, Layout& L) {
+  if (!c) return fail(AAA_E_ARG, "cfg is NULL");
+  if (c->B < 1 || c->T < 1) return fail(AAA_E_ARG, "B and T must be >= 1 (B=%d T=%d)", c->B, c->T);
+  if (c->nq != 4 && c->nq != 8) return fail(AAA_E_ARG, "nq must be 4 or 8 (got %d)", c->nq);
+  if (c->A < 1 || c->A > 256) return fail(AAA_E_ARG, "A out of range (%d)", c->A);
+  if (c->dtype != AAA_F32 && c->dtype != AAA_BF16) return fail(AAA_E_ARG, "bad dtype %d", c->dtype);
+  L.B = c->B; L.T = c->T; L.F = c->B * c->T; L.H = c->H; L.W = c->W;
+  L.H1 = conv_out(c->H, 8, 4, 1); L.W1 = conv_out(c->W, 8, 4, 1);
+  L.h = conv_out(L.H1, 4, 2, 2); L.w = conv_out(L.W1, 4, 2, 2);
+  if (L.H1 < 1 || L.W1 < 1 || L.h < 1 || L.w < 1) return fail(AAA_E_ARG, "frame %dx%d too small", c->H, c->W);
+  L.P1 = L.H1 * L.W1; L.P = L.h * L.w;
+  L.nq = c->nq; L.A = c->A; L.dt = c->dtype; L.esz = c->dtype == AAA_BF16 ? 2 : 4;
+  L.qd = 72 * L.nq; L.da = 184 * L.nq; L.ans_in = 256 * L.nq + 2;
+  L.ans_ld = (L.ans_in + 7) / 8 * 8;
+  L.ldy = (2 * L.A + 3) / 4 * 4;
+  const size_t shp[NPARAM] = {
+      32 * 3 * 64, 32, 64 * 32 * 16, 64,
+      128 * 64 * 9, 128, 128 * 128 * 9, 128 * 64 * 9, 128, 128 * 128 * 9,
+      128 * 64 * 9, 128, 128 * 128 * 9, 128 * 64 * 9, 128, 128 * 128 * 9,
+      128 * 256, 128, (size_t)L.qd * 128, (size_t)L.qd, (size_t)L.qd * L.qd, (size_t)L.qd,
+      512 * (size_t)L.ans_in, 512, 256 * 512, 256,
+      1024 * 256, 1024 * 256, 1024, 1024,
+      (size_t)L.A * 256, (size_t)L.A, (size_t)L.A * 256, (size_t)L.A};
+  size_t o = 0;
+  for (int i = 0; i < NPARAM; ++i) { L.poff[i] = o; L.psz[i] = shp[i]; o += shp[i]; }
+  L.ptotal = o;
+  // packed weights
+  size_t p = 0;
+  auto take = [&](size_t bytes) { size_t r = p; p = al256(p + bytes); return r; };
+  const size_t e = L.esz;
+  L.k_Wp1 = take(32 * 192 * e);
+  L.k_Wp2 = take(64 * 512 * e);
+  L.k_WdT2 = take(32 * 1024 * e);
+  L.k_Wpl = take(512 * 1728 * e);
+  L.k_WdTl = take(192 * 4608 * e);
+  L.k_bl = take(512 * 4);
+  L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
+  L.k_Wihp = take(1024 * 256 * 4);
+  L.k_blc = take(1024 * 4);
+  L.k_Whd = take((size_t)L.ldy * 256 * 4);
+  L.k_bhd = take((size_t)L.ldy * 4);
+  L.packed = p;
+  // workspace
+  p = 0;
+  const size_t F = L.F, P = L.P, M = (size_t)L.B * L.P;
+  L.Y1 = take(F * L.P1 * 32 * e);
+  L.XH = take((size_t)(L.T + 1) * M * 192 * e);
+  L.Hs = take(F * P * 128 * 4);
+  L.Cst = take((size_t)(L.T + 1) * M * 128 * 4);
+  L.Gt = take(F * P * 512 * 4);
+  L.q1 = take(128 * 4);
+  L.q2 = take((size_t)L.qd * 4);
+  L.Q = take((size_t)L.qd * 4);
+  L.SQ = take(P * L.nq * 4);
+  L.Am = take(F * P * L.nq * 4);
+  L.ans = take(F * L.ans_ld * 4);
+  L.hid1 = take(F * 512 * 4);
+  L.AO = take(F * 256 * 4);
+  L.LG = take(F * 1024 * 4);
+  L.LC = take(F * 256 * 4);
+  L.LH = take(F * 256 * 4);
+  L.dY = take(F * L.ldy * 4);
+  L.dLG = take(F * 1024 * 4);
+  L.dAO = take(F * 256 * 4);
+  L.dH1 = take(F * 512 * 4);
+  L.dAns = take(F * L.da * 4);
+  L.dO = take(F * P * 128 * 4);
+  L.dQp = take(F * L.qd * 4);
+  L.dC = take(M * 128 * 4);
+  L.dZ = take(F * P * 512 * 4);
+  L.dY2 = take(F * P * 64 * 4);
+  L.dY1 = take(F * L.P1 * 32 * 4);
+  // zero-initialised (atomic) accumulation region: one memset covers it
+  L.dQs = take((size_t)L.qd * 4);
+  L.gWp1 = take(32 * 192 * 4);
+  L.gWp2 = take(64 * 512 * 4);
+  L.gWpl = take(512 * 1728 * 4);
+  L.gbl = take(512 * 4);
+  L.gW1p = take(512 * (size_t)L.ans_ld * 4);
+  L.gWihp = take(1024 * 256 * 4);
+  L.gblc = take(1024 * 4);
+  L.gWhd = take((size_t)L.ldy * 256 * 4);
+  L.gbhd = take((size_t)L.ldy * 4);
+  L.ws = p;
+  return AAA_OK;
+}
+
+static int check_device() {
+  static std::mutex mu;
+  static int checked[64] = {0};  // 0 unknown, 1 ok, -1 bad
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(AAA_E_DEVICE, "no HIP device");
+  if (dev < 0 || dev >= 64) return AAA_OK;
+  std::lock_guard<std::mutex> lk(mu);
+  if (checked[dev] == 0) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(AAA_E_DEVICE, "hipGetDeviceProperties failed");
+    checked[dev] = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : -1;
+    if (checked[dev] < 0) g_err = std::string("device is ") + prop.gcnArchName + ", need gfx950";
+  }
+  return checked[dev] > 0 ? AAA_OK : fail(AAA_E_DEVICE, "%s", g_err.c_str());
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// --------------------------------------------------------- tile configs ---
+using CF = GemmCfg<float, 64, 64, 32, 2, 2>;     // fp32: exact v_mfma_f32_32x32x2_f32
+using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;    // bf16 operands, fp32 accumulate
+template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
+
+static int wgrad_splits(int tiles, int K, int BK) {
+  int s = std::max(1, 1024 / std::max(tiles, 1));
+  int maxs = std::max(1, K / (8 * BK));
+  return std::min(s, maxs);
+}
+
+// ------------------------------------------------------------- packing ----
+template <typename T>
+static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
+  HIPCHK(pack_conv<T>(prm + L.poff[C0W], 32, 3, 8, (T*)(pk + L.k_Wp1), st));
+  HIPCHK(pack_conv<T>(prm + L.poff[C1W], 64, 32, 4, (T*)(pk + L.k_Wp2), st));
+  HIPCHK(pack_dgradT<T>((const T*)(pk + L.k_Wp2), 64, 16, 32, (T*)(pk + L.k_WdT2), st));
+  LstmPtrs lp;
+  for (int g = 0; g < 4; ++g) {
+    lp.wx[g] = prm + L.poff[XI_W + 3 * g];
+    lp.bx[g] = prm + L.poff[XI_B + 3 * g];
+    lp.wh[g] = prm + L.poff[HI_W + 3 * g];
+  }
+  HIPCHK(pack_lstm<T>(lp, (T*)(pk + L.k_Wpl), (float*)(pk + L.k_bl), st));
+  HIPCHK(pack_dgradT<T>((const T*)(pk + L.k_Wpl), 512, 9, 192, (T*)(pk + L.k_WdTl), st));
+  F32Pack fp;
+  fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
+  fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
+  fp.W1p = (float*)(pk + L.k_W1p); fp.Wihp = (float*)(pk + L.k_Wihp); fp.blc = (float*)(pk + L.k_blc);
+  fp.Whd = (float*)(pk + L.k_Whd); fp.bhd = (float*)(pk + L.k_bhd);
+  fp.ans_in = L.ans_in; fp.ans_ld = L.ans_ld; fp.A = L.A; fp.ldy = L.ldy;
+  HIPCHK(pack_f32(fp, st));
+  return AAA_OK;
+}
+
+// ------------------------------------------------------------- forward ----
+template <typename T>
+static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  constexpr int NTF = CF::NT;
+  char* ws = (char*)io->workspace;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  auto Wf = [&](size_t off) { return (float*)(ws + off); };
+  auto Wt = [&](size_t off) { return (T*)(ws + off); };
+  const int F = L.F, P = L.P, M = L.B * L.P;
+
+  {  // conv1 (attention.py:156-162): frames (fp32, Cin=3) -> Y1
+    using LA = LdRows<T, T, C::BI, C::BK, NT>;
+    using LB = LdIm2col<float, T, C::BJ, C::BK, NT, false>;
+    typename LA::Params pa{(const T*)(pk + L.k_Wp1), 192, 32};
+    typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}, F * L.P1};
+    EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
+    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, F * L.P1, 192, 1, st)));
+  }
+  {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
+    using LA = LdRows<T, T, C::BI, C::BK, NT>;
+    using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
+    typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};
+    typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}, F * P};
+    EpiStoreT<T> ep{Wt(L.XH), 192, 64, F * P, prm + L.poff[C1B], 0};
+    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, F * P, 512, 1, st)));
+  }
+  // initial state (reset(): zeros, attention.py:142-149) or carried state
+  HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
+  if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126)
+    using LA = LdRows<T, T, C::BI, C::BK, NT>;
+    using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
+    typename LA::Params pa{(const T*)(pk + L.k_Wpl), 1728, 512};
+    typename LB::Params pb{Wt(L.XH) + (size_t)t * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}, M};
+    EpiConvLstmFwd<T> ep{(const float*)(pk + L.k_bl), Wf(L.Cst) + (size_t)t * M * 128,
+                         Wf(L.Cst) + (size_t)(t + 1) * M * 128, Wf(L.Hs) + (size_t)t * M * 128,
+                         Wt(L.XH) + (size_t)(t + 1) * M * 192, Wf(L.Gt) + (size_t)t * M * 512, M};
+    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, M, 1728, 1, st)));
+  }
+  // constant query (Q1) + fused attention readout over all T*B frames
+  HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
+                   io->basis, P, L.nq, Wf(L.q1), Wf(L.q2), Wf(L.Q), Wf(L.SQ), st));
+  HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
+                  Wf(L.ans), L.ans_ld, st));
+  if (io->attn) HIPCHK(hipMemcpyAsync(io->attn, Wf(L.Am), (size_t)F * P * L.nq * 4, hipMemcpyDeviceToDevice, st));
+  using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
+  using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
+  {  // answer_processor.0 + ReLU (attention.py:277-282, 350)
+    LRf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, 512};
+    LRfj::Params pb{Wf(L.ans), L.ans_ld, F};
+    EpiStoreT<float> ep{Wf(L.hid1), 512, 512, F, prm + L.poff[A0B], 1};
+    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 512, F, L.ans_ld, 1, st)));
+  }
+  {  // answer_processor.2
+    LRf::Params pa{prm + L.poff[A2W], 512, 256};
+    LRfj::Params pb{Wf(L.hid1), 512, F};
+    EpiStoreT<float> ep{Wf(L.AO), 256, 256, F, prm + L.poff[A2B], 0};
+    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 256, F, 512, 1, st)));
+  }
+  {  // policy_core LSTMCell from zero state (attention.py:354-355)
+    LRf::Params pa{(const float*)(pk + L.k_Wihp), 256, 1024};
+    LRfj::Params pb{Wf(L.AO), 256, F};
+    EpiLstmCellFwd ep{(const float*)(pk + L.k_blc), Wf(L.LG), Wf(L.LC), Wf(L.LH), F};
+    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 1024, F, 256, 1, st)));
+  }
+  {  // policy / values heads (attention.py:365-367)
+    LRf::Params pa{(const float*)(pk + L.k_Whd), 256, 2 * L.A};
+    LRfj::Params pb{Wf(L.LH), 256, F};
+    EpiHeads ep{io->logits, io->values, (const float*)(pk + L.k_bhd), L.A, F};
+    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 2 * L.A, F, 256, 1, st)));
+  }
+  if (io->hT)
+    HIPCHK(hipMemcpyAsync(io->hT, Wf(L.Hs) + (size_t)(L.T - 1) * M * 128, (size_t)M * 128 * 4,
+                          hipMemcpyDeviceToDevice, st));
+  if (io->cT)
+    HIPCHK(hipMemcpyAsync(io->cT, Wf(L.Cst) + (size_t)L.T * M * 128, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  return AAA_OK;
+}
+
+// ------------------------------------------------------------ backward ----
+template <typename T>
+static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  constexpr int NTF = CF::NT;
+  char* ws = (char*)io->workspace;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  float* grads = io->grads;
+  auto Wf = [&](size_t off) { return (float*)(ws + off); };
+  auto Wt = [&](size_t off) { return (T*)(ws + off); };
+  const int F = L.F, P = L.P, M = L.B * L.P;
+  using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
+  using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
+  using LTf = LdRowsT<float, float, CF::BI, CF::BK, NTF>;
+  using LTfj = LdRowsT<float, float, CF::BJ, CF::BK, NTF>;
+
+  if (phases & AAA_BWD_HEAD) {
+    HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
+    HIPCHK(hipMemsetAsync(ws + L.dQs, 0, L.ws - L.dQs, st));
+    HIPCHK(concat_dy(F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
+    {  // heads dgrad fused with the zero-state LSTMCell backward
+      LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
+      LRfj::Params pb{Wf(L.dY), L.ldy, F};
+      EpiLstmCellBwd ep{Wf(L.LG), Wf(L.LC), Wf(L.dLG), F};
+      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 256, F, L.ldy, 1, st)));
+    }
+    {  // heads wgrad
+      LTf::Params pa{Wf(L.dY), L.ldy, L.ldy};
+      LTfj::Params pb{Wf(L.LH), 256, 256};
+      EpiStore<true> ep{Wf(L.gWhd), 256, L.ldy, 256};
+      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), st)));
+      HIPCHK(colsum(Wf(L.dY), L.ldy, F, L.ldy, Wf(L.gbhd), st));
+    }
+    {  // LSTMCell input dgrad
+      LTf::Params pa{(const float*)(pk + L.k_Wihp), 256, 256};
+      LRfj::Params pb{Wf(L.dLG), 1024, F};
+      EpiStoreT<float> ep{Wf(L.dAO), 256, 256, F, nullptr, 0};
+      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 256, F, 1024, 1, st)));
+    }
+    {  // LSTMCell weight_ih grad (weight_hh grad is exactly zero: h0 = 0, Q1)
+      LTf::Params pa{Wf(L.dLG), 1024, 1024};
+      LTfj::Params pb{Wf(L.AO), 256, 256};
+      EpiStore<true> ep{Wf(L.gWihp), 256, 1024, 256};
+      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), st)));
+      HIPCHK(colsum(Wf(L.dLG), 1024, F, 1024, Wf(L.gblc), st));
+    }
+    {  // answer_processor.2 dgrad fused with ReLU backward
+      LTf::Params pa{prm + L.poff[A2W], 512, 512};
+      LRfj::Params pb{Wf(L.dAO), 256, F};
+      EpiReluBwdT ep{Wf(L.dH1), Wf(L.hid1), 512, 512, 512, F};
+      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 512, F, 256, 1, st)));
+    }
+    {  // answer_processor.2 wgrad / bias
+      LTf::Params pa{Wf(L.dAO), 256, 256};
+      LTfj::Params pb{Wf(L.hid1), 512, 512};
+      EpiStore<true> ep{grads + L.poff[A2W], 512, 256, 512};
+      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), st)));
+      HIPCHK(colsum(Wf(L.dAO), 256, F, 256, grads + L.poff[A2B], st));
+    }
+    {  // answer_processor.0 dgrad (readout columns only)
+      LTf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, L.da};
+      LRfj::Params pb{Wf(L.dH1), 512, F};
+      EpiStoreT<float> ep{Wf(L.dAns), L.da, L.da, F, nullptr, 0};
+      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, L.da, F, 512, 1, st)));
+    }
+    {  // answer_processor.0 wgrad / bias
+      LTf::Params pa{Wf(L.dH1), 512, 512};
+      LTfj::Params pb{Wf(L.ans), L.ans_ld, L.ans_ld};
+      EpiStore<true> ep{Wf(L.gW1p), L.ans_ld, 512, L.ans_ld};
+      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 512, L.ans_ld, F,
+                                        wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), st)));
+      HIPCHK(colsum(Wf(L.dH1), 512, F, 512, grads + L.poff[A0B], st));
+    }
+    // attention readout / softmax / logits backward, then the query MLP
+    HIPCHK(attn_bwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq, Wf(L.dO), Wf(L.dQp), st));
+    HIPCHK(colsum(Wf(L.dQp), L.qd, F, L.qd, Wf(L.dQs), st));
+    HIPCHK(query_bwd(Wf(L.dQs), grads + L.poff[A0B], prm + L.poff[A0W], L.ans_in, L.nq, prm + L.poff[Q2W],
+                     prm + L.poff[Q4W], Wf(L.q1), Wf(L.q2), grads + L.poff[Q4W], grads + L.poff[Q4B],
+                     grads + L.poff[Q2W], grads + L.poff[Q2B], grads + L.poff[Q0B], st));
+    F32Unpack up;
+    up.gW1p = Wf(L.gW1p); up.gWihp = Wf(L.gWihp); up.gblc = Wf(L.gblc); up.gWhd = Wf(L.gWhd); up.gbhd = Wf(L.gbhd);
+    up.a0w = grads + L.poff[A0W]; up.wih = grads + L.poff[WIH]; up.bih = grads + L.poff[BIH];
+    up.bhh = grads + L.poff[BHH]; up.pw = grads + L.poff[PW]; up.vw = grads + L.poff[VW];
+    up.pb = grads + L.poff[PB]; up.vb = grads + L.poff[VB];
+    up.ans_in = L.ans_in; up.ans_ld = L.ans_ld; up.A = L.A;
+    HIPCHK(unpack_f32(up, st));
+  }
+
+  if (phases & AAA_BWD_CORE) {
+    // ConvLSTM BPTT, t = T-1 .. 0
+    if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
+    const int t1 = L.T - 1;
+    HIPCHK(gate_bwd_last(M, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
+                         Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
+                         Wf(L.dZ) + (size_t)t1 * M * 512, st));
+    for (int t = t1; t >= 0; --t) {
+      using LA = LdRows<T, T, C::BI, C::BK, NT>;
+      using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
+      const bool prev = t > 0;
+      typename LA::Params pa{(const T*)(pk + L.k_WdTl), 4608, 192};
+      typename LB::Params pb{Wf(L.dZ) + (size_t)t * M * 512, ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}, M};
+      EpiConvLstmBwd ep{Wf(L.dY2) + (size_t)t * M * 64,
+                        prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
+                        prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
+                        Wf(L.Cst) + (size_t)t * M * 128,
+                        prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
+                        Wf(L.dC),
+                        prev ? Wf(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
+                        prev ? nullptr : io->dh0, prev ? 1 : 0, M};
+      const int rows = (prev || io->dh0) ? 192 : 64;
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, rows, M, 4608, 1, st)));
+    }
+    if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    {  // all 8 ConvLSTM weight grads as one long-K GEMM over every (t, b, p)
+      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colT<T, T, C::BJ, C::BK, NT, true>;
+      typename LA::Params pa{Wf(L.dZ), 512, 512};
+      typename LB::Params pb{Wt(L.XH), ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}, 1728};
+      EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
+      const int tiles = cdiv(512, C::BI) * cdiv(1728, C::BJ);
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, 1728, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
+      HIPCHK(colsum(Wf(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
+    }
+    LstmGrads lg;
+    for (int g = 0; g < 4; ++g) {
+      lg.wx[g] = grads + L.poff[XI_W + 3 * g];
+      lg.bx[g] = grads + L.poff[XI_B + 3 * g];
+      lg.wh[g] = grads + L.poff[HI_W + 3 * g];
+    }
+    HIPCHK(unpack_lstm(Wf(L.gWpl), Wf(L.gbl), lg, st));
+  }
+
+  if (phases & AAA_BWD_VISION) {
+    {  // conv2 wgrad / bias
+      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colT<T, T, C::BJ, C::BK, NT, true>;
+      typename LA::Params pa{Wf(L.dY2), 64, 64};
+      typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}, 512};
+      EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
+      const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
+      HIPCHK(colsum(Wf(L.dY2), 64, F * P, 64, grads + L.poff[C1B], st));
+    }
+    {  // conv2 dgrad (stride-2 transposed gather) -> dY1
+      using LA = LdRows<T, T, C::BI, C::BK, NT>;
+      using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
+      typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
+      typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}, F * L.P1};
+      EpiStoreT<float> ep{Wf(L.dY1), 32, 32, F * L.P1, nullptr, 0};
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, F * L.P1, 1024, 1, st)));
+    }
+    {  // conv1 wgrad / bias (frames need no grad)
+      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colT<float, T, C::BJ, C::BK, NT, false>;
+      typename LA::Params pa{Wf(L.dY1), 32, 32};
+      typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}, 192};
+      EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
+      const int tiles = cdiv(32, C::BI) * cdiv(192, C::BJ);
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, 192, F * L.P1, wgrad_splits(tiles, F * L.P1, C::BK), st)));
+      HIPCHK(colsum(Wf(L.dY1), 32, F * L.P1, 32, grads + L.poff[C0B], st));
+    }
+    HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
+    HIPCHK(unpack_conv(Wf(L.gWp1), 32, 3, 8, grads + L.poff[C0W], st));
+  }
+  return AAA_OK;
+}
+
+// ----------------------------------------------------- unit-test entries --
+template <typename T>
+static int conv_nhwc_impl(const aaa_conv_desc* d, const float* x, const float* w, const float* bias, float* y,
+                          hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  const int K = d->KH * d->KW * d->Cin, M = d->N * d->Hout * d->Wout;
+  using LA = LdRows<float, T, C::BI, C::BK, NT>;
+  typename LA::Params pa{w, K, d->Cout};
+  ConvGeo g{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0};
+  EpiStoreT<float> ep{y, d->Cout, d->Cout, M, bias, 0};
+  if (d->Cin % 4 == 0) {
+    using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
+    HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, M}, ep, d->Cout, M, K, 1, st)));
+  } else {
+    using LB = LdIm2col<float, T, C::BJ, C::BK, NT, false>;
+    HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, M}, ep, d->Cout, M, K, 1, st)));
+  }
+  return AAA_OK;
+}
+
+template <typename T>
+static int dgrad_nhwc_impl(const aaa_conv_desc* d, const float* dy, const float* wT, float* dx, hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  const int K = d->KH * d->KW * d->Cout, M = d->N * d->Hin * d->Win;
+  using LA = LdRows<float, T, C::BI, C::BK, NT>;
+  using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
+  typename LA::Params pa{wT, K, d->Cin};
+  ConvGeo g{d->Cout, d->Cout, 0, d->Hout, d->Wout, d->Hin, d->Win, d->KW, d->stride, d->pad, 1};
+  EpiStoreT<float> ep{dx, d->Cin, d->Cin, M, nullptr, 0};
+  HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{dy, g, M}, ep, d->Cin, M, K, 1, st)));
+  return AAA_OK;
+}
+
+template <typename T>
+static int wgrad_nhwc_impl(const aaa_conv_desc* d, const float* x, const float* dy, float* dw, hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  const int Kp = d->KH * d->KW * d->Cin, M = d->N * d->Hout * d->Wout;
+  HIPCHK(hipMemsetAsync(dw, 0, (size_t)d->Cout * Kp * 4, st));
+  using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
+  typename LA::Params pa{dy, d->Cout, d->Cout};
+  ConvGeo g{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0};
+  EpiStore<true> ep{dw, Kp, d->Cout, Kp};
+  const int tiles = cdiv(d->Cout, C::BI) * cdiv(Kp, C::BJ);
+  const int ns = wgrad_splits(tiles, M, C::BK);
+  if (d->Cin % 4 == 0) {
+    using LB = LdIm2colT<float, T, C::BJ, C::BK, NT, true>;
+    HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, Kp}, ep, d->Cout, Kp, M, ns, st)));
+  } else {
+    using LB = LdIm2colT<float, T, C::BJ, C::BK, NT, false>;
+    HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, Kp}, ep, d->Cout, Kp, M, ns, st)));
+  }
+  return AAA_OK;
+}
+
+}  // namespace aaa
+
+using namespace aaa;
+
+extern "C" {
+
+int aaa_abi_version(void) { return AAA_ABI_VERSION; }
+
+const char* aaa_last_error(void) { return g_err.c_str(); }
+
+int aaa_grid(int H, int W, int* h, int* w) {
+  if (!h || !w) return fail(AAA_E_ARG, "NULL output");
+  *h = conv_out(conv_out(H, 8, 4, 1), 4, 2, 2);
+  *w = conv_out(conv_out(W, 8, 4, 1), 4, 2, 2);
+  return (*h >= 1 && *w >= 1) ? AAA_OK : fail(AAA_E_ARG, "frame too small");
+}
+
+int aaa_param_layout(const aaa_cfg* cfg, size_t* total, size_t* offsets, size_t* sizes) {
+  Layout L;
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if (total) *total = L.ptotal;
+  for (int i = 0; i < NPARAM; ++i) {
+    if (offsets) offsets[i] = L.poff[i];
+    if (sizes) sizes[i] = L.psz[i];
+  }
+  return AAA_OK;
+}
+
+size_t aaa_packed_bytes(const aaa_cfg* cfg) {
+  Layout L;
+  return build_layout(cfg, L) ? 0 : L.packed;
+}
+
+size_t aaa_workspace_bytes(const aaa_cfg* cfg) {
+  Layout L;
+  return build_layout(cfg, L) ? 0 : L.ws;
+}
+
+int aaa_pack_weights(const aaa_cfg* cfg, const float* params, void* packed, hipStream_t stream) {
+  Layout L;
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!params || !packed) return fail(AAA_E_ARG, "NULL params/packed");
+  if (!aligned16(params) || !aligned16(packed)) return fail(AAA_E_ALIGN, "params/packed must be 16-byte aligned");
+  return L.dt == AAA_BF16 ? pack_impl<__bf16>(L, params, (char*)packed, stream)
+                          : pack_impl<float>(L, params, (char*)packed, stream);
+}
+
+static int check_io(const Layout& L, const aaa_io* io, bool bwd) {
+  if (!io) return fail(AAA_E_ARG, "io is NULL");
+  if (!io->params || !io->packed || !io->basis || !io->frames || !io->workspace)
+    return fail(AAA_E_ARG, "params/packed/basis/frames/workspace must be set");
+  if (!bwd && (!io->logits || !io->values)) return fail(AAA_E_ARG, "logits/values outputs must be set");
+  if (bwd && (!io->dlogits || !io->grads)) return fail(AAA_E_ARG, "dlogits/grads must be set");
+  const void* ptrs[] = {io->params, io->packed, io->basis, io->frames, io->workspace, io->h0, io->c0, io->hT,
+                        io->cT, io->dhT, io->dcT, io->dh0, io->dc0, io->grads};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(AAA_E_ALIGN, "buffers must be 16-byte aligned");
+  (void)L;
+  return AAA_OK;
+}
+
+int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream) {
+  Layout L;
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if ((r = check_io(L, io, false))) return r;
+  return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream) : forward_impl<float>(L, io, stream);
+}
+
+int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream) {
+  Layout L;
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if ((r = check_io(L, io, true))) return r;
+  if (phases & ~AAA_BWD_ALL || !phases) return fail(AAA_E_ARG, "bad phase mask %d", phases);
+  return L.dt == AAA_BF16 ? backward_impl<__bf16>(L, io, phases, stream)
+                          : backward_impl<float>(L, io, phases, stream);
+}
+
+static int check_conv(const aaa_conv_desc* d) {
+  if (!d) return fail(AAA_E_ARG, "NULL desc");
+  if (d->N < 1 || d->Cin < 1 || d->Cout < 1 || d->KH != d->KW || d->stride < 1 || d->pad < 0)
+    return fail(AAA_E_ARG, "bad conv desc");
+  if (d->Hout != conv_out(d->Hin, d->KH, d->stride, d->pad) || d->Wout != conv_out(d->Win, d->KW, d->stride, d->pad))
+    return fail(AAA_E_ARG, "Hout/Wout inconsistent with Hin/Win/K/stride/pad");
+  if ((d->KH * d->KW * d->Cin) % 4 || d->Cout % 4) return fail(AAA_E_ARG, "KH*KW*Cin and Cout must be multiples of 4");
+  return check_device();
+}
+
+int aaa_conv2d_nhwc(const aaa_conv_desc* d, const float* x, const float* w, const float* bias, float* y,
+                    hipStream_t stream) {
+  int r = check_conv(d);
+  if (r) return r;
+  return d->dtype == AAA_BF16 ? conv_nhwc_impl<__bf16>(d, x, w, bias, y, stream)
+                              : conv_nhwc_impl<float>(d, x, w, bias, y, stream);
+}
+
+int aaa_conv2d_nhwc_dgrad(const aaa_conv_desc* d, const float* dy, const float* wT, float* dx, hipStream_t stream) {
+  int r = check_conv(d);
+  if (r) return r;
+  if (d->Cout % 4) return fail(AAA_E_ARG, "Cout must be a multiple of 4");
+  return d->dtype == AAA_BF16 ? dgrad_nhwc_impl<__bf16>(d, dy, wT, dx, stream)
+                              : dgrad_nhwc_impl<float>(d, dy, wT, dx, stream);
+}
+
+int aaa_conv2d_nhwc_wgrad(const aaa_conv_desc* d, const float* x, const float* dy, float* dw, hipStream_t stream) {
+  int r = check_conv(d);
+  if (r) return r;
+  return d->dtype == AAA_BF16 ? wgrad_nhwc_impl<__bf16>(d, x, dy, dw, stream)
+                              : wgrad_nhwc_impl<float>(d, x, dy, dw, stream);
+}
+
+int aaa_linear(int M, int N, int K, const float* x, const float* w, const float* bias, float* y,
+               hipStream_t stream) {
+  if (M < 1 || N < 1 || K < 1 || K % 4) return fail(AAA_E_ARG, "linear: need M,N,K >= 1 and K %% 4 == 0");
+  int r = check_device();
+  if (r) return r;
+  using LA = LdRows<float, float, CF::BI, CF::BK, CF::NT>;
+  using LB = LdRows<float, float, CF::BJ, CF::BK, CF::NT>;
+  EpiStoreT<float> ep{y, N, N, M, bias, 0};
+  HIPCHK((launch_gemm<CF, LA, LB>(LA::Params{w, K, N}, LB::Params{x, K, M}, ep, N, M, K, 1, stream)));
+  return AAA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+"""Host runtime around the C ABI: buffers for one unroll configuration.
+
+``UnrollRunner`` owns nothing but torch-allocated device memory (the caching
+allocator is the allocator, per the C ABI's ownership rule) and issues the
+library calls on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native as N
+
+
+class UnrollRunner:
+    def __init__(self, B: int, T: int, H: int, W: int, nq: int = 4, A: int = 18,
+                 dtype: str = "fp32", device=None):
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
+        self.lib = N.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
+        self.cfg = N.Cfg(B, T, H, W, nq, A, N.BF16 if dtype == "bf16" else N.F32, 0)
+        self.B, self.T, self.H, self.W, self.nq, self.A, self.dtype = B, T, H, W, nq, A, dtype
+        self.h, self.w = N.grid(H, W)
+        self.P = self.h * self.w
+        self.n_params, self.offsets, self.sizes = N.param_layout(self.cfg)
+        self.ws_bytes = self.lib.aaa_workspace_bytes(ctypes.byref(self.cfg))
+        self.pk_bytes = self.lib.aaa_packed_bytes(ctypes.byref(self.cfg))
+        if not self.ws_bytes or not self.pk_bytes:
+            N.check(-1, "layout")
+
+    # -- buffers ----------------------------------------------------------
+    def new_workspace(self):
+        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+
+    def new_packed(self):
+        return torch.empty(self.pk_bytes, dtype=torch.uint8, device=self.device)
+
+    def state_shape(self):
+        return (self.B, self.h, self.w, 128)
+
+    # -- calls ------------------------------------------------------------
+    def pack(self, flat_params, packed):
+        assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
+        assert flat_params.numel() == self.n_params, (flat_params.numel(), self.n_params)
+        N.check(self.lib.aaa_pack_weights(ctypes.byref(self.cfg), N.ptr(flat_params), N.ptr(packed),
+                                          N.stream_ptr(self.device)), "pack_weights")
+
+    def _io(self, **kw):
+        io = N.IO()
+        for k, v in kw.items():
+            setattr(io, k, None if v is None else (v if isinstance(v, int) else v.data_ptr()))
+        return io
+
+    def forward(self, flat_params, packed, basis, frames, workspace, prev_reward=None, prev_action=None,
+                h0=None, c0=None, want_attn=True, want_state=False):
+        T, B, A = self.T, self.B, self.A
+        dev = self.device
+        self._check_frames(frames)
+        logits = torch.empty(T, B, A, device=dev)
+        values = torch.empty(T, B, A, device=dev)
+        attn = torch.empty(T, B, self.h, self.w, self.nq, device=dev) if want_attn else None
+        hT = torch.empty(self.state_shape(), device=dev) if want_state else None
+        cT = torch.empty(self.state_shape(), device=dev) if want_state else None
+        # keep converted inputs alive until the launches are enqueued
+        keep = dict(prev_reward=_f32(prev_reward, (T, B)), prev_action=_f32(prev_action, (T, B)),
+                    h0=_f32(h0, self.state_shape()), c0=_f32(c0, self.state_shape()))
+        io = self._io(params=flat_params, packed=packed, basis=basis, frames=frames,
+                      logits=logits, values=values, attn=attn, hT=hT, cT=cT, workspace=workspace, **keep)
+        N.check(self.lib.aaa_forward(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(dev)), "forward")
+        return logits, values, attn, hT, cT
+
+    def backward(self, flat_params, packed, basis, frames, workspace, dlogits, dvalues=None, dhT=None,
+                 dcT=None, grads=None, want_state_grads=False, phases=N.BWD_ALL):
+        dev = self.device
+        if grads is None:
+            grads = torch.empty(self.n_params, device=dev)
+        dh0 = torch.empty(self.state_shape(), device=dev) if want_state_grads else None
+        dc0 = torch.empty(self.state_shape(), device=dev) if want_state_grads else None
+        keep = dict(dlogits=_f32(dlogits, (self.T, self.B, self.A)),
+                    dvalues=_f32(dvalues, (self.T, self.B, self.A)),
+                    dhT=_f32(dhT, self.state_shape()), dcT=_f32(dcT, self.state_shape()))
+        io = self._io(params=flat_params, packed=packed, basis=basis, frames=frames, workspace=workspace,
+                      grads=grads, dh0=dh0, dc0=dc0, **keep)
+        N.check(self.lib.aaa_backward(ctypes.byref(self.cfg), ctypes.byref(io), phases, N.stream_ptr(dev)),
+                "backward")
+        return grads, dh0, dc0
+
+    def _check_frames(self, frames):
+        exp = (self.T, self.B, self.H, self.W, 3)
+        if tuple(frames.shape) != exp or frames.dtype != torch.float32 or not frames.is_contiguous():
+            raise ValueError(f"frames must be contiguous fp32 {exp}, got {tuple(frames.shape)} {frames.dtype}")
+        if frames.device != self.device and frames.device.type != "cuda":
+            raise RuntimeError("frames must be on the GPU")
+
+
+def _f32(t, shape):
+    if t is None:
+        return None
+    t = t.reshape(shape)
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
