@@ -1,0 +1,202 @@
+#!/usr/bin/env python
+"""Learner-throughput benchmark (BASELINE.json metric).
+
+One step = pack weights -> T-step unroll forward -> loss cotangents ->
+backward with all 34 parameter gradients ready (and SUM-all-reduced over
+ranks when N > 1).  The optimizer is excluded, as the metric defines.
+value = frames (B*T per rank, all ranks) / max-over-ranks wall time of K steps.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+N > 1 is launched by the driver with torch.distributed.run (one rank per GPU,
+RCCL).  Rank 0 prints ONE JSON line.  Inputs are synthetic (seeded uint8
+frames cast to fp32, seeded weights of the reference architecture).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "learner frames/sec (fwd+bwd, T=20 unroll) at 1/2/4/8 MI355X + % roofline"
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # MI355X dense MFMA (MI355X_MICROARCH.md)
+CONFIGS = {
+    "c2": dict(B=32, T=20, H=84, W=84, nq=4, dtype="fp32",
+               desc="C2 (BASELINE.json configs[1]): B=32 per GPU x T=20 unroll, 84x84, 4 heads, fp32"),
+    "c3": dict(B=256, T=20, H=84, W=84, nq=4, dtype="bf16",
+               desc="C3: B=256 per GPU x T=20, 84x84, 4 heads, bf16 conv/ConvLSTM operands"),
+    "c4": dict(B=128, T=20, H=84, W=84, nq=4, dtype="bf16",
+               desc="C4: B=128 per GPU (1024 over 8) x T=20, 84x84, 4 heads, bf16"),
+    "c5": dict(B=64, T=50, H=168, W=168, nq=8, dtype="bf16",
+               desc="C5: B=64 per GPU (512 over 8) x T=50, 168x168, 8 heads, bf16"),
+}
+# Dense algorithmic FLOP per frame, fwd+bwd (SURVEY.md §8d / BASELINE.md).
+FLOP_PER_FRAME = {(84, 4): 684.7e6, (168, 8): 2487.4e6}
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def flop_per_frame(H, W, nq, A=18):
+    if (H, nq) in FLOP_PER_FRAME and H == W:
+        return FLOP_PER_FRAME[(H, nq)]
+    def o(n, k, s, p):
+        return (n + 2 * p - k) // s + 1
+    H1, W1 = o(H, 8, 4, 1), o(W, 8, 4, 1)
+    P1, P = H1 * W1, o(H1, 4, 2, 2) * o(W1, 4, 2, 2)
+    c1 = 2 * P1 * 32 * 192
+    fwd = (c1 + 2 * P * 64 * 512 + 2 * P * 512 * 1728 + 2 * P * nq * (72 + 184)
+           + 2 * ((256 * nq + 2) * 512 + 512 * 256) + 2 * 256 * 1024 + 2 * 256 * 2 * A)
+    return 3 * fwd - c1
+
+
+def cpu_baseline(cfg):
+    """Time the CPU oracle (the reference op sequence, oracle/ref_cpu.py) on the host."""
+    import numpy as np
+    import torch
+    from oracle import ref_cpu
+    from aaa_amd import detinit
+    cores = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(cores)
+    T, nq = cfg["T"], cfg["nq"]
+    B = min(cfg["B"], 32)
+    H, W = cfg["H"], cfg["W"]
+    mode = "bf16" if cfg["dtype"] == "bf16" else "fp32"
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, 18, nq))
+
+    def it(Tn, Bn):
+        for p in P.values():
+            p.grad = None
+        X = torch.from_numpy(detinit.frames_u8(1234, (Tn, Bn, H, W, 3)).astype(np.float32))
+        lg, vl, _ = ref_cpu.unroll(P, X, nq=nq, conv_mode=mode)
+        Gl = torch.from_numpy(detinit.cotangent(2, tuple(lg.shape)))
+        Gv = torch.from_numpy(detinit.cotangent(3, tuple(vl.shape)))
+        ((lg * Gl).sum() + (vl * Gv).sum()).backward()
+
+    it(2, 2)   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:                      # bounded sample: whole iterations, >= ~10 s of CPU work
+        it(T, B)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= 10.0 or n >= 50:
+            break
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": round(n * B * T / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{n} iterations of oracle/ref_cpu.py (reference op sequence, torch CPU {mode}), "
+                      f"B={B} x T={T}, {H}x{W}, nq={nq}, {dt:.1f} s on {cores} threads ({model})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import attention  # noqa: F401  (registers aaa_amd)
+    from aaa_amd import _native as N, detinit
+    from aaa_amd.learner import Learner
+    from aaa_amd.parallel import init_from_env
+
+    rank, world, local = init_from_env("nccl")
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, T, H, W, nq, dtype = cfg["B"], cfg["T"], cfg["H"], cfg["W"], cfg["nq"], cfg["dtype"]
+    A = 18
+    learner = Learner(B, T, H, W, nq, A, dtype, dev)
+    frames = torch.from_numpy(detinit.frames_u8(1234 + rank, (T, B, H, W, 3)).astype(np.float32)).to(dev)
+    dl = torch.from_numpy(detinit.cotangent(2 + 7 * rank, (T, B, A))).to(dev)
+    dv = torch.from_numpy(detinit.cotangent(3 + 7 * rank, (T, B, A))).to(dev)
+    log(f"rank {rank}/{world} {cfg['desc']} workspace {learner.runner.ws_bytes / 2**20:.0f} MiB")
+
+    for i in range(args.warmup):
+        learner.step(frames, dl, dv, overlap=not args.no_overlap)
+    torch.cuda.synchronize()
+    log(f"warm-up done ({args.warmup} steps)")
+
+    N.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        learner.step(frames, dl, dv, overlap=not args.no_overlap)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = {k: N.timing_read(k) for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
+    N.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    frames_total = B * T * world * args.steps
+    value = frames_total / elapsed
+
+    # roofline of the dominant kernel class (largest total device time)
+    M = B * learner.runner.P
+    F = B * T
+    per_launch = {
+        N.TIMER_FWD_STEP: 2.0 * M * 512 * 1728,
+        N.TIMER_BPTT_STEP: 2.0 * M * 4608 * ((T - 1) * 192 + 64) / T,
+        N.TIMER_CORE_WGRAD: 2.0 * 512 * 1728 * F * learner.runner.P,
+    }
+    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step", N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dgrad + fused gate bwd)",
+             N.TIMER_CORE_WGRAD: "ConvLSTM weight-gradient GEMM"}
+    dom = max(kt, key=lambda k: kt[k][0])
+    tot_ms, launches = kt[dom]
+    avg_ms = tot_ms / max(launches, 1)
+    peak = PEAK_TFLOPS[dtype]
+    achieved = per_launch[dom] / (avg_ms * 1e-3) / 1e12
+    fpf = flop_per_frame(H, W, nq)
+    kernels = {names[k]: {"avg_us": round(v[0] / max(v[1], 1) * 1e3, 2), "launches": v[1],
+                          "tflops": round(per_launch[k] / (v[0] / max(v[1], 1) * 1e-3) / 1e12, 2)}
+               for k, v in kt.items()}
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": dtype,
+        "data": "synthetic: seeded uint8 frames cast to fp32 (raw 0..255), seeded uniform weights of the reference "
+                "architecture, uniform[-1,1) logits/values cotangents",
+        "config": {"workload": cfg["desc"], "global_batch": B * world, "seq_len": T, "frame": f"{H}x{W}",
+                   "heads": nq, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "flop_per_launch": per_launch[dom], "avg_launch_us": round(avg_ms * 1e3, 2)},
+        "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
+                         "frac": round(value * fpf / world / 1e12 / peak, 4)},
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("timing the CPU baseline (oracle on host cores)...")
+        out["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

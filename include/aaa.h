@@ -137,6 +137,20 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream);
  * are overwritten (not accumulated) by the phases that own them. */
 int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
 
+/* ---- optional kernel timing (benchmarks) ----
+ * While enabled, the runtime records a hipEvent pair on the launch stream
+ * around every launch of the kernel classes below.  aaa_timing_read()
+ * waits for the recorded events and returns the summed device time and the
+ * number of launches since the last enable/read, then clears that class. */
+enum aaa_timer {
+  AAA_TIMER_FWD_STEP = 0,    /* fused ConvLSTM forward step (one per t)          */
+  AAA_TIMER_BPTT_STEP = 1,   /* ConvLSTM dgrad + fused gate backward (one per t) */
+  AAA_TIMER_CORE_WGRAD = 2,  /* ConvLSTM weight-gradient GEMM over all frames    */
+  AAA_TIMER_N = 3
+};
+int aaa_timing_enable(int on);
+int aaa_timing_read(int kind, double* total_ms, long* launches);
+
 /* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
 
 /* NHWC convolution y[n,oy,ox,co] = b[co] + sum w[co,ky,kx,ci] x[n,iy,ix,ci]

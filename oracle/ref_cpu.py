@@ -124,7 +124,7 @@ def _vision_step(P, X_t, state, mode, peep):
 
 def _query(P, B, nq, hidden=256):
     """QueryNetwork on the zero prev_output (Q1), attention.py:184-198,325-331."""
-    z = torch.zeros(B, hidden)
+    z = torch.zeros(B, hidden, dtype=P["query.model.0.weight"].dtype)
     q = F.relu(F.linear(z, P["query.model.0.weight"], P["query.model.0.bias"]))
     q = F.relu(F.linear(q, P["query.model.2.weight"], P["query.model.2.bias"]))
     q = F.linear(q, P["query.model.4.weight"], P["query.model.4.bias"])
@@ -135,7 +135,7 @@ def _head(P, O, S, nq, prev_reward, prev_action):
     """Attention readout + answer MLP + zero-state LSTMCell + heads (one frame batch)."""
     B, h, w, _ = O.shape
     K, V = O.split([8, 120], dim=3)                                     # attention.py:319
-    Sb = torch.stack([S] * B)
+    Sb = torch.stack([S.to(O.dtype)] * B)
     K, V = torch.cat([K, Sb], dim=3), torch.cat([V, Sb], dim=3)         # :231-232
     Q = _query(P, B, nq)
     A = torch.matmul(K, Q.transpose(2, 1).unsqueeze(1))                  # :336
@@ -143,18 +143,18 @@ def _head(P, O, S, nq, prev_reward, prev_action):
     a = torch.matmul(A.reshape(B, h * w, nq).transpose(1, 2),
                      V.reshape(B, h * w, V.shape[3]))                   # :246-254
     if prev_reward is None:
-        r = torch.zeros(B, 1, 1)
+        r = torch.zeros(B, 1, 1, dtype=O.dtype)
     else:
-        r = prev_reward.float().reshape(B, 1, 1)
+        r = prev_reward.to(O.dtype).reshape(B, 1, 1)
     if prev_action is None:
-        act = torch.zeros(B, 1, 1)
+        act = torch.zeros(B, 1, 1, dtype=O.dtype)
     else:
-        act = prev_action.float().reshape(B, 1, 1)
+        act = prev_action.to(O.dtype).reshape(B, 1, 1)
     answer = torch.cat(torch.chunk(a, nq, dim=1) + torch.chunk(Q, nq, dim=1) + (r, act),
                        dim=2).squeeze(1)                                 # :343-348
     x = F.relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]))
     x = F.linear(x, P["answer_processor.2.weight"], P["answer_processor.2.bias"])
-    zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1])
+    zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1], dtype=O.dtype)
     hc, _ = torch._VF.lstm_cell(x, (zeros, zeros), P["policy_core.weight_ih"],
                                 P["policy_core.weight_hh"], P["policy_core.bias_ih"],
                                 P["policy_core.bias_hh"])               # :354-355 (Q1)

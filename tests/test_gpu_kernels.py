@@ -51,8 +51,9 @@ def test_conv_fwd(cuda, name, dtype):
     ref = F.conv2d(_r(x, dtype).double(), _r(w, dtype).double(), b.double(), stride=s, padding=p)
     xd = x.permute(0, 2, 3, 1).contiguous().to(cuda)
     wd = w.permute(0, 2, 3, 1).contiguous().to(cuda)
+    bd = b.to(cuda)
     y = torch.empty(n, Ho, Wo, co, device=cuda)
-    N.check(N.load().aaa_conv2d_nhwc(d, xd.data_ptr(), wd.data_ptr(), b.to(cuda).data_ptr(), y.data_ptr(),
+    N.check(N.load().aaa_conv2d_nhwc(d, xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), y.data_ptr(),
                                      N.stream_ptr()))
     assert_close(y.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), _tol(dtype), f"{name} fwd")
 
@@ -96,6 +97,8 @@ def test_linear(cuda, M, Nn, K):
     b = _rnd((Nn,), 7)
     ref = F.linear(x.double(), w.double(), b.double())
     y = torch.empty(M, Nn, device=cuda)
-    N.check(N.load().aaa_linear(M, Nn, K, x.to(cuda).data_ptr(), w.to(cuda).data_ptr(), b.to(cuda).data_ptr(),
-                                y.data_ptr(), N.stream_ptr()))
+    xd, wd, bd = x.to(cuda), w.to(cuda), b.to(cuda)   # keep alive until the kernel has run
+    N.check(N.load().aaa_linear(M, Nn, K, xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), y.data_ptr(),
+                                N.stream_ptr()))
+    torch.cuda.synchronize()
     assert_close(y.cpu().numpy(), ref.numpy(), 2e-5, "linear")

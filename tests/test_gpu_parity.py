@@ -36,11 +36,11 @@ def _grads(agent):
             for n, p in agent.named_parameters()}
 
 
-def _oracle(T, B, nq=4, scale=1.0, conv_mode="fp32", A=18, H=84, W=84, **kw):
-    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A, nq))
-    X = _frames(T, B, H, W, scale)
+def _oracle(T, B, nq=4, scale=1.0, conv_mode="fp32", A=18, H=84, W=84, dtype=torch.float32, **kw):
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A, nq), dtype=dtype)
+    X = _frames(T, B, H, W, scale).to(dtype)
     lg, vl, at = ref_cpu.unroll(P, X, nq=nq, conv_mode=conv_mode, **kw)
-    Gl, Gv = _cot(T, B, A)
+    Gl, Gv = (c.to(dtype) for c in _cot(T, B, A))
     ((lg * Gl).sum() + (vl * Gv).sum()).backward()
     g = {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}
     return lg.detach(), vl.detach(), at.detach(), g
@@ -58,7 +58,7 @@ def _run_unroll(agent, T, B, dev, scale=1.0, A=18, H=84, W=84, **kw):
 
 def _compare(out, ref, rtol, what=""):
     lg, vl, at, g = out
-    rl, rv, ra, rg = ref
+    rl, rv, ra, rg = tuple(x.float() for x in ref[:3]) + ({k: v.float() for k, v in ref[3].items()},)
     assert_close(lg.numpy(), rl.numpy(), rtol, what + "logits")
     assert_close(vl.numpy(), rv.numpy(), rtol, what + "values")
     assert_close(at.numpy(), ra.numpy(), rtol, what + "attn")
@@ -181,10 +181,17 @@ def test_bf16_vs_emulated_oracle(cuda):
 
 
 def test_c2_full_size_vs_oracle(cuda):
-    """Config 2 (B=32, T=20, fp32) in full against the oracle on the host CPU."""
+    """Config 2 (B=32, T=20, fp32) in full against the oracle evaluated in fp64.
+
+    At this batch the fp32 CPU evaluation itself is ill-conditioned: one of the
+    327,680 answer_processor.0 ReLU pre-activations is -2e-8 and flips sign in
+    fp32, which alone moves the CPU fp32 gradients ~1e-3 from the exact value
+    (DESIGN.md "Parity criterion").  The exact (fp64) evaluation of the same
+    op sequence is the well-defined target; the HIP path must be within 1e-4.
+    """
     T, B = 20, 32
     torch.set_num_threads(16)
-    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, "C2 ")
+    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B, dtype=torch.float64), RTOL, "C2 ")
 
 
 def test_repeat_is_deterministic_enough(cuda):

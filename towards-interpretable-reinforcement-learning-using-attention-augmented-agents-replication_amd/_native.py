@@ -20,8 +20,9 @@ BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 EXPORTS = (
     "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
     "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
-    "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear",
+    "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
 )
+TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD = 0, 1, 2
 
 
 class Cfg(ctypes.Structure):
@@ -73,6 +74,8 @@ def load(path: str = LIB_PATH):
             "aaa_conv2d_nhwc_dgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),
             "aaa_conv2d_nhwc_wgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),
             "aaa_linear": (I, [I, I, I, P, P, P, P, P]),
+            "aaa_timing_enable": (I, [I]),
+            "aaa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -111,3 +114,14 @@ def param_layout(cfg: Cfg):
     sizes = (ctypes.c_size_t * 34)()
     check(load().aaa_param_layout(ctypes.byref(cfg), ctypes.byref(total), offs, sizes), "param_layout")
     return total.value, list(offs), list(sizes)
+
+
+def timing_enable(on: bool = True) -> None:
+    check(load().aaa_timing_enable(1 if on else 0), "timing_enable")
+
+
+def timing_read(kind: int):
+    """(total_ms, launches) of kernel class ``kind`` since the last read."""
+    ms, n = ctypes.c_double(), ctypes.c_long()
+    check(load().aaa_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)), "timing_read")
+    return ms.value, n.value

@@ -18,6 +18,8 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "aaa.h"
 #include "epilogues.h"
@@ -171,6 +173,40 @@ static int check_device() {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ------------------------------------------------- optional kernel timing --
+struct Timers {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[AAA_TIMER_N];
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+};
+static Timers g_timers;
+
+struct TimerScope {
+  int kind;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  TimerScope(int k, hipStream_t s) : kind(k), st(s) {
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    if (!g_timers.on) return;
+    a = g_timers.get();
+    b = g_timers.get();
+    if (a && b) (void)hipEventRecord(a, st);
+  }
+  ~TimerScope() {
+    if (!a || !b) return;
+    (void)hipEventRecord(b, st);
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    g_timers.pending[kind].emplace_back(a, b);
+  }
+};
+
 // --------------------------------------------------------- tile configs ---
 using CF = GemmCfg<float, 64, 64, 32, 2, 2>;     // fp32: exact v_mfma_f32_32x32x2_f32
 using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;    // bf16 operands, fp32 accumulate
@@ -247,6 +283,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     EpiConvLstmFwd<T> ep{(const float*)(pk + L.k_bl), Wf(L.Cst) + (size_t)t * M * 128,
                          Wf(L.Cst) + (size_t)(t + 1) * M * 128, Wf(L.Hs) + (size_t)t * M * 128,
                          Wt(L.XH) + (size_t)(t + 1) * M * 192, Wf(L.Gt) + (size_t)t * M * 512, M};
+    TimerScope tim(AAA_TIMER_FWD_STEP, st);
     HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, M, 1728, 1, st)));
   }
   // constant query (Q1) + fused attention readout over all T*B frames
@@ -402,6 +439,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                         prev ? Wf(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
                         prev ? nullptr : io->dh0, prev ? 1 : 0, M};
       const int rows = (prev || io->dh0) ? 192 : 64;
+      TimerScope tim(AAA_TIMER_BPTT_STEP, st);
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, rows, M, 4608, 1, st)));
     }
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
@@ -412,6 +450,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       typename LB::Params pb{Wt(L.XH), ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}, 1728};
       EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
       const int tiles = cdiv(512, C::BI) * cdiv(1728, C::BJ);
+      TimerScope tim(AAA_TIMER_CORE_WGRAD, st);
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, 1728, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
       HIPCHK(colsum(Wf(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     }
@@ -525,6 +564,40 @@ extern "C" {
 int aaa_abi_version(void) { return AAA_ABI_VERSION; }
 
 const char* aaa_last_error(void) { return g_err.c_str(); }
+
+int aaa_timing_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_timers.mu);
+  g_timers.on = on != 0;
+  for (auto& v : g_timers.pending) {
+    for (auto& pr : v) { g_timers.pool.push_back(pr.first); g_timers.pool.push_back(pr.second); }
+    v.clear();
+  }
+  return AAA_OK;
+}
+
+int aaa_timing_read(int kind, double* total_ms, long* launches) {
+  if (kind < 0 || kind >= AAA_TIMER_N || !total_ms || !launches) return fail(AAA_E_ARG, "bad timer query");
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> v;
+  {
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    v.swap(g_timers.pending[kind]);
+  }
+  double tot = 0.0;
+  int rc = AAA_OK;
+  for (auto& pr : v) {
+    float ms = 0.f;
+    if (hipEventSynchronize(pr.second) != hipSuccess || hipEventElapsedTime(&ms, pr.first, pr.second) != hipSuccess)
+      rc = fail(AAA_E_LAUNCH, "event timing failed");
+    tot += ms;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    for (auto& pr : v) { g_timers.pool.push_back(pr.first); g_timers.pool.push_back(pr.second); }
+  }
+  *total_ms = tot;
+  *launches = (long)v.size();
+  return rc;
+}
 
 int aaa_grid(int H, int W, int* h, int* w) {
   if (!h || !w) return fail(AAA_E_ARG, "NULL output");
