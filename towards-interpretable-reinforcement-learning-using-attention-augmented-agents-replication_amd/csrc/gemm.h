@@ -43,7 +43,7 @@ struct LdRows {
   const G* rowp[PER];
   int kc[PER], lr[PER];
   bool ok[PER], act[PER];
-  u32x4 buf[PER];
+  using Regs = u32x4[PER];
   __device__ __forceinline__ LdRows(const Params& p, int row0) {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
@@ -56,7 +56,7 @@ struct LdRows {
       rowp[c] = p.src + (size_t)(ok[c] ? row : 0) * p.ld;
     }
   }
-  __device__ __forceinline__ void fetch(int k0, int kend) {
+  __device__ __forceinline__ void fetch(int k0, int kend, Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       int k = k0 + kc[c];
@@ -64,10 +64,10 @@ struct LdRows {
       else buf[c] = u32x4{0, 0, 0, 0};
     }
   }
-  __device__ __forceinline__ void commit(T* lds) {
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
   }
 };
 
@@ -84,7 +84,7 @@ struct LdRowsT {
   int ld, nrows;
   int kr[PER], rc[PER], row[PER];
   bool act[PER];
-  u32x4 buf[PER];
+  using Regs = u32x4[PER];
   __device__ __forceinline__ LdRowsT(const Params& p, int row0) : src(p.src), ld(p.ld), nrows(p.nrows) {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
@@ -95,7 +95,7 @@ struct LdRowsT {
       row[c] = row0 + rc[c];
     }
   }
-  __device__ __forceinline__ void fetch(int k0, int kend) {
+  __device__ __forceinline__ void fetch(int k0, int kend, Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       int k = k0 + kr[c];
@@ -114,11 +114,22 @@ struct LdRowsT {
       buf[c] = v;
     }
   }
-  __device__ __forceinline__ void commit(T* lds) {
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
   }
+};
+
+// Division by a runtime constant as one 32x32->64 multiply: q = (n * m) >> 32
+// with m = ceil(2^32 / d).  Exact whenever n * d < 2^32, which holds for every
+// index divided here (pixels * frames < 2^26, k < 2^16).
+struct FastDiv {
+  uint32_t d;
+  uint64_t m;
+  __host__ __device__ FastDiv() : d(1), m(1ull << 32) {}
+  __host__ __device__ explicit FastDiv(uint32_t dd) : d(dd), m(((1ull << 32) + dd - 1) / dd) {}
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (uint32_t)(((uint64_t)n * m) >> 32); }
 };
 
 // Convolution geometry shared by the im2col loaders.  NHWC input with pixel
@@ -128,6 +139,15 @@ struct ConvGeo {
   int Hin, Win, Hout, Wout;
   int KW, stride, pad;
   int transposed;  // 0: forward gather, 1: dgrad (transposed-conv) gather
+  FastDiv dCin, dKW, dWout, dHW;  // filled by prep()
+  ConvGeo prep() const {
+    ConvGeo g = *this;
+    g.dCin = FastDiv((uint32_t)Cin);
+    g.dKW = FastDiv((uint32_t)KW);
+    g.dWout = FastDiv((uint32_t)Wout);
+    g.dHW = FastDiv((uint32_t)(Hout * Wout));
+    return g;
+  }
 };
 
 __device__ __forceinline__ bool conv_src(const ConvGeo& g, int oy, int ox, int ky, int kx, int& iy, int& ix) {
@@ -139,7 +159,10 @@ __device__ __forceinline__ bool conv_src(const ConvGeo& g, int oy, int ox, int k
   int ty = oy + g.pad - ky, tx = ox + g.pad - kx;
   if (ty < 0 || tx < 0) return false;
   if (g.stride == 1) { iy = ty; ix = tx; }
-  else {
+  else if (g.stride == 2) {
+    if ((ty | tx) & 1) return false;
+    iy = ty >> 1; ix = tx >> 1;
+  } else {
     if ((ty % g.stride) | (tx % g.stride)) return false;
     iy = ty / g.stride; ix = tx / g.stride;
   }
@@ -159,7 +182,7 @@ struct LdIm2col {
   const G* fbase[PER];
   int oy[PER], ox[PER], kc[PER], lr[PER];
   bool ok[PER], act[PER];
-  u32x4 buf[PER];
+  using Regs = u32x4[PER];
   __device__ __forceinline__ LdIm2col(const Params& p, int row0) : g(p.g) {
     const int hw = g.Hout * g.Wout;
 #pragma unroll
@@ -171,21 +194,21 @@ struct LdIm2col {
       int m = row0 + lr[c];
       ok[c] = act[c] && m < p.nrows;
       int mm = ok[c] ? m : 0;
-      int f = mm / hw, pix = mm - f * hw;
-      oy[c] = pix / g.Wout;
+      int f = (int)g.dHW.div(mm), pix = mm - f * hw;
+      oy[c] = (int)g.dWout.div(pix);
       ox[c] = pix - oy[c] * g.Wout;
       fbase[c] = p.src + (size_t)f * g.Hin * g.Win * g.cs + g.coff;
     }
   }
-  __device__ __forceinline__ void fetch(int k0, int kend) {
+  __device__ __forceinline__ void fetch(int k0, int kend, Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       u32x4 v = u32x4{0, 0, 0, 0};
       int k = k0 + kc[c];
       if constexpr (VEC) {
         if (ok[c] && k < kend) {
-          int tap = k / g.Cin, ci = k - tap * g.Cin;
-          int ky = tap / g.KW, kx = tap - ky * g.KW, iy, ix;
+          int tap = (int)g.dCin.div(k), ci = k - tap * g.Cin;
+          int ky = (int)g.dKW.div(tap), kx = tap - ky * g.KW, iy, ix;
           if (conv_src(g, oy[c], ox[c], ky, kx, iy, ix))
             v = *reinterpret_cast<const u32x4*>(fbase[c] + (size_t)(iy * g.Win + ix) * g.cs + ci);
         }
@@ -197,8 +220,8 @@ struct LdIm2col {
           for (int e = 0; e < 4; ++e) {
             int ke = k + e;
             if (ke < kend) {
-              int tap = ke / g.Cin, ci = ke - tap * g.Cin;
-              int ky = tap / g.KW, kx = tap - ky * g.KW, iy, ix;
+              int tap = (int)g.dCin.div(ke), ci = ke - tap * g.Cin;
+              int ky = (int)g.dKW.div(tap), kx = tap - ky * g.KW, iy, ix;
               if (conv_src(g, oy[c], ox[c], ky, kx, iy, ix))
                 tmp[e] = (float)fbase[c][(size_t)(iy * g.Win + ix) * g.cs + ci];
             }
@@ -209,10 +232,10 @@ struct LdIm2col {
       buf[c] = v;
     }
   }
-  __device__ __forceinline__ void commit(T* lds) {
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
   }
 };
 
@@ -231,7 +254,7 @@ struct LdIm2colT {
   int kr[PER], rc[PER];
   int ky[PER][VEC ? 1 : 4], kx[PER][VEC ? 1 : 4], ci[PER][VEC ? 1 : 4];
   bool act[PER], rok[PER][VEC ? 1 : 4];
-  u32x4 buf[PER];
+  using Regs = u32x4[PER];
   __device__ __forceinline__ LdIm2colT(const Params& p, int row0) : g(p.g), src(p.src) {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
@@ -245,22 +268,22 @@ struct LdIm2colT {
         int kp = row0 + rc[c] + e;
         rok[c][e] = act[c] && kp < p.nrows;
         int kq = rok[c][e] ? kp : 0;
-        int tap = kq / g.Cin;
+        int tap = (int)g.dCin.div(kq);
         ci[c][e] = kq - tap * g.Cin;
-        ky[c][e] = tap / g.KW;
+        ky[c][e] = (int)g.dKW.div(tap);
         kx[c][e] = tap - ky[c][e] * g.KW;
       }
     }
   }
-  __device__ __forceinline__ void fetch(int k0, int kend) {
+  __device__ __forceinline__ void fetch(int k0, int kend, Regs& buf) const {
     const int hw = g.Hout * g.Wout;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       u32x4 v = u32x4{0, 0, 0, 0};
       int m = k0 + kr[c];
       if (act[c] && m < kend) {
-        int f = m / hw, pix = m - f * hw;
-        int oy = pix / g.Wout, ox = pix - oy * g.Wout;
+        int f = (int)g.dHW.div(m), pix = m - f * hw;
+        int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
         const G* fb = src + (size_t)f * g.Hin * g.Win * g.cs + g.coff;
         if constexpr (VEC) {
           int iy, ix;
@@ -281,10 +304,10 @@ struct LdIm2colT {
       buf[c] = v;
     }
   }
-  __device__ __forceinline__ void commit(T* lds) {
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      if (act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(rc[c], kr[c]), buf[c]);
   }
 };
 
@@ -318,20 +341,25 @@ template <typename T, int R, int BK, bool KC>
 struct TileK : Tile<T, R, BK, KC> { static constexpr bool KC_ = KC; };
 
 // ------------------------------------------------------------- kernel -----
-template <typename T, int BI_, int BJ_, int BK_, int WI_, int WJ_>
+// WI x WJ waves tile the output; WK > 1 additionally splits every BK slab
+// among WK wave groups (intra-workgroup split-K), whose partial accumulators
+// are summed through LDS before the epilogue.  That multiplies the number of
+// waves for GEMMs whose output has fewer 32x32 tiles than the chip has SIMDs
+// (the per-step ConvLSTM kernels at small batch).
+template <typename T, int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
 struct GemmCfg {
   using type = T;
-  static constexpr int BI = BI_, BJ = BJ_, BK = BK_, WI = WI_, WJ = WJ_;
-  static constexpr int NT = WI * WJ * 64;
+  static constexpr int BI = BI_, BJ = BJ_, BK = BK_, WI = WI_, WJ = WJ_, WK = WK_;
+  static constexpr int NT = WI * WJ * WK * 64;
 };
 
 template <class C, class LA, class LB, class EP>
 __global__ void __launch_bounds__(C::NT)
 gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk) {
   using T = typename C::type;
-  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ;
+  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
-  static_assert(MI >= 1 && MJ >= 1 && BK % 16 == 0, "tile shape");
+  static_assert(MI >= 1 && MJ >= 1 && BK % (16 * WK) == 0, "tile shape");
   using TA = TileK<T, BI, BK, LA::KC>;
   using TB = TileK<T, BJ, BK, LB::KC>;
   __shared__ __attribute__((aligned(16))) T smem[2 * (TA::ELEMS + TB::ELEMS)];
@@ -348,7 +376,8 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
   LA la(pa, i0);
   LB lb(pb, j0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wi = wave / WJ, wj = wave - (wave / WJ) * WJ;
+  const int wk = wave / (WI * WJ), wr = wave - wk * (WI * WJ);
+  const int wi = wr / WJ, wj = wr - (wr / WJ) * WJ;
   const int r32 = lane & 31, h = lane >> 5;
 
   f32x16 acc[MI][MJ];
@@ -360,23 +389,28 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
   const int nk = (ke - kb + BK - 1) / BK;
-  la.fetch(kb, ke);
-  lb.fetch(kb, ke);
-  la.commit(As0);
-  lb.commit(Bs0);
+  // One register stage + two LDS buffers: the global loads of tile k+1 are in
+  // flight under the MFMAs of tile k; one barrier per K tile.
+  typename LA::Regs ra;
+  typename LB::Regs rb;
+  la.fetch(kb, ke, ra);
+  lb.fetch(kb, ke, rb);
+  la.commit(As0, ra);
+  lb.commit(Bs0, rb);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const bool odd = kt & 1;
     const T* Ac = odd ? As1 : As0;
     const T* Bc = odd ? Bs1 : Bs0;
-    if (kt + 1 < nk) {
-      la.fetch(kb + (kt + 1) * BK, ke);
-      lb.fetch(kb + (kt + 1) * BK, ke);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.fetch(kb + (kt + 1) * BK, ke, ra);
+      lb.fetch(kb + (kt + 1) * BK, ke, rb);
     }
 #pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const int kofs = 16 * s + 8 * h;
+    for (int s2 = 0; s2 < BK / 16 / WK; ++s2) {
+      const int kofs = 16 * (s2 * WK + wk) + 8 * h;
       if constexpr (is_f32<T>::value) {
         float af[MI][8], bfr[MJ][8];
 #pragma unroll
@@ -403,13 +437,39 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) {
-      la.commit(odd ? As0 : As1);
-      lb.commit(odd ? Bs0 : Bs1);
+    if (more) {
+      la.commit(odd ? As0 : As1, ra);
+      lb.commit(odd ? Bs0 : Bs1, rb);
     }
     __syncthreads();
   }
 
+  if constexpr (WK > 1) {
+    // sum the WK partial accumulators through LDS (the staging buffers are free now)
+    constexpr int RED = (WK - 1) * WI * WJ * MI * MJ * 16 * 64;
+    static_assert(RED * sizeof(float) <= sizeof(smem), "split-K reduction does not fit in LDS");
+    float* red = reinterpret_cast<float*>(smem);
+    if (wk > 0) {
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            red[((((wk - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane] = acc[a][b][e];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll
+    for (int w = 1; w < WK; ++w)
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            acc[a][b][e] += red[((((w - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane];
+  }
 #pragma unroll
   for (int a = 0; a < MI; ++a)
 #pragma unroll

@@ -1,0 +1,222 @@
+// Buffer-descriptor loaders for the convolution GEMMs (the hot path).
+//
+// Same interface as the generic loaders in gemm.h, but built for a low VALU
+// count per MFMA: every per-thread quantity that does not change along K
+// (row base offsets, which taps of a pixel are inside the image) is computed
+// once in the constructor, the per-K-tile part is wave-uniform (scalar), and
+// out-of-range / padding lanes are handled by the buffer descriptor's range
+// check (offset >= num_records returns 0) instead of branches.
+//
+// Preconditions (checked by the host launcher): the source tensor is < 2 GiB;
+// LdRowsB: K % BK == 0 (no partial k tiles); LdIm2colB: Cin % BK == 0 (a K
+// tile never crosses a tap) and stride 1 for the transposed gather;
+// LdRowsTB / LdIm2colTB: nrows % VG == 0 / Cin % VG == 0.
+#pragma once
+#include "gemm.h"
+
+namespace aaa {
+
+constexpr uint32_t kOOB = 0x80000000u;  // >= num_records of every buffer we build
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0);
+}
+
+// Plain rows (weights): element (row, k) at src[row*ld + k], K % BK == 0.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdRowsB {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPR = BK / VG;
+  static constexpr int NCH = R * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  using Regs = u32x4[PER];
+  struct Params { const G* src; int ld; int nrows; };
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t voff[PER];
+  int ldo[PER];
+  bool act[PER];
+  __device__ __forceinline__ LdRowsB(const Params& p, int row0) {
+    rs = make_rsrc(p.src, (uint32_t)((size_t)p.nrows * p.ld * sizeof(G)));
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      const int lr = ch / CPR, kc = (ch % CPR) * VG, row = row0 + lr;
+      voff[c] = (act[c] && row < p.nrows) ? (uint32_t)((row * p.ld + kc) * (int)sizeof(G)) : kOOB;
+      ldo[c] = Tile<T, R, BK, true>::off(lr, kc);
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int, Regs& buf) const {
+    const uint32_t ko = (uint32_t)(k0 * (int)sizeof(G));
+#pragma unroll
+    for (int c = 0; c < PER; ++c) buf[c] = bload(rs, voff[c] + ko);
+  }
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+};
+
+// Transposed rows: element (row, k) at src[k*ld + row] (activation grads for
+// weight gradients, k = pixel).  ktotal = rows of src; nrows % VG == 0.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdRowsTB {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPK = R / VG;
+  static constexpr int NCH = BK * CPK;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  using Regs = u32x4[PER];
+  struct Params { const G* src; int ld; int nrows; int ktotal; };
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t voff[PER];
+  int ldo[PER];
+  int rowbytes;
+  bool act[PER];
+  __device__ __forceinline__ LdRowsTB(const Params& p, int row0) {
+    rs = make_rsrc(p.src, (uint32_t)((size_t)p.ktotal * p.ld * sizeof(G)));
+    rowbytes = p.ld * (int)sizeof(G);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      const int kr = ch / CPK, rc = (ch % CPK) * VG, row = row0 + rc;
+      voff[c] = (act[c] && row < p.nrows) ? (uint32_t)((kr * p.ld + row) * (int)sizeof(G)) : kOOB;
+      ldo[c] = Tile<T, R, BK, false>::off(rc, kr);
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int, Regs& buf) const {
+    const uint32_t ko = (uint32_t)(k0 * rowbytes);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) buf[c] = bload(rs, voff[c] + ko);
+  }
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+};
+
+// Implicit-GEMM gather, rows = output pixels, k = (tap, ci), Cin % BK == 0:
+// the tap is uniform over a K tile, so per chunk a fetch is one bit test of
+// the pixel's precomputed valid-tap mask and one add.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdIm2colB {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPR = BK / VG;
+  static constexpr int NCH = R * CPR;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  using Regs = u32x4[PER];
+  struct Params { const G* src; ConvGeo g; int nrows; uint32_t src_bytes; };
+  __amdgpu_buffer_rsrc_t rs;
+  ConvGeo g;
+  int base[PER];            // element offset of the pixel's tap-(0,0) source (+ kc, coff)
+  uint64_t vmask[PER];      // bit tap = that tap reads inside the input
+  int ldo[PER];
+  bool act[PER];
+  __device__ __forceinline__ LdIm2colB(const Params& p, int row0) : g(p.g) {
+    rs = make_rsrc(p.src, p.src_bytes);
+    const int hw = g.Hout * g.Wout;
+    const int KH = g.KW;  // square kernels
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      act[c] = ch < NCH;
+      const int lr = ch / CPR, kc = (ch % CPR) * VG, m = row0 + lr;
+      const bool ok = act[c] && m < p.nrows;
+      const int mm = ok ? m : 0;
+      const int f = (int)g.dHW.div(mm), pix = mm - f * hw;
+      const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
+      uint64_t msk = 0;
+      for (int ky = 0; ky < KH; ++ky)
+        for (int kx = 0; kx < g.KW; ++kx) {
+          int iy, ix;
+          if (ok && conv_src(g, oy, ox, ky, kx, iy, ix)) msk |= 1ull << (ky * g.KW + kx);
+        }
+      vmask[c] = msk;
+      const int oy0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;
+      const int ox0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
+      base[c] = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + kc;
+      ldo[c] = Tile<T, R, BK, true>::off(lr, kc);
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int, Regs& buf) const {
+    const int tap = __builtin_amdgcn_readfirstlane((int)g.dCin.div(k0));
+    const int ci0 = k0 - tap * g.Cin;
+    const int ky = __builtin_amdgcn_readfirstlane((int)g.dKW.div(tap));
+    const int kx = tap - ky * g.KW;
+    const int toff = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs + ci0;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const bool v = (vmask[c] >> tap) & 1ull;
+      buf[c] = bload(rs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(G)) : kOOB);
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+};
+
+// Weight-gradient gather: rows = k' = (tap, ci) fixed per thread, k = output
+// pixel m (forward geometry).  Cin % VG == 0.
+template <typename G, typename T, int R, int BK, int NT>
+struct LdIm2colTB {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(G);
+  static constexpr int CPK = R / VG;
+  static constexpr int NCH = BK * CPK;
+  static constexpr int PER = (NCH + NT - 1) / NT;
+  using Regs = u32x4[PER];
+  struct Params { const G* src; ConvGeo g; int nrows; uint32_t src_bytes; };
+  __amdgpu_buffer_rsrc_t rs;
+  ConvGeo g;
+  int kr[PER], ky[PER], kx[PER], toff[PER];
+  int ldo[PER];
+  bool act[PER];
+  __device__ __forceinline__ LdIm2colTB(const Params& p, int row0) : g(p.g) {
+    rs = make_rsrc(p.src, p.src_bytes);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      const int rc = (ch % CPK) * VG, kp = row0 + rc;
+      act[c] = ch < NCH;
+      kr[c] = ch / CPK;
+      const bool ok = act[c] && kp < p.nrows;
+      const int kq = ok ? kp : 0;
+      const int tap = (int)g.dCin.div(kq), ci = kq - tap * g.Cin;
+      ky[c] = ok ? (int)g.dKW.div(tap) : -100000;  // invalid rows never pass the bounds test
+      kx[c] = tap - (int)g.dKW.div(tap) * g.KW;
+      toff[c] = (ky[c] * g.Win + kx[c]) * g.cs + ci + g.coff;
+      ldo[c] = Tile<T, R, BK, false>::off(rc, kr[c]);
+    }
+  }
+  __device__ __forceinline__ void fetch(int k0, int kend, Regs& buf) const {
+    const int hw = g.Hout * g.Wout;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int m = k0 + kr[c];
+      const int f = (int)g.dHW.div(m), pix = m - f * hw;
+      const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
+      const int iy0 = oy * g.stride - g.pad, ix0 = ox * g.stride - g.pad;
+      const int iy = iy0 + ky[c], ix = ix0 + kx[c];
+      const bool v = m < kend && (unsigned)iy < (unsigned)g.Hin && (unsigned)ix < (unsigned)g.Win;
+      const int off = ((f * g.Hin + iy0) * g.Win + ix0) * g.cs + toff[c];
+      buf[c] = bload(rs, v ? (uint32_t)(off * (int)sizeof(G)) : kOOB);
+    }
+  }
+  __device__ __forceinline__ void commit(T* lds, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+};
+
+}  // namespace aaa

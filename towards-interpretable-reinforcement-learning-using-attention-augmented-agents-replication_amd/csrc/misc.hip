@@ -16,31 +16,58 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Block-wide matrix-vector helpers (x and y in LDS).
+// rows:  y[o] = sum_k W[o*ldw + k] x[k]   -- one wave per row, lanes over k (coalesced)
+__device__ void gemv_rows(const float* __restrict__ W, int ldw, const float* x, int N, int K, float* y) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int o = wave; o < N; o += nw) {
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += W[(size_t)o * ldw + k] * x[k];
+    s = wave_sum(s);
+    if (lane == 0) y[o] = s;
+  }
+}
+// cols:  y[k] = sum_o W[o*ldw + k] x[o]   -- lanes over k, waves split o, LDS reduce
+__device__ void gemv_cols(const float* __restrict__ W, int ldw, const float* x, int N, int K, float* y,
+                          float* scratch /* nwaves*64 */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    const int k = k0 + lane;
+    float s = 0.f;
+    if (k < K) {
+#pragma unroll 4
+      for (int o = wave; o < N; o += nw) s += W[(size_t)o * ldw + k] * x[o];
+    }
+    scratch[wave * 64 + lane] = s;
+    __syncthreads();
+    if (wave == 0 && k < K) {
+      float t = 0.f;
+      for (int w = 0; w < nw; ++w) t += scratch[w * 64 + lane];
+      y[k] = t;
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // QueryNetwork on the always-zero prev_output (attention.py:184-198, 325-331;
 // Q1): q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4.  Also the basis
 // half of the attention logits, SQ[p][q] = sum_c S[p][c] * Q[q][8 + c].
-__global__ void k_query_fwd(const float* __restrict__ b0, const float* __restrict__ W2,
-                            const float* __restrict__ b2, const float* __restrict__ W4,
-                            const float* __restrict__ b4, const float* __restrict__ S, int P, int nq,
-                            float* q1, float* q2, float* Q, float* SQ) {
+__global__ void __launch_bounds__(1024)
+k_query_fwd(const float* __restrict__ b0, const float* __restrict__ W2, const float* __restrict__ b2,
+            const float* __restrict__ W4, const float* __restrict__ b4, const float* __restrict__ S, int P,
+            int nq, float* q1, float* q2, float* Q, float* SQ) {
   __shared__ float s1[128], s2[576], sq[576];
   const int qd = 72 * nq, tid = threadIdx.x;
   for (int o = tid; o < 128; o += blockDim.x) { float v = fmaxf(b0[o], 0.f); s1[o] = v; q1[o] = v; }
   __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) {
-    float acc = 0.f;
-    for (int k = 0; k < 128; ++k) acc += W2[o * 128 + k] * s1[k];
-    float v = fmaxf(acc + b2[o], 0.f);
-    s2[o] = v; q2[o] = v;
-  }
+  gemv_rows(W2, 128, s1, qd, 128, s2);
   __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) {
-    float acc = 0.f;
-    for (int k = 0; k < qd; ++k) acc += W4[o * qd + k] * s2[k];
-    float v = acc + b4[o];
-    sq[o] = v; Q[o] = v;
-  }
+  for (int o = tid; o < qd; o += blockDim.x) { float v = fmaxf(s2[o] + b2[o], 0.f); s2[o] = v; q2[o] = v; }
+  __syncthreads();
+  gemv_rows(W4, qd, s2, qd, qd, sq);
+  __syncthreads();
+  for (int o = tid; o < qd; o += blockDim.x) { float v = sq[o] + b4[o]; sq[o] = v; Q[o] = v; }
   __syncthreads();
   for (int idx = tid; idx < P * nq; idx += blockDim.x) {
     int p = idx / nq, q = idx - p * nq;
@@ -193,43 +220,33 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   }
 }
 
-// Backward of the query MLP (one workgroup).  dQ = sum over frames of the
-// logits-path grads + the answer-path grad, which summed over rows is
-// W1[:, Q-cols]^T · db1.
-__global__ void k_query_bwd(const float* __restrict__ dQs, const float* __restrict__ gb1,
-                            const float* __restrict__ W1, int ans_in, int nq,
-                            const float* __restrict__ W2, const float* __restrict__ W4,
-                            const float* __restrict__ q1, const float* __restrict__ q2,
-                            float* gW4, float* gb4, float* gW2, float* gb2, float* gb0) {
-  __shared__ float dQ[576], dq2[576], s2[576], s1[128];
+// Backward of the query MLP (one workgroup of 1024 threads).  dQ = sum over
+// frames of the logits-path grads + the answer-path grad, which summed over
+// rows is W1[:, Q-cols]^T . db1.
+__global__ void __launch_bounds__(1024)
+k_query_bwd(const float* __restrict__ dQs, const float* __restrict__ gb1, const float* __restrict__ W1,
+            int ans_in, int nq, const float* __restrict__ W2, const float* __restrict__ W4,
+            const float* __restrict__ q1, const float* __restrict__ q2, float* gW4, float* gb4, float* gW2,
+            float* gb2, float* gb0) {
+  __shared__ float dQ[576], dq2[576], s2[576], s1[128], b1s[512], dq1[128], scratch[16 * 64];
   const int qd = 72 * nq, tid = threadIdx.x, off = nq * 184;
   for (int i = tid; i < qd; i += blockDim.x) s2[i] = q2[i];
   for (int i = tid; i < 128; i += blockDim.x) s1[i] = q1[i];
-  for (int o = tid; o < qd; o += blockDim.x) {
-    float acc = 0.f;
-    for (int r = 0; r < 512; ++r) acc += gb1[r] * W1[(size_t)r * ans_in + off + o];
-    dQ[o] = dQs[o] + acc;
-  }
+  for (int i = tid; i < 512; i += blockDim.x) b1s[i] = gb1[i];
   __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) {
-    gb4[o] = dQ[o];
-    for (int k = 0; k < qd; ++k) gW4[o * qd + k] = dQ[o] * s2[k];
-  }
-  for (int k = tid; k < qd; k += blockDim.x) {
-    float acc = 0.f;
-    for (int o = 0; o < qd; ++o) acc += W4[o * qd + k] * dQ[o];
-    dq2[k] = s2[k] > 0.f ? acc : 0.f;
-  }
+  gemv_cols(W1 + off, ans_in, b1s, 512, qd, dQ, scratch);
   __syncthreads();
-  for (int k = tid; k < qd; k += blockDim.x) {
-    gb2[k] = dq2[k];
-    for (int j = 0; j < 128; ++j) gW2[k * 128 + j] = dq2[k] * s1[j];
-  }
-  for (int j = tid; j < 128; j += blockDim.x) {
-    float acc = 0.f;
-    for (int k = 0; k < qd; ++k) acc += W2[k * 128 + j] * dq2[k];
-    gb0[j] = s1[j] > 0.f ? acc : 0.f;
-  }
+  for (int o = tid; o < qd; o += blockDim.x) { dQ[o] += dQs[o]; gb4[o] = dQ[o]; }
+  __syncthreads();
+  for (int i = tid; i < qd * qd; i += blockDim.x) gW4[i] = dQ[i / qd] * s2[i - (i / qd) * qd];
+  gemv_cols(W4, qd, dQ, qd, qd, dq2, scratch);
+  __syncthreads();
+  for (int k = tid; k < qd; k += blockDim.x) { if (!(s2[k] > 0.f)) dq2[k] = 0.f; gb2[k] = dq2[k]; }
+  __syncthreads();
+  for (int i = tid; i < qd * 128; i += blockDim.x) gW2[i] = dq2[i >> 7] * s1[i & 127];
+  gemv_cols(W2, 128, dq2, qd, 128, dq1, scratch);
+  __syncthreads();
+  for (int j = tid; j < 128; j += blockDim.x) gb0[j] = s1[j] > 0.f ? dq1[j] : 0.f;
 }
 
 // out[n] += sum_{m} X[m*ld + n]; grid (ceil(N/64), nsplit), 256 threads.
@@ -238,8 +255,10 @@ __global__ void k_colsum(const float* __restrict__ X, int ld, int M, int N, int 
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float s = 0.f;
-  if (col < N)
+  if (col < N) {
+#pragma unroll 8
     for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += X[(size_t)r * ld + col];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x < 64 && col < N) {
@@ -450,7 +469,7 @@ static inline int nblk(long n, int bs = 256) {
 
 hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
                      const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st) {
-  hipLaunchKernelGGL(k_query_fwd, dim3(1), dim3(256), 0, st, b0, W2, b2, W4, b4, S, P, nq, q1, q2, Q, SQ);
+  hipLaunchKernelGGL(k_query_fwd, dim3(1), dim3(1024), 0, st, b0, W2, b2, W4, b4, S, P, nq, q1, q2, Q, SQ);
   return hipGetLastError();
 }
 
@@ -475,7 +494,7 @@ hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st) {
-  hipLaunchKernelGGL(k_query_bwd, dim3(1), dim3(256), 0, st, dQs, gb1, W1, ans_in, nq, W2, W4, q1, q2, gW4, gb4,
+  hipLaunchKernelGGL(k_query_bwd, dim3(1), dim3(1024), 0, st, dQs, gb1, W1, ans_in, nq, W2, W4, q1, q2, gW4, gb4,
                      gW2, gb2, gb0);
   return hipGetLastError();
 }

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -24,6 +25,7 @@
 #include "aaa.h"
 #include "epilogues.h"
 #include "gemm.h"
+#include "loaders_b.h"
 #include "misc.h"
 
 namespace aaa {
@@ -208,9 +210,31 @@ struct TimerScope {
 };
 
 // --------------------------------------------------------- tile configs ---
-using CF = GemmCfg<float, 64, 64, 32, 2, 2>;     // fp32: exact v_mfma_f32_32x32x2_f32
-using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;    // bf16 operands, fp32 accumulate
+// fp32 uses the exact v_mfma_f32_32x32x2_f32; bf16 v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
+using CF = GemmCfg<float, 64, 64, 32, 2, 2>;      // default 64x64 tile, 4 waves
+using CF32 = GemmCfg<float, 32, 64, 32, 1, 2>;    // 32-row tile, 2 waves: small-Mi GEMMs / more WGs
+using CFW = GemmCfg<float, 128, 128, 32, 2, 2>;   // long-K weight gradients: 64x64 per wave
+using CFK = GemmCfg<float, 32, 64, 64, 1, 2, 2>;  // per-step ConvLSTM kernels: 2-way split-K in the WG
+using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;
+using CB32 = GemmCfg<__bf16, 32, 64, 64, 1, 2>;
+using CBW = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
+using CBK = GemmCfg<__bf16, 32, 64, 64, 1, 2, 2>;
 template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
+template <typename T> using Cfg32For = std::conditional_t<std::is_same<T, float>::value, CF32, CB32>;
+template <typename T> using CfgWFor = std::conditional_t<std::is_same<T, float>::value, CFW, CBW>;
+template <typename T> using CfgKFor = std::conditional_t<std::is_same<T, float>::value, CFK, CBK>;
+
+// Step-kernel tile choice (env AAA_STEP_TILE: 0 = 64x64, 1 = 32x64 with 2-way
+// in-WG split-K; default picks by how many 32x32 output tiles the step has).
+static int step_tile(long out_tiles32) {
+  static int env = -2;
+  if (env == -2) {
+    const char* e = getenv("AAA_STEP_TILE");
+    env = e ? atoi(e) : -1;
+  }
+  if (env >= 0) return env;
+  return out_tiles32 < 1024 ? 1 : 0;   // measured: split-K pays for the 726-tile BPTT step, not the 1936-tile forward
+}
 
 static int wgrad_splits(int tiles, int K, int BK) {
   int s = std::max(1, 1024 / std::max(tiles, 1));
@@ -256,35 +280,54 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   const int F = L.F, P = L.P, M = L.B * L.P;
 
   {  // conv1 (attention.py:156-162): frames (fp32, Cin=3) -> Y1
-    using LA = LdRows<T, T, C::BI, C::BK, NT>;
-    using LB = LdIm2col<float, T, C::BJ, C::BK, NT, false>;
+    using C3 = Cfg32For<T>;
+    using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
+    using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, false>;
     typename LA::Params pa{(const T*)(pk + L.k_Wp1), 192, 32};
-    typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}, F * L.P1};
+    typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), F * L.P1};
     EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, F * L.P1, 192, 1, st)));
+    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 192, 1, st)));
   }
   {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
-    using LA = LdRows<T, T, C::BI, C::BK, NT>;
-    using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
+    using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
     typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};
-    typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}, F * P};
+    const ConvGeo g = ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep();
     EpiStoreT<T> ep{Wt(L.XH), 192, 64, F * P, prm + L.poff[C1B], 0};
-    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, F * P, 512, 1, st)));
+    if constexpr (32 % C::BK == 0) {
+      using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
+      HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P, (uint32_t)((size_t)F * L.P1 * 32 * L.esz)},
+                                     ep, 64, F * P, 512, 1, st)));
+    } else {
+      using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
+      HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P}, ep, 64, F * P, 512, 1, st)));
+    }
   }
   // initial state (reset(): zeros, attention.py:142-149) or carried state
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
   if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  const bool fwd_k = step_tile((long)(512 / 32) * cdiv(M, 32)) == 1;
+  const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);  // one step slice of XH
   for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126)
-    using LA = LdRows<T, T, C::BI, C::BK, NT>;
-    using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
-    typename LA::Params pa{(const T*)(pk + L.k_Wpl), 1728, 512};
-    typename LB::Params pb{Wt(L.XH) + (size_t)t * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}, M};
     EpiConvLstmFwd<T> ep{(const float*)(pk + L.k_bl), Wf(L.Cst) + (size_t)t * M * 128,
                          Wf(L.Cst) + (size_t)(t + 1) * M * 128, Wf(L.Hs) + (size_t)t * M * 128,
                          Wt(L.XH) + (size_t)(t + 1) * M * 192, Wf(L.Gt) + (size_t)t * M * 512, M};
+    const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     TimerScope tim(AAA_TIMER_FWD_STEP, st);
-    HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, M, 1728, 1, st)));
+    if (fwd_k) {
+      using CK = CfgKFor<T>;
+      using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+      using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
+      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_Wpl), 1728, 512},
+                                      typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
+                                      1728, 1, st)));
+    } else {
+      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
+      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_Wpl), 1728, 512},
+                                     typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
+                                     1728, 1, st)));
+    }
   }
   // constant query (Q1) + fused attention readout over all T*B frames
   HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
@@ -424,12 +467,11 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     HIPCHK(gate_bwd_last(M, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
                          Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
                          Wf(L.dZ) + (size_t)t1 * M * 512, st));
+    const bool bwd_k = step_tile((long)(192 / 32) * cdiv(M, 32)) == 1;
+    const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * 4);  // one step slice of dZ
     for (int t = t1; t >= 0; --t) {
-      using LA = LdRows<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
       const bool prev = t > 0;
-      typename LA::Params pa{(const T*)(pk + L.k_WdTl), 4608, 192};
-      typename LB::Params pb{Wf(L.dZ) + (size_t)t * M * 512, ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}, M};
+      const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       EpiConvLstmBwd ep{Wf(L.dY2) + (size_t)t * M * 64,
                         prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
                         prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
@@ -440,18 +482,33 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                         prev ? nullptr : io->dh0, prev ? 1 : 0, M};
       const int rows = (prev || io->dh0) ? 192 : 64;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, rows, M, 4608, 1, st)));
+      if (bwd_k) {
+        using CK = CfgKFor<T>;
+        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
+        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 192},
+                                        typename LB::Params{Wf(L.dZ) + (size_t)t * M * 512, g, M, dz_bytes}, ep, rows,
+                                        M, 4608, 1, st)));
+      } else {
+        using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+        using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+        HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 192},
+                                       typename LB::Params{Wf(L.dZ) + (size_t)t * M * 512, g, M, dz_bytes}, ep, rows,
+                                       M, 4608, 1, st)));
+      }
     }
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     {  // all 8 ConvLSTM weight grads as one long-K GEMM over every (t, b, p)
-      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colT<T, T, C::BJ, C::BK, NT, true>;
-      typename LA::Params pa{Wf(L.dZ), 512, 512};
-      typename LB::Params pb{Wt(L.XH), ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}, 1728};
+      using CW = CfgWFor<T>;
+      using LA = LdRowsTB<float, T, CW::BI, CW::BK, CW::NT>;
+      using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
+      typename LA::Params pa{Wf(L.dZ), 512, 512, F * P};
+      typename LB::Params pb{Wt(L.XH), ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(), 1728,
+                             (uint32_t)((size_t)(L.T + 1) * M * 192 * L.esz)};
       EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
-      const int tiles = cdiv(512, C::BI) * cdiv(1728, C::BJ);
+      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
       TimerScope tim(AAA_TIMER_CORE_WGRAD, st);
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 512, 1728, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
+      HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, F * P, wgrad_splits(tiles, F * P, CW::BK), st)));
       HIPCHK(colsum(Wf(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     }
     LstmGrads lg;
@@ -465,31 +522,34 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
 
   if (phases & AAA_BWD_VISION) {
     {  // conv2 wgrad / bias
-      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colT<T, T, C::BJ, C::BK, NT, true>;
-      typename LA::Params pa{Wf(L.dY2), 64, 64};
-      typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}, 512};
+      using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
+      typename LA::Params pa{Wf(L.dY2), 64, 64, F * P};
+      typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
+                             (uint32_t)((size_t)F * L.P1 * 32 * L.esz)};
       EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
       const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
       HIPCHK(colsum(Wf(L.dY2), 64, F * P, 64, grads + L.poff[C1B], st));
     }
     {  // conv2 dgrad (stride-2 transposed gather) -> dY1
-      using LA = LdRows<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
+      using C3 = Cfg32For<T>;
+      using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
+      using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
       typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
-      typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}, F * L.P1};
+      typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), F * L.P1};
       EpiStoreT<float> ep{Wf(L.dY1), 32, 32, F * L.P1, nullptr, 0};
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, F * L.P1, 1024, 1, st)));
+      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 1024, 1, st)));
     }
     {  // conv1 wgrad / bias (frames need no grad)
-      using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colT<float, T, C::BJ, C::BK, NT, false>;
-      typename LA::Params pa{Wf(L.dY1), 32, 32};
-      typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}, 192};
+      using C3 = Cfg32For<T>;
+      using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
+      using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
+      typename LA::Params pa{Wf(L.dY1), 32, 32, F * L.P1};
+      typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
       EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
-      const int tiles = cdiv(32, C::BI) * cdiv(192, C::BJ);
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 32, 192, F * L.P1, wgrad_splits(tiles, F * L.P1, C::BK), st)));
+      const int tiles = cdiv(32, C3::BI) * cdiv(192, C3::BJ);
+      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, F * L.P1, wgrad_splits(tiles, F * L.P1, C3::BK), st)));
       HIPCHK(colsum(Wf(L.dY1), 32, F * L.P1, 32, grads + L.poff[C0B], st));
     }
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
@@ -507,9 +567,15 @@ static int conv_nhwc_impl(const aaa_conv_desc* d, const float* x, const float* w
   const int K = d->KH * d->KW * d->Cin, M = d->N * d->Hout * d->Wout;
   using LA = LdRows<float, T, C::BI, C::BK, NT>;
   typename LA::Params pa{w, K, d->Cout};
-  ConvGeo g{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0};
+  const ConvGeo g = ConvGeo{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0}.prep();
   EpiStoreT<float> ep{y, d->Cout, d->Cout, M, bias, 0};
-  if (d->Cin % 4 == 0) {
+  if (d->Cin % C::BK == 0) {   // the hot-path loaders (buffer descriptors, tap-uniform K tiles)
+    using LAB = LdRowsB<float, T, C::BI, C::BK, NT>;
+    using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+    const uint32_t xb = (uint32_t)((size_t)d->N * d->Hin * d->Win * d->Cin * 4);
+    HIPCHK((launch_gemm<C, LAB, LB>(typename LAB::Params{w, K, d->Cout}, typename LB::Params{x, g, M, xb}, ep, d->Cout,
+                                    M, K, 1, st)));
+  } else if (d->Cin % 4 == 0) {
     using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
     HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, M}, ep, d->Cout, M, K, 1, st)));
   } else {
@@ -527,8 +593,16 @@ static int dgrad_nhwc_impl(const aaa_conv_desc* d, const float* dy, const float*
   using LA = LdRows<float, T, C::BI, C::BK, NT>;
   using LB = LdIm2col<float, T, C::BJ, C::BK, NT, true>;
   typename LA::Params pa{wT, K, d->Cin};
-  ConvGeo g{d->Cout, d->Cout, 0, d->Hout, d->Wout, d->Hin, d->Win, d->KW, d->stride, d->pad, 1};
+  const ConvGeo g = ConvGeo{d->Cout, d->Cout, 0, d->Hout, d->Wout, d->Hin, d->Win, d->KW, d->stride, d->pad, 1}.prep();
   EpiStoreT<float> ep{dx, d->Cin, d->Cin, M, nullptr, 0};
+  if (d->stride == 1 && d->Cout % C::BK == 0) {
+    using LAB = LdRowsB<float, T, C::BI, C::BK, NT>;
+    using LBB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+    const uint32_t yb = (uint32_t)((size_t)d->N * d->Hout * d->Wout * d->Cout * 4);
+    HIPCHK((launch_gemm<C, LAB, LBB>(typename LAB::Params{wT, K, d->Cin}, typename LBB::Params{dy, g, M, yb}, ep,
+                                     d->Cin, M, K, 1, st)));
+    return AAA_OK;
+  }
   HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{dy, g, M}, ep, d->Cin, M, K, 1, st)));
   return AAA_OK;
 }
@@ -541,11 +615,17 @@ static int wgrad_nhwc_impl(const aaa_conv_desc* d, const float* x, const float* 
   HIPCHK(hipMemsetAsync(dw, 0, (size_t)d->Cout * Kp * 4, st));
   using LA = LdRowsT<float, T, C::BI, C::BK, NT>;
   typename LA::Params pa{dy, d->Cout, d->Cout};
-  ConvGeo g{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0};
+  const ConvGeo g = ConvGeo{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0}.prep();
   EpiStore<true> ep{dw, Kp, d->Cout, Kp};
   const int tiles = cdiv(d->Cout, C::BI) * cdiv(Kp, C::BJ);
   const int ns = wgrad_splits(tiles, M, C::BK);
-  if (d->Cin % 4 == 0) {
+  if (d->Cin % 4 == 0 && d->Cout % 4 == 0) {   // hot-path loaders
+    using LAB = LdRowsTB<float, T, C::BI, C::BK, NT>;
+    using LB = LdIm2colTB<float, T, C::BJ, C::BK, NT>;
+    const uint32_t xb = (uint32_t)((size_t)d->N * d->Hin * d->Win * d->Cin * 4);
+    HIPCHK((launch_gemm<C, LAB, LB>(typename LAB::Params{dy, d->Cout, d->Cout, M}, typename LB::Params{x, g, Kp, xb},
+                                    ep, d->Cout, Kp, M, ns, st)));
+  } else if (d->Cin % 4 == 0) {
     using LB = LdIm2colT<float, T, C::BJ, C::BK, NT, true>;
     HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{x, g, Kp}, ep, d->Cout, Kp, M, ns, st)));
   } else {
