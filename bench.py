@@ -159,7 +159,7 @@ def main():
     F = B * T
     per_launch = {
         N.TIMER_FWD_STEP: 2.0 * M * 512 * 1728,
-        N.TIMER_BPTT_STEP: 2.0 * M * 4608 * ((T - 1) * 192 + 64) / T,
+        N.TIMER_BPTT_STEP: 2.0 * M * 4608 * 128,   # h rows only; t=0 is skipped (no dh0 wanted)
         N.TIMER_CORE_WGRAD: 2.0 * 512 * 1728 * F * learner.runner.P,
     }
     names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step", N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dgrad + fused gate bwd)",

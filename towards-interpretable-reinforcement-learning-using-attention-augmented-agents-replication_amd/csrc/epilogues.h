@@ -144,7 +144,9 @@ struct EpiConvLstmBwd {
   float* dz;            // [M][512] slot t-1
   float* dh0;           // [M][128] or null (only when t == 0)
   int has_prev, Nj;
+  int ioff;             // 64 when the GEMM computes only the h rows (dx batched separately)
   __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    i += ioff;
     if (j >= Nj || i >= 192) return;
     if (i < 64) {
       *reinterpret_cast<f32x4*>(dx + (size_t)j * 64 + i) = f32x4{v0, v1, v2, v3};

@@ -215,25 +215,30 @@ using CF = GemmCfg<float, 64, 64, 32, 2, 2>;      // default 64x64 tile, 4 waves
 using CF32 = GemmCfg<float, 32, 64, 32, 1, 2>;    // 32-row tile, 2 waves: small-Mi GEMMs / more WGs
 using CFW = GemmCfg<float, 128, 128, 32, 2, 2>;   // long-K weight gradients: 64x64 per wave
 using CFK = GemmCfg<float, 32, 64, 64, 1, 2, 2>;  // per-step ConvLSTM kernels: 2-way split-K in the WG
+using CFK4 = GemmCfg<float, 32, 64, 64, 1, 2, 4>; // 4-way split-K (8 waves)
 using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;
 using CB32 = GemmCfg<__bf16, 32, 64, 64, 1, 2>;
 using CBW = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
 using CBK = GemmCfg<__bf16, 32, 64, 64, 1, 2, 2>;
+using CBK4 = GemmCfg<__bf16, 32, 64, 64, 1, 2, 4>;
 template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
 template <typename T> using Cfg32For = std::conditional_t<std::is_same<T, float>::value, CF32, CB32>;
 template <typename T> using CfgWFor = std::conditional_t<std::is_same<T, float>::value, CFW, CBW>;
 template <typename T> using CfgKFor = std::conditional_t<std::is_same<T, float>::value, CFK, CBK>;
+template <typename T> using CfgK4For = std::conditional_t<std::is_same<T, float>::value, CFK4, CBK4>;
 
-// Step-kernel tile choice (env AAA_STEP_TILE: 0 = 64x64, 1 = 32x64 with 2-way
-// in-WG split-K; default picks by how many 32x32 output tiles the step has).
-static int step_tile(long out_tiles32) {
-  static int env = -2;
-  if (env == -2) {
-    const char* e = getenv("AAA_STEP_TILE");
-    env = e ? atoi(e) : -1;
-  }
-  if (env >= 0) return env;
-  return out_tiles32 < 1024 ? 1 : 0;   // measured: split-K pays for the 726-tile BPTT step, not the 1936-tile forward
+// Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE: 0 = 64x64,
+// 1 = 32x64 with 2-way in-WG split-K, 2 = 4-way; default picks by how many
+// 32x32 output tiles the step has, i.e. how many waves it can feed).
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int step_tile(long out_tiles32, const char* env) {
+  const int v = env_int(env, -1);
+  if (v >= 0) return v;
+  if (out_tiles32 < 1024) return 2;
+  return out_tiles32 < 1536 ? 1 : 0;   // measured on C2: forward step (1936 tiles) best at 64x64
 }
 
 static int wgrad_splits(int tiles, int K, int BK) {
@@ -306,7 +311,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
   if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
-  const bool fwd_k = step_tile((long)(512 / 32) * cdiv(M, 32)) == 1;
+  const bool fwd_k = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE") >= 1;
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);  // one step slice of XH
   for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126)
     EpiConvLstmFwd<T> ep{(const float*)(pk + L.k_bl), Wf(L.Cst) + (size_t)t * M * 128,
@@ -467,35 +472,52 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     HIPCHK(gate_bwd_last(M, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
                          Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
                          Wf(L.dZ) + (size_t)t1 * M * 512, st));
-    const bool bwd_k = step_tile((long)(192 / 32) * cdiv(M, 32)) == 1;
+    // Sequential part: only the h rows (dh_{t-1}, fused with the gate backward
+    // of step t-1); the x rows (dx_t for conv2) are one batched GEMM below.
+    const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE");
     const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * 4);  // one step slice of dZ
+    const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
     for (int t = t1; t >= 0; --t) {
       const bool prev = t > 0;
+      if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
-      EpiConvLstmBwd ep{Wf(L.dY2) + (size_t)t * M * 64,
+      EpiConvLstmBwd ep{nullptr,
                         prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
                         prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
                         Wf(L.Cst) + (size_t)t * M * 128,
                         prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
                         Wf(L.dC),
                         prev ? Wf(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
-                        prev ? nullptr : io->dh0, prev ? 1 : 0, M};
-      const int rows = (prev || io->dh0) ? 192 : 64;
+                        prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64};
+      const float* dzt = Wf(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
-      if (bwd_k) {
+      if (bwd_tile == 2) {
+        using CK = CfgK4For<T>;
+        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
+        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
+                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
+      } else if (bwd_tile == 1) {
         using CK = CfgKFor<T>;
         using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
         using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
-        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 192},
-                                        typename LB::Params{Wf(L.dZ) + (size_t)t * M * 512, g, M, dz_bytes}, ep, rows,
-                                        M, 4608, 1, st)));
+        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
+                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
       } else {
         using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
         using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
-        HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 192},
-                                       typename LB::Params{Wf(L.dZ) + (size_t)t * M * 512, g, M, dz_bytes}, ep, rows,
-                                       M, 4608, 1, st)));
+        HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{WdTh, 4608, 128},
+                                       typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
       }
+    }
+    {  // dx_t for every t at once: D[64][F*P] = WdT[0:64] * gather(dZ)
+      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+      const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
+      EpiStoreT<float> ep{Wf(L.dY2), 64, 64, F * P, nullptr, 0};
+      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
+                                     typename LB::Params{Wf(L.dZ), g, F * P, (uint32_t)((size_t)F * P * 512 * 4)}, ep,
+                                     64, F * P, 4608, 1, st)));
     }
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     {  // all 8 ConvLSTM weight grads as one long-K GEMM over every (t, b, p)
