@@ -154,16 +154,19 @@ def main():
     frames_total = B * T * world * args.steps
     value = frames_total / elapsed
 
-    # roofline of the dominant kernel class (largest total device time)
+    # roofline of the dominant kernel class (largest total device time); work per
+    # launch = the class's algorithmic FLOP per iteration / its launches per iteration
     M = B * learner.runner.P
     F = B * T
-    per_launch = {
-        N.TIMER_FWD_STEP: 2.0 * M * 512 * 1728,
-        N.TIMER_BPTT_STEP: 2.0 * M * 4608 * 128,   # h rows only; t=0 is skipped (no dh0 wanted)
+    per_iter = {
+        N.TIMER_FWD_STEP: (T - 1) * 2.0 * M * 512 * 1152,      # h-part of steps 1..T-1 (x-part batched)
+        N.TIMER_BPTT_STEP: (T - 1) * 2.0 * M * 128 * 4608,     # dh rows of steps T-1..1
         N.TIMER_CORE_WGRAD: 2.0 * 512 * 1728 * F * learner.runner.P,
     }
-    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step", N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dgrad + fused gate bwd)",
+    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step (h-part)",
+             N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dh dgrad + fused gate bwd)",
              N.TIMER_CORE_WGRAD: "ConvLSTM weight-gradient GEMM"}
+    per_launch = {k: per_iter[k] * args.steps / max(kt[k][1], 1) for k in kt}
     dom = max(kt, key=lambda k: kt[k][0])
     tot_ms, launches = kt[dom]
     avg_ms = tot_ms / max(launches, 1)

@@ -108,22 +108,23 @@ __device__ __forceinline__ void gate_bwd(float dh, const f32x4& g, float cprev, 
   dc = dcc * gf;
 }
 
-// ConvLSTM forward step epilogue: D[n = 4ch+g][m] = Wx*x_t + Wh*h_{t-1}.
+// ConvLSTM forward step epilogue: D[n = 4ch+g][m] = Wh*h_{t-1}; the x-part
+// (Wx*x_t + b, batched over all frames beforehand) is read from ``gates``
+// and overwritten in place with the activations.
 template <typename T>
 struct EpiConvLstmFwd {
-  const float* bias;   // [512] gate-interleaved
   const float* cprev;  // [M][128]  c_{t-1}
   float* cnext;        // [M][128]  c_t
   float* hout;         // [M][128]  h_t (fp32, attention input)
   T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
-  float* gates;        // [M][512]  post-activation (i,f,c~,o)
+  float* gates;        // [M][512]  in: Wx*x_t + b;  out: post-activation (i,f,c~,o)
   int Nj;              // M = B*P
   __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
     if (j >= Nj || i >= 512) return;
     const int ch = i >> 2;
-    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + i);
+    const f32x4 zx = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
     float gi, gf, gc, go, c, h;
-    GateFwd::run(v0 + b[0], v1 + b[1], v2 + b[2], v3 + b[3], cprev[(size_t)j * 128 + ch], gi, gf, gc, go, c, h);
+    GateFwd::run(zx[0] + v0, zx[1] + v1, zx[2] + v2, zx[3] + v3, cprev[(size_t)j * 128 + ch], gi, gf, gc, go, c, h);
     cnext[(size_t)j * 128 + ch] = c;
     hout[(size_t)j * 128 + ch] = h;
     xhnext[(size_t)j * 192 + 64 + ch] = (T)h;

@@ -41,7 +41,9 @@ hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, fl
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
 template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);
 template <typename T> hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st);
-template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* Wp, float* bl, hipStream_t st);
+template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st);
+template <typename T>
+hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);
 hipError_t unpack_conv(const float* g, int Cout, int Cin, int K, float* dst, hipStream_t st);
 hipError_t unpack_lstm(const float* gW, const float* gb, const LstmGrads& L, hipStream_t st);

@@ -328,20 +328,59 @@ __global__ void k_pack_dgradT(const T* __restrict__ Wp, int Cout, int taps, int 
   }
 }
 
-// ConvLSTM: 8 convs -> one [512][9*192] operand, row n = 4*ch + gate, input
-// channels [x (64) | h (128)]; biases interleaved the same way.
+// ConvLSTM weight (gate g, channel ch) for tap (ky,kx) and input channel ci of
+// [x (64) | h (128)], in the reference's (Cout, Cin, kx, ky) orientation (Q3).
+__device__ __forceinline__ float lstm_w(const LstmPtrs& L, int row, int ky, int kx, int ci) {
+  const int ch = row >> 2, g = row & 3;
+  return ci < 64 ? L.wx[g][((size_t)(ch * 64 + ci) * 3 + kx) * 3 + ky]
+                 : L.wh[g][((size_t)(ch * 128 + ci - 64) * 3 + kx) * 3 + ky];
+}
+
+// ConvLSTM forward operands, row n = 4*ch + gate: x-part [512][9*64] (batched
+// over all frames) and h-part [512][9*128] (the recurrent step); biases
+// interleaved the same way.
 template <typename T>
-__global__ void k_pack_lstm(LstmPtrs L, T* Wp, float* bl) {
-  const int n = 512 * 1728;
+__global__ void k_pack_lstm(LstmPtrs L, T* WpX, T* WpH, float* bl) {
+  const int nx = 512 * 576, nh = 512 * 1152;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nx + nh; idx += gridDim.x * blockDim.x) {
+    if (idx < nx) {
+      const int row = idx / 576, k = idx - row * 576;
+      const int tap = k / 64, ci = k - tap * 64, ky = tap / 3, kx = tap - ky * 3;
+      WpX[idx] = (T)lstm_w(L, row, ky, kx, ci);
+      if (k == 0) bl[row] = L.bx[row & 3][row >> 2];
+    } else {
+      const int i = idx - nx, row = i / 1152, k = i - row * 1152;
+      const int tap = k / 128, ci = k - tap * 128, ky = tap / 3, kx = tap - ky * 3;
+      WpH[i] = (T)lstm_w(L, row, ky, kx, 64 + ci);
+    }
+  }
+}
+
+// ConvLSTM dgrad operand: WdT[c'][tap*512 + n] = W(n, tap, c'), c' over [x | h].
+template <typename T>
+__global__ void k_pack_lstm_dgradT(LstmPtrs L, T* WdT) {
+  const int n = 192 * 4608;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int row = idx / 1728, k = idx - row * 1728;
-    const int ch = row >> 2, g = row & 3;
-    const int tap = k / 192, ci = k - tap * 192, ky = tap / 3, kx = tap - ky * 3;
-    float v;
-    if (ci < 64) v = L.wx[g][((size_t)(ch * 64 + ci) * 3 + kx) * 3 + ky];
-    else v = L.wh[g][((size_t)(ch * 128 + ci - 64) * 3 + kx) * 3 + ky];
-    Wp[idx] = (T)v;
-    if (k == 0) bl[row] = L.bx[g][ch];
+    const int cp = idx / 4608, r = idx - cp * 4608;
+    const int tap = r >> 9, row = r & 511, ky = tap / 3, kx = tap - ky * 3;
+    WdT[idx] = (T)lstm_w(L, row, ky, kx, cp);
+  }
+}
+
+// Step 0 from a zero state: the gates come from the batched x-part alone.
+template <typename T>
+__global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gates, float* cnext, float* hout,
+                              T* xhnext) {
+  const int n = M * 128;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int m = idx >> 7, ch = idx & 127;
+    const f32x4 z = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
+    float gi, gf, gc, go, c, h;
+    GateFwd::run(z[0], z[1], z[2], z[3], cprev[idx], gi, gf, gc, go, c, h);
+    cnext[idx] = c;
+    hout[idx] = h;
+    xhnext[(size_t)m * 192 + 64 + ch] = (T)h;
+    *reinterpret_cast<f32x4*>(gates + (size_t)m * 512 + 4 * ch) = f32x4{gi, gf, gc, go};
   }
 }
 
@@ -541,8 +580,17 @@ hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStre
 }
 
 template <typename T>
-hipError_t pack_lstm(const LstmPtrs& L, T* Wp, float* bl, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_lstm<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, Wp, bl);
+hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lstm<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, WpX, WpH, bl);
+  hipLaunchKernelGGL(k_pack_lstm_dgradT<T>, dim3(nblk(192L * 4608)), dim3(256), 0, st, L, WdT);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_gate_fwd_zx<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, cprev, gates, cnext, hout,
+                     xhnext);
   return hipGetLastError();
 }
 
@@ -575,7 +623,9 @@ template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStr
 template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);
 template hipError_t pack_dgradT<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t pack_dgradT<__bf16>(const __bf16*, int, int, int, __bf16*, hipStream_t);
-template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, hipStream_t);
-template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, float*, hipStream_t);
+template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, float*, float*, hipStream_t);
+template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, hipStream_t);
+template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);
+template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t);
 
 }  // namespace aaa

@@ -64,7 +64,7 @@ struct Layout {
   int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_Wpl, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
@@ -103,7 +103,8 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.k_Wp1 = take(32 * 192 * e);
   L.k_Wp2 = take(64 * 512 * e);
   L.k_WdT2 = take(32 * 1024 * e);
-  L.k_Wpl = take(512 * 1728 * e);
+  L.k_WpX = take(512 * 576 * e);
+  L.k_WpH = take(512 * 1152 * e);
   L.k_WdTl = take(192 * 4608 * e);
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
@@ -175,6 +176,69 @@ static int check_device() {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ------------------------------------------------------------ aux stream --
+// Work that is off the sequential ConvLSTM chain (the batched x-part of the
+// forward, every weight/bias gradient and dx/conv backward) is issued on a
+// per-device low-priority stream, chunked every few steps and ordered against
+// the caller's stream by events; the caller's stream waits for it before the
+// call returns (fork/join inside each call).  Created lazily, once per device.
+struct AuxStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[64] = {};
+  unsigned next = 0;
+};
+static AuxStream g_aux[64];
+static std::mutex g_aux_mu;
+
+static int env_int(const char* name, int dflt);
+
+// Measured on C2 (round 1): running the off-chain chunks concurrently slows the
+// chain's step kernels ~2x (stream priority does not keep CUs free for them),
+// 6.31-6.55 ms vs 6.15 ms serial; so overlap is opt-in (AAA_OVERLAP=1).
+static hipStream_t aux_stream() {
+  if (env_int("AAA_OVERLAP", 0) == 0) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  AuxStream& a = g_aux[dev];
+  if (!a.s) {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, lo) != hipSuccess) { a.s = nullptr; return nullptr; }
+    for (auto& e : a.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { (void)hipStreamDestroy(a.s); a.s = nullptr; return nullptr; }
+  }
+  return a.s;
+}
+
+// Record a pooled event on ``s`` (everything enqueued on s so far).
+static hipError_t record_event(hipStream_t s, hipEvent_t* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    AuxStream& a = g_aux[dev];
+    *out = a.ev[a.next++ & 63];
+  }
+  return hipEventRecord(*out, s);
+}
+
+// ``to`` waits for everything enqueued on ``from`` so far.
+static hipError_t stream_order(hipStream_t from, hipStream_t to) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipEvent_t ev;
+  {
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    AuxStream& a = g_aux[dev];
+    ev = a.ev[a.next++ & 63];
+  }
+  if ((e = hipEventRecord(ev, from)) != hipSuccess) return e;
+  return hipStreamWaitEvent(to, ev, 0);
+}
+
 // ------------------------------------------------- optional kernel timing --
 struct Timers {
   std::mutex mu;
@@ -234,6 +298,10 @@ static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unless overlapping)
+  const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : T);
+  return std::max(1, std::min(c, T));
+}
 static int step_tile(long out_tiles32, const char* env) {
   const int v = env_int(env, -1);
   if (v >= 0) return v;
@@ -259,8 +327,7 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     lp.bx[g] = prm + L.poff[XI_B + 3 * g];
     lp.wh[g] = prm + L.poff[HI_W + 3 * g];
   }
-  HIPCHK(pack_lstm<T>(lp, (T*)(pk + L.k_Wpl), (float*)(pk + L.k_bl), st));
-  HIPCHK(pack_dgradT<T>((const T*)(pk + L.k_Wpl), 512, 9, 192, (T*)(pk + L.k_WdTl), st));
+  HIPCHK(pack_lstm<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl), st));
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
@@ -311,27 +378,59 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
   if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  // x-part of the ConvLSTM steps (not recurrent): Gt <- Wx * x_t + b, in
+  // chunks of ``cs`` steps on the aux stream; step t waits only for its chunk.
+  hipStream_t ax = aux_stream();
+  const int cs = chunk_steps(L.T);
+  hipStream_t xs = ax ? ax : st;
+  if (ax) HIPCHK(stream_order(st, ax));
+  auto xpart = [&](int lo, int hi) -> int {
+    using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+    using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
+    const ConvGeo g = ConvGeo{64, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
+    const int rows = (hi - lo) * M;
+    EpiStoreT<float> ep{Wf(L.Gt) + (size_t)lo * M * 512, 512, 512, rows, (const float*)(pk + L.k_bl), 0};
+    HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpX), 576, 512},
+                                   typename LB::Params{Wt(L.XH) + (size_t)lo * M * 192, g, rows,
+                                                       (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)},
+                                   ep, 512, rows, 576, 1, xs)));
+    return AAA_OK;
+  };
+  hipEvent_t xev[64];
+  const int nchunks = (L.T + cs - 1) / cs;
+  if (ax && nchunks > 48) return fail(AAA_E_ARG, "too many overlap chunks (T=%d, AAA_CHUNK=%d)", L.T, cs);
+  for (int k = 0; k < nchunks; ++k) {
+    int rc = xpart(k * cs, std::min(L.T, (k + 1) * cs));
+    if (rc) return rc;
+    if (ax) HIPCHK(record_event(ax, &xev[k]));
+  }
   const bool fwd_k = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE") >= 1;
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);  // one step slice of XH
-  for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126)
-    EpiConvLstmFwd<T> ep{(const float*)(pk + L.k_bl), Wf(L.Cst) + (size_t)t * M * 128,
-                         Wf(L.Cst) + (size_t)(t + 1) * M * 128, Wf(L.Hs) + (size_t)t * M * 128,
-                         Wt(L.XH) + (size_t)(t + 1) * M * 192, Wf(L.Gt) + (size_t)t * M * 512, M};
-    const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
+  for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126): h-part only
+    if (ax && t % cs == 0) HIPCHK(hipStreamWaitEvent(st, xev[t / cs], 0));   // x-part of steps [t, t+cs) done
+    if (t == 0 && !io->h0) {       // zero state: gates come from the x-part alone
+      HIPCHK(gate_fwd_zx<T>(M, Wf(L.Cst), Wf(L.Gt), Wf(L.Cst) + (size_t)M * 128, Wf(L.Hs), Wt(L.XH) + (size_t)M * 192,
+                            st));
+      continue;
+    }
+    EpiConvLstmFwd<T> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
+                         Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
+                         Wf(L.Gt) + (size_t)t * M * 512, M};
+    const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     TimerScope tim(AAA_TIMER_FWD_STEP, st);
     if (fwd_k) {
       using CK = CfgKFor<T>;
       using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
       using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
-      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_Wpl), 1728, 512},
+      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
                                       typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
-                                      1728, 1, st)));
+                                      1152, 1, st)));
     } else {
       using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
       using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
-      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_Wpl), 1728, 512},
+      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
                                      typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
-                                     1728, 1, st)));
+                                     1152, 1, st)));
     }
   }
   // constant query (Q1) + fused attention readout over all T*B frames
@@ -464,7 +563,87 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     HIPCHK(unpack_f32(up, st));
   }
 
+  // Off-chain backward work for the steps [lo, hi): weight/bias grads of the
+  // ConvLSTM, dx (conv2 output grad) and -- when VISION runs in the same call
+  // -- the conv2/conv1 backward of those frames.  Every gradient accumulates
+  // atomically into zeroed buffers, so chunks may run in any order.
+  const bool vision_here = (phases & AAA_BWD_VISION) && (phases & AAA_BWD_CORE);
+  auto core_chunk = [&](int lo, int hi, hipStream_t s) -> int {
+    const int rows = (hi - lo) * M;                       // pixels of these frames
+    const int F1 = (hi - lo) * L.B;                       // frames
+    const float* dz = Wf(L.dZ) + (size_t)lo * M * 512;
+    auto wgrad_lstm = [&](auto cfg) -> int {   // all 8 ConvLSTM weight grads: D[512][1728] += dZ^T * im2col(XH)
+      using CW = decltype(cfg);
+      using LA = LdRowsTB<float, T, CW::BI, CW::BK, CW::NT>;
+      using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
+      typename LA::Params pa{dz, 512, 512, rows};
+      typename LB::Params pb{Wt(L.XH) + (size_t)lo * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(),
+                             1728, (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)};
+      EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
+      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
+      TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+      HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
+      return AAA_OK;
+    };
+    {
+      // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
+      const int wide = env_int("AAA_AUX_WIDE", s == st ? 1 : 0);
+      const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
+      if (rc) return rc;
+    }
+    HIPCHK(colsum(dz, 512, rows, 512, Wf(L.gbl), s));
+    {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
+      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+      const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
+      EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
+      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
+                                     typename LB::Params{dz, g, rows, (uint32_t)((size_t)rows * 512 * 4)}, ep, 64, rows,
+                                     4608, 1, s)));
+    }
+    if (!vision_here) return AAA_OK;
+    const float* dy2 = Wf(L.dY2) + (size_t)lo * M * 64;
+    float* dy1 = Wf(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
+    const int rows1 = F1 * L.P1;
+    {  // conv2 wgrad / bias
+      using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
+      using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
+      typename LA::Params pa{dy2, 64, 64, rows};
+      typename LB::Params pb{Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(),
+                             512, (uint32_t)((size_t)rows1 * 32 * L.esz)};
+      EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
+      const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
+      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
+      HIPCHK(colsum(dy2, 64, rows, 64, grads + L.poff[C1B], s));
+    }
+    {  // conv2 dgrad (stride-2 transposed gather) -> dY1
+      using C3 = Cfg32For<T>;
+      using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
+      using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
+      typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
+      typename LB::Params pb{dy2, ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), rows1};
+      EpiStoreT<float> ep{dy1, 32, 32, rows1, nullptr, 0};
+      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows1, 1024, 1, s)));
+    }
+    {  // conv1 wgrad / bias (frames need no grad)
+      using C3 = Cfg32For<T>;
+      using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
+      using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
+      typename LA::Params pa{dy1, 32, 32, rows1};
+      typename LB::Params pb{io->frames + (size_t)lo * L.B * L.H * L.W * 3,
+                             ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
+      EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
+      const int tiles = cdiv(32, C3::BI) * cdiv(192, C3::BJ);
+      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
+      HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
+    }
+    return AAA_OK;
+  };
+
   if (phases & AAA_BWD_CORE) {
+    hipStream_t ax = aux_stream();
+    hipStream_t os = ax ? ax : st;     // stream for the off-chain chunks
+    const int cs = chunk_steps(L.T);
     // ConvLSTM BPTT, t = T-1 .. 0
     if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
@@ -473,11 +652,24 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                          Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
                          Wf(L.dZ) + (size_t)t1 * M * 512, st));
     // Sequential part: only the h rows (dh_{t-1}, fused with the gate backward
-    // of step t-1); the x rows (dx_t for conv2) are one batched GEMM below.
+    // of step t-1); everything else runs in chunks off the chain.
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE");
     const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * 4);  // one step slice of dZ
     const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
+    int done_hi = L.T;   // chunks [lo, done_hi) not yet issued
+    auto flush = [&](int ready_lo) -> int {   // dz of steps >= ready_lo are final
+      while (done_hi - ready_lo >= cs || (ready_lo == 0 && done_hi > 0)) {
+        const int lo = std::max(ready_lo, done_hi - cs);
+        if (ax) HIPCHK(stream_order(st, ax));
+        int rc = core_chunk(lo, done_hi, os);
+        if (rc) return rc;
+        done_hi = lo;
+      }
+      return AAA_OK;
+    };
     for (int t = t1; t >= 0; --t) {
+      const int rc0 = flush(t);   // dz_t .. dz_{T-1} are final here
+      if (rc0) return rc0;
       const bool prev = t > 0;
       if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
@@ -510,29 +702,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
       }
     }
-    {  // dx_t for every t at once: D[64][F*P] = WdT[0:64] * gather(dZ)
-      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
-      const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
-      EpiStoreT<float> ep{Wf(L.dY2), 64, 64, F * P, nullptr, 0};
-      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
-                                     typename LB::Params{Wf(L.dZ), g, F * P, (uint32_t)((size_t)F * P * 512 * 4)}, ep,
-                                     64, F * P, 4608, 1, st)));
-    }
+    { const int rc0 = flush(0); if (rc0) return rc0; }
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
-    {  // all 8 ConvLSTM weight grads as one long-K GEMM over every (t, b, p)
-      using CW = CfgWFor<T>;
-      using LA = LdRowsTB<float, T, CW::BI, CW::BK, CW::NT>;
-      using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
-      typename LA::Params pa{Wf(L.dZ), 512, 512, F * P};
-      typename LB::Params pb{Wt(L.XH), ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(), 1728,
-                             (uint32_t)((size_t)(L.T + 1) * M * 192 * L.esz)};
-      EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
-      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-      TimerScope tim(AAA_TIMER_CORE_WGRAD, st);
-      HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, F * P, wgrad_splits(tiles, F * P, CW::BK), st)));
-      HIPCHK(colsum(Wf(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
-    }
+    if (ax) HIPCHK(stream_order(ax, st));   // join
     LstmGrads lg;
     for (int g = 0; g < 4; ++g) {
       lg.wx[g] = grads + L.poff[XI_W + 3 * g];
@@ -543,36 +715,36 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   }
 
   if (phases & AAA_BWD_VISION) {
-    {  // conv2 wgrad / bias
-      using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
-      typename LA::Params pa{Wf(L.dY2), 64, 64, F * P};
-      typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
-                             (uint32_t)((size_t)F * L.P1 * 32 * L.esz)};
-      EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
-      const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, F * P, wgrad_splits(tiles, F * P, C::BK), st)));
-      HIPCHK(colsum(Wf(L.dY2), 64, F * P, 64, grads + L.poff[C1B], st));
-    }
-    {  // conv2 dgrad (stride-2 transposed gather) -> dY1
+    if (!vision_here) {   // VISION alone: its chunk work over all frames, here
       using C3 = Cfg32For<T>;
-      using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
-      using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
-      typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
-      typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), F * L.P1};
-      EpiStoreT<float> ep{Wf(L.dY1), 32, 32, F * L.P1, nullptr, 0};
-      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 1024, 1, st)));
-    }
-    {  // conv1 wgrad / bias (frames need no grad)
-      using C3 = Cfg32For<T>;
-      using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
-      using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
-      typename LA::Params pa{Wf(L.dY1), 32, 32, F * L.P1};
-      typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
-      EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
-      const int tiles = cdiv(32, C3::BI) * cdiv(192, C3::BJ);
-      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, F * L.P1, wgrad_splits(tiles, F * L.P1, C3::BK), st)));
-      HIPCHK(colsum(Wf(L.dY1), 32, F * L.P1, 32, grads + L.poff[C0B], st));
+      const int rows = F * P, rows1 = F * L.P1;
+      {
+        using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
+        using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
+        typename LA::Params pa{Wf(L.dY2), 64, 64, rows};
+        typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
+                               (uint32_t)((size_t)rows1 * 32 * L.esz)};
+        EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
+        HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(cdiv(512, C::BJ), rows, C::BK), st)));
+        HIPCHK(colsum(Wf(L.dY2), 64, rows, 64, grads + L.poff[C1B], st));
+      }
+      {
+        using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
+        using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
+        typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
+        typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), rows1};
+        EpiStoreT<float> ep{Wf(L.dY1), 32, 32, rows1, nullptr, 0};
+        HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows1, 1024, 1, st)));
+      }
+      {
+        using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
+        using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
+        typename LA::Params pa{Wf(L.dY1), 32, 32, rows1};
+        typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
+        EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
+        HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, rows1, wgrad_splits(cdiv(192, C3::BJ), rows1, C3::BK), st)));
+        HIPCHK(colsum(Wf(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
+      }
     }
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
     HIPCHK(unpack_conv(Wf(L.gWp1), 32, 3, 8, grads + L.poff[C0W], st));
