@@ -19,6 +19,7 @@ CONVS = {
     "conv2": (3, 20, 20, 32, 64, 4, 2, 2),
     "convlstm": (2, 11, 11, 192, 512, 3, 1, 1),
     "odd": (2, 13, 9, 8, 12, 3, 2, 1),
+    "conv1_rgbx": (2, 84, 84, 4, 32, 8, 4, 1),   # conv1 on RGBx frames (multi-tap K tiles)
 }
 
 

@@ -28,6 +28,21 @@ struct EpiStoreT {
   }
 };
 
+// Stride-2 conv dgrad, one parity class (py, px): column j = (frame, a, b) of
+// the class grid (Ha x Wa) lands at output pixel (2a+py, 2b+px) of H1 x W1.
+struct EpiStoreParity {
+  float* out;          // [F][H1][W1][C]
+  int C, Nj, Ha, Wa, H1, W1, py, px;
+  uint64_t mHW, mW;    // magic divisors for Ha*Wa and Wa (FastDiv)
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= C) return;
+    const int f = (int)(((uint64_t)j * mHW) >> 32), r = j - f * Ha * Wa;
+    const int a = (int)(((uint64_t)r * mW) >> 32), b = r - a * Wa;
+    float* o = out + ((size_t)(f * H1 + 2 * a + py) * W1 + 2 * b + px) * C + i;
+    *reinterpret_cast<f32x4*>(o) = f32x4{v0, v1, v2, v3};
+  }
+};
+
 // dx[j*ld + i] = v * (mask[j*ldm + i] > 0)   (ReLU backward through a saved output)
 struct EpiReluBwdT {
   float* out;

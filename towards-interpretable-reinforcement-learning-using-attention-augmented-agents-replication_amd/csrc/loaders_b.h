@@ -102,9 +102,11 @@ struct LdRowsTB {
   }
 };
 
-// Implicit-GEMM gather, rows = output pixels, k = (tap, ci), Cin % BK == 0:
-// the tap is uniform over a K tile, so per chunk a fetch is one bit test of
-// the pixel's precomputed valid-tap mask and one add.
+// Implicit-GEMM gather, rows = output pixels, k = (tap, ci).  Either Cin % BK
+// == 0 (a K tile lies inside one tap: the tap is wave-uniform) or BK % Cin == 0
+// with the tile's BK/Cin taps forming whole kernel rows or part of one row (the
+// per-chunk tap offset is then a per-thread constant).  Per chunk a fetch is
+// one bit test of the pixel's precomputed valid-tap mask and one add.
 template <typename G, typename T, int R, int BK, int NT>
 struct LdIm2colB {
   static constexpr bool KC = true;
@@ -116,14 +118,22 @@ struct LdIm2colB {
   struct Params { const G* src; ConvGeo g; int nrows; uint32_t src_bytes; };
   __amdgpu_buffer_rsrc_t rs;
   ConvGeo g;
-  int base[PER];            // element offset of the pixel's tap-(0,0) source (+ kc, coff)
+  int base[PER];            // element offset of the chunk's source at the tile's first tap
+  int dt[PER];              // tap of this chunk relative to the tile's first tap
   uint64_t vmask[PER];      // bit tap = that tap reads inside the input
   int ldo[PER];
   bool act[PER];
+  __device__ static bool ok_shape(const ConvGeo& g) {
+    if (g.Cin % BK == 0) return true;
+    if (BK % g.Cin) return false;
+    const int tpt = BK / g.Cin;
+    return tpt % g.KW == 0 || g.KW % tpt == 0;
+  }
   __device__ __forceinline__ LdIm2colB(const Params& p, int row0) : g(p.g) {
     rs = make_rsrc(p.src, p.src_bytes);
     const int hw = g.Hout * g.Wout;
     const int KH = g.KW;  // square kernels
+    const int sgn = g.transposed ? -1 : 1;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const int ch = threadIdx.x + c * NT;
@@ -140,9 +150,13 @@ struct LdIm2colB {
           if (ok && conv_src(g, oy, ox, ky, kx, iy, ix)) msk |= 1ull << (ky * g.KW + kx);
         }
       vmask[c] = msk;
+      const int d = g.Cin >= BK ? 0 : kc / g.Cin;       // taps inside the tile before this chunk
+      const int ci = kc - d * g.Cin;
+      dt[c] = d;
+      const int dky = d / g.KW, dkx = d - dky * g.KW;
       const int oy0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;
       const int ox0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
-      base[c] = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + kc;
+      base[c] = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + ci + sgn * (dky * g.Win + dkx) * g.cs;
       ldo[c] = Tile<T, R, BK, true>::off(lr, kc);
     }
   }
@@ -154,7 +168,7 @@ struct LdIm2colB {
     const int toff = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs + ci0;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
-      const bool v = (vmask[c] >> tap) & 1ull;
+      const bool v = (vmask[c] >> (tap + dt[c])) & 1ull;
       buf[c] = bload(rs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(G)) : kOOB);
     }
   }

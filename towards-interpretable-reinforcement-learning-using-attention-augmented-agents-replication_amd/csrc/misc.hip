@@ -27,25 +27,46 @@ __device__ void gemv_rows(const float* __restrict__ W, int ldw, const float* x, 
     if (lane == 0) y[o] = s;
   }
 }
-// cols:  y[k] = sum_o W[o*ldw + k] x[o]   -- lanes over k, waves split o, LDS reduce
+// cols:  y[k] = sum_o W[o*ldw + k] x[o]   -- lanes over k (all K/64 column
+// groups of a row loaded together for memory-level parallelism), waves split
+// o, LDS reduce.  K <= 64*MAXJ.
+template <int MAXJ>
 __device__ void gemv_cols(const float* __restrict__ W, int ldw, const float* x, int N, int K, float* y,
-                          float* scratch /* nwaves*64 */) {
+                          float* scratch /* nwaves*64*MAXJ */) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int k0 = 0; k0 < K; k0 += 64) {
-    const int k = k0 + lane;
+  float s[MAXJ];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) s[j] = 0.f;
+#pragma unroll 2
+  for (int o = wave; o < N; o += nw) {
+    const float xo = x[o];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k < K) s[j] += W[(size_t)o * ldw + k] * xo;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) scratch[(wave * MAXJ + j) * 64 + lane] = s[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    const int j = k >> 6, l = k & 63;
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += scratch[(w * MAXJ + j) * 64 + l];
+    y[k] = t;
+  }
+  __syncthreads();
+}
+
+// y[k] += sum over this workgroup's rows o of W[o*ldw + k] x[o]  (multi-WG, atomics)
+__global__ void k_gemv_cols_atomic(const float* __restrict__ W, int ldw, const float* __restrict__ x, int N, int K,
+                                   int rows_per, float* y) {
+  const int o0 = blockIdx.x * rows_per, o1 = min(N, o0 + rows_per);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
     float s = 0.f;
-    if (k < K) {
-#pragma unroll 4
-      for (int o = wave; o < N; o += nw) s += W[(size_t)o * ldw + k] * x[o];
-    }
-    scratch[wave * 64 + lane] = s;
-    __syncthreads();
-    if (wave == 0 && k < K) {
-      float t = 0.f;
-      for (int w = 0; w < nw; ++w) t += scratch[w * 64 + lane];
-      y[k] = t;
-    }
-    __syncthreads();
+#pragma unroll 8
+    for (int o = o0; o < o1; ++o) s += W[(size_t)o * ldw + k] * x[o];
+    atomicAdd(y + k, s);
   }
 }
 
@@ -69,11 +90,13 @@ k_query_fwd(const float* __restrict__ b0, const float* __restrict__ W2, const fl
   __syncthreads();
   for (int o = tid; o < qd; o += blockDim.x) { float v = sq[o] + b4[o]; sq[o] = v; Q[o] = v; }
   __syncthreads();
-  for (int idx = tid; idx < P * nq; idx += blockDim.x) {
-    int p = idx / nq, q = idx - p * nq;
-    float acc = 0.f;
-    for (int c = 0; c < 64; ++c) acc += S[p * 64 + c] * sq[q * 72 + 8 + c];
-    SQ[idx] = acc;
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  for (int p = wave; p < P; p += nw) {          // one wave per grid position, lanes over the 64 basis channels
+    const float sv = S[p * 64 + lane];
+    for (int q = 0; q < nq; ++q) {
+      const float acc = wave_sum(sv * sq[q * 72 + 8 + lane]);
+      if (lane == 0) SQ[p * nq + q] = acc;
+    }
   }
 }
 
@@ -228,24 +251,19 @@ k_query_bwd(const float* __restrict__ dQs, const float* __restrict__ gb1, const 
             int ans_in, int nq, const float* __restrict__ W2, const float* __restrict__ W4,
             const float* __restrict__ q1, const float* __restrict__ q2, float* gW4, float* gb4, float* gW2,
             float* gb2, float* gb0) {
-  __shared__ float dQ[576], dq2[576], s2[576], s1[128], b1s[512], dq1[128], scratch[16 * 64];
-  const int qd = 72 * nq, tid = threadIdx.x, off = nq * 184;
+  __shared__ float dQ[576], dq2[576], s2[576], s1[128], dq1[128], scratch[16 * 64 * 9];
+  const int qd = 72 * nq, tid = threadIdx.x;
+  (void)gb1; (void)W1; (void)ans_in;
   for (int i = tid; i < qd; i += blockDim.x) s2[i] = q2[i];
   for (int i = tid; i < 128; i += blockDim.x) s1[i] = q1[i];
-  for (int i = tid; i < 512; i += blockDim.x) b1s[i] = gb1[i];
-  __syncthreads();
-  gemv_cols(W1 + off, ans_in, b1s, 512, qd, dQ, scratch);
-  __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) { dQ[o] += dQs[o]; gb4[o] = dQ[o]; }
+  for (int o = tid; o < qd; o += blockDim.x) { dQ[o] = dQs[o]; gb4[o] = dQs[o]; }   // dQs already holds W1_Q^T db1
   __syncthreads();
   for (int i = tid; i < qd * qd; i += blockDim.x) gW4[i] = dQ[i / qd] * s2[i - (i / qd) * qd];
-  gemv_cols(W4, qd, dQ, qd, qd, dq2, scratch);
-  __syncthreads();
+  gemv_cols<9>(W4, qd, dQ, qd, qd, dq2, scratch);
   for (int k = tid; k < qd; k += blockDim.x) { if (!(s2[k] > 0.f)) dq2[k] = 0.f; gb2[k] = dq2[k]; }
   __syncthreads();
   for (int i = tid; i < qd * 128; i += blockDim.x) gW2[i] = dq2[i >> 7] * s1[i & 127];
-  gemv_cols(W2, 128, dq2, qd, 128, dq1, scratch);
-  __syncthreads();
+  gemv_cols<2>(W2, 128, dq2, qd, 128, dq1, scratch);
   for (int j = tid; j < 128; j += blockDim.x) gb0[j] = s1[j] > 0.f ? dq1[j] : 0.f;
 }
 
@@ -314,6 +332,53 @@ __global__ void k_pack_conv(const float* __restrict__ w, int Cout, int Cin, int 
     const int o = idx / (K * K * Cin), r = idx - o * (K * K * Cin);
     const int tap = r / Cin, ci = r - tap * Cin, ky = tap / K, kx = tap - ky * K;
     dst[idx] = (T)w[((size_t)(o * Cin + ci) * K + kx) * K + ky];
+  }
+}
+
+// Frames (F,H,W,3) -> (F,H,W,4) with a zero 4th channel, so conv1's gather
+// is 16-byte vectors (Cin 4) instead of scalar loads (Cin 3).
+template <typename T>
+__global__ void k_frames_rgbx(long npix, const float* __restrict__ x, T* __restrict__ y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < npix; i += (long)gridDim.x * blockDim.x) {
+    const float* s = x + i * 3;
+    T* d = y + i * 4;
+    d[0] = (T)s[0]; d[1] = (T)s[1]; d[2] = (T)s[2]; d[3] = (T)0.f;
+  }
+}
+
+// conv2 dgrad by parity class (py, px) of the output pixel: a 2x2, stride-1,
+// pad-0 conv over dY2 with W_c[ci][(ty*2+tx)*64 + co] = W2[co][ci][kx][ky],
+// ky = py + 2(1-ty), kx = px + 2(1-tx) (reference (Cout,Cin,kx,ky) layout, Q3).
+template <typename T>
+__global__ void k_pack_conv2_classes(const float* __restrict__ w2, T* dst) {
+  const int n = 4 * 32 * 256;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int cls = idx >> 13, r = idx & 8191, ci = r >> 8, k = r & 255;
+    const int t = k >> 6, co = k & 63, ty = t >> 1, tx = t & 1;
+    const int py = cls >> 1, px = cls & 1;
+    const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
+    dst[idx] = (T)w2[((size_t)(co * 32 + ci) * 4 + kx) * 4 + ky];
+  }
+}
+
+// conv1 weights with a zero 4th input channel: [32][(ky*8 + kx)*4 + ci]
+template <typename T>
+__global__ void k_pack_conv1_rgbx(const float* __restrict__ w, T* dst) {
+  const int n = 32 * 256;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int o = idx >> 8, r = idx & 255, tap = r >> 2, ci = r & 3, ky = tap >> 3, kx = tap & 7;
+    dst[idx] = ci < 3 ? (T)w[((size_t)(o * 3 + ci) * 8 + kx) * 8 + ky] : (T)0.f;
+  }
+}
+
+__global__ void k_unpack_conv1_rgbx(const float* __restrict__ g, float* dst) {
+  const int n = 32 * 3 * 64;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    int r = idx;
+    const int ky = r % 8; r /= 8;
+    const int kx = r % 8; r /= 8;
+    const int ci = r % 3, o = r / 3;
+    dst[idx] = g[o * 256 + (ky * 8 + kx) * 4 + ci];
   }
 }
 
@@ -533,6 +598,9 @@ hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st) {
+  // dQ += W1[:, Q-cols]^T . db1 (the answer path summed over rows), 512 rows over 32 WGs
+  hipLaunchKernelGGL(k_gemv_cols_atomic, dim3(32), dim3(256), 0, st, W1 + nq * 184, ans_in, gb1, 512, 72 * nq, 16,
+                     const_cast<float*>(dQs));
   hipLaunchKernelGGL(k_query_bwd, dim3(1), dim3(1024), 0, st, dQs, gb1, W1, ans_in, nq, W2, W4, q1, q2, gW4, gb4,
                      gW2, gb2, gb0);
   return hipGetLastError();
@@ -617,6 +685,31 @@ hipError_t unpack_f32(const F32Unpack& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <typename T>
+hipError_t frames_rgbx(long npix, const float* x, T* y, hipStream_t st) {
+  hipLaunchKernelGGL(k_frames_rgbx<T>, dim3(nblk(npix)), dim3(256), 0, st, npix, x, y);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t pack_conv2_classes(const float* w2, T* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_conv2_classes<T>, dim3(nblk(4 * 32 * 256)), dim3(256), 0, st, w2, dst);
+  return hipGetLastError();
+}
+template <typename T>
+hipError_t pack_conv1_rgbx(const float* w, T* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_conv1_rgbx<T>, dim3(nblk(32 * 256)), dim3(256), 0, st, w, dst);
+  return hipGetLastError();
+}
+hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack_conv1_rgbx, dim3(nblk(32 * 3 * 64)), dim3(256), 0, st, g, dst);
+  return hipGetLastError();
+}
+template hipError_t frames_rgbx<float>(long, const float*, float*, hipStream_t);
+template hipError_t frames_rgbx<__bf16>(long, const float*, __bf16*, hipStream_t);
+template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t);
+template hipError_t pack_conv2_classes<__bf16>(const float*, __bf16*, hipStream_t);
+template hipError_t pack_conv1_rgbx<float>(const float*, float*, hipStream_t);
+template hipError_t pack_conv1_rgbx<__bf16>(const float*, __bf16*, hipStream_t);
 template hipError_t state_to_xh<float>(int, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<__bf16>(int, const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStream_t);

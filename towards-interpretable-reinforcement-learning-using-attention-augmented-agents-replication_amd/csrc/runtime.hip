@@ -65,7 +65,7 @@ struct Layout {
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
-  size_t Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
+  size_t Xp, Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
 };
@@ -100,9 +100,9 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   size_t p = 0;
   auto take = [&](size_t bytes) { size_t r = p; p = al256(p + bytes); return r; };
   const size_t e = L.esz;
-  L.k_Wp1 = take(32 * 192 * e);
+  L.k_Wp1 = take(32 * 256 * e);        // RGBx: 4th input channel zero
   L.k_Wp2 = take(64 * 512 * e);
-  L.k_WdT2 = take(32 * 1024 * e);
+  L.k_WdT2 = take(4 * 32 * 256 * e);   // conv2 dgrad, 4 parity classes
   L.k_WpX = take(512 * 576 * e);
   L.k_WpH = take(512 * 1152 * e);
   L.k_WdTl = take(192 * 4608 * e);
@@ -116,6 +116,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   // workspace
   p = 0;
   const size_t F = L.F, P = L.P, M = (size_t)L.B * L.P;
+  L.Xp = take(F * L.H * L.W * 4 * 4);  // frames as RGBx fp32
   L.Y1 = take(F * L.P1 * 32 * e);
   L.XH = take((size_t)(L.T + 1) * M * 192 * e);
   L.Hs = take(F * P * 128 * 4);
@@ -145,7 +146,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.dY1 = take(F * L.P1 * 32 * 4);
   // zero-initialised (atomic) accumulation region: one memset covers it
   L.dQs = take((size_t)L.qd * 4);
-  L.gWp1 = take(32 * 192 * 4);
+  L.gWp1 = take(32 * 256 * 4);
   L.gWp2 = take(64 * 512 * 4);
   L.gWpl = take(512 * 1728 * 4);
   L.gbl = take(512 * 4);
@@ -318,9 +319,9 @@ static int wgrad_splits(int tiles, int K, int BK) {
 // ------------------------------------------------------------- packing ----
 template <typename T>
 static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
-  HIPCHK(pack_conv<T>(prm + L.poff[C0W], 32, 3, 8, (T*)(pk + L.k_Wp1), st));
+  HIPCHK(pack_conv1_rgbx<T>(prm + L.poff[C0W], (T*)(pk + L.k_Wp1), st));
   HIPCHK(pack_conv<T>(prm + L.poff[C1W], 64, 32, 4, (T*)(pk + L.k_Wp2), st));
-  HIPCHK(pack_dgradT<T>((const T*)(pk + L.k_Wp2), 64, 16, 32, (T*)(pk + L.k_WdT2), st));
+  HIPCHK(pack_conv2_classes<T>(prm + L.poff[C1W], (T*)(pk + L.k_WdT2), st));
   LstmPtrs lp;
   for (int g = 0; g < 4; ++g) {
     lp.wx[g] = prm + L.poff[XI_W + 3 * g];
@@ -351,14 +352,16 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   auto Wt = [&](size_t off) { return (T*)(ws + off); };
   const int F = L.F, P = L.P, M = L.B * L.P;
 
-  {  // conv1 (attention.py:156-162): frames (fp32, Cin=3) -> Y1
+  {  // conv1 (attention.py:156-162): frames -> RGBx (Cin 4) -> Y1
+    HIPCHK(frames_rgbx<float>((long)F * L.H * L.W, io->frames, Wf(L.Xp), st));
     using C3 = Cfg32For<T>;
     using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
-    using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, false>;
-    typename LA::Params pa{(const T*)(pk + L.k_Wp1), 192, 32};
-    typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), F * L.P1};
+    using LB = LdIm2colB<float, T, C3::BJ, C3::BK, C3::NT>;
+    typename LA::Params pa{(const T*)(pk + L.k_Wp1), 256, 32};
+    typename LB::Params pb{Wf(L.Xp), ConvGeo{4, 4, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), F * L.P1,
+                           (uint32_t)((size_t)F * L.H * L.W * 4 * 4)};
     EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 192, 1, st)));
+    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 256, 1, st)));
   }
   {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
     using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
@@ -473,6 +476,44 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   return AAA_OK;
 }
 
+// conv2 dgrad (stride 2, k4, pad 2) as four parity-class 2x2 convs over dY2:
+// output pixel (2a+py, 2b+px) only receives taps ky = py + 2(1-ty), kx = px + 2(1-tx).
+template <typename T>
+static int conv2_dgrad(const Layout& L, const char* pk, const float* dy2, float* dy1, int frames, hipStream_t s) {
+  using C3 = Cfg32For<T>;
+  using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
+  using LB = LdIm2colB<float, T, C3::BJ, C3::BK, C3::NT>;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int py = cls >> 1, px = cls & 1;
+    const int Ha = (L.H1 - py + 1) / 2, Wa = (L.W1 - px + 1) / 2;
+    if (Ha <= 0 || Wa <= 0) continue;
+    const int rows = frames * Ha * Wa;
+    typename LA::Params pa{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32};
+    typename LB::Params pb{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
+                           (uint32_t)((size_t)frames * L.P * 64 * 4)};
+    EpiStoreParity ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
+                      ((1ull << 32) + Wa - 1) / Wa};
+    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows, 256, 1, s)));
+  }
+  return AAA_OK;
+}
+
+// conv1 weight gradient over RGBx frames (Cin 4; the 4th channel's grad is dropped on unpack)
+template <typename T>
+static int conv1_wgrad(const Layout& L, const float* dy1, const float* xp, int frames, float* gW, hipStream_t s) {
+  using C3 = Cfg32For<T>;
+  using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
+  using LB = LdIm2colTB<float, T, C3::BJ, C3::BK, C3::NT>;
+  const int rows1 = frames * L.P1;
+  typename LA::Params pa{dy1, 32, 32, rows1};
+  typename LB::Params pb{xp, ConvGeo{4, 4, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 256,
+                         (uint32_t)((size_t)frames * L.H * L.W * 4 * 4)};
+  EpiStore<true> ep{gW, 256, 32, 256};
+  const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
+  HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
+  return AAA_OK;
+}
+
 // ------------------------------------------------------------ backward ----
 template <typename T>
 static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st) {
@@ -486,7 +527,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   auto Wf = [&](size_t off) { return (float*)(ws + off); };
   auto Wt = [&](size_t off) { return (T*)(ws + off); };
   const int F = L.F, P = L.P, M = L.B * L.P;
-  using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
   using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
   using LTf = LdRowsT<float, float, CF::BI, CF::BK, NTF>;
   using LTfj = LdRowsT<float, float, CF::BJ, CF::BK, NTF>;
@@ -616,25 +656,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
       HIPCHK(colsum(dy2, 64, rows, 64, grads + L.poff[C1B], s));
     }
-    {  // conv2 dgrad (stride-2 transposed gather) -> dY1
-      using C3 = Cfg32For<T>;
-      using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
-      using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
-      typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
-      typename LB::Params pb{dy2, ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), rows1};
-      EpiStoreT<float> ep{dy1, 32, 32, rows1, nullptr, 0};
-      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows1, 1024, 1, s)));
-    }
-    {  // conv1 wgrad / bias (frames need no grad)
-      using C3 = Cfg32For<T>;
-      using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
-      using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
-      typename LA::Params pa{dy1, 32, 32, rows1};
-      typename LB::Params pb{io->frames + (size_t)lo * L.B * L.H * L.W * 3,
-                             ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
-      EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
-      const int tiles = cdiv(32, C3::BI) * cdiv(192, C3::BJ);
-      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
+    {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
+      int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, s);
+      if (!rc) rc = conv1_wgrad<T>(L, dy1, Wf(L.Xp) + (size_t)lo * L.B * L.H * L.W * 4, F1, Wf(L.gWp1), s);
+      if (rc) return rc;
       HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
     return AAA_OK;
@@ -716,7 +741,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
 
   if (phases & AAA_BWD_VISION) {
     if (!vision_here) {   // VISION alone: its chunk work over all frames, here
-      using C3 = Cfg32For<T>;
       const int rows = F * P, rows1 = F * L.P1;
       {
         using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
@@ -729,25 +753,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         HIPCHK(colsum(Wf(L.dY2), 64, rows, 64, grads + L.poff[C1B], st));
       }
       {
-        using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
-        using LB = LdIm2col<float, T, C3::BJ, C3::BK, C3::NT, true>;
-        typename LA::Params pa{(const T*)(pk + L.k_WdT2), 1024, 32};
-        typename LB::Params pb{Wf(L.dY2), ConvGeo{64, 64, 0, L.h, L.w, L.H1, L.W1, 4, 2, 2, 1}.prep(), rows1};
-        EpiStoreT<float> ep{Wf(L.dY1), 32, 32, rows1, nullptr, 0};
-        HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows1, 1024, 1, st)));
-      }
-      {
-        using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
-        using LB = LdIm2colT<float, T, C3::BJ, C3::BK, C3::NT, false>;
-        typename LA::Params pa{Wf(L.dY1), 32, 32, rows1};
-        typename LB::Params pb{io->frames, ConvGeo{3, 3, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 192};
-        EpiStore<true> ep{Wf(L.gWp1), 192, 32, 192};
-        HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 192, rows1, wgrad_splits(cdiv(192, C3::BJ), rows1, C3::BK), st)));
+        int rc = conv2_dgrad<T>(L, pk, Wf(L.dY2), Wf(L.dY1), F, st);
+        if (!rc) rc = conv1_wgrad<T>(L, Wf(L.dY1), Wf(L.Xp), F, Wf(L.gWp1), st);
+        if (rc) return rc;
         HIPCHK(colsum(Wf(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
     }
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
-    HIPCHK(unpack_conv(Wf(L.gWp1), 32, 3, 8, grads + L.poff[C0W], st));
+    HIPCHK(unpack_conv1_rgbx(Wf(L.gWp1), grads + L.poff[C0W], st));
   }
   return AAA_OK;
 }
@@ -763,7 +776,8 @@ static int conv_nhwc_impl(const aaa_conv_desc* d, const float* x, const float* w
   typename LA::Params pa{w, K, d->Cout};
   const ConvGeo g = ConvGeo{d->Cin, d->Cin, 0, d->Hin, d->Win, d->Hout, d->Wout, d->KW, d->stride, d->pad, 0}.prep();
   EpiStoreT<float> ep{y, d->Cout, d->Cout, M, bias, 0};
-  if (d->Cin % C::BK == 0) {   // the hot-path loaders (buffer descriptors, tap-uniform K tiles)
+  const int tpt = C::BK / std::max(1, d->Cin);
+  if (d->Cin % C::BK == 0 || (C::BK % d->Cin == 0 && (tpt % d->KW == 0 || d->KW % tpt == 0))) {   // hot-path loaders
     using LAB = LdRowsB<float, T, C::BI, C::BK, NT>;
     using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
     const uint32_t xb = (uint32_t)((size_t)d->N * d->Hin * d->Win * d->Cin * 4);
