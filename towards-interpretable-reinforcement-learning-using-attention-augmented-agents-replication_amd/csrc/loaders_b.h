@@ -143,12 +143,31 @@ struct LdIm2colB {
       const int mm = ok ? m : 0;
       const int f = (int)g.dHW.div(mm), pix = mm - f * hw;
       const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
-      uint64_t msk = 0;
-      for (int ky = 0; ky < KH; ++ky)
-        for (int kx = 0; kx < g.KW; ++kx) {
-          int iy, ix;
-          if (ok && conv_src(g, oy, ox, ky, kx, iy, ix)) msk |= 1ull << (ky * g.KW + kx);
+      // validity is separable: tap (ky,kx) is inside iff row ky and column kx are
+      uint32_t rowm = 0, colm = 0;
+      for (int k = 0; k < KH; ++k) {
+        const int ty = g.transposed ? oy + g.pad - k : oy * g.stride + k - g.pad;
+        bool v = ok;
+        if (g.transposed) {
+          v = v && ty >= 0 && (g.stride == 1 || ty % g.stride == 0) && ty / g.stride < g.Hin;
+        } else {
+          v = v && ty >= 0 && ty < g.Hin;
         }
+        if (v) rowm |= 1u << k;
+      }
+      for (int k = 0; k < g.KW; ++k) {
+        const int tx = g.transposed ? ox + g.pad - k : ox * g.stride + k - g.pad;
+        bool v = true;
+        if (g.transposed) {
+          v = tx >= 0 && (g.stride == 1 || tx % g.stride == 0) && tx / g.stride < g.Win;
+        } else {
+          v = tx >= 0 && tx < g.Win;
+        }
+        if (v) colm |= 1u << k;
+      }
+      uint64_t msk = 0;
+      for (int k = 0; k < KH; ++k)
+        if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
       vmask[c] = msk;
       const int d = g.Cin >= BK ? 0 : kc / g.Cin;       // taps inside the tile before this chunk
       const int ci = kc - d * g.Cin;

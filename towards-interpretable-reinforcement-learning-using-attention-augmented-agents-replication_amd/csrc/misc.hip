@@ -16,48 +16,6 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Block-wide matrix-vector helpers (x and y in LDS).
-// rows:  y[o] = sum_k W[o*ldw + k] x[k]   -- one wave per row, lanes over k (coalesced)
-__device__ void gemv_rows(const float* __restrict__ W, int ldw, const float* x, int N, int K, float* y) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int o = wave; o < N; o += nw) {
-    float s = 0.f;
-    for (int k = lane; k < K; k += 64) s += W[(size_t)o * ldw + k] * x[k];
-    s = wave_sum(s);
-    if (lane == 0) y[o] = s;
-  }
-}
-// cols:  y[k] = sum_o W[o*ldw + k] x[o]   -- lanes over k (all K/64 column
-// groups of a row loaded together for memory-level parallelism), waves split
-// o, LDS reduce.  K <= 64*MAXJ.
-template <int MAXJ>
-__device__ void gemv_cols(const float* __restrict__ W, int ldw, const float* x, int N, int K, float* y,
-                          float* scratch /* nwaves*64*MAXJ */) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float s[MAXJ];
-#pragma unroll
-  for (int j = 0; j < MAXJ; ++j) s[j] = 0.f;
-#pragma unroll 2
-  for (int o = wave; o < N; o += nw) {
-    const float xo = x[o];
-#pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-      const int k = lane + 64 * j;
-      if (k < K) s[j] += W[(size_t)o * ldw + k] * xo;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < MAXJ; ++j) scratch[(wave * MAXJ + j) * 64 + lane] = s[j];
-  __syncthreads();
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    const int j = k >> 6, l = k & 63;
-    float t = 0.f;
-    for (int w = 0; w < nw; ++w) t += scratch[(w * MAXJ + j) * 64 + l];
-    y[k] = t;
-  }
-  __syncthreads();
-}
-
 // y[k] += sum over this workgroup's rows o of W[o*ldw + k] x[o]  (multi-WG, atomics)
 __global__ void k_gemv_cols_atomic(const float* __restrict__ W, int ldw, const float* __restrict__ x, int N, int K,
                                    int rows_per, float* y) {
@@ -74,29 +32,35 @@ __global__ void k_gemv_cols_atomic(const float* __restrict__ W, int ldw, const f
 // QueryNetwork on the always-zero prev_output (attention.py:184-198, 325-331;
 // Q1): q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4.  Also the basis
 // half of the attention logits, SQ[p][q] = sum_c S[p][c] * Q[q][8 + c].
-__global__ void __launch_bounds__(1024)
-k_query_fwd(const float* __restrict__ b0, const float* __restrict__ W2, const float* __restrict__ b2,
-            const float* __restrict__ W4, const float* __restrict__ b4, const float* __restrict__ S, int P,
-            int nq, float* q1, float* q2, float* Q, float* SQ) {
-  __shared__ float s1[128], s2[576], sq[576];
-  const int qd = 72 * nq, tid = threadIdx.x;
-  for (int o = tid; o < 128; o += blockDim.x) { float v = fmaxf(b0[o], 0.f); s1[o] = v; q1[o] = v; }
-  __syncthreads();
-  gemv_rows(W2, 128, s1, qd, 128, s2);
-  __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) { float v = fmaxf(s2[o] + b2[o], 0.f); s2[o] = v; q2[o] = v; }
-  __syncthreads();
-  gemv_rows(W4, qd, s2, qd, qd, sq);
-  __syncthreads();
-  for (int o = tid; o < qd; o += blockDim.x) { float v = sq[o] + b4[o]; sq[o] = v; Q[o] = v; }
-  __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  for (int p = wave; p < P; p += nw) {          // one wave per grid position, lanes over the 64 basis channels
-    const float sv = S[p * 64 + lane];
-    for (int q = 0; q < nq; ++q) {
-      const float acc = wave_sum(sv * sq[q * 72 + 8 + lane]);
-      if (lane == 0) SQ[p * nq + q] = acc;
-    }
+// One wave per output row, 4 rows per workgroup, so the weight rows stream in
+// from many CUs at once (a single workgroup was latency-bound at ~80 us):
+// y[o] = act(sum_k W[o][k] act_in(x[k]) + b[o]).  xcopy (optional) <- act_in(x).
+__global__ void __launch_bounds__(256)
+k_query_layer(const float* __restrict__ W, int K, const float* __restrict__ x, int relu_in,
+              const float* __restrict__ b, int relu_out, int N, float* __restrict__ y, float* __restrict__ xcopy) {
+  const int lane = threadIdx.x & 63, o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (xcopy && blockIdx.x == 0)
+    for (int k = threadIdx.x; k < K; k += 256) xcopy[k] = relu_in ? fmaxf(x[k], 0.f) : x[k];
+  if (o >= N) return;
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float xk = relu_in ? fmaxf(x[k], 0.f) : x[k];
+    s += W[(size_t)o * K + k] * xk;
+  }
+  s = wave_sum(s) + b[o];
+  if (lane == 0) y[o] = relu_out ? fmaxf(s, 0.f) : s;
+}
+
+// Basis half of the attention logits, SQ[p][q] = sum_c S[p][c] * Q[q][8 + c]:
+// one wave per grid position, lanes over the 64 basis channels.
+__global__ void __launch_bounds__(256)
+k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int nq, float* __restrict__ SQ) {
+  const int lane = threadIdx.x & 63, p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const float sv = S[p * 64 + lane];
+  for (int q = 0; q < nq; ++q) {
+    const float acc = wave_sum(sv * Q[q * 72 + 8 + lane]);
+    if (lane == 0) SQ[p * nq + q] = acc;
   }
 }
 
@@ -246,25 +210,37 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
 // Backward of the query MLP (one workgroup of 1024 threads).  dQ = sum over
 // frames of the logits-path grads + the answer-path grad, which summed over
 // rows is W1[:, Q-cols]^T . db1.
+// y[k] = (mask[k] > 0) * sum_o W[o][k] x[o]  for W [N][K]: lanes over 64
+// columns, 16 waves split the rows, LDS reduce.  grid ceil(K/64), 1024 threads.
 __global__ void __launch_bounds__(1024)
-k_query_bwd(const float* __restrict__ dQs, const float* __restrict__ gb1, const float* __restrict__ W1,
-            int ans_in, int nq, const float* __restrict__ W2, const float* __restrict__ W4,
-            const float* __restrict__ q1, const float* __restrict__ q2, float* gW4, float* gb4, float* gW2,
-            float* gb2, float* gb0) {
-  __shared__ float dQ[576], dq2[576], s2[576], s1[128], dq1[128], scratch[16 * 64 * 9];
-  const int qd = 72 * nq, tid = threadIdx.x;
-  (void)gb1; (void)W1; (void)ans_in;
-  for (int i = tid; i < qd; i += blockDim.x) s2[i] = q2[i];
-  for (int i = tid; i < 128; i += blockDim.x) s1[i] = q1[i];
-  for (int o = tid; o < qd; o += blockDim.x) { dQ[o] = dQs[o]; gb4[o] = dQs[o]; }   // dQs already holds W1_Q^T db1
+k_query_colgemv(const float* __restrict__ W, int N, int K, const float* __restrict__ x,
+                const float* __restrict__ mask, float* __restrict__ y) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6, k = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (k < K) {
+#pragma unroll 4
+    for (int o = g; o < N; o += 16) s += W[(size_t)o * K + k] * x[o];
+  }
+  red[g][lane] = s;
   __syncthreads();
-  for (int i = tid; i < qd * qd; i += blockDim.x) gW4[i] = dQ[i / qd] * s2[i - (i / qd) * qd];
-  gemv_cols<9>(W4, qd, dQ, qd, qd, dq2, scratch);
-  for (int k = tid; k < qd; k += blockDim.x) { if (!(s2[k] > 0.f)) dq2[k] = 0.f; gb2[k] = dq2[k]; }
-  __syncthreads();
-  for (int i = tid; i < qd * 128; i += blockDim.x) gW2[i] = dq2[i >> 7] * s1[i & 127];
-  gemv_cols<2>(W2, 128, dq2, qd, 128, dq1, scratch);
-  for (int j = tid; j < 128; j += blockDim.x) gb0[j] = s1[j] > 0.f ? dq1[j] : 0.f;
+  if (g == 0 && k < K) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    y[k] = mask[k] > 0.f ? t : 0.f;
+  }
+}
+
+// out[o][k] = a[o] * b[k] (weight grad of a rank-1 layer), acopy <- a (bias grad).
+__global__ void k_query_outer(const float* __restrict__ a, int N, const float* __restrict__ b, int K,
+                              float* __restrict__ out, float* acopy) {
+  const int n = N * K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int o = i / K;
+    out[i] = a[o] * b[i - o * K];
+    if (acopy && i < N) acopy[i] = a[i];
+  }
 }
 
 // out[n] += sum_{m} X[m*ld + n]; grid (ceil(N/64), nsplit), 256 threads.
@@ -573,7 +549,13 @@ static inline int nblk(long n, int bs = 256) {
 
 hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
                      const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st) {
-  hipLaunchKernelGGL(k_query_fwd, dim3(1), dim3(1024), 0, st, b0, W2, b2, W4, b4, S, P, nq, q1, q2, Q, SQ);
+  // QueryNetwork on the always-zero prev_output (attention.py:184-198, 325-331; Q1):
+  // q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4.
+  const int qd = 72 * nq;
+  hipLaunchKernelGGL(k_query_layer, dim3((qd + 3) / 4), dim3(256), 0, st, W2, 128, b0, 1, b2, 1, qd, q2, q1);
+  hipLaunchKernelGGL(k_query_layer, dim3((qd + 3) / 4), dim3(256), 0, st, W4, qd, q2, 0, b4, 0, qd, Q,
+                     (float*)nullptr);
+  hipLaunchKernelGGL(k_query_sq, dim3((P + 3) / 4), dim3(256), 0, st, S, Q, P, nq, SQ);
   return hipGetLastError();
 }
 
@@ -601,8 +583,16 @@ hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int an
   // dQ += W1[:, Q-cols]^T . db1 (the answer path summed over rows), 512 rows over 32 WGs
   hipLaunchKernelGGL(k_gemv_cols_atomic, dim3(32), dim3(256), 0, st, W1 + nq * 184, ans_in, gb1, 512, 72 * nq, 16,
                      const_cast<float*>(dQs));
-  hipLaunchKernelGGL(k_query_bwd, dim3(1), dim3(1024), 0, st, dQs, gb1, W1, ans_in, nq, W2, W4, q1, q2, gW4, gb4,
-                     gW2, gb2, gb0);
+  // Back through Q = W4 q2 + b4, q2 = relu(W2 q1 + b2), q1 = relu(b0).  The
+  // pre-ReLU masks are q2 > 0 and q1 > 0; gb2 = dq2 and gb0 = dq1 are written
+  // straight into the grad buffer (gb2 doubles as dq2 for the next layer).
+  const int qd = 72 * nq;
+  (void)W1; (void)ans_in;
+  hipLaunchKernelGGL(k_query_colgemv, dim3((qd + 63) / 64), dim3(1024), 0, st, W4, qd, qd, dQs, q2, gb2);
+  hipLaunchKernelGGL(k_query_outer, dim3(nblk((long)qd * qd)), dim3(256), 0, st, dQs, qd, q2, qd, gW4, gb4);
+  hipLaunchKernelGGL(k_query_colgemv, dim3(2), dim3(1024), 0, st, W2, qd, 128, gb2, q1, gb0);
+  hipLaunchKernelGGL(k_query_outer, dim3(nblk((long)qd * 128)), dim3(256), 0, st, gb2, qd, q1, 128, gW2,
+                     (float*)nullptr);
   return hipGetLastError();
 }
 

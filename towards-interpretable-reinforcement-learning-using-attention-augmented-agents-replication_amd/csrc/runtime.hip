@@ -281,16 +281,25 @@ using CF32 = GemmCfg<float, 32, 64, 32, 1, 2>;    // 32-row tile, 2 waves: small
 using CFW = GemmCfg<float, 128, 128, 32, 2, 2>;   // long-K weight gradients: 64x64 per wave
 using CFK = GemmCfg<float, 32, 64, 64, 1, 2, 2>;  // per-step ConvLSTM kernels: 2-way split-K in the WG
 using CFK4 = GemmCfg<float, 32, 64, 64, 1, 2, 4>; // 4-way split-K (8 waves)
+using CFK4B = GemmCfg<float, 32, 64, 128, 1, 2, 4>; // 4-way split-K, 2 k-steps per wave per barrier
+using CF64 = GemmCfg<float, 64, 64, 64, 2, 2>;     // 64x64, BK 64
+using CFJ = GemmCfg<float, 64, 128, 32, 2, 2>;     // 64-row GEMMs with long N (batched dx)
 using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;
 using CB32 = GemmCfg<__bf16, 32, 64, 64, 1, 2>;
 using CBW = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
 using CBK = GemmCfg<__bf16, 32, 64, 64, 1, 2, 2>;
 using CBK4 = GemmCfg<__bf16, 32, 64, 64, 1, 2, 4>;
+using CBK4B = GemmCfg<__bf16, 32, 64, 128, 1, 2, 4>;
+using CB64 = GemmCfg<__bf16, 64, 64, 128, 2, 2>;
+using CBJ = GemmCfg<__bf16, 64, 128, 64, 2, 2>;
 template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
 template <typename T> using Cfg32For = std::conditional_t<std::is_same<T, float>::value, CF32, CB32>;
 template <typename T> using CfgWFor = std::conditional_t<std::is_same<T, float>::value, CFW, CBW>;
 template <typename T> using CfgKFor = std::conditional_t<std::is_same<T, float>::value, CFK, CBK>;
 template <typename T> using CfgK4For = std::conditional_t<std::is_same<T, float>::value, CFK4, CBK4>;
+template <typename T> using CfgK4BFor = std::conditional_t<std::is_same<T, float>::value, CFK4B, CBK4B>;
+template <typename T> using Cfg64For = std::conditional_t<std::is_same<T, float>::value, CF64, CB64>;
+template <typename T> using CfgJFor = std::conditional_t<std::is_same<T, float>::value, CFJ, CBJ>;
 
 // Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE: 0 = 64x64,
 // 1 = 32x64 with 2-way in-WG split-K, 2 = 4-way; default picks by how many
@@ -306,7 +315,7 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 static int step_tile(long out_tiles32, const char* env) {
   const int v = env_int(env, -1);
   if (v >= 0) return v;
-  if (out_tiles32 < 1024) return 2;
+  if (out_tiles32 < 1024) return 3;   // 4-way in-WG split-K, BK 128 (measured best for the BPTT step)
   return out_tiles32 < 1536 ? 1 : 0;   // measured on C2: forward step (1936 tiles) best at 64x64
 }
 
@@ -388,12 +397,13 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   hipStream_t xs = ax ? ax : st;
   if (ax) HIPCHK(stream_order(st, ax));
   auto xpart = [&](int lo, int hi) -> int {
-    using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-    using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
+    using CX = CfgFor<T>;   // 64x64: measured faster than 128x128 here (K is only 576)
+    using LA = LdRowsB<T, T, CX::BI, CX::BK, CX::NT>;
+    using LB = LdIm2colB<T, T, CX::BJ, CX::BK, CX::NT>;
     const ConvGeo g = ConvGeo{64, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const int rows = (hi - lo) * M;
     EpiStoreT<float> ep{Wf(L.Gt) + (size_t)lo * M * 512, 512, 512, rows, (const float*)(pk + L.k_bl), 0};
-    HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpX), 576, 512},
+    HIPCHK((launch_gemm<CX, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpX), 576, 512},
                                    typename LB::Params{Wt(L.XH) + (size_t)lo * M * 192, g, rows,
                                                        (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)},
                                    ep, 512, rows, 576, 1, xs)));
@@ -407,7 +417,8 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     if (rc) return rc;
     if (ax) HIPCHK(record_event(ax, &xev[k]));
   }
-  const bool fwd_k = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE") >= 1;
+  const int fwd_tile = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE");
+  const bool fwd_k = fwd_tile == 1 || fwd_tile == 2;
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);  // one step slice of XH
   for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126): h-part only
     if (ax && t % cs == 0) HIPCHK(hipStreamWaitEvent(st, xev[t / cs], 0));   // x-part of steps [t, t+cs) done
@@ -421,7 +432,14 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                          Wf(L.Gt) + (size_t)t * M * 512, M};
     const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     TimerScope tim(AAA_TIMER_FWD_STEP, st);
-    if (fwd_k) {
+    if (fwd_tile == 3) {
+      using CK = Cfg64For<T>;
+      using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+      using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
+      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
+                                      typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
+                                      1152, 1, st)));
+    } else if (fwd_k) {
       using CK = CfgKFor<T>;
       using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
       using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
@@ -633,13 +651,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     HIPCHK(colsum(dz, 512, rows, 512, Wf(L.gbl), s));
     {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
-      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
+      using CJ = CfgFor<T>;   // 64x64: measured faster than 64x128 (occupancy)
+      using LA = LdRowsB<T, T, CJ::BI, CJ::BK, CJ::NT>;
+      using LB = LdIm2colB<float, T, CJ::BJ, CJ::BK, CJ::NT>;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
-      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
-                                     typename LB::Params{dz, g, rows, (uint32_t)((size_t)rows * 512 * 4)}, ep, 64, rows,
-                                     4608, 1, s)));
+      HIPCHK((launch_gemm<CJ, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
+                                      typename LB::Params{dz, g, rows, (uint32_t)((size_t)rows * 512 * 4)}, ep, 64,
+                                      rows, 4608, 1, s)));
     }
     if (!vision_here) return AAA_OK;
     const float* dy2 = Wf(L.dY2) + (size_t)lo * M * 64;
@@ -708,7 +727,13 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                         prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64};
       const float* dzt = Wf(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
-      if (bwd_tile == 2) {
+      if (bwd_tile == 3) {
+        using CK = CfgK4BFor<T>;
+        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
+        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
+                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
+      } else if (bwd_tile == 2) {
         using CK = CfgK4For<T>;
         using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
         using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
