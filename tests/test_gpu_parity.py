@@ -74,6 +74,22 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL)
 
 
+# Every per-step tile variant of the ConvLSTM forward / BPTT GEMMs (runtime.hip
+# step_tile: 0 64x64, 1/2 split-K, 3 BK=128 split-K, 4-6 the LDS-DMA ring of
+# glds.h) must give the same answer; B=5 makes B*P = 605 pixels (ragged tiles).
+@pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6)])
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
+    monkeypatch.setenv("AAA_STEP_TILE", str(fwd))
+    monkeypatch.setenv("AAA_BPTT_TILE", str(bwd))
+    T, B = 3, 5
+    if conv_dtype == "fp32":
+        _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"tiles {fwd}/{bwd}: ")
+    else:
+        ref = _oracle(T, B, conv_mode="bf16")
+        _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), ref, 2e-2, f"bf16 tiles {fwd}/{bwd}: ")
+
+
 def test_c1_against_reference_fixture(cuda, golden):
     """Config 1 (B=1, T=20) against the fixture made by the reference itself."""
     g = golden("G3")

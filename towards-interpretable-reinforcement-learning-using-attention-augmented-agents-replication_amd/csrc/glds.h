@@ -1,0 +1,282 @@
+// LDS-DMA pipelined variant of the MFMA GEMM for k-contiguous operands.
+//
+// Operands go global -> LDS with `buffer_load_dwordx4 ... lds` (no VGPR
+// staging, no ds_write pass).  NBUF LDS stages form a ring: at K tile kt the
+// waves wait (counted vmcnt) until their own DMA for tile kt has landed,
+// barrier, re-issue the DMA for tile kt+NBUF-1 into the stage that every wave
+// finished reading before that barrier, then run the MFMAs of tile kt.  With
+// NBUF = 3 one tile stays in flight across every barrier, so a tile's global
+// latency is covered by two tiles of MFMA work instead of one.
+//
+// LDS image: one DMA wave-instruction writes 64 lanes x 16 B contiguously, so
+// the image is lane-linear: 16-B slot s of the stage holds chunk s, i.e. row
+// s / RS, physical column s % RS (RS = 16-B slots per row).  The XOR swizzle
+// that makes the fragment reads (ds_read_b128 over 32 rows at one logical
+// column) bank-conflict-free is applied on the SOURCE side: physical slot pc
+// of row r holds logical column pc ^ lds_swz(r), and the reader applies the
+// same XOR.  Masked lanes (conv zero padding, rows past the end) read through
+// the buffer descriptor's range check and land as zeros.
+//
+// Preconditions (host-checked): G == T (no conversion while staging), each
+// loader's chunk count is a multiple of the thread count (every wave issues
+// the same number of DMA instructions per tile, which the counted vmcnt
+// relies on), and the K slice is a multiple of BK.
+#pragma once
+#include "loaders_b.h"
+
+namespace aaa {
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+
+// 16-B slot XOR for a row of RS slots: rows that share a 256-B bank line
+// (16/RS of them) keep their natural offset; successive lines rotate.
+template <int RS>
+__device__ __forceinline__ int lds_swz(int row) {
+  constexpr int RPL = RS >= 16 ? 1 : 16 / RS;
+  return (row / RPL) & (RS - 1);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Barrier that does NOT drain the VM counter (an LDS-DMA in flight survives it).
+__device__ __forceinline__ void barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Plain rows (weights): element (row, k) at src[row*ld + k].
+template <typename T, int R, int BK, int NT>
+struct GRowsB {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(T);
+  static constexpr int RS = BK / VG;
+  static constexpr int NCH = R * RS;
+  static constexpr int PER = NCH / NT;
+  static constexpr int ELEMS = R * BK;
+  static_assert(NCH % NT == 0, "every wave must issue the same number of DMA pieces");
+  struct Params { const T* src; int ld; int nrows; };
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t voff[PER];
+  int wofs;
+  __device__ __forceinline__ GRowsB(const Params& p, int row0) {
+    rs = make_rsrc(p.src, (uint32_t)((size_t)p.nrows * p.ld * sizeof(T)));
+    wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      const int lr = ch / RS, lc = (ch % RS) ^ lds_swz<RS>(lr), row = row0 + lr;
+      voff[c] = row < p.nrows ? (uint32_t)((row * p.ld + lc * VG) * (int)sizeof(T)) : kOOB;
+    }
+  }
+  __device__ __forceinline__ void issue(T* lds, int k0) const {
+    const uint32_t ko = (uint32_t)(k0 * (int)sizeof(T));
+#pragma unroll
+    for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, voff[c] + ko);
+  }
+};
+
+// Implicit-GEMM gather (rows = output pixels, k = (tap, ci)); same geometry
+// rules as LdIm2colB, whose per-pixel setup it shares.
+template <typename T, int R, int BK, int NT>
+struct GIm2colB {
+  static constexpr bool KC = true;
+  static constexpr int VG = 16 / (int)sizeof(T);
+  static constexpr int RS = BK / VG;
+  static constexpr int NCH = R * RS;
+  static constexpr int PER = NCH / NT;
+  static constexpr int ELEMS = R * BK;
+  static_assert(NCH % NT == 0, "every wave must issue the same number of DMA pieces");
+  struct Params { const T* src; ConvGeo g; int nrows; uint32_t src_bytes; };
+  __amdgpu_buffer_rsrc_t rs;
+  ConvGeo g;
+  int base[PER], dt[PER];
+  uint64_t vmask[PER];
+  int wofs;
+  __device__ static bool ok_shape(const ConvGeo& g) { return LdIm2colB<T, T, R, BK, NT>::ok_shape(g); }
+  __device__ __forceinline__ GIm2colB(const Params& p, int row0) : g(p.g) {
+    rs = make_rsrc(p.src, p.src_bytes);
+    wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      const int lr = ch / RS, kc = ((ch % RS) ^ lds_swz<RS>(lr)) * VG, m = row0 + lr;
+      im2col_setup(g, BK, m < p.nrows, m, kc, base[c], dt[c], vmask[c]);
+    }
+  }
+  __device__ __forceinline__ void issue(T* lds, int k0) const {
+    const int tap = __builtin_amdgcn_readfirstlane((int)g.dCin.div(k0));
+    const int ci0 = k0 - tap * g.Cin;
+    const int ky = __builtin_amdgcn_readfirstlane((int)g.dKW.div(tap));
+    const int kx = tap - ky * g.KW;
+    const int toff = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs + ci0;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const bool v = (vmask[c] >> (tap + dt[c])) & 1ull;
+      dma16(rs, lds + c * NT * VG + wofs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(T)) : kOOB);
+    }
+  }
+};
+
+// Fragment of 8 consecutive logical k at row r from a swizzled KC stage.
+template <int BK>
+__device__ __forceinline__ void frag_sw(const float* t, int r, int kofs, float (&a)[8]) {
+  constexpr int RS = BK / 4;
+  const int g = lds_swz<RS>(r), c0 = kofs >> 2;
+  const f32x4 x = *reinterpret_cast<const f32x4*>(t + r * BK + ((c0 ^ g) << 2));
+  const f32x4 y = *reinterpret_cast<const f32x4*>(t + r * BK + (((c0 + 1) ^ g) << 2));
+  a[0] = x[0]; a[1] = x[1]; a[2] = x[2]; a[3] = x[3];
+  a[4] = y[0]; a[5] = y[1]; a[6] = y[2]; a[7] = y[3];
+}
+template <int BK>
+__device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
+  constexpr int RS = BK / 8;
+  const int g = lds_swz<RS>(r);
+  return *reinterpret_cast<const bf16x8*>(t + r * BK + (((kofs >> 3) ^ g) << 3));
+}
+
+template <class C, class LA, class LB, class EP, int NBUF>
+__global__ void __launch_bounds__(C::NT)
+gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk) {
+  using T = typename C::type;
+  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
+  constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
+  static_assert(MI >= 1 && MJ >= 1 && BK % (16 * WK) == 0, "tile shape");
+  static_assert(NBUF >= 2, "ring depth");
+  constexpr int AEL = LA::ELEMS, STG = LA::ELEMS + LB::ELEMS;
+  constexpr int PIECES = LA::PER + LB::PER;   // DMA instructions per wave per K tile
+  // ONE shared array for everything (a second __shared__ object can make the
+  // compiler drain vmcnt before the fragment reads).
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * STG];
+
+  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
+  const int kb = blockIdx.z * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+
+  LA la(pa, i0);
+  LB lb(pb, j0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wk = wave / (WI * WJ), wr = wave - wk * (WI * WJ);
+  const int wi = wr / WJ, wj = wr - (wr / WJ) * WJ;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[MI][MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nk = (ke - kb) / BK;
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nk) {
+      la.issue(smem + s * STG, kb + s * BK);
+      lb.issue(smem + s * STG + AEL, kb + s * BK);
+    }
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt is the oldest of the (up to NBUF-1) tiles in flight
+    if (kt + NBUF - 2 < nk) wait_vmcnt<PIECES * (NBUF - 2)>();
+    else wait_vmcnt<0>();
+    barrier_lds();
+    if (kt + NBUF - 1 < nk) {
+      T* st = smem + ((kt + NBUF - 1) % NBUF) * STG;
+      la.issue(st, kb + (kt + NBUF - 1) * BK);
+      lb.issue(st + AEL, kb + (kt + NBUF - 1) * BK);
+    }
+    const T* Ac = smem + (kt % NBUF) * STG;
+    const T* Bc = Ac + AEL;
+#pragma unroll
+    for (int s2 = 0; s2 < BK / 16 / WK; ++s2) {
+      const int kofs = 16 * (s2 * WK + wk) + 8 * h;
+      if constexpr (is_f32<T>::value) {
+        float af[MI][8], bfr[MJ][8];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+          for (int a = 0; a < MI; ++a)
+#pragma unroll
+            for (int b = 0; b < MJ; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+      } else {
+        bf16x8 af[MI], bfr[MJ];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) af[a] = frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) bfr[b] = frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
+#pragma unroll
+        for (int a = 0; a < MI; ++a)
+#pragma unroll
+          for (int b = 0; b < MJ; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  }
+
+  if constexpr (WK > 1) {
+    constexpr int RED = (WK - 1) * WI * WJ * MI * MJ * 16 * 64;
+    static_assert(RED * sizeof(float) <= sizeof(smem), "split-K reduction does not fit in LDS");
+    float* red = reinterpret_cast<float*>(smem);
+    barrier_lds();   // every wave is done reading the last stage (all DMA retired: vmcnt(0) above)
+    if (wk > 0) {
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            red[((((wk - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane] = acc[a][b][e];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll
+    for (int w = 1; w < WK; ++w)
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            acc[a][b][e] += red[((((w - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane];
+  }
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = i0 + wi * WTI + a * 32 + 8 * g + 4 * h;
+        const int j = j0 + wj * WTJ + b * 32 + r32;
+        ep(i, j, acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+      }
+}
+
+template <class C, class LA, class LB, class EP, int NBUF = 3>
+inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep, int Mi,
+                              int Nj, int K, int nsplit, hipStream_t st) {
+  if (Mi <= 0 || Nj <= 0 || K <= 0) return hipSuccess;
+  if (K % C::BK) return hipErrorInvalidValue;
+  if (nsplit < 1) nsplit = 1;
+  int kchunk = (K + nsplit - 1) / nsplit;
+  kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
+  hipLaunchKernelGGL((gemm_pipe_kernel<C, LA, LB, EP, NBUF>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk);
+  return hipGetLastError();
+}
+
+}  // namespace aaa

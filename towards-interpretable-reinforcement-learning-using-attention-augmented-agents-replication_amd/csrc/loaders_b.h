@@ -102,6 +102,53 @@ struct LdRowsTB {
   }
 };
 
+// Per-(pixel row m, chunk column kc) constants of the implicit-GEMM gather:
+// the element offset of the chunk's source at the K tile's first tap (base),
+// the chunk's tap relative to that first tap (dt; BK % Cin == 0 tiles), and
+// the pixel's valid-tap bitmask (validity is separable: tap (ky,kx) is inside
+// iff row ky and column kx are).  ok = false gives an all-invalid mask.
+__device__ __forceinline__ void im2col_setup(const ConvGeo& g, int BK, bool ok, int m, int kc, int& base, int& dt,
+                                             uint64_t& vmask) {
+  const int hw = g.Hout * g.Wout;
+  const int KH = g.KW;  // square kernels
+  const int sgn = g.transposed ? -1 : 1;
+  const int mm = ok ? m : 0;
+  const int f = (int)g.dHW.div(mm), pix = mm - f * hw;
+  const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
+  uint32_t rowm = 0, colm = 0;
+  for (int k = 0; k < KH; ++k) {
+    const int ty = g.transposed ? oy + g.pad - k : oy * g.stride + k - g.pad;
+    bool v = ok;
+    if (g.transposed) {
+      v = v && ty >= 0 && (g.stride == 1 || ty % g.stride == 0) && ty / g.stride < g.Hin;
+    } else {
+      v = v && ty >= 0 && ty < g.Hin;
+    }
+    if (v) rowm |= 1u << k;
+  }
+  for (int k = 0; k < g.KW; ++k) {
+    const int tx = g.transposed ? ox + g.pad - k : ox * g.stride + k - g.pad;
+    bool v = true;
+    if (g.transposed) {
+      v = tx >= 0 && (g.stride == 1 || tx % g.stride == 0) && tx / g.stride < g.Win;
+    } else {
+      v = tx >= 0 && tx < g.Win;
+    }
+    if (v) colm |= 1u << k;
+  }
+  uint64_t msk = 0;
+  for (int k = 0; k < KH; ++k)
+    if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
+  vmask = msk;
+  const int d = g.Cin >= BK ? 0 : kc / g.Cin;       // taps inside the tile before this chunk
+  const int ci = kc - d * g.Cin;
+  dt = d;
+  const int dky = d / g.KW, dkx = d - dky * g.KW;
+  const int oy0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;
+  const int ox0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
+  base = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + ci + sgn * (dky * g.Win + dkx) * g.cs;
+}
+
 // Implicit-GEMM gather, rows = output pixels, k = (tap, ci).  Either Cin % BK
 // == 0 (a K tile lies inside one tap: the tap is wave-uniform) or BK % Cin == 0
 // with the tile's BK/Cin taps forming whole kernel rows or part of one row (the
@@ -131,51 +178,12 @@ struct LdIm2colB {
   }
   __device__ __forceinline__ LdIm2colB(const Params& p, int row0) : g(p.g) {
     rs = make_rsrc(p.src, p.src_bytes);
-    const int hw = g.Hout * g.Wout;
-    const int KH = g.KW;  // square kernels
-    const int sgn = g.transposed ? -1 : 1;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const int ch = threadIdx.x + c * NT;
       act[c] = ch < NCH;
       const int lr = ch / CPR, kc = (ch % CPR) * VG, m = row0 + lr;
-      const bool ok = act[c] && m < p.nrows;
-      const int mm = ok ? m : 0;
-      const int f = (int)g.dHW.div(mm), pix = mm - f * hw;
-      const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
-      // validity is separable: tap (ky,kx) is inside iff row ky and column kx are
-      uint32_t rowm = 0, colm = 0;
-      for (int k = 0; k < KH; ++k) {
-        const int ty = g.transposed ? oy + g.pad - k : oy * g.stride + k - g.pad;
-        bool v = ok;
-        if (g.transposed) {
-          v = v && ty >= 0 && (g.stride == 1 || ty % g.stride == 0) && ty / g.stride < g.Hin;
-        } else {
-          v = v && ty >= 0 && ty < g.Hin;
-        }
-        if (v) rowm |= 1u << k;
-      }
-      for (int k = 0; k < g.KW; ++k) {
-        const int tx = g.transposed ? ox + g.pad - k : ox * g.stride + k - g.pad;
-        bool v = true;
-        if (g.transposed) {
-          v = tx >= 0 && (g.stride == 1 || tx % g.stride == 0) && tx / g.stride < g.Win;
-        } else {
-          v = tx >= 0 && tx < g.Win;
-        }
-        if (v) colm |= 1u << k;
-      }
-      uint64_t msk = 0;
-      for (int k = 0; k < KH; ++k)
-        if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
-      vmask[c] = msk;
-      const int d = g.Cin >= BK ? 0 : kc / g.Cin;       // taps inside the tile before this chunk
-      const int ci = kc - d * g.Cin;
-      dt[c] = d;
-      const int dky = d / g.KW, dkx = d - dky * g.KW;
-      const int oy0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;
-      const int ox0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
-      base[c] = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + ci + sgn * (dky * g.Win + dkx) * g.cs;
+      im2col_setup(g, BK, act[c] && m < p.nrows, m, kc, base[c], dt[c], vmask[c]);
       ldo[c] = Tile<T, R, BK, true>::off(lr, kc);
     }
   }

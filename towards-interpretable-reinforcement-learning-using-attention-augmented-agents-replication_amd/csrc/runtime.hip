@@ -26,6 +26,7 @@
 #include "epilogues.h"
 #include "gemm.h"
 #include "loaders_b.h"
+#include "glds.h"
 #include "misc.h"
 
 namespace aaa {
@@ -301,9 +302,12 @@ template <typename T> using CfgK4BFor = std::conditional_t<std::is_same<T, float
 template <typename T> using Cfg64For = std::conditional_t<std::is_same<T, float>::value, CF64, CB64>;
 template <typename T> using CfgJFor = std::conditional_t<std::is_same<T, float>::value, CFJ, CBJ>;
 
-// Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE: 0 = 64x64,
-// 1 = 32x64 with 2-way in-WG split-K, 2 = 4-way; default picks by how many
-// 32x32 output tiles the step has, i.e. how many waves it can feed).
+// Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE override):
+//   0 64x64 BK32 | 1 32x64 BK64 2-way in-WG split-K | 2 ... 4-way | 3 32x64 BK128 4-way
+//   (forward: 3 = 64x64 BK64) | 4-6 the same shapes on the LDS-DMA ring of glds.h
+//   (forward 4 = 64x64, 5 = 32x64 split-K, 6 = 64x64 BK64; BPTT 4 = 32x64 BK128
+//   4-way, 5 = BK64 4-way, 6 = 64x64).  The default picks by how many 32x32
+//   output tiles the step has, i.e. how many waves it can feed; measured on C2.
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
@@ -312,11 +316,30 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
   const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : T);
   return std::max(1, std::min(c, T));
 }
-static int step_tile(long out_tiles32, const char* env) {
+static int step_tile(long out_tiles32, const char* env, bool bptt) {
   const int v = env_int(env, -1);
   if (v >= 0) return v;
-  if (out_tiles32 < 1024) return 3;   // 4-way in-WG split-K, BK 128 (measured best for the BPTT step)
-  return out_tiles32 < 1536 ? 1 : 0;   // measured on C2: forward step (1936 tiles) best at 64x64
+  if (bptt) return out_tiles32 < 1024 ? 4 : (out_tiles32 < 1536 ? 1 : 0);   // C2: 484 tiles, 66 us (reg 71)
+  return out_tiles32 < 1024 ? 5 : 4;                                          // C2: 1936 tiles, 56 us (reg 58)
+}
+
+// One per-step ConvLSTM GEMM: D[Mi][M] = W[Mi][K] x im2col(src)[K][M] with
+// epilogue ep.  PIPE = LDS-DMA ring (glds.h; needs src already in T),
+// otherwise the register-staged kernel (which can convert fp32 -> bf16).
+template <class CK, bool PIPE, typename T, typename G, class EP>
+static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const ConvGeo& g, int M, uint32_t src_bytes,
+                            const EP& ep, int Mi, int K, hipStream_t st) {
+  if constexpr (PIPE && std::is_same<G, T>::value) {
+    using LA = GRowsB<T, CK::BI, CK::BK, CK::NT>;
+    using LB = GIm2colB<T, CK::BJ, CK::BK, CK::NT>;
+    return launch_pipe<CK, LA, LB>(typename LA::Params{W, ldw, wrows}, typename LB::Params{src, g, M, src_bytes}, ep,
+                                   Mi, M, K, 1, st);
+  } else {
+    using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+    using LB = LdIm2colB<G, T, CK::BJ, CK::BK, CK::NT>;
+    return launch_gemm<CK, LA, LB>(typename LA::Params{W, ldw, wrows}, typename LB::Params{src, g, M, src_bytes}, ep,
+                                   Mi, M, K, 1, st);
+  }
 }
 
 static int wgrad_splits(int tiles, int K, int BK) {
@@ -417,8 +440,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     if (rc) return rc;
     if (ax) HIPCHK(record_event(ax, &xev[k]));
   }
-  const int fwd_tile = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE");
-  const bool fwd_k = fwd_tile == 1 || fwd_tile == 2;
+  const int fwd_tile = step_tile((long)(512 / 32) * cdiv(M, 32), "AAA_STEP_TILE", false);
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);  // one step slice of XH
   for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126): h-part only
     if (ax && t % cs == 0) HIPCHK(hipStreamWaitEvent(st, xev[t / cs], 0));   // x-part of steps [t, t+cs) done
@@ -432,27 +454,18 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                          Wf(L.Gt) + (size_t)t * M * 512, M};
     const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     TimerScope tim(AAA_TIMER_FWD_STEP, st);
-    if (fwd_tile == 3) {
-      using CK = Cfg64For<T>;
-      using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
-      using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
-      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
-                                      typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
-                                      1152, 1, st)));
-    } else if (fwd_k) {
-      using CK = CfgKFor<T>;
-      using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
-      using LB = LdIm2colB<T, T, CK::BJ, CK::BK, CK::NT>;
-      HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
-                                      typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
-                                      1152, 1, st)));
-    } else {
-      using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
-      HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpH), 1152, 512},
-                                     typename LB::Params{Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes}, ep, 512, M,
-                                     1152, 1, st)));
+    const T* WpH = (const T*)(pk + L.k_WpH);
+    const T* xh = Wt(L.XH) + (size_t)t * M * 192;
+    hipError_t e;
+    switch (fwd_tile) {
+      case 1: case 2: e = step_gemm<CfgKFor<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 3: e = step_gemm<Cfg64For<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 4: e = step_gemm<C, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 5: e = step_gemm<CfgKFor<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 6: e = step_gemm<Cfg64For<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      default: e = step_gemm<C, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
     }
+    HIPCHK(e);
   }
   // constant query (Q1) + fused attention readout over all T*B frames
   HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
@@ -697,7 +710,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                          Wf(L.dZ) + (size_t)t1 * M * 512, st));
     // Sequential part: only the h rows (dh_{t-1}, fused with the gate backward
     // of step t-1); everything else runs in chunks off the chain.
-    const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE");
+    const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true);
     const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * 4);  // one step slice of dZ
     const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
     int done_hi = L.T;   // chunks [lo, done_hi) not yet issued
@@ -727,30 +740,17 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                         prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64};
       const float* dzt = Wf(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
-      if (bwd_tile == 3) {
-        using CK = CfgK4BFor<T>;
-        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
-        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
-        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
-                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
-      } else if (bwd_tile == 2) {
-        using CK = CfgK4For<T>;
-        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
-        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
-        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
-                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
-      } else if (bwd_tile == 1) {
-        using CK = CfgKFor<T>;
-        using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
-        using LB = LdIm2colB<float, T, CK::BJ, CK::BK, CK::NT>;
-        HIPCHK((launch_gemm<CK, LA, LB>(typename LA::Params{WdTh, 4608, 128},
-                                        typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
-      } else {
-        using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-        using LB = LdIm2colB<float, T, C::BJ, C::BK, NT>;
-        HIPCHK((launch_gemm<C, LA, LB>(typename LA::Params{WdTh, 4608, 128},
-                                       typename LB::Params{dzt, g, M, dz_bytes}, ep, 128, M, 4608, 1, st)));
+      hipError_t e;
+      switch (bwd_tile) {
+        case 1: e = step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 2: e = step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 3: e = step_gemm<CfgK4BFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 4: e = step_gemm<CfgK4BFor<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 5: e = step_gemm<CfgK4For<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 6: e = step_gemm<C, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        default: e = step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
       }
+      HIPCHK(e);
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
