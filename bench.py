@@ -96,6 +96,23 @@ def cpu_baseline(cfg):
                       f"B={B} x T={T}, {H}x{W}, nq={nq}, {dt:.1f} s on {cores} threads ({model})"}
 
 
+def pmc_traffic(config, dtype, world, kernel):
+    """HBM bytes per launch of ``kernel`` from the committed PMC passes
+    (tools/pmc.sh -> tools/pmc_traffic.py -> profiles/rNN/pmc_traffic_<config>.json).
+    rocprofv3 counters cannot be read from inside the timed run, so the value is
+    the profile of the same binary and config; null when none is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{config}.json")))
+    if not files or world != 1:
+        return {"traffic": None}
+    d = json.load(open(files[-1]))
+    c = d.get("classes", {}).get(kernel)
+    if not c:
+        return {"traffic": None}
+    return {"traffic": round(c["hbm_bytes_per_launch"]), "traffic_unit": "bytes/launch",
+            "traffic_source": os.path.relpath(files[-1], ROOT) + " (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,7 +203,8 @@ def main():
         "config": {"workload": cfg["desc"], "global_batch": B * world, "seq_len": T, "frame": f"{H}x{W}",
                    "heads": nq, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved, 2), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                     **pmc_traffic(args.config, dtype, world, names[dom]),
                      "flop_per_launch": per_launch[dom], "avg_launch_us": round(avg_ms * 1e3, 2)},
         "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
                          "frac": round(value * fpf / world / 1e12 / peak, 4)},

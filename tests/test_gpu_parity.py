@@ -82,6 +82,7 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     monkeypatch.setenv("AAA_STEP_TILE", str(fwd))
     monkeypatch.setenv("AAA_BPTT_TILE", str(bwd))
+    monkeypatch.setenv("AAA_PIPE_BATCHED", "0" if fwd == 0 else "1")   # batched conv GEMMs: register vs LDS-DMA
     T, B = 3, 5
     if conv_dtype == "fp32":
         _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"tiles {fwd}/{bwd}: ")

@@ -1,0 +1,48 @@
+"""HBM traffic per launch of the roofline kernel classes, from rocprofv3 PMC passes.
+
+usage: python tools/pmc_traffic.py PMC_DIR OUT_JSON
+
+PMC_DIR holds the counter_collection.csv files of tools/pmc.sh (FETCH_SIZE and
+WRITE_SIZE in their own passes).  Correction per MI355X_MICROARCH.md §HBM:
+on gfx950 FETCH_SIZE reports half the bytes of a 16-B-per-lane read (both
+buffer_load and buffer_load...lds), WRITE_SIZE is exact for 16-B stores and
+fp32 atomics, so HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (rocprofv3 reports KB).
+Memory-side counters include Infinity-Cache hits: an upper bound on DRAM bytes.
+bench.py reads OUT_JSON to fill roofline.traffic.
+"""
+import json
+import sys
+
+sys.path.insert(0, __file__.rsplit("/", 1)[0])
+from pmcsum import load  # noqa: E402
+
+# kernel class (bench.py names) -> all substrings that must appear in the kernel name
+CLASSES = {
+    "ConvLSTM BPTT step (dh dgrad + fused gate bwd)": ["EpiConvLstmBwd"],
+    "fused ConvLSTM forward step (h-part)": ["EpiConvLstmFwd"],
+    "ConvLSTM weight-gradient GEMM": ["128, 128, 32", "LdIm2colTB", "EpiStore<true>"],
+}
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    acc = load(d)
+    res = {}
+    for cls, subs in CLASSES.items():
+        fetch, write, n = [], [], 0
+        for k, cs in acc.items():
+            if all(s in k for s in subs):
+                fetch += cs.get("FETCH_SIZE", [])
+                write += cs.get("WRITE_SIZE", [])
+        if not fetch or not write:
+            continue
+        f = sum(fetch) / len(fetch) * 1024.0
+        w = sum(write) / len(write) * 1024.0
+        res[cls] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes_per_launch": 2.0 * f + w,
+                    "dispatches": len(fetch), "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)"}
+    json.dump({"source": d, "classes": res}, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -134,16 +134,28 @@ struct EpiConvLstmFwd {
   T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
   float* gates;        // [M][512]  in: Wx*x_t + b;  out: post-activation (i,f,c~,o)
   int Nj;              // M = B*P
-  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+  // Inputs of one (4-row, column) group, loadable before the K loop (glds.h).
+  struct Pre { f32x4 zx; float cp; };
+  __device__ __forceinline__ Pre prefetch(int i, int j) const {
+    Pre p{f32x4{0.f, 0.f, 0.f, 0.f}, 0.f};
+    if (j < Nj && i < 512) {
+      p.zx = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
+      p.cp = cprev[(size_t)j * 128 + (i >> 2)];
+    }
+    return p;
+  }
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre& p) const {
     if (j >= Nj || i >= 512) return;
     const int ch = i >> 2;
-    const f32x4 zx = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
     float gi, gf, gc, go, c, h;
-    GateFwd::run(zx[0] + v0, zx[1] + v1, zx[2] + v2, zx[3] + v3, cprev[(size_t)j * 128 + ch], gi, gf, gc, go, c, h);
+    GateFwd::run(p.zx[0] + v0, p.zx[1] + v1, p.zx[2] + v2, p.zx[3] + v3, p.cp, gi, gf, gc, go, c, h);
     cnext[(size_t)j * 128 + ch] = c;
     hout[(size_t)j * 128 + ch] = h;
     xhnext[(size_t)j * 192 + 64 + ch] = (T)h;
     *reinterpret_cast<f32x4*>(gates + (size_t)j * 512 + i) = f32x4{gi, gf, gc, go};
+  }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    finish(i, j, v0, v1, v2, v3, prefetch(i, j));
   }
 };
 
@@ -161,7 +173,23 @@ struct EpiConvLstmBwd {
   float* dh0;           // [M][128] or null (only when t == 0)
   int has_prev, Nj;
   int ioff;             // 64 when the GEMM computes only the h rows (dx batched separately)
-  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+  // Inputs of one (4-row, column) group of the fused gate backward, loadable
+  // before the K loop (glds.h); only the has_prev h-row path has any.
+  struct Pre { f32x4 g[4], dov, cp, cc, dcv; };
+  __device__ __forceinline__ Pre prefetch(int i, int j) const {
+    Pre p;
+    i += ioff;
+    if (j >= Nj || i < 64 || i >= 192 || !has_prev) return p;
+    const int ch = i - 64;
+    p.dov = *reinterpret_cast<const f32x4*>(dO + (size_t)j * 128 + ch);
+    p.cp = *reinterpret_cast<const f32x4*>(cprev + (size_t)j * 128 + ch);
+    p.cc = *reinterpret_cast<const f32x4*>(ccur + (size_t)j * 128 + ch);
+    p.dcv = *reinterpret_cast<const f32x4*>(dC + (size_t)j * 128 + ch);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p.g[e] = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + 4 * (ch + e));
+    return p;
+  }
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre& p) const {
     i += ioff;
     if (j >= Nj || i >= 192) return;
     if (i < 64) {
@@ -174,19 +202,18 @@ struct EpiConvLstmBwd {
       return;
     }
     const float v[4] = {v0, v1, v2, v3};
-    const f32x4 dov = *reinterpret_cast<const f32x4*>(dO + (size_t)j * 128 + ch);
-    const f32x4 cp = *reinterpret_cast<const f32x4*>(cprev + (size_t)j * 128 + ch);
-    const f32x4 cc = *reinterpret_cast<const f32x4*>(ccur + (size_t)j * 128 + ch);
-    f32x4 dcv = *reinterpret_cast<const f32x4*>(dC + (size_t)j * 128 + ch);
+    f32x4 dcv = p.dcv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + 4 * (ch + e));
       float dc = dcv[e], di, df, dcg, dout;
-      gate_bwd(v[e] + dov[e], g, cp[e], cc[e], dc, di, df, dcg, dout);
+      gate_bwd(v[e] + p.dov[e], p.g[e], p.cp[e], p.cc[e], dc, di, df, dcg, dout);
       dcv[e] = dc;
       *reinterpret_cast<f32x4*>(dz + (size_t)j * 512 + 4 * (ch + e)) = f32x4{di, df, dcg, dout};
     }
     *reinterpret_cast<f32x4*>(dC + (size_t)j * 128 + ch) = dcv;
+  }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    finish(i, j, v0, v1, v2, v3, prefetch(i, j));
   }
 };
 

@@ -337,6 +337,28 @@ __device__ __forceinline__ bf16x8 frag_bf16(const __bf16* t, int r, int k) {
   }
 }
 
+// Output tile (row block ti, column block tj, K slice tz) of this workgroup.
+// remap != 0: bijective XCD remap -- dispatch places linear block id b on XCD
+// b % 8, so logical tile t = that XCD's running index; t runs over the row
+// blocks of a column block first, then column blocks, then K slices.  One
+// XCD's L2 then holds a contiguous slice of the gathered operand (and, for
+// split-K weight gradients, one K window shared by all its tiles).
+__device__ __forceinline__ void tile_of(int remap, int& ti, int& tj, int& tz) {
+  if (!remap) { ti = blockIdx.y; tj = blockIdx.x; tz = blockIdx.z; return; }
+  const int nx = gridDim.x, ny = gridDim.y, nxy = nx * ny, n = nxy * gridDim.z;
+  const int b = (blockIdx.z * ny + blockIdx.y) * nx + blockIdx.x;
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  tz = t / nxy;
+  const int u = t - tz * nxy;
+  ti = u % ny;
+  tj = u / ny;
+}
+inline int xcd_remap_enabled() {
+  const char* e = getenv("AAA_XCD_REMAP");
+  return e ? atoi(e) != 0 : 1;
+}
+
 template <typename T, int R, int BK, bool KC>
 struct TileK : Tile<T, R, BK, KC> { static constexpr bool KC_ = KC; };
 
@@ -355,7 +377,7 @@ struct GemmCfg {
 
 template <class C, class LA, class LB, class EP>
 __global__ void __launch_bounds__(C::NT)
-gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk) {
+gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, int remap) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
@@ -368,8 +390,10 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
   T* const Bs0 = smem + 2 * TA::ELEMS;
   T* const Bs1 = Bs0 + TB::ELEMS;
 
-  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
-  const int kb = blockIdx.z * kchunk;
+  int ti, tj, tz;
+  tile_of(remap, ti, tj, tz);
+  const int i0 = ti * BI, j0 = tj * BJ;
+  const int kb = tz * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke) return;
 
@@ -493,7 +517,8 @@ inline hipError_t launch_gemm(const typename LA::Params& pa, const typename LB::
   kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
-  hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk);
+  hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
+                     xcd_remap_enabled());
   return hipGetLastError();
 }
 

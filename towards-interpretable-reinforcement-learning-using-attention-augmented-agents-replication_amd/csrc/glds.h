@@ -22,6 +22,7 @@
 // the same number of DMA instructions per tile, which the counted vmcnt
 // relies on), and the K slice is a multiple of BK.
 #pragma once
+#include <type_traits>
 #include "loaders_b.h"
 
 namespace aaa {
@@ -39,6 +40,13 @@ __device__ __forceinline__ int lds_swz(int row) {
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, 0, 0, 0);
 }
+
+// Epilogues with a split prefetch()/finish() (EP::Pre) have their global
+// inputs loaded before the K loop, so the loads' latency hides under it.
+template <class EP, class = void> struct has_pre : std::false_type {};
+template <class EP> struct has_pre<EP, std::void_t<typename EP::Pre>> : std::true_type {};
+template <class EP, bool> struct pre_of { using type = int; };
+template <class EP> struct pre_of<EP, true> { using type = typename EP::Pre; };
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -142,9 +150,14 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
   return *reinterpret_cast<const bf16x8*>(t + r * BK + (((kofs >> 3) ^ g) << 3));
 }
 
-template <class C, class LA, class LB, class EP, int NBUF>
+// ABL (diagnostic builds only, tools/ubench): bit 0 = no in-loop DMA, bit 1 =
+// no MFMA, bit 2 = no epilogue.  Production launches use ABL = 0.
+// ILV: issue the next tile's DMA between the MFMA groups of this tile (A
+// pieces after the first 16-deep k step, B after the last) instead of all at
+// once after the barrier, so the DMA issue overlaps MFMA execution.
+template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, bool ILV = false>
 __global__ void __launch_bounds__(C::NT)
-gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk) {
+gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, int remap) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
@@ -156,8 +169,10 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   // compiler drain vmcnt before the fragment reads).
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STG];
 
-  const int i0 = blockIdx.y * BI, j0 = blockIdx.x * BJ;
-  const int kb = blockIdx.z * kchunk;
+  int ti, tj, tz;
+  tile_of(remap, ti, tj, tz);
+  const int i0 = ti * BI, j0 = tj * BJ;
+  const int kb = tz * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke) return;
 
@@ -177,6 +192,21 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
   const int nk = (ke - kb) / BK;
+  // Epilogue groups of this thread (see the epilogue below) and, when the
+  // epilogue supports it, their inputs, requested first (vmcnt retires in issue order) and consumed after the
+  // K loop (ordinary loads: the compiler waits for them only at their use).
+  constexpr int G4 = BI / 4, NG = G4 * BJ, NPT = (NG + C::NT - 1) / C::NT;
+  constexpr bool PRE = has_pre<EP>::value && (ABL & 4) == 0;
+  using PreT = typename pre_of<EP, PRE>::type;
+  PreT pre[NPT];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int c = q * C::NT + (int)threadIdx.x;
+      if (NG % C::NT == 0 || c < NG) pre[q] = ep.prefetch(i0 + 4 * (c % G4), j0 + c / G4);
+    }
+  }
+
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
     if (s < nk) {
@@ -189,15 +219,17 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     if (kt + NBUF - 2 < nk) wait_vmcnt<PIECES * (NBUF - 2)>();
     else wait_vmcnt<0>();
     barrier_lds();
-    if (kt + NBUF - 1 < nk) {
-      T* st = smem + ((kt + NBUF - 1) % NBUF) * STG;
-      la.issue(st, kb + (kt + NBUF - 1) * BK);
-      lb.issue(st + AEL, kb + (kt + NBUF - 1) * BK);
+    const bool pf = !(ABL & 1) && kt + NBUF - 1 < nk;
+    T* const st = smem + ((kt + NBUF - 1) % NBUF) * STG;
+    const int kn = kb + (kt + NBUF - 1) * BK;
+    if (!ILV && pf) {
+      la.issue(st, kn);
+      lb.issue(st + AEL, kn);
     }
     const T* Ac = smem + (kt % NBUF) * STG;
     const T* Bc = Ac + AEL;
 #pragma unroll
-    for (int s2 = 0; s2 < BK / 16 / WK; ++s2) {
+    for (int s2 = 0; s2 < ((ABL & 2) ? 0 : BK / 16 / WK); ++s2) {
       const int kofs = 16 * (s2 * WK + wk) + 8 * h;
       if constexpr (is_f32<T>::value) {
         float af[MI][8], bfr[MJ][8];
@@ -224,48 +256,58 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
           for (int b = 0; b < MJ; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
       }
+      if constexpr (ILV) {
+        constexpr int S2 = BK / 16 / WK;
+        if (pf && s2 == 0) la.issue(st, kn);
+        if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+      }
     }
   }
 
-  if constexpr (WK > 1) {
-    constexpr int RED = (WK - 1) * WI * WJ * MI * MJ * 16 * 64;
-    static_assert(RED * sizeof(float) <= sizeof(smem), "split-K reduction does not fit in LDS");
-    float* red = reinterpret_cast<float*>(smem);
-    barrier_lds();   // every wave is done reading the last stage (all DMA retired: vmcnt(0) above)
-    if (wk > 0) {
-#pragma unroll
-      for (int a = 0; a < MI; ++a)
-#pragma unroll
-        for (int b = 0; b < MJ; ++b)
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            red[((((wk - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane] = acc[a][b][e];
-    }
-    __syncthreads();
-    if (wk > 0) return;
-#pragma unroll
-    for (int w = 1; w < WK; ++w)
-#pragma unroll
-      for (int a = 0; a < MI; ++a)
-#pragma unroll
-        for (int b = 0; b < MJ; ++b)
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            acc[a][b][e] += red[((((w - 1) * WI * WJ + wr) * MI * MJ + a * MJ + b) * 16 + e) * 64 + lane];
+  if constexpr ((ABL & 4) != 0) {   // keep acc alive without the epilogue's memory traffic
+    if (acc[0][0][0] == 1234.5f) ep(i0, j0, acc[0][0][1], 0.f, 0.f, 0.f);
+    return;
   }
+  // Epilogue through LDS.  Every wave (all WK groups) stores its partial tile
+  // pixel-major, E[wk][j][i]; then the whole workgroup walks the tile in
+  // 4-row groups with consecutive lanes on consecutive row groups of ONE
+  // column, so the epilogue's global loads/stores (gate activations, cell
+  // state, outputs: all [pixel][channel]) are contiguous per column instead
+  // of one 16-B access per lane at a 2 KB stride, and all waves share it.
+  constexpr int ELD = BI + 4;                 // pad: conflict-free b128 writes over 32 columns
+  static_assert(WK * BJ * ELD * sizeof(float) <= sizeof(smem), "epilogue tile does not fit in LDS");
+  float* E = reinterpret_cast<float*>(smem);
+  barrier_lds();                              // every wave is done reading the last stage
 #pragma unroll
   for (int a = 0; a < MI; ++a)
 #pragma unroll
     for (int b = 0; b < MJ; ++b)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int i = i0 + wi * WTI + a * 32 + 8 * g + 4 * h;
-        const int j = j0 + wj * WTJ + b * 32 + r32;
-        ep(i, j, acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+        const int i = wi * WTI + a * 32 + 8 * g + 4 * h;
+        const int j = wj * WTJ + b * 32 + r32;
+        *reinterpret_cast<f32x4*>(E + (wk * BJ + j) * ELD + i) =
+            f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
       }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    const int c = q * C::NT + (int)threadIdx.x;
+    if (NG % C::NT == 0 || c < NG) {
+      const int r4 = c % G4, j = c / G4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(E + j * ELD + 4 * r4);
+#pragma unroll
+      for (int w = 1; w < WK; ++w) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
+        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+      }
+      if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
+      else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
+    }
+  }
 }
 
-template <class C, class LA, class LB, class EP, int NBUF = 3>
+template <class C, class LA, class LB, class EP, int NBUF = 2, bool ILV = false>
 inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep, int Mi,
                               int Nj, int K, int nsplit, hipStream_t st) {
   if (Mi <= 0 || Nj <= 0 || K <= 0) return hipSuccess;
@@ -275,7 +317,8 @@ inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::
   kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
-  hipLaunchKernelGGL((gemm_pipe_kernel<C, LA, LB, EP, NBUF>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk);
+  hipLaunchKernelGGL((gemm_pipe_kernel<C, LA, LB, EP, NBUF, 0, ILV>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
+                     xcd_remap_enabled());
   return hipGetLastError();
 }
 

@@ -115,28 +115,20 @@ __device__ __forceinline__ void im2col_setup(const ConvGeo& g, int BK, bool ok, 
   const int mm = ok ? m : 0;
   const int f = (int)g.dHW.div(mm), pix = mm - f * hw;
   const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
+  // transposed gathers here are stride 1 (host-checked), so no divisibility test
   uint32_t rowm = 0, colm = 0;
+#pragma clang loop vectorize(disable)
   for (int k = 0; k < KH; ++k) {
     const int ty = g.transposed ? oy + g.pad - k : oy * g.stride + k - g.pad;
-    bool v = ok;
-    if (g.transposed) {
-      v = v && ty >= 0 && (g.stride == 1 || ty % g.stride == 0) && ty / g.stride < g.Hin;
-    } else {
-      v = v && ty >= 0 && ty < g.Hin;
-    }
-    if (v) rowm |= 1u << k;
+    if (ok && (unsigned)ty < (unsigned)g.Hin) rowm |= 1u << k;
   }
+#pragma clang loop vectorize(disable)
   for (int k = 0; k < g.KW; ++k) {
     const int tx = g.transposed ? ox + g.pad - k : ox * g.stride + k - g.pad;
-    bool v = true;
-    if (g.transposed) {
-      v = tx >= 0 && (g.stride == 1 || tx % g.stride == 0) && tx / g.stride < g.Win;
-    } else {
-      v = tx >= 0 && tx < g.Win;
-    }
-    if (v) colm |= 1u << k;
+    if ((unsigned)tx < (unsigned)g.Win) colm |= 1u << k;
   }
   uint64_t msk = 0;
+#pragma clang loop vectorize(disable)
   for (int k = 0; k < KH; ++k)
     if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
   vmask = msk;

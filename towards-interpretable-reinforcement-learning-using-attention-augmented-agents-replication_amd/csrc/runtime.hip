@@ -326,14 +326,14 @@ static int step_tile(long out_tiles32, const char* env, bool bptt) {
 // One per-step ConvLSTM GEMM: D[Mi][M] = W[Mi][K] x im2col(src)[K][M] with
 // epilogue ep.  PIPE = LDS-DMA ring (glds.h; needs src already in T),
 // otherwise the register-staged kernel (which can convert fp32 -> bf16).
-template <class CK, bool PIPE, typename T, typename G, class EP>
+template <class CK, bool PIPE, typename T, typename G, class EP, int NBUF = 2, bool ILV = false>
 static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const ConvGeo& g, int M, uint32_t src_bytes,
                             const EP& ep, int Mi, int K, hipStream_t st) {
   if constexpr (PIPE && std::is_same<G, T>::value) {
     using LA = GRowsB<T, CK::BI, CK::BK, CK::NT>;
     using LB = GIm2colB<T, CK::BJ, CK::BK, CK::NT>;
-    return launch_pipe<CK, LA, LB>(typename LA::Params{W, ldw, wrows}, typename LB::Params{src, g, M, src_bytes}, ep,
-                                   Mi, M, K, 1, st);
+    return launch_pipe<CK, LA, LB, EP, NBUF, ILV>(typename LA::Params{W, ldw, wrows},
+                                                  typename LB::Params{src, g, M, src_bytes}, ep, Mi, M, K, 1, st);
   } else {
     using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
     using LB = LdIm2colB<G, T, CK::BJ, CK::BK, CK::NT>;
@@ -341,6 +341,9 @@ static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const 
                                    Mi, M, K, 1, st);
   }
 }
+
+// Batched (off-chain) conv GEMMs on the LDS-DMA ring (env AAA_PIPE_BATCHED=0: register-staged).
+static bool pipe_batched() { return env_int("AAA_PIPE_BATCHED", 1) != 0; }
 
 static int wgrad_splits(int tiles, int K, int BK) {
   int s = std::max(1, 1024 / std::max(tiles, 1));
@@ -420,16 +423,15 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   hipStream_t xs = ax ? ax : st;
   if (ax) HIPCHK(stream_order(st, ax));
   auto xpart = [&](int lo, int hi) -> int {
-    using CX = CfgFor<T>;   // 64x64: measured faster than 128x128 here (K is only 576)
-    using LA = LdRowsB<T, T, CX::BI, CX::BK, CX::NT>;
-    using LB = LdIm2colB<T, T, CX::BJ, CX::BK, CX::NT>;
+    // 64x64 tiles (128x128 measured slower: K is only 576)
     const ConvGeo g = ConvGeo{64, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const int rows = (hi - lo) * M;
     EpiStoreT<float> ep{Wf(L.Gt) + (size_t)lo * M * 512, 512, 512, rows, (const float*)(pk + L.k_bl), 0};
-    HIPCHK((launch_gemm<CX, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WpX), 576, 512},
-                                   typename LB::Params{Wt(L.XH) + (size_t)lo * M * 192, g, rows,
-                                                       (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)},
-                                   ep, 512, rows, 576, 1, xs)));
+    const T* WpX = (const T*)(pk + L.k_WpX);
+    const T* xs0 = Wt(L.XH) + (size_t)lo * M * 192;
+    const uint32_t xb = (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz);
+    HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)
+                           : step_gemm<CfgFor<T>, false>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)));
     return AAA_OK;
   };
   hipEvent_t xev[64];
@@ -664,14 +666,13 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     HIPCHK(colsum(dz, 512, rows, 512, Wf(L.gbl), s));
     {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
-      using CJ = CfgFor<T>;   // 64x64: measured faster than 64x128 (occupancy)
-      using LA = LdRowsB<T, T, CJ::BI, CJ::BK, CJ::NT>;
-      using LB = LdIm2colB<float, T, CJ::BJ, CJ::BK, CJ::NT>;
+      // 64x64 tiles (64x128 measured slower: occupancy)
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
-      HIPCHK((launch_gemm<CJ, LA, LB>(typename LA::Params{(const T*)(pk + L.k_WdTl), 4608, 64},
-                                      typename LB::Params{dz, g, rows, (uint32_t)((size_t)rows * 512 * 4)}, ep, 64,
-                                      rows, 4608, 1, s)));
+      const T* WdT = (const T*)(pk + L.k_WdTl);
+      const uint32_t zb = (uint32_t)((size_t)rows * 512 * 4);
+      HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
+                             : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
     }
     if (!vision_here) return AAA_OK;
     const float* dy2 = Wf(L.dY2) + (size_t)lo * M * 64;
@@ -745,7 +746,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         case 1: e = step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 2: e = step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 3: e = step_gemm<CfgK4BFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 4: e = step_gemm<CfgK4BFor<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 4:   // 3-stage ring, DMA interleaved with the MFMAs (tools/ubench/step_ablate: 57.9 vs 59.4 us)
+          e = step_gemm<CfgK4BFor<T>, true, T, float, EpiConvLstmBwd, 3, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
+                                                                               128, 4608, st);
+          break;
         case 5: e = step_gemm<CfgK4For<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 6: e = step_gemm<C, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         default: e = step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
