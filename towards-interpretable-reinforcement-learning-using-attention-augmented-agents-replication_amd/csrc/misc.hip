@@ -140,53 +140,65 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
 // answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
 // this frame's contribution to dQ.
 template <int NQ>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(128 * NQ)
 k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q,
            const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int P,
            float* __restrict__ dO, float* __restrict__ dQp) {
+  constexpr int NT = 128 * NQ;     // thread (q, p0): head q, grid positions p0, p0+128, ...
+  constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT; LDS < 64 KB at P=441, NQ=8)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* A = sm;                 // P*NQ
   float* dA = A + P * NQ;        // P*NQ  (becomes dlogits)
   float* da = dA + P * NQ;       // NQ*184
   float* Qs = da + NQ * 184;     // NQ*72
-  float* ss = Qs + NQ * 72;      // NQ
+  float* ss = Qs + NQ * 72;      // NQ (padded to 4)
+  float* red = ss + 4 * ((NQ + 3) / 4);   // G*NQ*72
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
-  for (int i = tid; i < P * NQ; i += 256) A[i] = Am[(size_t)f * P * NQ + i];
-  for (int i = tid; i < NQ * 184; i += 256) da[i] = dAns[(size_t)f * da_ld + i];
-  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Q[i];
+  for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
+  for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
+  for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[i];
   __syncthreads();
-  // dA[p][q] = sum_c da[q][c] * V[p][c], V = [O[8:128] | S]; one wave per p.
-  for (int p = wave; p < P; p += 4) {
-    float acc[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-    for (int c = lane; c < 184; c += 64) {
-      const float v = c < 120 ? O[p * 128 + 8 + c] : S[p * 64 + c - 120];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] += da[q * 184 + c] * v;
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const float s = wave_sum(acc[q]);
-      if (lane == 0) dA[p * NQ + q] = s;
+  // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S]: one thread per (p, q),
+  // q uniform per 128 threads (da reads broadcast), rows of V as float4.
+  {
+    const int q = tid >> 7;
+    const float* dq = da + q * 184;
+    for (int p = tid & 127; p < P; p += 128) {
+      const f32x4* o4 = reinterpret_cast<const f32x4*>(O + p * 128 + 8);
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(S + p * 64);
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 6
+      for (int c = 0; c < 30; ++c) {
+        const f32x4 v = o4[c];
+        a0 += dq[4 * c] * v[0] + dq[4 * c + 1] * v[1];
+        a1 += dq[4 * c + 2] * v[2] + dq[4 * c + 3] * v[3];
+      }
+#pragma unroll 4
+      for (int c = 0; c < 16; ++c) {
+        const f32x4 v = s4[c];
+        a0 += dq[120 + 4 * c] * v[0] + dq[121 + 4 * c] * v[1];
+        a1 += dq[122 + 4 * c] * v[2] + dq[123 + 4 * c] * v[3];
+      }
+      dA[p * NQ + q] = a0 + a1;
     }
   }
   __syncthreads();
-  for (int q = wave; q < NQ; q += 4) {
+  // softmax backward: dlogit = A (dA - sum_p A dA)
+  for (int q = wave; q < NQ; q += NT / 64) {
     float s = 0.f;
     for (int p = lane; p < P; p += 64) s += A[p * NQ + q] * dA[p * NQ + q];
     s = wave_sum(s);
     if (lane == 0) ss[q] = s;
   }
   __syncthreads();
-  for (int i = tid; i < P * NQ; i += 256) {
+  for (int i = tid; i < P * NQ; i += NT) {
     const int q = i - (i / NQ) * NQ;
     dA[i] = A[i] * (dA[i] - ss[q]);
   }
   __syncthreads();
   float* dOf = dO + (size_t)f * P * 128;
-  for (int i = tid; i < P * 128; i += 256) {
+  for (int i = tid; i < P * 128; i += NT) {
     const int p = i >> 7, c = i & 127;
     float acc = 0.f;
     if (c < 8) {
@@ -198,11 +210,26 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
     dOf[i] = acc;
   }
-  for (int i = tid; i < NQ * 72; i += 256) {
-    const int q = i / 72, c = i - q * 72;
+  // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] | S]: G position groups,
+  // every loaded K element feeds all NQ heads, partials reduced through LDS.
+  if (tid < G * 72) {
+    const int g = tid / 72, c = tid - g * 72;
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    for (int p = g; p < P; p += G) {
+      const float k = c < 8 ? O[p * 128 + c] : S[p * 64 + c - 8];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] += dA[p * NQ + q] * k;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) red[(g * NQ + q) * 72 + c] = acc[q];
+  }
+  __syncthreads();
+  for (int i = tid; i < NQ * 72; i += NT) {
     float acc = 0.f;
-    if (c < 8) for (int p = 0; p < P; ++p) acc += dA[p * NQ + q] * O[p * 128 + c];
-    else for (int p = 0; p < P; ++p) acc += dA[p * NQ + q] * S[p * 64 + c - 8];
+#pragma unroll 4
+    for (int g = 0; g < G; ++g) acc += red[g * NQ * 72 + i];
     dQp[(size_t)f * NQ * 72 + i] = acc;
   }
 }
@@ -570,9 +597,10 @@ hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float
 
 hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
                     int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st) {
-  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8) * sizeof(float);
-  if (nq == 4) hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
-  else if (nq == 8) hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
+  const int G = 7;   // k_attn_bwd's dQ position groups
+  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72) * sizeof(float);
+  if (nq == 4) hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(512), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
+  else if (nq == 8) hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(1024), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -396,17 +396,26 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     typename LB::Params pb{Wf(L.Xp), ConvGeo{4, 4, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), F * L.P1,
                            (uint32_t)((size_t)F * L.H * L.W * 4 * 4)};
     EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 256, 1, st)));
+    if constexpr (std::is_same<T, float>::value) {
+      // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
+      using CP = GemmCfg<float, 32, 128, 32, 1, 4>;
+      using PA = GRowsB<float, CP::BI, CP::BK, CP::NT>;
+      using PB = GIm2colB<float, CP::BJ, CP::BK, CP::NT>;
+      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(typename PA::Params{pa.src, pa.ld, pa.nrows},
+                                                       typename PB::Params{pb.src, pb.g, pb.nrows, pb.src_bytes}, ep,
+                                                       32, F * L.P1, 256, 1, st)));
+    } else {   // bf16: the fp32 RGBx frames are rounded while staging (register path)
+      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 256, 1, st)));
+    }
   }
   {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
     using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
     typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};
     const ConvGeo g = ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep();
     EpiStoreT<T> ep{Wt(L.XH), 192, 64, F * P, prm + L.poff[C1B], 0};
-    if constexpr (32 % C::BK == 0) {
-      using LB = LdIm2colB<T, T, C::BJ, C::BK, NT>;
-      HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P, (uint32_t)((size_t)F * L.P1 * 32 * L.esz)},
-                                     ep, 64, F * P, 512, 1, st)));
+    if constexpr (32 % C::BK == 0) {   // LDS-DMA ring (tools/ubench/conv_cfg: 62 vs 67 us)
+      HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Wt(L.Y1), g, F * P,
+                                 (uint32_t)((size_t)F * L.P1 * 32 * L.esz), ep, 64, 512, st)));
     } else {
       using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
       HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P}, ep, 64, F * P, 512, 1, st)));
