@@ -3,6 +3,7 @@
 // (glds.h ABL bits) to show where a step's time goes.  Diagnostic only.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics -I../../include -I<csrc> step_ablate.hip
 #include <cstdio>
+#include <type_traits>
 #include <vector>
 #include "glds.h"
 #include "epilogues.h"
@@ -61,7 +62,7 @@ int main(int argc, char** argv) {
     typename LB::Params pb{dz, g, M, (uint32_t)((size_t)M * 512 * 4)};
     dim3 grid((M + 63) / 64, 128 / 32, 1);
     auto run = [&](auto kern, const char* name) {
-      const float us = time_us([&] { hipLaunchKernelGGL(kern, grid, dim3(K4B::NT), 0, 0, pa, pb, ep, 4608, 4608, 1); });
+      const float us = time_us([&] { hipLaunchKernelGGL(kern, grid, dim3(K4B::NT), 0, 0, pa, pb, ep, 4608, 4608, tile_map(grid)); });
       printf("bptt %-34s %8.2f us  %6.1f TF/s\n", name, us, flop / (us * 1e-6) / 1e12);
     };
     run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 0>, "pipe3 full");
@@ -78,26 +79,55 @@ int main(int argc, char** argv) {
   {  // forward step: D[512][M] = WpH x gather(h_{t-1}) + fused gates
     const ConvGeo g = ConvGeo{128, 192, 64, h, w, h, w, 3, 1, 1, 0}.prep();
     EpiConvLstmFwd<float> ep{cprev, cn, hs, xh + (size_t)M * 192, gt, M};
-    using LA = GRowsB<float, CF::BI, CF::BK, CF::NT>;
-    using LB = GIm2colB<float, CF::BJ, CF::BK, CF::NT>;
-    typename LA::Params pa{WpH, 1152, 512};
-    typename LB::Params pb{xh, g, M, (uint32_t)((size_t)M * 192 * 4)};
-    dim3 grid((M + 63) / 64, 512 / 64, 1);
     const double fl = 2.0 * M * 512 * 1152;
-    auto run = [&](auto kern, const char* name) {
-      const float us = time_us([&] { hipLaunchKernelGGL(kern, grid, dim3(CF::NT), 0, 0, pa, pb, ep, 1152, 1152, 1); });
-      printf("fwd  %-34s %8.2f us  %6.1f TF/s\n", name, us, fl / (us * 1e-6) / 1e12);
+    auto run = [&](auto cfg, auto nbuf, const char* name) {
+      using C = decltype(cfg);
+      constexpr int NB = decltype(nbuf)::value;
+      using LA = GRowsB<float, C::BI, C::BK, C::NT>;
+      using LB = GIm2colB<float, C::BJ, C::BK, C::NT>;
+      const float us = time_us([&] {
+        CK((launch_pipe<C, LA, LB, EpiConvLstmFwd<float>, NB>(typename LA::Params{WpH, 1152, 512},
+                                                               typename LB::Params{xh, g, M, (uint32_t)((size_t)M * 768)},
+                                                               ep, 512, M, 1152, 1, 0)));
+      });
+      printf("fwd  %-40s %8.2f us  %6.1f TF/s\n", name, us, fl / (us * 1e-6) / 1e12);
     };
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 0>, "pipe3 full");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 2, 0>, "pipe2 full");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 2, 0, true>, "pipe2 interleaved DMA");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 0, true>, "pipe3 interleaved DMA");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 4, 0>, "pipe4 full");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 1>, "pipe3 no-loop-DMA");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 2>, "pipe3 no-MFMA");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 4>, "pipe3 no-epilogue");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 3>, "pipe3 skeleton (no DMA, no MFMA)");
-    run(gemm_pipe_kernel<CF, LA, LB, EpiConvLstmFwd<float>, 3, 5>, "pipe3 MFMA only (no DMA, no epi)");
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    run(GemmCfg<float, 64, 64, 32, 2, 2>{}, I2{}, "64x64 BK32 4w pipe2 (current)");
+    run(GemmCfg<float, 128, 64, 32, 4, 2>{}, I2{}, "128x64 BK32 8w pipe2");
+    run(GemmCfg<float, 128, 64, 32, 4, 2>{}, I3{}, "128x64 BK32 8w pipe3");
+    run(GemmCfg<float, 64, 128, 32, 2, 4>{}, I2{}, "64x128 BK32 8w pipe2");
+    run(GemmCfg<float, 128, 64, 64, 4, 2>{}, I2{}, "128x64 BK64 8w pipe2");
+    run(GemmCfg<float, 128, 64, 32, 2, 2>{}, I2{}, "128x64 BK32 4w (64x32/wave) pipe2");
+    run(GemmCfg<float, 128, 64, 64, 2, 2, 2>{}, I2{}, "128x64 BK64 8w 2-way split-K pipe2");
+    run(GemmCfg<float, 128, 128, 32, 2, 2>{}, I2{}, "128x128 BK32 4w pipe2");
+  }
+  {  // BPTT alternatives
+    const ConvGeo g = ConvGeo{512, 512, 0, h, w, h, w, 3, 1, 1, 1}.prep();
+    EpiConvLstmBwd ep{nullptr, gates, cprev, ccur, dO, dC, dzo, nullptr, 1, M, 64};
+    auto run = [&](auto cfg, auto nbuf, auto ilv, const char* name) {
+      using C = decltype(cfg);
+      constexpr int NB = decltype(nbuf)::value;
+      constexpr bool IL = decltype(ilv)::value;
+      using LA = GRowsB<float, C::BI, C::BK, C::NT>;
+      using LB = GIm2colB<float, C::BJ, C::BK, C::NT>;
+      const float us = time_us([&] {
+        CK((launch_pipe<C, LA, LB, EpiConvLstmBwd, NB, IL>(typename LA::Params{WdT, 4608, 128},
+                                                            typename LB::Params{dz, g, M, (uint32_t)((size_t)M * 2048)},
+                                                            ep, 128, M, 4608, 1, 0)));
+      });
+      printf("bptt %-40s %8.2f us  %6.1f TF/s\n", name, us, flop / (us * 1e-6) / 1e12);
+    };
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using T1 = std::true_type;
+    using F0 = std::false_type;
+    run(GemmCfg<float, 32, 64, 128, 1, 2, 4>{}, I3{}, T1{}, "32x64 BK128 4-way pipe3 ilv (current)");
+    run(GemmCfg<float, 32, 64, 64, 1, 2, 4>{}, I3{}, T1{}, "32x64 BK64 4-way pipe3 ilv");
+    run(GemmCfg<float, 32, 64, 64, 1, 2, 4>{}, I2{}, F0{}, "32x64 BK64 4-way pipe2");
+    run(GemmCfg<float, 64, 32, 128, 2, 1, 4>{}, I3{}, T1{}, "64x32 BK128 4-way pipe3 ilv");
+    run(GemmCfg<float, 32, 128, 64, 1, 4, 2>{}, I3{}, T1{}, "32x128 BK64 2-way pipe3 ilv");
   }
   printf("done\n");
   return 0;

@@ -343,20 +343,31 @@ __device__ __forceinline__ bf16x8 frag_bf16(const __bf16* t, int r, int k) {
 // blocks of a column block first, then column blocks, then K slices.  One
 // XCD's L2 then holds a contiguous slice of the gathered operand (and, for
 // split-K weight gradients, one K window shared by all its tiles).
-__device__ __forceinline__ void tile_of(int remap, int& ti, int& tj, int& tz) {
-  if (!remap) { ti = blockIdx.y; tj = blockIdx.x; tz = blockIdx.z; return; }
-  const int nx = gridDim.x, ny = gridDim.y, nxy = nx * ny, n = nxy * gridDim.z;
-  const int b = (blockIdx.z * ny + blockIdx.y) * nx + blockIdx.x;
+struct TileMap {
+  int remap;
+  FastDiv ny, nxy;   // row blocks, row blocks x column blocks (host-computed magics: no divisions on device)
+};
+__device__ __forceinline__ void tile_of(const TileMap& m, int& ti, int& tj, int& tz) {
+  if (!m.remap) { ti = blockIdx.y; tj = blockIdx.x; tz = blockIdx.z; return; }
+  const int ny = (int)m.ny.d, nxy = (int)m.nxy.d, n = nxy * gridDim.z;
+  const int b = (blockIdx.z * ny + blockIdx.y) * gridDim.x + blockIdx.x;
   const int q = n >> 3, r = n & 7, x = b & 7;
   const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-  tz = t / nxy;
+  tz = (int)m.nxy.div((uint32_t)t);
   const int u = t - tz * nxy;
-  ti = u % ny;
-  tj = u / ny;
+  tj = (int)m.ny.div((uint32_t)u);
+  ti = u - tj * ny;
 }
 inline int xcd_remap_enabled() {
   const char* e = getenv("AAA_XCD_REMAP");
   return e ? atoi(e) != 0 : 1;
+}
+inline TileMap tile_map(dim3 grid) {
+  TileMap m;
+  m.remap = xcd_remap_enabled();
+  m.ny = FastDiv(grid.y);
+  m.nxy = FastDiv(grid.x * grid.y);
+  return m;
 }
 
 template <typename T, int R, int BK, bool KC>
@@ -377,7 +388,7 @@ struct GemmCfg {
 
 template <class C, class LA, class LB, class EP>
 __global__ void __launch_bounds__(C::NT)
-gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, int remap) {
+gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
@@ -391,7 +402,7 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
   T* const Bs1 = Bs0 + TB::ELEMS;
 
   int ti, tj, tz;
-  tile_of(remap, ti, tj, tz);
+  tile_of(tm, ti, tj, tz);
   const int i0 = ti * BI, j0 = tj * BJ;
   const int kb = tz * kchunk;
   const int ke = min(K, kb + kchunk);
@@ -518,7 +529,7 @@ inline hipError_t launch_gemm(const typename LA::Params& pa, const typename LB::
   nsplit = (K + kchunk - 1) / kchunk;
   dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
   hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
-                     xcd_remap_enabled());
+                     tile_map(grid));
   return hipGetLastError();
 }
 

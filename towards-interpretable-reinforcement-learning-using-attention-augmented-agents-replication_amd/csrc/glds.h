@@ -48,6 +48,20 @@ template <class EP> struct has_pre<EP, std::void_t<typename EP::Pre>> : std::tru
 template <class EP, bool> struct pre_of { using type = int; };
 template <class EP> struct pre_of<EP, true> { using type = typename EP::Pre; };
 
+#ifdef AAA_STAMPS
+// Diagnostic builds only (tools/ubench): per-workgroup phase timestamps
+// (s_memrealtime, 100 MHz): [wg][0] entry, [1] K loop start, [2] K loop end, [3] exit.
+__device__ uint64_t aaa_stamps[8192 * 4];
+#define AAA_STAMP(k)                                                                                  \
+  do {                                                                                                \
+    if (threadIdx.x == 0)                                                                             \
+      aaa_stamps[(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + (k)] =        \
+          __builtin_amdgcn_s_memrealtime();                                                           \
+  } while (0)
+#else
+#define AAA_STAMP(k) do {} while (0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -157,7 +171,7 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
 // once after the barrier, so the DMA issue overlaps MFMA execution.
 template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, bool ILV = false>
 __global__ void __launch_bounds__(C::NT)
-gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, int remap) {
+gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
@@ -167,10 +181,13 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   constexpr int PIECES = LA::PER + LB::PER;   // DMA instructions per wave per K tile
   // ONE shared array for everything (a second __shared__ object can make the
   // compiler drain vmcnt before the fragment reads).
-  __shared__ __attribute__((aligned(16))) T smem[NBUF * STG];
+  constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
+  constexpr int EPI_T = (int)((WK * BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * STG > EPI_T ? NBUF * STG : EPI_T];
+  AAA_STAMP(0);
 
   int ti, tj, tz;
-  tile_of(remap, ti, tj, tz);
+  tile_of(tm, ti, tj, tz);
   const int i0 = ti * BI, j0 = tj * BJ;
   const int kb = tz * kchunk;
   const int ke = min(K, kb + kchunk);
@@ -214,6 +231,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       lb.issue(smem + s * STG + AEL, kb + s * BK);
     }
 
+  AAA_STAMP(1);
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt is the oldest of the (up to NBUF-1) tiles in flight
     if (kt + NBUF - 2 < nk) wait_vmcnt<PIECES * (NBUF - 2)>();
@@ -268,14 +286,13 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     if (acc[0][0][0] == 1234.5f) ep(i0, j0, acc[0][0][1], 0.f, 0.f, 0.f);
     return;
   }
+  AAA_STAMP(2);
   // Epilogue through LDS.  Every wave (all WK groups) stores its partial tile
   // pixel-major, E[wk][j][i]; then the whole workgroup walks the tile in
   // 4-row groups with consecutive lanes on consecutive row groups of ONE
   // column, so the epilogue's global loads/stores (gate activations, cell
   // state, outputs: all [pixel][channel]) are contiguous per column instead
   // of one 16-B access per lane at a 2 KB stride, and all waves share it.
-  constexpr int ELD = BI + 4;                 // pad: conflict-free b128 writes over 32 columns
-  static_assert(WK * BJ * ELD * sizeof(float) <= sizeof(smem), "epilogue tile does not fit in LDS");
   float* E = reinterpret_cast<float*>(smem);
   barrier_lds();                              // every wave is done reading the last stage
 #pragma unroll
@@ -305,6 +322,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
     }
   }
+  AAA_STAMP(3);
 }
 
 template <class C, class LA, class LB, class EP, int NBUF = 2, bool ILV = false>
@@ -318,7 +336,7 @@ inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::
   nsplit = (K + kchunk - 1) / kchunk;
   dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
   hipLaunchKernelGGL((gemm_pipe_kernel<C, LA, LB, EP, NBUF, 0, ILV>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
-                     xcd_remap_enabled());
+                     tile_map(grid));
   return hipGetLastError();
 }
 

@@ -117,28 +117,35 @@ __device__ __forceinline__ void im2col_setup(const ConvGeo& g, int BK, bool ok, 
   const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
   // transposed gathers here are stride 1 (host-checked), so no divisibility test
   uint32_t rowm = 0, colm = 0;
-#pragma clang loop vectorize(disable)
-  for (int k = 0; k < KH; ++k) {
-    const int ty = g.transposed ? oy + g.pad - k : oy * g.stride + k - g.pad;
-    if (ok && (unsigned)ty < (unsigned)g.Hin) rowm |= 1u << k;
-  }
-#pragma clang loop vectorize(disable)
-  for (int k = 0; k < g.KW; ++k) {
-    const int tx = g.transposed ? ox + g.pad - k : ox * g.stride + k - g.pad;
-    if ((unsigned)tx < (unsigned)g.Win) colm |= 1u << k;
-  }
   uint64_t msk = 0;
+  const int ty0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;   // row of tap 0; tap k at ty0 -/+ k
+  const int tx0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
+  const int sg = g.transposed ? -1 : 1;
+  if (KH == 3) {   // the ConvLSTM steps: straight-line
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (ok && (unsigned)(ty0 + sg * k) < (unsigned)g.Hin) rowm |= 1u << k;
+      if ((unsigned)(tx0 + sg * k) < (unsigned)g.Win) colm |= 1u << k;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (3 * k);
+  } else {
 #pragma clang loop vectorize(disable)
-  for (int k = 0; k < KH; ++k)
-    if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
+    for (int k = 0; k < KH; ++k) {
+      if (ok && (unsigned)(ty0 + sg * k) < (unsigned)g.Hin) rowm |= 1u << k;
+      if ((unsigned)(tx0 + sg * k) < (unsigned)g.Win) colm |= 1u << k;
+    }
+#pragma clang loop vectorize(disable)
+    for (int k = 0; k < KH; ++k)
+      if ((rowm >> k) & 1u) msk |= (uint64_t)colm << (k * g.KW);
+  }
   vmask = msk;
-  const int d = g.Cin >= BK ? 0 : kc / g.Cin;       // taps inside the tile before this chunk
+  const int d = g.Cin >= BK ? 0 : (int)g.dCin.div((uint32_t)kc);   // taps inside the tile before this chunk
   const int ci = kc - d * g.Cin;
   dt = d;
-  const int dky = d / g.KW, dkx = d - dky * g.KW;
-  const int oy0 = g.transposed ? oy + g.pad : oy * g.stride - g.pad;
-  const int ox0 = g.transposed ? ox + g.pad : ox * g.stride - g.pad;
-  base = ((f * g.Hin + oy0) * g.Win + ox0) * g.cs + g.coff + ci + sgn * (dky * g.Win + dkx) * g.cs;
+  const int dky = (int)g.dKW.div((uint32_t)d), dkx = d - dky * g.KW;
+  base = ((f * g.Hin + ty0) * g.Win + tx0) * g.cs + g.coff + ci + sgn * (dky * g.Win + dkx) * g.cs;
 }
 
 // Implicit-GEMM gather, rows = output pixels, k = (tap, ci).  Either Cin % BK

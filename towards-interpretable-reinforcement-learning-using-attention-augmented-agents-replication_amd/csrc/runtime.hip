@@ -285,6 +285,7 @@ using CFK4 = GemmCfg<float, 32, 64, 64, 1, 2, 4>; // 4-way split-K (8 waves)
 using CFK4B = GemmCfg<float, 32, 64, 128, 1, 2, 4>; // 4-way split-K, 2 k-steps per wave per barrier
 using CF64 = GemmCfg<float, 64, 64, 64, 2, 2>;     // 64x64, BK 64
 using CFJ = GemmCfg<float, 64, 128, 32, 2, 2>;     // 64-row GEMMs with long N (batched dx)
+using CFS = GemmCfg<float, 128, 64, 32, 4, 2>;     // forward step: 8 waves, ~1 WG per CU at C2 (balanced)
 using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;
 using CB32 = GemmCfg<__bf16, 32, 64, 64, 1, 2>;
 using CBW = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
@@ -293,6 +294,7 @@ using CBK4 = GemmCfg<__bf16, 32, 64, 64, 1, 2, 4>;
 using CBK4B = GemmCfg<__bf16, 32, 64, 128, 1, 2, 4>;
 using CB64 = GemmCfg<__bf16, 64, 64, 128, 2, 2>;
 using CBJ = GemmCfg<__bf16, 64, 128, 64, 2, 2>;
+using CBS = GemmCfg<__bf16, 128, 64, 64, 4, 2>;
 template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
 template <typename T> using Cfg32For = std::conditional_t<std::is_same<T, float>::value, CF32, CB32>;
 template <typename T> using CfgWFor = std::conditional_t<std::is_same<T, float>::value, CFW, CBW>;
@@ -301,6 +303,7 @@ template <typename T> using CfgK4For = std::conditional_t<std::is_same<T, float>
 template <typename T> using CfgK4BFor = std::conditional_t<std::is_same<T, float>::value, CFK4B, CBK4B>;
 template <typename T> using Cfg64For = std::conditional_t<std::is_same<T, float>::value, CF64, CB64>;
 template <typename T> using CfgJFor = std::conditional_t<std::is_same<T, float>::value, CFJ, CBJ>;
+template <typename T> using CfgSFor = std::conditional_t<std::is_same<T, float>::value, CFS, CBS>;
 
 // Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE override):
 //   0 64x64 BK32 | 1 32x64 BK64 2-way in-WG split-K | 2 ... 4-way | 3 32x64 BK128 4-way
@@ -471,7 +474,10 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     switch (fwd_tile) {
       case 1: case 2: e = step_gemm<CfgKFor<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 3: e = step_gemm<Cfg64For<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
-      case 4: e = step_gemm<C, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 4:   // 128x64, 8 waves (tools/ubench/step_ablate: 45.8 vs 47.4 us for 64x64)
+        e = step_gemm<CfgSFor<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st);
+        break;
+      case 7: e = step_gemm<C, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 5: e = step_gemm<CfgKFor<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 6: e = step_gemm<Cfg64For<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       default: e = step_gemm<C, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
