@@ -345,6 +345,29 @@ static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const 
   }
 }
 
+// Small GEMMs of the head (F = T*B rows; answer MLP, LSTMCell, policy/value
+// heads): 64x64 tiles leave most CUs idle, so below ~192 tiles use the 32x64
+// tile (twice the workgroups).  AAA_HEAD_TILE=1 forces 64x64, =2 forces 32x64.
+template <template <typename, typename, int, int, int> class LA_,
+          template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
+static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, int nsplit,
+                            hipStream_t st) {
+  const int mode = env_int("AAA_HEAD_TILE", 0);
+  const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
+  if (mode == 1 || (mode == 0 && tiles >= 192)) {
+    using C = CF;
+    using A = LA_<float, float, C::BI, C::BK, C::NT>;
+    using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+    return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
+                                ep, Mi, Nj, K, nsplit, st);
+  }
+  using C = CF32;
+  using A = LA_<float, float, C::BI, C::BK, C::NT>;
+  using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+  return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows}, ep,
+                              Mi, Nj, K, nsplit, st);
+}
+
 // Batched (off-chain) conv GEMMs on the LDS-DMA ring (env AAA_PIPE_BATCHED=0: register-staged).
 static bool pipe_batched() { return env_int("AAA_PIPE_BATCHED", 1) != 0; }
 
@@ -496,25 +519,25 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     LRf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, 512};
     LRfj::Params pb{Wf(L.ans), L.ans_ld, F};
     EpiStoreT<float> ep{Wf(L.hid1), 512, 512, F, prm + L.poff[A0B], 1};
-    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 512, F, L.ans_ld, 1, st)));
+    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 512, F, L.ans_ld, 1, st)));
   }
   {  // answer_processor.2
     LRf::Params pa{prm + L.poff[A2W], 512, 256};
     LRfj::Params pb{Wf(L.hid1), 512, F};
     EpiStoreT<float> ep{Wf(L.AO), 256, 256, F, prm + L.poff[A2B], 0};
-    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 256, F, 512, 1, st)));
+    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 256, F, 512, 1, st)));
   }
   {  // policy_core LSTMCell from zero state (attention.py:354-355)
     LRf::Params pa{(const float*)(pk + L.k_Wihp), 256, 1024};
     LRfj::Params pb{Wf(L.AO), 256, F};
     EpiLstmCellFwd ep{(const float*)(pk + L.k_blc), Wf(L.LG), Wf(L.LC), Wf(L.LH), F};
-    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 1024, F, 256, 1, st)));
+    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 1024, F, 256, 1, st)));
   }
   {  // policy / values heads (attention.py:365-367)
     LRf::Params pa{(const float*)(pk + L.k_Whd), 256, 2 * L.A};
     LRfj::Params pb{Wf(L.LH), 256, F};
     EpiHeads ep{io->logits, io->values, (const float*)(pk + L.k_bhd), L.A, F};
-    HIPCHK((launch_gemm<CF, LRf, LRfj>(pa, pb, ep, 2 * L.A, F, 256, 1, st)));
+    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 2 * L.A, F, 256, 1, st)));
   }
   if (io->hT)
     HIPCHK(hipMemcpyAsync(io->hT, Wf(L.Hs) + (size_t)(L.T - 1) * M * 128, (size_t)M * 128 * 4,
@@ -587,52 +610,52 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
       LRfj::Params pb{Wf(L.dY), L.ldy, F};
       EpiLstmCellBwd ep{Wf(L.LG), Wf(L.LC), Wf(L.dLG), F};
-      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 256, F, L.ldy, 1, st)));
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, F, L.ldy, 1, st)));
     }
     {  // heads wgrad
       LTf::Params pa{Wf(L.dY), L.ldy, L.ldy};
       LTfj::Params pb{Wf(L.LH), 256, 256};
       EpiStore<true> ep{Wf(L.gWhd), 256, L.ldy, 256};
-      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), st)));
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), st)));
       HIPCHK(colsum(Wf(L.dY), L.ldy, F, L.ldy, Wf(L.gbhd), st));
     }
     {  // LSTMCell input dgrad
       LTf::Params pa{(const float*)(pk + L.k_Wihp), 256, 256};
       LRfj::Params pb{Wf(L.dLG), 1024, F};
       EpiStoreT<float> ep{Wf(L.dAO), 256, 256, F, nullptr, 0};
-      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 256, F, 1024, 1, st)));
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, F, 1024, 1, st)));
     }
     {  // LSTMCell weight_ih grad (weight_hh grad is exactly zero: h0 = 0, Q1)
       LTf::Params pa{Wf(L.dLG), 1024, 1024};
       LTfj::Params pb{Wf(L.AO), 256, 256};
       EpiStore<true> ep{Wf(L.gWihp), 256, 1024, 256};
-      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), st)));
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), st)));
       HIPCHK(colsum(Wf(L.dLG), 1024, F, 1024, Wf(L.gblc), st));
     }
     {  // answer_processor.2 dgrad fused with ReLU backward
       LTf::Params pa{prm + L.poff[A2W], 512, 512};
       LRfj::Params pb{Wf(L.dAO), 256, F};
       EpiReluBwdT ep{Wf(L.dH1), Wf(L.hid1), 512, 512, 512, F};
-      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, 512, F, 256, 1, st)));
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 512, F, 256, 1, st)));
     }
     {  // answer_processor.2 wgrad / bias
       LTf::Params pa{Wf(L.dAO), 256, 256};
       LTfj::Params pb{Wf(L.hid1), 512, 512};
       EpiStore<true> ep{grads + L.poff[A2W], 512, 256, 512};
-      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), st)));
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), st)));
       HIPCHK(colsum(Wf(L.dAO), 256, F, 256, grads + L.poff[A2B], st));
     }
     {  // answer_processor.0 dgrad (readout columns only)
       LTf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, L.da};
       LRfj::Params pb{Wf(L.dH1), 512, F};
       EpiStoreT<float> ep{Wf(L.dAns), L.da, L.da, F, nullptr, 0};
-      HIPCHK((launch_gemm<CF, LTf, LRfj>(pa, pb, ep, L.da, F, 512, 1, st)));
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, L.da, F, 512, 1, st)));
     }
     {  // answer_processor.0 wgrad / bias
       LTf::Params pa{Wf(L.dH1), 512, 512};
       LTfj::Params pb{Wf(L.ans), L.ans_ld, L.ans_ld};
       EpiStore<true> ep{Wf(L.gW1p), L.ans_ld, 512, L.ans_ld};
-      HIPCHK((launch_gemm<CF, LTf, LTfj>(pa, pb, ep, 512, L.ans_ld, F,
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 512, L.ans_ld, F,
                                         wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), st)));
       HIPCHK(colsum(Wf(L.dH1), 512, F, 512, grads + L.poff[A0B], st));
     }
