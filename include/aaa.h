@@ -151,6 +151,24 @@ enum aaa_timer {
 int aaa_timing_enable(int on);
 int aaa_timing_read(int kind, double* total_ms, long* launches);
 
+/* ---- optimizer ----
+ * One fused multi-tensor Adam step with torch.optim.Adam semantics (the
+ * reference's optimizer: main_mp.py:92 builds Adam(policy.parameters(),
+ * lr=1e-3), main_mp.py:78 steps it).  ``step`` is the step count after this
+ * update (1 on the first call).  Tensor i has numel[i] fp32 elements at
+ * params[i] / grads[i] / exp_avg[i] / exp_avg_sq[i] (and max_exp_avg_sq[i]
+ * when amsgrad; the array may be NULL otherwise), all updated in place on
+ * ``stream``.  The pointer arrays are host memory; the tensors are device
+ * memory.  A flat parameter buffer is simply ntensors = 1. */
+typedef struct aaa_adam_hparams {
+  double lr, beta1, beta2, eps, weight_decay;
+  int amsgrad, maximize;
+} aaa_adam_hparams;
+
+int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* const* params,
+                  const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                  float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream);
+
 /* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
 
 /* NHWC convolution y[n,oy,ox,co] = b[co] + sum w[co,ky,kx,ci] x[n,iy,ix,ci]

@@ -78,3 +78,25 @@ def test_state_dict_keys_match_reference_order():
     keys = list(agent.state_dict().keys())
     assert keys == [n for n, _ in detinit.param_shapes(18, 4)]
     assert len(list(agent.buffers())) == 0
+
+
+def test_adam_rejects_bad_args_without_gpu():
+    lib = N.load()
+    hp = N.AdamHP(1e-3, 0.9, 0.999, 1e-8, 0.0, 0, 0)
+    assert lib.aaa_adam_step(ctypes.byref(hp), 0, 0, None, None, None, None, None, None, None) == -1   # step < 1
+    assert b"step" in lib.aaa_last_error()
+    bad = N.AdamHP(1e-3, 1.0, 0.999, 1e-8, 0.0, 0, 0)
+    assert lib.aaa_adam_step(ctypes.byref(bad), 1, 0, None, None, None, None, None, None, None) == -1
+    ams = N.AdamHP(1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0)
+    one = (ctypes.c_void_p * 1)(16)
+    n = (ctypes.c_size_t * 1)(4)
+    assert lib.aaa_adam_step(ctypes.byref(ams), 1, 1, one, one, one, one, None, n, None) == -1     # amsgrad w/o vmax
+
+
+def test_adam_optimizer_has_no_cpu_fallback():
+    import torch
+    from aaa_amd.optim import Adam
+    p = torch.nn.Parameter(torch.zeros(4))
+    p.grad = torch.ones(4)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        Adam([p]).step()

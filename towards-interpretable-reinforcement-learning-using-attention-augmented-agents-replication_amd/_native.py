@@ -21,6 +21,7 @@ EXPORTS = (
     "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
     "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
     "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
+    "aaa_adam_step",
 )
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD = 0, 1, 2
 
@@ -37,6 +38,12 @@ IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action"
 
 class IO(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in IO_FIELDS]
+
+
+class AdamHP(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("amsgrad", ctypes.c_int),
+                ("maximize", ctypes.c_int)]
 
 
 class ConvDesc(ctypes.Structure):
@@ -76,6 +83,7 @@ def load(path: str = LIB_PATH):
             "aaa_linear": (I, [I, I, I, P, P, P, P, P]),
             "aaa_timing_enable": (I, [I]),
             "aaa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
+            "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)
@@ -125,3 +133,18 @@ def timing_read(kind: int):
     ms, n = ctypes.c_double(), ctypes.c_long()
     check(load().aaa_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)), "timing_read")
     return ms.value, n.value
+
+
+def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None) -> None:
+    """One fused Adam launch over lists of same-length fp32 device tensors (aaa_adam_step)."""
+    n = len(params)
+    VP = ctypes.c_void_p * max(n, 1)
+    def arr(ts):
+        return VP(*[t.data_ptr() for t in ts]) if ts is not None else None
+    numel = (ctypes.c_size_t * max(n, 1))(*[t.numel() for t in params])
+    for group in (grads, exp_avg, exp_avg_sq) + ((max_exp_avg_sq,) if max_exp_avg_sq is not None else ()):
+        assert len(group) == n
+    mx = arr(max_exp_avg_sq)
+    check(load().aaa_adam_step(ctypes.byref(hp), int(step), n, arr(params), arr(grads), arr(exp_avg),
+                               arr(exp_avg_sq), mx, numel, stream if stream is not None else stream_ptr()),
+          "adam_step")

@@ -1,0 +1,29 @@
+#pragma once
+#include "common.h"
+
+namespace aaa {
+
+constexpr int kAdamMaxTensors = 48;   // per launch (kernel-argument table)
+
+struct AdamTable {
+  float* p[kAdamMaxTensors];
+  const float* g[kAdamMaxTensors];
+  float* m[kAdamMaxTensors];
+  float* v[kAdamMaxTensors];
+  float* vmax[kAdamMaxTensors];
+  size_t numel[kAdamMaxTensors];
+  int chunk0[kAdamMaxTensors];        // first workgroup of each tensor
+  unsigned char vec[kAdamMaxTensors]; // all four pointers 16-byte aligned
+  int n;
+};
+
+struct AdamHost {
+  double lr, beta1, beta2, eps, weight_decay;
+  long step;
+  int amsgrad, maximize;
+};
+
+int adam_chunks(size_t numel);
+hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st);
+
+}  // namespace aaa

@@ -28,6 +28,7 @@
 #include "loaders_b.h"
 #include "glds.h"
 #include "misc.h"
+#include "optim.h"
 
 namespace aaa {
 
@@ -1059,6 +1060,43 @@ int aaa_conv2d_nhwc_wgrad(const aaa_conv_desc* d, const float* x, const float* d
   if (r) return r;
   return d->dtype == AAA_BF16 ? wgrad_nhwc_impl<__bf16>(d, x, dy, dw, stream)
                               : wgrad_nhwc_impl<float>(d, x, dy, dw, stream);
+}
+
+int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* const* params,
+                  const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
+                  float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream) {
+  if (!hp || ntensors < 0 || (ntensors > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel)))
+    return fail(AAA_E_ARG, "adam: NULL argument");
+  if (step < 1) return fail(AAA_E_ARG, "adam: step must be >= 1 (got %ld)", step);
+  if (hp->amsgrad && !max_exp_avg_sq) return fail(AAA_E_ARG, "adam: amsgrad needs max_exp_avg_sq");
+  if (!(hp->lr >= 0.0) || !(hp->eps >= 0.0) || !(hp->beta1 >= 0.0 && hp->beta1 < 1.0) ||
+      !(hp->beta2 >= 0.0 && hp->beta2 < 1.0) || !(hp->weight_decay >= 0.0))
+    return fail(AAA_E_ARG, "adam: invalid hyper-parameters");
+  int r = check_device();
+  if (r) return r;
+  AdamHost h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, step, hp->amsgrad ? 1 : 0, hp->maximize ? 1 : 0};
+  for (int t0 = 0; t0 < ntensors; t0 += kAdamMaxTensors) {
+    AdamTable tab;
+    memset(&tab, 0, sizeof tab);
+    int nch = 0;
+    for (int t = t0; t < std::min(ntensors, t0 + kAdamMaxTensors); ++t) {
+      if (numel[t] == 0) continue;
+      const int i = tab.n++;
+      if (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t] || (h.amsgrad && !max_exp_avg_sq[t]))
+        return fail(AAA_E_ARG, "adam: NULL pointer for tensor %d", t);
+      tab.p[i] = params[t]; tab.g[i] = grads[t]; tab.m[i] = exp_avg[t]; tab.v[i] = exp_avg_sq[t];
+      tab.vmax[i] = h.amsgrad ? max_exp_avg_sq[t] : nullptr;
+      tab.numel[i] = numel[t];
+      tab.chunk0[i] = nch;
+      tab.vec[i] = aligned16(params[t]) && aligned16(grads[t]) && aligned16(exp_avg[t]) && aligned16(exp_avg_sq[t]) &&
+                   (!tab.vmax[i] || aligned16(tab.vmax[i]));
+      const long c = adam_chunks(numel[t]);
+      if (nch + c > (1L << 30)) return fail(AAA_E_ARG, "adam: tensor %d too large", t);
+      nch += (int)c;
+    }
+    HIPCHK(adam_launch(tab, nch, h, stream));
+  }
+  return AAA_OK;
 }
 
 int aaa_linear(int M, int N, int K, const float* x, const float* w, const float* bias, float* y,

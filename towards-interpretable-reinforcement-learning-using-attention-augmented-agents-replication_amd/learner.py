@@ -2,6 +2,8 @@
 
 step():  pack weights -> T-step forward -> backward (3 phases) with each
 phase's gradient bucket all-reduced (RCCL) while the next phase runs.
+train_step(): step() followed by the fused Adam update of the flat params
+(main_mp.py:78; csrc/optim.hip), i.e. one complete learner iteration.
 Weights live in one flat fp32 buffer in state_dict order, grads likewise, so
 a bucket is a contiguous slice and no flatten/unflatten copies are needed.
 """
@@ -14,13 +16,14 @@ import torch.distributed as dist
 from . import _native as N
 from . import detinit
 from .attention import SpatialBasis
+from .optim import adam_flat_
 from .parallel import allreduce_buckets, bucket_bounds
 from .runtime import UnrollRunner
 
 
 class Learner:
     def __init__(self, B: int, T: int, H: int = 84, W: int = 84, nq: int = 4, A: int = 18,
-                 dtype: str = "fp32", device=None, seed: int = 0, group=None):
+                 dtype: str = "fp32", device=None, seed: int = 0, group=None, lr: float = 1e-3):
         self.runner = r = UnrollRunner(B, T, H, W, nq, A, dtype, device)
         self.device = r.device
         params = detinit.deterministic_params(seed, A, nq)
@@ -29,6 +32,10 @@ class Learner:
         self.packed = r.new_packed()
         self.ws = r.new_workspace()
         self.grads = torch.zeros(r.n_params, device=self.device)
+        self.lr = lr
+        self.exp_avg = torch.zeros_like(self.grads)
+        self.exp_avg_sq = torch.zeros_like(self.grads)
+        self.opt_steps = 0
         self.basis = SpatialBasis(r.h, r.w).S.to(self.device).contiguous()
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -54,3 +61,13 @@ class Learner:
         for w in works:
             w.wait()
         return logits, values
+
+    def optimizer_step(self):
+        """Adam (lr=1e-3, torch defaults; main_mp.py:92) on the flat params, one launch."""
+        self.opt_steps += 1
+        adam_flat_(self.flat, self.grads, self.exp_avg, self.exp_avg_sq, self.opt_steps, lr=self.lr)
+
+    def train_step(self, frames, dlogits, dvalues, overlap: bool = True):
+        out = self.step(frames, dlogits, dvalues, overlap=overlap)
+        self.optimizer_step()
+        return out
