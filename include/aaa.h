@@ -169,6 +169,18 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
                   const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream);
 
+/* ---- REINFORCE loss ----
+ * finish_episode's loss (reference main_mp.py:62-77) for B independent
+ * episodes of T steps, on device: discounted returns R_t = r_t + gamma R_{t+1}
+ * (double, then fp32), normalised (R - mean) / (std_unbiased + FLT_EPSILON)
+ * into returns_norm (T, B); loss[b] = sum_t -log pi(a_t) R^_t with pi =
+ * Categorical(softmax(logits_t)) and its probability clamp to [eps, 1-eps]
+ * (main_mp.py:55-58); dlogits (T, B, A) = d(sum_b loss[b]) / d logits, the
+ * cotangent aaa_backward takes.  logits (T, B, A) fp32, actions (T, B) int32
+ * in [0, A), rewards (T, B) fp32; every pointer is device memory. */
+int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, const float* rewards, double gamma,
+                  float* loss, float* returns_norm, float* dlogits, hipStream_t stream);
+
 /* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
 
 /* NHWC convolution y[n,oy,ox,co] = b[co] + sum w[co,ky,kx,ci] x[n,iy,ix,ci]

@@ -100,3 +100,18 @@ def test_adam_optimizer_has_no_cpu_fallback():
     p.grad = torch.ones(4)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         Adam([p]).step()
+
+
+def test_reinforce_rejects_bad_args_without_gpu():
+    lib = N.load()
+    assert lib.aaa_reinforce(0, 1, 18, 16, 16, 16, 0.99, 16, 16, 16, None) == -1
+    assert lib.aaa_reinforce(4, 1, 18, None, 16, 16, 0.99, 16, 16, 16, None) == -1
+    assert lib.aaa_reinforce(4, 1, 18, 16, 16, 16, 1.5, 16, 16, 16, None) == -1
+    assert b"gamma" in lib.aaa_last_error()
+
+
+def test_reinforce_loss_has_no_cpu_fallback():
+    import torch
+    from aaa_amd.reinforce import reinforce_loss
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        reinforce_loss(torch.zeros(3, 1, 18), [0, 1, 2], [1.0, 0.0, 1.0])

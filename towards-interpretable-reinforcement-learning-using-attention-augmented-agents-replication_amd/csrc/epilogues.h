@@ -5,6 +5,13 @@
 
 namespace aaa {
 
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{a, b, c, d};
+}
+__device__ __forceinline__ void store4(__bf16* p, float a, float b, float c, float d) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+}
+
 // out[j*ld + i + e] = v[e] (+ bias[i+e]) (relu?)  -- D stored transposed, e.g.
 // a conv output [pixel][channel] or a linear output [row][feature].
 template <typename OT>
@@ -161,7 +168,16 @@ struct EpiConvLstmFwd {
 
 // ConvLSTM backward step epilogue on D[c'][m] = dgrad of dz_t into [x_t | h_{t-1}]:
 // rows c' < 64 -> dx_t (conv2 output grad); rows >= 64 -> dh_{t-1}, fused with
-// the gate backward of step t-1 (writes dz_{t-1} and the dc carry), or dh0.
+// the gate backward of step t-1 (writes dz_{t-1} as TZ -- the GEMM operand type
+// of the later dgrad / wgrad passes -- and the dc carry), or dh0.
+//
+// Gate-bias gradient (sum of dz over pixels): with ``part`` set, every thread
+// sums the fp32 dz it produces (Acc), and flush() reduces them over the
+// workgroup's columns into one 4*BI-wide row part[tile_j][4*(row0-64) ...] --
+// the bias gradient then needs only a column sum over T x (column tiles) rows
+// instead of a pass over the whole dZ tensor, and it is taken before dz is
+// rounded to TZ (the reference sums fp32 gradients).
+template <typename TZ>
 struct EpiConvLstmBwd {
   float* dx;            // [M][64]  dY2 slot t
   const float* gates;   // [M][512] slot t-1
@@ -169,13 +185,15 @@ struct EpiConvLstmBwd {
   const float* ccur;    // [M][128] c_{t-1}
   const float* dO;      // [M][128] attention-path grad of h_{t-1}
   float* dC;            // [M][128] dc carry (in/out)
-  float* dz;            // [M][512] slot t-1
+  TZ* dz;               // [M][512] slot t-1
   float* dh0;           // [M][128] or null (only when t == 0)
   int has_prev, Nj;
   int ioff;             // 64 when the GEMM computes only the h rows (dx batched separately)
+  float* part;          // [column tiles][512] bias partials of slot t-1, or null
   // Inputs of one (4-row, column) group of the fused gate backward, loadable
   // before the K loop (glds.h); only the has_prev h-row path has any.
   struct Pre { f32x4 g[4], dov, cp, cc, dcv; };
+  struct Acc { f32x4 s[4]; };   // dz sums of the thread's 4 channels x 4 gates
   __device__ __forceinline__ Pre prefetch(int i, int j) const {
     Pre p;
     i += ioff;
@@ -189,7 +207,8 @@ struct EpiConvLstmBwd {
     for (int e = 0; e < 4; ++e) p.g[e] = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + 4 * (ch + e));
     return p;
   }
-  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre& p) const {
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre& p,
+                                         Acc* acc = nullptr) const {
     i += ioff;
     if (j >= Nj || i >= 192) return;
     if (i < 64) {
@@ -208,12 +227,35 @@ struct EpiConvLstmBwd {
       float dc = dcv[e], di, df, dcg, dout;
       gate_bwd(v[e] + p.dov[e], p.g[e], p.cp[e], p.cc[e], dc, di, df, dcg, dout);
       dcv[e] = dc;
-      *reinterpret_cast<f32x4*>(dz + (size_t)j * 512 + 4 * (ch + e)) = f32x4{di, df, dcg, dout};
+      store4(dz + (size_t)j * 512 + 4 * (ch + e), di, df, dcg, dout);
+      if (acc) {
+        acc->s[e][0] += di; acc->s[e][1] += df; acc->s[e][2] += dcg; acc->s[e][3] += dout;
+      }
     }
     *reinterpret_cast<f32x4*>(dC + (size_t)j * 128 + ch) = dcv;
   }
   __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
     finish(i, j, v0, v1, v2, v3, prefetch(i, j));
+  }
+  // Workgroup reduction of the Acc of threads that share a row group (r4 =
+  // tid % G4: the pipe kernel's epilogue walks columns with a fixed row group
+  // per thread when NT % G4 == 0), then one row of partials per column tile.
+  template <int G4, int NT>
+  __device__ __forceinline__ void flush(const Acc& acc, float* red, int i0, int tj) const {
+    static_assert(NT % G4 == 0, "fixed row group per thread");
+    constexpr int NS = NT / G4;            // threads per row group
+    if (!part || !has_prev) return;
+    const int r4 = threadIdx.x % G4, sl = threadIdx.x / G4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) *reinterpret_cast<f32x4*>(red + (sl * G4 + r4) * 16 + 4 * e) = acc.s[e];
+    __syncthreads();
+    const int row0 = i0 + ioff - 64;       // first dh channel of this tile
+    for (int c = threadIdx.x; c < G4 * 16; c += NT) {
+      float t = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < NS; ++k) t += red[k * G4 * 16 + c];
+      if (row0 >= 0 && row0 * 4 + c < 512) part[(size_t)tj * 512 + row0 * 4 + c] = t;
+    }
   }
 };
 

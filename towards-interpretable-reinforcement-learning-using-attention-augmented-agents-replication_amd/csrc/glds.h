@@ -47,6 +47,12 @@ template <class EP, class = void> struct has_pre : std::false_type {};
 template <class EP> struct has_pre<EP, std::void_t<typename EP::Pre>> : std::true_type {};
 template <class EP, bool> struct pre_of { using type = int; };
 template <class EP> struct pre_of<EP, true> { using type = typename EP::Pre; };
+// Epilogues with a per-thread accumulator (EP::Acc) get it passed to finish()
+// and reduced by EP::flush<G4, NT>() after the epilogue (e.g. bias partials).
+template <class EP, class = void> struct has_acc : std::false_type {};
+template <class EP> struct has_acc<EP, std::void_t<typename EP::Acc>> : std::true_type {};
+template <class EP, bool> struct acc_of { using type = int; };
+template <class EP> struct acc_of<EP, true> { using type = typename EP::Acc; };
 
 #ifdef AAA_STAMPS
 // Diagnostic builds only (tools/ubench): per-workgroup phase timestamps
@@ -307,6 +313,8 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
             f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
       }
   __syncthreads();
+  constexpr bool ACC = has_acc<EP>::value && PRE && C::NT % G4 == 0;
+  typename acc_of<EP, ACC>::type eacc{};
 #pragma unroll
   for (int q = 0; q < NPT; ++q) {
     const int c = q * C::NT + (int)threadIdx.x;
@@ -318,9 +326,15 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
         const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
         v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
       }
-      if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
+      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q], &eacc);
+      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
       else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
     }
+  }
+  if constexpr (ACC) {
+    static_assert(C::NT * 16 * sizeof(float) <= sizeof(smem), "accumulator reduction does not fit in LDS");
+    __syncthreads();                          // every thread is done reading E
+    ep.template flush<G4, C::NT>(eacc, reinterpret_cast<float*>(smem), i0, tj);
   }
   AAA_STAMP(3);
 }

@@ -34,9 +34,10 @@ hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st);
-hipError_t colsum(const float* X, int ld, int M, int N, float* out, hipStream_t st);
-hipError_t gate_bwd_last(int M, const float* dO, const float* dhT, const float* gates, const float* cprev,
-                         const float* ccur, float* dC, float* dz, hipStream_t st);
+template <typename TI> hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st);
+template <typename TZ>
+hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const float* gates, const float* cprev,
+                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
 template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);

@@ -271,14 +271,15 @@ __global__ void k_query_outer(const float* __restrict__ a, int N, const float* _
 }
 
 // out[n] += sum_{m} X[m*ld + n]; grid (ceil(N/64), nsplit), 256 threads.
-__global__ void k_colsum(const float* __restrict__ X, int ld, int M, int N, int rows_per, float* out) {
+template <typename TI>
+__global__ void k_colsum(const TI* __restrict__ X, int ld, int M, int N, int rows_per, float* out) {
   __shared__ float red[256];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float s = 0.f;
   if (col < N) {
 #pragma unroll 8
-    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += X[(size_t)r * ld + col];
+    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += (float)X[(size_t)r * ld + col];
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -289,17 +290,37 @@ __global__ void k_colsum(const float* __restrict__ X, int ld, int M, int N, int 
 }
 
 // Gate backward of the LAST step (t = T-1): dh = dO + dhT, dc = carry (dcT).
-__global__ void k_gate_bwd_last(int n, const float* __restrict__ dO, const float* __restrict__ dhT,
-                                const float* __restrict__ gates, const float* __restrict__ cprev,
-                                const float* __restrict__ ccur, float* dC, float* dz) {
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int m = idx >> 7, ch = idx & 127;
+// One workgroup per tile of ``bj`` pixels (the BPTT GEMM's column tile), 128
+// channels x 4 pixel lanes; dz is stored as TZ and, when ``part`` is set, the
+// tile's fp32 gate-bias partials go to part[tile][512] (EpiConvLstmBwd::flush).
+template <typename TZ>
+__global__ void __launch_bounds__(512)
+k_gate_bwd_last(int M, int bj, const float* __restrict__ dO, const float* __restrict__ dhT,
+                const float* __restrict__ gates, const float* __restrict__ cprev, const float* __restrict__ ccur,
+                float* dC, TZ* dz, float* part) {
+  __shared__ f32x4 red[4][128];
+  const int ch = threadIdx.x & 127, sl = threadIdx.x >> 7;
+  const int m0 = blockIdx.x * bj, m1 = min(M, m0 + bj);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int m = m0 + sl; m < m1; m += 4) {
+    const size_t idx = (size_t)m * 128 + ch;
     const float dh = dO[idx] + (dhT ? dhT[idx] : 0.f);
     const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
     float dc = dC[idx], di, df, dcg, dout;
     gate_bwd(dh, g, cprev[idx], ccur[idx], dc, di, df, dcg, dout);
     dC[idx] = dc;
-    *reinterpret_cast<f32x4*>(dz + (size_t)m * 512 + 4 * ch) = f32x4{di, df, dcg, dout};
+    store4(dz + (size_t)m * 512 + 4 * ch, di, df, dcg, dout);
+    acc[0] += di; acc[1] += df; acc[2] += dcg; acc[3] += dout;
+  }
+  if (!part) return;
+  red[sl][ch] = acc;
+  __syncthreads();
+  if (sl == 0) {
+    f32x4 t = red[0][ch];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) { t[0] += red[k][ch][0]; t[1] += red[k][ch][1]; t[2] += red[k][ch][2]; t[3] += red[k][ch][3]; }
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * 512 + 4 * ch) = t;
   }
 }
 
@@ -316,6 +337,7 @@ __global__ void k_concat_dy(int F, int A, int ldy, const float* dl, const float*
 }
 
 // XH slot 0 channels 64..191 <- h0 (or zero)
+
 template <typename T>
 __global__ void k_state_to_xh(int M, const float* h0, T* xh) {
   const int n = M * 128;
@@ -624,21 +646,23 @@ hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int an
   return hipGetLastError();
 }
 
-hipError_t colsum(const float* X, int ld, int M, int N, float* out, hipStream_t st) {
+template <typename TI>
+hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const int cols = (N + 63) / 64;
   int split = (1024 + cols - 1) / cols;
   int rows_per = (M + split - 1) / split;
   if (rows_per < 64) rows_per = 64;
   split = (M + rows_per - 1) / rows_per;
-  hipLaunchKernelGGL(k_colsum, dim3(cols, split), dim3(256), 0, st, X, ld, M, N, rows_per, out);
+  hipLaunchKernelGGL(k_colsum<TI>, dim3(cols, split), dim3(256), 0, st, X, ld, M, N, rows_per, out);
   return hipGetLastError();
 }
 
-hipError_t gate_bwd_last(int M, const float* dO, const float* dhT, const float* gates, const float* cprev,
-                         const float* ccur, float* dC, float* dz, hipStream_t st) {
-  hipLaunchKernelGGL(k_gate_bwd_last, dim3(nblk((long)M * 128)), dim3(256), 0, st, M * 128, dO, dhT, gates,
-                     cprev, ccur, dC, dz);
+template <typename TZ>
+hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const float* gates, const float* cprev,
+                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st) {
+  hipLaunchKernelGGL(k_gate_bwd_last<TZ>, dim3((M + bj - 1) / bj), dim3(512), 0, st, M, bj, dO, dhT, gates, cprev,
+                     ccur, dC, dz, part);
   return hipGetLastError();
 }
 
@@ -722,6 +746,12 @@ hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st) {
   hipLaunchKernelGGL(k_unpack_conv1_rgbx, dim3(nblk(32 * 3 * 64)), dim3(256), 0, st, g, dst);
   return hipGetLastError();
 }
+template hipError_t colsum<float>(const float*, int, int, int, float*, hipStream_t);
+template hipError_t colsum<__bf16>(const __bf16*, int, int, int, float*, hipStream_t);
+template hipError_t gate_bwd_last<float>(int, int, const float*, const float*, const float*, const float*, const float*,
+                                         float*, float*, float*, hipStream_t);
+template hipError_t gate_bwd_last<__bf16>(int, int, const float*, const float*, const float*, const float*,
+                                          const float*, float*, __bf16*, float*, hipStream_t);
 template hipError_t frames_rgbx<float>(long, const float*, float*, hipStream_t);
 template hipError_t frames_rgbx<__bf16>(long, const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t);

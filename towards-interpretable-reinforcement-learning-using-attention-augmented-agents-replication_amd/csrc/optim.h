@@ -26,4 +26,8 @@ struct AdamHost {
 int adam_chunks(size_t numel);
 hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st);
 
+// loss.hip: REINFORCE (finish_episode) loss + logits cotangent, one workgroup per episode
+hipError_t reinforce_launch(int T, int B, int A, const float* logits, const int* actions, const float* rewards,
+                            double gamma, float* loss, float* rn, float* dlogits, hipStream_t st);
+
 }  // namespace aaa

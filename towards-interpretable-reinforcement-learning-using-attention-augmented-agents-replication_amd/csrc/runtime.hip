@@ -68,7 +68,7 @@ struct Layout {
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
-  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dY2, dY1;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
 };
 
@@ -143,7 +143,8 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.dO = take(F * P * 128 * 4);
   L.dQp = take(F * L.qd * 4);
   L.dC = take(M * 128 * 4);
-  L.dZ = take(F * P * 512 * 4);
+  L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
+  L.dZp = take((size_t)L.T * ((M + 31) / 32) * 512 * 4);  // gate-bias partials per (step, column tile)
   L.dY2 = take(F * P * 64 * 4);
   L.dY1 = take(F * L.P1 * 32 * 4);
   // zero-initialised (atomic) accumulation region: one memset covers it
@@ -320,11 +321,19 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
   const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : T);
   return std::max(1, std::min(c, T));
 }
-static int step_tile(long out_tiles32, const char* env, bool bptt) {
+static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
-  if (v >= 0) return v;
+  if (v >= 0) return (v == 7 && !bf16) ? 4 : v;   // tile 7 exists for bf16 only
+  if (bptt && bf16) return 7;
   if (bptt) return out_tiles32 < 1024 ? 4 : (out_tiles32 < 1536 ? 1 : 0);   // C2: 484 tiles, 66 us (reg 71)
   return out_tiles32 < 1024 ? 5 : 4;                                          // C2: 1936 tiles, 56 us (reg 58)
+}
+
+// Whether the LDS-DMA ring can run tile config CK (every wave issues the same DMA count).
+template <class CK>
+constexpr bool pipe_even() {
+  constexpr int VG = 16 / (int)sizeof(typename CK::type);
+  return (CK::BI * CK::BK / VG) % CK::NT == 0 && (CK::BJ * CK::BK / VG) % CK::NT == 0;
 }
 
 // One per-step ConvLSTM GEMM: D[Mi][M] = W[Mi][K] x im2col(src)[K][M] with
@@ -333,7 +342,7 @@ static int step_tile(long out_tiles32, const char* env, bool bptt) {
 template <class CK, bool PIPE, typename T, typename G, class EP, int NBUF = 2, bool ILV = false>
 static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const ConvGeo& g, int M, uint32_t src_bytes,
                             const EP& ep, int Mi, int K, hipStream_t st) {
-  if constexpr (PIPE && std::is_same<G, T>::value) {
+  if constexpr (PIPE && pipe_even<CK>() && std::is_same<G, T>::value) {
     using LA = GRowsB<T, CK::BI, CK::BK, CK::NT>;
     using LB = GIm2colB<T, CK::BJ, CK::BK, CK::NT>;
     return launch_pipe<CK, LA, LB, EP, NBUF, ILV>(typename LA::Params{W, ldw, wrows},
@@ -683,10 +692,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   auto core_chunk = [&](int lo, int hi, hipStream_t s) -> int {
     const int rows = (hi - lo) * M;                       // pixels of these frames
     const int F1 = (hi - lo) * L.B;                       // frames
-    const float* dz = Wf(L.dZ) + (size_t)lo * M * 512;
+    const T* dz = Wt(L.dZ) + (size_t)lo * M * 512;
     auto wgrad_lstm = [&](auto cfg) -> int {   // all 8 ConvLSTM weight grads: D[512][1728] += dZ^T * im2col(XH)
       using CW = decltype(cfg);
-      using LA = LdRowsTB<float, T, CW::BI, CW::BK, CW::NT>;
+      using LA = LdRowsTB<T, T, CW::BI, CW::BK, CW::NT>;
       using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
       typename LA::Params pa{dz, 512, 512, rows};
       typename LB::Params pb{Wt(L.XH) + (size_t)lo * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(),
@@ -703,13 +712,12 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
       if (rc) return rc;
     }
-    HIPCHK(colsum(dz, 512, rows, 512, Wf(L.gbl), s));
     {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
       // 64x64 tiles (64x128 measured slower: occupancy)
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
       const T* WdT = (const T*)(pk + L.k_WdTl);
-      const uint32_t zb = (uint32_t)((size_t)rows * 512 * 4);
+      const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
       HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
                              : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
     }
@@ -745,13 +753,20 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
     const int t1 = L.T - 1;
-    HIPCHK(gate_bwd_last(M, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
-                         Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
-                         Wf(L.dZ) + (size_t)t1 * M * 512, st));
     // Sequential part: only the h rows (dh_{t-1}, fused with the gate backward
     // of step t-1); everything else runs in chunks off the chain.
-    const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true);
-    const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * 4);  // one step slice of dZ
+    const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
+    // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
+    // the register-staged ones leave the bias to a column sum over dZ
+    const int bj = bwd_tile == 7 ? 128 : 64;
+    const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
+                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7;
+    const int ntj = cdiv(M, bj);
+    float* part = pipe ? Wf(L.dZp) : nullptr;
+    HIPCHK(gate_bwd_last<T>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
+                            Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
+                            Wt(L.dZ) + (size_t)t1 * M * 512, part ? part + (size_t)t1 * ntj * 512 : nullptr, st));
+    const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * L.esz);  // one step slice of dZ
     const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
     int done_hi = L.T;   // chunks [lo, done_hi) not yet issued
     auto flush = [&](int ready_lo) -> int {   // dz of steps >= ready_lo are final
@@ -770,32 +785,41 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       const bool prev = t > 0;
       if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
-      EpiConvLstmBwd ep{nullptr,
-                        prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
-                        prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
-                        Wf(L.Cst) + (size_t)t * M * 128,
-                        prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
-                        Wf(L.dC),
-                        prev ? Wf(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
-                        prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64};
-      const float* dzt = Wf(L.dZ) + (size_t)t * M * 512;
+      EpiConvLstmBwd<T> ep{nullptr,
+                           prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
+                           prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
+                           Wf(L.Cst) + (size_t)t * M * 128,
+                           prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
+                           Wf(L.dC),
+                           prev ? Wt(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
+                           prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64,
+                           part && prev ? part + (size_t)(t - 1) * ntj * 512 : nullptr};
+      const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
+      using EB = EpiConvLstmBwd<T>;
       hipError_t e;
       switch (bwd_tile) {
         case 1: e = step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 2: e = step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 3: e = step_gemm<CfgK4BFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 4:   // 3-stage ring, DMA interleaved with the MFMAs (tools/ubench/step_ablate: 57.9 vs 59.4 us)
-          e = step_gemm<CfgK4BFor<T>, true, T, float, EpiConvLstmBwd, 3, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
-                                                                               128, 4608, st);
+          e = step_gemm<CfgK4BFor<T>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
           break;
         case 5: e = step_gemm<CfgK4For<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
         case 6: e = step_gemm<C, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
+        case 7:   // bf16: 128x128, BK128, 2-way in-WG split-K (tools/ubench/bf16_tiles: 48 vs 53-60 us at C3)
+          if constexpr (std::is_same<T, float>::value) e = hipErrorInvalidValue;
+          else e = step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                       4608, st);
+          break;
         default: e = step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
       }
       HIPCHK(e);
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
+    // gate-bias gradient: column sum of the per-(step, tile) partials, or of dZ itself
+    if (part) HIPCHK(colsum<float>(part, 512, L.T * ntj, 512, Wf(L.gbl), st));
+    else HIPCHK(colsum<T>(Wt(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     if (ax) HIPCHK(stream_order(ax, st));   // join
     LstmGrads lg;
@@ -1096,6 +1120,18 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
     }
     HIPCHK(adam_launch(tab, nch, h, stream));
   }
+  return AAA_OK;
+}
+
+int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, const float* rewards, double gamma,
+                  float* loss, float* returns_norm, float* dlogits, hipStream_t stream) {
+  if (T < 1 || B < 1 || A < 1) return fail(AAA_E_ARG, "reinforce: need T, B, A >= 1 (T=%d B=%d A=%d)", T, B, A);
+  if (!logits || !actions || !rewards || !loss || !returns_norm || !dlogits)
+    return fail(AAA_E_ARG, "reinforce: NULL argument");
+  if (!(gamma >= 0.0 && gamma <= 1.0)) return fail(AAA_E_ARG, "reinforce: gamma must be in [0, 1]");
+  int r = check_device();
+  if (r) return r;
+  HIPCHK(reinforce_launch(T, B, A, logits, actions, rewards, gamma, loss, returns_norm, dlogits, stream));
   return AAA_OK;
 }
 
