@@ -22,9 +22,12 @@
 
 namespace aaa {
 
+// Row-contiguous bf16 tiles are read with ds_read_b64_tr_b16 (frag_bf16): a
+// 32-lane half reads 4 k-rows x 64 B, so the row pitch is padded to 16 dwords
+// mod 64 banks (+32 elements) to keep those reads conflict-free.
 template <typename T, int R, int BK, bool KC>
 struct Tile {
-  static constexpr int PAD = 16 / (int)sizeof(T);
+  static constexpr int PAD = (!KC && sizeof(T) == 2) ? 32 : 16 / (int)sizeof(T);
   static constexpr int LD = KC ? (BK + PAD) : (R + PAD);
   static constexpr int ELEMS = (KC ? R : BK) * LD;
   __device__ static __forceinline__ int off(int r, int k) { return KC ? r * LD + k : k * LD + r; }
@@ -325,15 +328,24 @@ __device__ __forceinline__ void frag_f32(const float* t, int r, int k, float (&a
   }
 }
 
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
 template <typename TL>
 __device__ __forceinline__ bf16x8 frag_bf16(const __bf16* t, int r, int k) {
   if constexpr (TL::KC_) {
     return *reinterpret_cast<const bf16x8*>(t + r * TL::LD + k);
   } else {
-    bf16x8 a;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) a[kk] = t[(k + kk) * TL::LD + r];
-    return a;
+    // [k][r] image: two hardware transpose reads.  In each 16-lane group (one
+    // h, rows c0..c0+15) lane 4q+p addresses k-row k+q, columns c0+4p..+3 and
+    // receives column c0 + (lane & 15) of the 4 k-rows.
+    const int li = (int)(threadIdx.x & 15), q = li >> 2, p = li & 3;
+    const __bf16* a0 = t + (k + q) * TL::LD + (r - li) + 4 * p;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(a0)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(a0 + 4 * TL::LD)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
   }
 }
 
