@@ -206,7 +206,8 @@ struct LdIm2colB {
 };
 
 // Weight-gradient gather: rows = k' = (tap, ci) fixed per thread, k = output
-// pixel m (forward geometry).  Cin % VG == 0.
+// pixel m (forward geometry).  Cin % VG == 0, or (conv1's bordered bf16 RGBx
+// image) a chunk spanning adjacent taps of one kernel row that are all in bounds.
 template <typename G, typename T, int R, int BK, int NT>
 struct LdIm2colTB {
   static constexpr bool KC = false;

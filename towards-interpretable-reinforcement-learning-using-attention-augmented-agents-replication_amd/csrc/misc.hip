@@ -360,14 +360,26 @@ __global__ void k_pack_conv(const float* __restrict__ w, int Cout, int Cin, int 
   }
 }
 
-// Frames (F,H,W,3) -> (F,H,W,4) with a zero 4th channel, so conv1's gather
-// is 16-byte vectors (Cin 4) instead of scalar loads (Cin 3).
+// Frames (F,H,W,3) -> (F,H+2,W+2,4): a zero 4th channel (conv1's gather is
+// 16-byte vectors instead of scalar loads) and conv1's one-pixel zero padding
+// stored in the image, so every tap of the conv reads in-bounds memory -- a
+// bf16 16-byte chunk (two adjacent taps x 4 channels) never straddles the
+// image border.  Raw pixels 0..255 are exact in bf16; other values are
+// rounded exactly where the bf16 oracle rounds conv1's input.
 template <typename T>
-__global__ void k_frames_rgbx(long npix, const float* __restrict__ x, T* __restrict__ y) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < npix; i += (long)gridDim.x * blockDim.x) {
-    const float* s = x + i * 3;
-    T* d = y + i * 4;
-    d[0] = (T)s[0]; d[1] = (T)s[1]; d[2] = (T)s[2]; d[3] = (T)0.f;
+__global__ void k_frames_rgbx(int F, int H, int W, const float* __restrict__ x, T* __restrict__ y) {
+  const int Hp = H + 2, Wp = W + 2;
+  const long n = (long)F * Hp * Wp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int f = (int)(i / (Hp * Wp)), r = (int)(i - (long)f * Hp * Wp);
+    const int py = r / Wp, px = r - py * Wp;
+    const int iy = py - 1, ix = px - 1;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      const float* s = x + (((long)f * H + iy) * W + ix) * 3;
+      v0 = s[0]; v1 = s[1]; v2 = s[2];
+    }
+    store4(y + i * 4, v0, v1, v2, 0.f);
   }
 }
 
@@ -728,8 +740,8 @@ hipError_t unpack_f32(const F32Unpack& p, hipStream_t st) {
 }
 
 template <typename T>
-hipError_t frames_rgbx(long npix, const float* x, T* y, hipStream_t st) {
-  hipLaunchKernelGGL(k_frames_rgbx<T>, dim3(nblk(npix)), dim3(256), 0, st, npix, x, y);
+hipError_t frames_rgbx(int F, int H, int W, const float* x, T* y, hipStream_t st) {
+  hipLaunchKernelGGL(k_frames_rgbx<T>, dim3(nblk((long)F * (H + 2) * (W + 2))), dim3(256), 0, st, F, H, W, x, y);
   return hipGetLastError();
 }
 template <typename T>
@@ -752,8 +764,8 @@ template hipError_t gate_bwd_last<float>(int, int, const float*, const float*, c
                                          float*, float*, float*, hipStream_t);
 template hipError_t gate_bwd_last<__bf16>(int, int, const float*, const float*, const float*, const float*,
                                           const float*, float*, __bf16*, float*, hipStream_t);
-template hipError_t frames_rgbx<float>(long, const float*, float*, hipStream_t);
-template hipError_t frames_rgbx<__bf16>(long, const float*, __bf16*, hipStream_t);
+template hipError_t frames_rgbx<float>(int, int, int, const float*, float*, hipStream_t);
+template hipError_t frames_rgbx<__bf16>(int, int, int, const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t);
 template hipError_t pack_conv2_classes<__bf16>(const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv1_rgbx<float>(const float*, float*, hipStream_t);

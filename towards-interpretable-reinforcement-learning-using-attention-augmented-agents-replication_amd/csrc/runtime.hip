@@ -118,7 +118,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   // workspace
   p = 0;
   const size_t F = L.F, P = L.P, M = (size_t)L.B * L.P;
-  L.Xp = take(F * L.H * L.W * 4 * 4);  // frames as RGBx fp32
+  L.Xp = take(F * (L.H + 2) * (L.W + 2) * 4 * e);  // frames as zero-bordered RGBx (conv1 operand type)
   L.Y1 = take(F * L.P1 * 32 * e);
   L.XH = take((size_t)(L.T + 1) * M * 192 * e);
   L.Hs = take(F * P * 128 * 4);
@@ -423,26 +423,19 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   auto Wt = [&](size_t off) { return (T*)(ws + off); };
   const int F = L.F, P = L.P, M = L.B * L.P;
 
-  {  // conv1 (attention.py:156-162): frames -> RGBx (Cin 4) -> Y1
-    HIPCHK(frames_rgbx<float>((long)F * L.H * L.W, io->frames, Wf(L.Xp), st));
-    using C3 = Cfg32For<T>;
-    using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
-    using LB = LdIm2colB<float, T, C3::BJ, C3::BK, C3::NT>;
-    typename LA::Params pa{(const T*)(pk + L.k_Wp1), 256, 32};
-    typename LB::Params pb{Wf(L.Xp), ConvGeo{4, 4, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), F * L.P1,
-                           (uint32_t)((size_t)F * L.H * L.W * 4 * 4)};
+  {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
+    HIPCHK(frames_rgbx<T>(F, L.H, L.W, io->frames, Wt(L.Xp), st));
+    // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
+    constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
+    using CP = GemmCfg<T, 32, 128, BKc, 1, 4>;
+    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
     EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    if constexpr (std::is_same<T, float>::value) {
-      // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
-      using CP = GemmCfg<float, 32, 128, 32, 1, 4>;
-      using PA = GRowsB<float, CP::BI, CP::BK, CP::NT>;
-      using PB = GIm2colB<float, CP::BJ, CP::BK, CP::NT>;
-      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(typename PA::Params{pa.src, pa.ld, pa.nrows},
-                                                       typename PB::Params{pb.src, pb.g, pb.nrows, pb.src_bytes}, ep,
-                                                       32, F * L.P1, 256, 1, st)));
-    } else {   // bf16: the fp32 RGBx frames are rounded while staging (register path)
-      HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, F * L.P1, 256, 1, st)));
-    }
+    HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
+        typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
+        typename PB::Params{Wt(L.Xp), ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
+                            (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
+        ep, 32, F * L.P1, 256, 1, st)));
   }
   {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
     using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
@@ -581,14 +574,14 @@ static int conv2_dgrad(const Layout& L, const char* pk, const float* dy2, float*
 
 // conv1 weight gradient over RGBx frames (Cin 4; the 4th channel's grad is dropped on unpack)
 template <typename T>
-static int conv1_wgrad(const Layout& L, const float* dy1, const float* xp, int frames, float* gW, hipStream_t s) {
+static int conv1_wgrad(const Layout& L, const float* dy1, const T* xp, int frames, float* gW, hipStream_t s) {
   using C3 = Cfg32For<T>;
   using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
-  using LB = LdIm2colTB<float, T, C3::BJ, C3::BK, C3::NT>;
+  using LB = LdIm2colTB<T, T, C3::BJ, C3::BK, C3::NT>;   // bf16 chunks = 2 taps x 4 ch, in-bounds (bordered image)
   const int rows1 = frames * L.P1;
   typename LA::Params pa{dy1, 32, 32, rows1};
-  typename LB::Params pb{xp, ConvGeo{4, 4, 0, L.H, L.W, L.H1, L.W1, 8, 4, 1, 0}.prep(), 256,
-                         (uint32_t)((size_t)frames * L.H * L.W * 4 * 4)};
+  typename LB::Params pb{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
+                         (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
   EpiStore<true> ep{gW, 256, 32, 256};
   const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
   HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
@@ -738,7 +731,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
       int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, s);
-      if (!rc) rc = conv1_wgrad<T>(L, dy1, Wf(L.Xp) + (size_t)lo * L.B * L.H * L.W * 4, F1, Wf(L.gWp1), s);
+      if (!rc) rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
       if (rc) return rc;
       HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
@@ -846,7 +839,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       }
       {
         int rc = conv2_dgrad<T>(L, pk, Wf(L.dY2), Wf(L.dY1), F, st);
-        if (!rc) rc = conv1_wgrad<T>(L, Wf(L.dY1), Wf(L.Xp), F, Wf(L.gWp1), st);
+        if (!rc) rc = conv1_wgrad<T>(L, Wf(L.dY1), Wt(L.Xp), F, Wf(L.gWp1), st);
         if (rc) return rc;
         HIPCHK(colsum(Wf(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
