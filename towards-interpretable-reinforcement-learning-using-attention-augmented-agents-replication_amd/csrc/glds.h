@@ -170,6 +170,77 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
   return *reinterpret_cast<const bf16x8*>(t + r * BK + (((kofs >> 3) ^ g) << 3));
 }
 
+// Epilogue through LDS, shared by the ring GEMM and the halo conv (halo.h).
+// Every wave (all WK groups) stores its partial tile pixel-major, E[wk][j][i];
+// then the whole workgroup walks the tile in 4-row groups with consecutive
+// lanes on consecutive row groups of ONE column, so the epilogue's global
+// loads/stores (gate activations, cell state, outputs: all [pixel][channel])
+// are contiguous per column instead of one 16-B access per lane at a 2 KB
+// stride, and all waves share it.  ``smem`` must hold WK*BJ*(BI+4) floats.
+template <class C, class EP, bool PRE, typename T, int MI, int MJ, class PreT, int NPT>
+__device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32x16 (&acc)[MI][MJ], int i0, int j0,
+                                                int tj, const PreT (&pre)[NPT]) {
+  constexpr int BI = C::BI, BJ = C::BJ, WI = C::WI, WJ = C::WJ, WK = C::WK;
+  constexpr int WTI = BI / WI, WTJ = BJ / WJ;
+  constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
+  constexpr int G4 = BI / 4, NG = G4 * BJ;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wk = wave / (WI * WJ), wr = wave - wk * (WI * WJ);
+  const int wi = wr / WJ, wj = wr - (wr / WJ) * WJ;
+  const int r32 = lane & 31, h = lane >> 5;
+  float* E = reinterpret_cast<float*>(smem);
+  barrier_lds();                              // every wave is done reading the last stage
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = wi * WTI + a * 32 + 8 * g + 4 * h;
+        const int j = wj * WTJ + b * 32 + r32;
+        *reinterpret_cast<f32x4*>(E + (wk * BJ + j) * ELD + i) =
+            f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+      }
+  __syncthreads();
+  constexpr bool ACC = has_acc<EP>::value && PRE && C::NT % G4 == 0;
+  typename acc_of<EP, ACC>::type eacc{};
+#pragma unroll
+  for (int q = 0; q < NPT; ++q) {
+    const int c = q * C::NT + (int)threadIdx.x;
+    if (NG % C::NT == 0 || c < NG) {
+      const int r4 = c % G4, j = c / G4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(E + j * ELD + 4 * r4);
+#pragma unroll
+      for (int w = 1; w < WK; ++w) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
+        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+      }
+      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q], &eacc);
+      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
+      else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
+    }
+  }
+  if constexpr (ACC) {
+    __syncthreads();                          // every thread is done reading E
+    ep.template flush<G4, C::NT>(eacc, E, i0, tj);
+  }
+}
+
+// Epilogue inputs of this thread's (4-row group, column) items, requested
+// before the K loop (vmcnt retires in issue order; the compiler waits for
+// these ordinary loads only at their use after the loop).
+template <class C, class EP, bool PRE, class PreT, int NPT>
+__device__ __forceinline__ void epilogue_prefetch(const EP& ep, int i0, int j0, PreT (&pre)[NPT]) {
+  constexpr int G4 = C::BI / 4, NG = G4 * C::BJ;
+  if constexpr (PRE) {
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int c = q * C::NT + (int)threadIdx.x;
+      if (NG % C::NT == 0 || c < NG) pre[q] = ep.prefetch(i0 + 4 * (c % G4), j0 + c / G4);
+    }
+  }
+}
+
 // ABL (diagnostic builds only, tools/ubench): bit 0 = no in-loop DMA, bit 1 =
 // no MFMA, bit 2 = no epilogue.  Production launches use ABL = 0.
 // ILV: issue the next tile's DMA between the MFMA groups of this tile (A
@@ -190,6 +261,8 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
   constexpr int EPI_T = (int)((WK * BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STG > EPI_T ? NBUF * STG : EPI_T];
+  static_assert(!has_acc<EP>::value || C::NT * 16 * sizeof(float) <= sizeof(smem),
+                "accumulator reduction does not fit in LDS");
   AAA_STAMP(0);
 
   int ti, tj, tz;
@@ -222,13 +295,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   constexpr bool PRE = has_pre<EP>::value && (ABL & 4) == 0;
   using PreT = typename pre_of<EP, PRE>::type;
   PreT pre[NPT];
-  if constexpr (PRE) {
-#pragma unroll
-    for (int q = 0; q < NPT; ++q) {
-      const int c = q * C::NT + (int)threadIdx.x;
-      if (NG % C::NT == 0 || c < NG) pre[q] = ep.prefetch(i0 + 4 * (c % G4), j0 + c / G4);
-    }
-  }
+  epilogue_prefetch<C, EP, PRE>(ep, i0, j0, pre);
 
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
@@ -293,49 +360,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     return;
   }
   AAA_STAMP(2);
-  // Epilogue through LDS.  Every wave (all WK groups) stores its partial tile
-  // pixel-major, E[wk][j][i]; then the whole workgroup walks the tile in
-  // 4-row groups with consecutive lanes on consecutive row groups of ONE
-  // column, so the epilogue's global loads/stores (gate activations, cell
-  // state, outputs: all [pixel][channel]) are contiguous per column instead
-  // of one 16-B access per lane at a 2 KB stride, and all waves share it.
-  float* E = reinterpret_cast<float*>(smem);
-  barrier_lds();                              // every wave is done reading the last stage
-#pragma unroll
-  for (int a = 0; a < MI; ++a)
-#pragma unroll
-    for (int b = 0; b < MJ; ++b)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = wi * WTI + a * 32 + 8 * g + 4 * h;
-        const int j = wj * WTJ + b * 32 + r32;
-        *reinterpret_cast<f32x4*>(E + (wk * BJ + j) * ELD + i) =
-            f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-      }
-  __syncthreads();
-  constexpr bool ACC = has_acc<EP>::value && PRE && C::NT % G4 == 0;
-  typename acc_of<EP, ACC>::type eacc{};
-#pragma unroll
-  for (int q = 0; q < NPT; ++q) {
-    const int c = q * C::NT + (int)threadIdx.x;
-    if (NG % C::NT == 0 || c < NG) {
-      const int r4 = c % G4, j = c / G4;
-      f32x4 v = *reinterpret_cast<const f32x4*>(E + j * ELD + 4 * r4);
-#pragma unroll
-      for (int w = 1; w < WK; ++w) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
-        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
-      }
-      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q], &eacc);
-      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
-      else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
-    }
-  }
-  if constexpr (ACC) {
-    static_assert(C::NT * 16 * sizeof(float) <= sizeof(smem), "accumulator reduction does not fit in LDS");
-    __syncthreads();                          // every thread is done reading E
-    ep.template flush<G4, C::NT>(eacc, reinterpret_cast<float*>(smem), i0, tj);
-  }
+  staged_epilogue<C, EP, PRE>(ep, smem, acc, i0, j0, tj, pre);
   AAA_STAMP(3);
 }
 
