@@ -170,6 +170,44 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
   return *reinterpret_cast<const bf16x8*>(t + r * BK + (((kofs >> 3) ^ g) << 3));
 }
 
+// Epilogue work split: the tile's (4-row group, column) items, G4 row groups
+// per column, NPT items per thread.  Items with a split prefetch() (EP::Pre)
+// keep at most PD of them in registers: the first PD are requested before the
+// K loop, and each later one right after the item PD places before it is
+// finished, so the loads of a wide tile (e.g. the BPTT gate backward, 32 floats
+// per item) overlap the epilogue's own math instead of spilling.
+template <class C, class EP, bool PRE_>
+struct EpiPlan {
+  static constexpr bool PRE = PRE_;
+  using PreT = typename pre_of<EP, PRE>::type;
+  static constexpr int G4 = C::BI / 4, NG = G4 * C::BJ, NPT = (NG + C::NT - 1) / C::NT;
+  static constexpr int PRE_FLOATS = 64;         // register budget for prefetched epilogue inputs
+  static constexpr int PW = (int)(sizeof(PreT) / 4) > 0 ? (int)(sizeof(PreT) / 4) : 1;
+  static constexpr int PD0 = PRE_FLOATS / PW < 1 ? 1 : PRE_FLOATS / PW;
+  static constexpr int PD = PD0 < NPT ? PD0 : NPT;
+};
+
+// Request the epilogue inputs of item q (slot q % PD).  ``jn`` = valid tile columns.
+template <class C, class EP, class PL>
+__device__ __forceinline__ void epilogue_load(const EP& ep, int i0, int j0, int jn, int q,
+                                              typename PL::PreT (&pre)[PL::PD]) {
+  if constexpr (PL::PRE) {
+    const int c = q * C::NT + (int)threadIdx.x;
+    if ((PL::NG % C::NT == 0 || c < PL::NG) && c / PL::G4 < jn)
+      pre[q % PL::PD] = ep.prefetch(i0 + 4 * (c % PL::G4), j0 + c / PL::G4);
+  }
+}
+
+// Epilogue inputs of this thread's first PD items, requested before the K loop
+// (vmcnt retires in issue order; the compiler waits for these ordinary loads
+// only at their use after the loop).
+template <class C, class EP, class PL>
+__device__ __forceinline__ void epilogue_prefetch(const EP& ep, int i0, int j0, int jn,
+                                                  typename PL::PreT (&pre)[PL::PD]) {
+#pragma unroll
+  for (int q = 0; q < PL::PD; ++q) epilogue_load<C, EP, PL>(ep, i0, j0, jn, q, pre);
+}
+
 // Epilogue through LDS, shared by the ring GEMM and the halo conv (halo.h).
 // Every wave (all WK groups) stores its partial tile pixel-major, E[wk][j][i];
 // then the whole workgroup walks the tile in 4-row groups with consecutive
@@ -177,13 +215,15 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
 // loads/stores (gate activations, cell state, outputs: all [pixel][channel])
 // are contiguous per column instead of one 16-B access per lane at a 2 KB
 // stride, and all waves share it.  ``smem`` must hold WK*BJ*(BI+4) floats.
-template <class C, class EP, bool PRE, typename T, int MI, int MJ, class PreT, int NPT>
+// Tile columns >= jn are skipped (the halo conv's tiles end at a frame edge).
+template <class C, class EP, class PL, typename T, int MI, int MJ>
 __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32x16 (&acc)[MI][MJ], int i0, int j0,
-                                                int tj, const PreT (&pre)[NPT]) {
+                                                int jn, int tj, typename PL::PreT (&pre)[PL::PD]) {
   constexpr int BI = C::BI, BJ = C::BJ, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ;
   constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
-  constexpr int G4 = BI / 4, NG = G4 * BJ;
+  constexpr int G4 = PL::G4, NG = PL::NG, NPT = PL::NPT, PD = PL::PD;
+  constexpr bool PRE = PL::PRE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave / (WI * WJ), wr = wave - wk * (WI * WJ);
   const int wi = wr / WJ, wj = wr - (wr / WJ) * WJ;
@@ -207,7 +247,7 @@ __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32
 #pragma unroll
   for (int q = 0; q < NPT; ++q) {
     const int c = q * C::NT + (int)threadIdx.x;
-    if (NG % C::NT == 0 || c < NG) {
+    if ((NG % C::NT == 0 || c < NG) && c / G4 < jn) {
       const int r4 = c % G4, j = c / G4;
       f32x4 v = *reinterpret_cast<const f32x4*>(E + j * ELD + 4 * r4);
 #pragma unroll
@@ -215,29 +255,15 @@ __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32
         const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
         v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
       }
-      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q], &eacc);
-      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q]);
+      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD], &eacc);
+      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD]);
       else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
     }
+    if (q + PD < NPT) epilogue_load<C, EP, PL>(ep, i0, j0, jn, q + PD, pre);
   }
   if constexpr (ACC) {
     __syncthreads();                          // every thread is done reading E
     ep.template flush<G4, C::NT>(eacc, E, i0, tj);
-  }
-}
-
-// Epilogue inputs of this thread's (4-row group, column) items, requested
-// before the K loop (vmcnt retires in issue order; the compiler waits for
-// these ordinary loads only at their use after the loop).
-template <class C, class EP, bool PRE, class PreT, int NPT>
-__device__ __forceinline__ void epilogue_prefetch(const EP& ep, int i0, int j0, PreT (&pre)[NPT]) {
-  constexpr int G4 = C::BI / 4, NG = G4 * C::BJ;
-  if constexpr (PRE) {
-#pragma unroll
-    for (int q = 0; q < NPT; ++q) {
-      const int c = q * C::NT + (int)threadIdx.x;
-      if (NG % C::NT == 0 || c < NG) pre[q] = ep.prefetch(i0 + 4 * (c % G4), j0 + c / G4);
-    }
   }
 }
 
@@ -291,11 +317,9 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   // Epilogue groups of this thread (see the epilogue below) and, when the
   // epilogue supports it, their inputs, requested first (vmcnt retires in issue order) and consumed after the
   // K loop (ordinary loads: the compiler waits for them only at their use).
-  constexpr int G4 = BI / 4, NG = G4 * BJ, NPT = (NG + C::NT - 1) / C::NT;
-  constexpr bool PRE = has_pre<EP>::value && (ABL & 4) == 0;
-  using PreT = typename pre_of<EP, PRE>::type;
-  PreT pre[NPT];
-  epilogue_prefetch<C, EP, PRE>(ep, i0, j0, pre);
+  using PL = EpiPlan<C, EP, has_pre<EP>::value && (ABL & 4) == 0>;
+  typename PL::PreT pre[PL::PD];
+  epilogue_prefetch<C, EP, PL>(ep, i0, j0, BJ, pre);
 
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
@@ -360,7 +384,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     return;
   }
   AAA_STAMP(2);
-  staged_epilogue<C, EP, PRE>(ep, smem, acc, i0, j0, tj, pre);
+  staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, BJ, tj, pre);
   AAA_STAMP(3);
 }
 
