@@ -181,6 +181,20 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
 int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, const float* rewards, double gamma,
                   float* loss, float* returns_norm, float* dlogits, hipStream_t stream);
 
+/* ---- actor: action sampling ----
+ * Policy.forward's draw (reference main_mp.py:54-58: F.softmax over the
+ * logits, Categorical(probs).sample(), .log_prob(action)) for B rows of
+ * logits (B, A) fp32, on device and without a host round trip: actions (B)
+ * int32 by inverse-CDF sampling of softmax(logits) with a counter-based
+ * uniform u = rng(seed, *counter, row) (splitmix64 finaliser, 24-bit);
+ * logp (B) = log(clamp(p_a, FLT_EPSILON, 1 - FLT_EPSILON)) as Categorical
+ * computes it; dlogp_dlogits (B, A) = 1[k == a] - p_k (0 where the clamp is
+ * active), or NULL.  ``counter`` is a device uint64 advanced by one per call
+ * (NULL = draw index 0), so a captured hipGraph replays fresh draws.  The
+ * draws are not torch's multinomial stream; the distribution is the same. */
+int aaa_sample_actions(int B, int A, const float* logits, unsigned long long seed, unsigned long long* counter,
+                       int* actions, float* logp, float* dlogp_dlogits, hipStream_t stream);
+
 /* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
 
 /* NHWC convolution y[n,oy,ox,co] = b[co] + sum w[co,ky,kx,ci] x[n,iy,ix,ci]

@@ -204,3 +204,53 @@ def reinforce_loss(logits: torch.Tensor, actions, rewards, gamma: float = 0.99):
         lp = torch.distributions.Categorical(probs).log_prob(torch.tensor([int(a)]))
         terms.append(-lp * Rt)
     return torch.cat(terms).sum()
+
+
+# ---------------------------------------------------------------- actor ----
+# Policy.forward's draw (main_mp.py:54-58): softmax -> Categorical -> sample ->
+# log_prob.  The HIP sampler (aaa_sample_actions, csrc/loss.hip) replaces
+# torch's multinomial stream with a counter-based uniform; this restates that
+# generator and the inverse-CDF draw in plain Python/numpy so the device draws
+# can be checked action for action.  log_prob follows Categorical(probs):
+# probs normalised, then log(clamp(p, eps, 1 - eps)).
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def sample_uniform(seed: int, counter: int, row: int) -> float:
+    """u in [0, 1) with 24 bits, exactly the kernel's sample_uniform()."""
+    x = _mix64(_mix64(seed & _M64) ^ ((counter * 0xD1B54A32D192ED03 + row) & _M64))
+    return float(np.float32(x >> 40) * np.float32(1.0 / 16777216.0))
+
+
+def sample_actions(logits, seed: int, counter: int):
+    """Inverse-CDF draw of one action per row of logits (B, A).
+
+    Returns (actions int64 (B,), log_prob float32 (B,), margin (B,)): margin is
+    the distance of u*Z from the nearest CDF boundary, relative to Z -- draws
+    within fp32 rounding of a boundary may legitimately differ from the kernel.
+    """
+    l = np.asarray(logits, dtype=np.float32)
+    B, A = l.shape
+    acts = np.zeros(B, np.int64)
+    logp = np.zeros(B, np.float32)
+    margin = np.zeros(B, np.float64)
+    eps = np.float32(np.finfo(np.float32).eps)
+    for b in range(B):
+        e = np.exp(l[b] - l[b].max()).astype(np.float32)
+        z = np.float32(e.sum(dtype=np.float32))
+        cum = np.cumsum(e, dtype=np.float32)
+        target = np.float32(sample_uniform(seed, counter, b)) * z
+        hit = np.nonzero(cum > target)[0]
+        a = int(hit[0]) if hit.size else int(np.nonzero(e > 0)[0][-1])
+        acts[b] = a
+        pa = np.float32(e[a] / z)
+        logp[b] = np.log(np.clip(pa, eps, np.float32(1) - eps))
+        margin[b] = float(np.min(np.abs(cum.astype(np.float64) - float(target)))) / float(z)
+    return acts, logp, margin

@@ -1,0 +1,180 @@
+"""Actor path: the device sampler (aaa_sample_actions)
+against the oracle's restatement, and the drop-in Policy (main_mp.py:40-59)
+through a whole episode + finish_episode (main_mp.py:62-77) against the oracle
+unroll with the same actions.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import assert_close, detinit
+from oracle import ref_cpu
+
+import attention
+from aaa_amd.policy import ActionSampler, Policy, sample_actions
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,A,scale", [(4096, 18, 1.0), (1000, 18, 8.0), (257, 5, 0.2), (64, 130, 2.0)])
+def test_sampler_matches_oracle(cuda, B, A, scale):
+    g = torch.Generator().manual_seed(B + A)
+    logits = torch.randn(B, A, generator=g) * scale
+    counter = torch.tensor([41], dtype=torch.int64, device=cuda)
+    a, lp = sample_actions(logits.to(cuda), seed=1234, counter=counter)
+    torch.cuda.synchronize()
+    ra, rlp, margin = ref_cpu.sample_actions(logits.numpy(), 1234, 41)
+    a = a.cpu().numpy()
+    sure = margin > 1e-5          # draws within fp32 rounding of a CDF boundary may differ
+    assert sure.mean() > 0.99
+    assert np.array_equal(a[sure], ra[sure]), int((a[sure] != ra[sure]).sum())
+    ref = torch.distributions.Categorical(torch.softmax(logits, -1)).log_prob(torch.from_numpy(a).long())
+    assert np.abs(lp.cpu().numpy() - ref.numpy()).max() <= 2e-6 * max(1.0, float(ref.abs().max()))
+    assert int(counter.item()) == 42
+
+
+def test_sampler_counter_advances_and_seeds_differ(cuda):
+    logits = torch.zeros(512, 18, device=cuda)
+    s = ActionSampler(7, cuda)
+    a0, _ = s(logits)
+    a1, _ = s(logits)
+    b0, _ = ActionSampler(8, cuda)(logits)
+    torch.cuda.synchronize()
+    assert int(s.counter.item()) == 2
+    assert (a0 != a1).float().mean() > 0.8 and (a0 != b0).float().mean() > 0.8
+    ra0, _, _ = ref_cpu.sample_actions(np.zeros((512, 18), np.float32), 7, 0)
+    ra1, _, _ = ref_cpu.sample_actions(np.zeros((512, 18), np.float32), 7, 1)
+    assert np.array_equal(a0.cpu().numpy(), ra0) and np.array_equal(a1.cpu().numpy(), ra1)
+
+
+def test_sampler_distribution(cuda):
+    logits = torch.tensor([[2.0, 0.0, -1.0, 1.0, 0.5, -3.0]])
+    p = torch.softmax(logits, -1)[0].numpy()
+    n = 200000
+    a, _ = sample_actions(logits.repeat(n, 1).to(cuda), seed=3)
+    freq = np.bincount(a.cpu().numpy(), minlength=6) / n
+    chi2 = float((((freq - p) ** 2) / p).sum() * n)
+    assert chi2 < 25.0, (chi2, freq, p)
+
+
+def test_sampler_log_prob_gradient(cuda):
+    g = torch.Generator().manual_seed(5)
+    logits = torch.randn(32, 18, generator=g) * 2
+    logits[0, 3] = 60.0                       # saturated row: clamp at 1 - eps passes no gradient
+    w = torch.randn(32, generator=g)
+    dl = logits.to(cuda).requires_grad_(True)
+    a, lp = sample_actions(dl, seed=11)
+    (lp * w.to(cuda)).sum().backward()
+    rl = logits.clone().requires_grad_(True)
+    ref = torch.distributions.Categorical(torch.softmax(rl, -1)).log_prob(a.cpu().long())
+    (ref * w).sum().backward()
+    assert torch.allclose(dl.grad.cpu(), rl.grad, rtol=1e-5, atol=1e-6)
+    assert float(dl.grad[0].abs().max()) == 0.0
+
+
+def _finish_episode_loss(saved_log_probs, rewards, gamma=0.99):
+    """finish_episode's loss (main_mp.py:62-76) on the saved log-prob tensors."""
+    eps = np.finfo(np.float32).eps.item()
+    R, returns = 0, []
+    for r in rewards[::-1]:
+        R = r + gamma * R
+        returns.insert(0, R)
+    returns = torch.tensor(returns, device=saved_log_probs[0].device)
+    returns = (returns - returns.mean()) / (returns.std() + eps)
+    return torch.cat([-lp * Rt for lp, Rt in zip(saved_log_probs, returns)]).sum()
+
+
+@pytest.mark.parametrize("T", [1 + 5, 12])
+def test_policy_episode_matches_oracle(cuda, T):
+    """Policy.forward per step (uint8 frames, device draw, .item()) -> finish_episode
+    -> loss.backward through T chained per-step agent calls, vs the oracle unroll
+    of the same frames and actions."""
+    params = detinit.deterministic_params(0, 18, 4)
+    agent = attention.Agent(18, grid=(11, 11))
+    detinit.load_into(agent, params)
+    agent.to(cuda)
+    policy = Policy(agent, seed=17)
+    frames = detinit.frames_u8(1234 + T, (T, 84, 84, 3))
+    rewards = [float(r) for r in (np.arange(T) % 3 == 1) * 5.0]
+    agent.reset()
+    actions = [policy(frames[t]) for t in range(T)]
+    policy.rewards = rewards
+    loss = _finish_episode_loss(policy.saved_log_probs, policy.rewards)
+    loss.backward()
+    torch.cuda.synchronize()
+
+    P = ref_cpu.tensor_params(params)
+    X = torch.from_numpy(frames.astype(np.float32)).unsqueeze(1)
+    rl, _, _ = ref_cpu.unroll(P, X)
+    ref_loss = ref_cpu.reinforce_loss(rl, actions, rewards)
+    ref_loss.backward()
+    # the policy drew from its own logits: check those draws are the oracle's for the oracle logits
+    for t in range(T):
+        ra, _, margin = ref_cpu.sample_actions(rl[t].detach().numpy(), 17, t)
+        if margin[0] > 1e-4:
+            assert actions[t] == int(ra[0]), t
+    assert abs(float(loss) - float(ref_loss)) <= 1e-4 * max(1.0, abs(float(ref_loss)))
+    for n, p in agent.named_parameters():
+        gr = P[n].grad if P[n].grad is not None else torch.zeros_like(P[n])
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        if float(gr.norm()) > 0:
+            assert_close(g.cpu().numpy(), gr.numpy(), 1e-4, n)
+        else:
+            assert float(g.abs().max()) == 0.0, n
+
+
+def test_packed_weights_follow_parameter_updates(cuda):
+    """The per-runner packed-weight cache re-packs after an in-place update."""
+    params = detinit.deterministic_params(0, 18, 4)
+    agent = attention.Agent(18, grid=(11, 11))
+    detinit.load_into(agent, params)
+    agent.to(cuda)
+    x = torch.from_numpy(detinit.frames_u8(5, (1, 84, 84, 3)).astype(np.float32)).to(cuda)
+    agent.reset()
+    l0, _ = agent(x)
+    agent.reset()
+    l1, _ = agent(x)
+    assert torch.equal(l0, l1)
+    opt = torch.optim.Adam(agent.parameters(), lr=1e-2)
+    (l1.sum()).backward()
+    opt.step()
+    agent.reset()
+    l2, _ = agent(x)
+    P = ref_cpu.tensor_params({n: p.detach().cpu().numpy() for n, p in agent.named_parameters()})
+    rl, _, _ = ref_cpu.unroll(P, x.cpu().unsqueeze(0))
+    assert not torch.equal(l1, l2)
+    assert_close(l2.detach().cpu().numpy(), rl[0].detach().numpy(), 1e-4, "logits after update")
+
+
+def test_graph_actor_matches_eager_steps(cuda):
+    """The captured one-step graph reproduces the eager per-step agent (same
+    logits, carried ConvLSTM state, the same draws for the same counter), and
+    picks up a parameter update."""
+    from aaa_amd.policy import GraphActor
+    params = detinit.deterministic_params(0, 18, 4)
+    agent = attention.Agent(18, grid=(11, 11))
+    detinit.load_into(agent, params)
+    agent.to(cuda)
+    T = 5
+    frames = detinit.frames_u8(31, (T, 84, 84, 3))
+    ga = GraphActor(agent, 84, 84, B=1, seed=9)
+    ga.reset()
+    got_a, got_l = [], []
+    for t in range(T):
+        a = ga.step(frames[t])
+        got_a.append(int(a.item()))
+        got_l.append(ga.logits.clone())
+    P = ref_cpu.tensor_params(params, requires_grad=False)
+    rl, _, ra = ref_cpu.unroll(P, torch.from_numpy(frames.astype(np.float32)).unsqueeze(1))
+    for t in range(T):
+        assert_close(got_l[t].cpu().numpy(), rl[t].numpy(), 1e-4, f"logits t={t}")
+        oa, _, margin = ref_cpu.sample_actions(rl[t].numpy(), 9, t)
+        if margin[0] > 1e-4:
+            assert got_a[t] == int(oa[0]), t
+    assert_close(ga.attention.cpu().numpy(), ra[T - 1].numpy(), 1e-4, "attention")
+    # reset restarts the episode; an in-place update is re-packed
+    with torch.no_grad():
+        agent.policy_head[0].bias.add_(1.0)
+    ga.reset()
+    ga.step(frames[0])
+    assert_close(ga.logits.cpu().numpy(), rl[0].numpy() + 1.0, 1e-4, "logits after bias update")

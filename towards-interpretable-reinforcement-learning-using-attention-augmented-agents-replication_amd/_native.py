@@ -22,7 +22,7 @@ EXPORTS = (
     "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
     "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
     "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
-    "aaa_adam_step", "aaa_reinforce",
+    "aaa_adam_step", "aaa_reinforce", "aaa_sample_actions",
 )
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD = 0, 1, 2
 
@@ -86,6 +86,7 @@ def load(path: str = LIB_PATH):
             "aaa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
+            "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(lib, name):   # an older build (A/B runs); calling it raises AttributeError

@@ -143,10 +143,7 @@ class _UnrollFn(torch.autograd.Function):
     """One library forward over T steps; its backward is the hand-written BPTT."""
 
     @staticmethod
-    def forward(ctx, runner, S, X, pr, pa, h0, c0, *params):
-        flat = torch.cat([p.detach().reshape(-1) for p in params])
-        packed = runner.new_packed()
-        runner.pack(flat, packed)
+    def forward(ctx, runner, flat, packed, S, X, pr, pa, h0, c0, *params):
         ws = runner.new_workspace()
         logits, values, attn, hT, cT = runner.forward(flat, packed, S, X, ws, pr, pa, h0, c0,
                                                       want_attn=True, want_state=True)
@@ -158,12 +155,12 @@ class _UnrollFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dl, dv, _dattn, dhT, dcT):
         r = ctx.runner
-        want_state = bool(ctx.needs_input_grad[5] or ctx.needs_input_grad[6])
+        want_state = bool(ctx.needs_input_grad[7] or ctx.needs_input_grad[8])
         grads, dh0, dc0 = r.backward(ctx.flat, ctx.packed, ctx.S, ctx.X, ctx.ws, dl, dv, dhT, dcT,
                                      want_state_grads=want_state)
         ctx.ws = None
         views = [g.view(s) for g, s in zip(grads.split(r.sizes), ctx.shapes)]
-        return (None, None, None, None, None, dh0, dc0, *views)
+        return (None, None, None, None, None, None, None, dh0, dc0, *views)
 
 
 class Agent(nn.Module):
@@ -247,11 +244,30 @@ class Agent(nn.Module):
             raise RuntimeError(f"carried ConvLSTM state {tuple(h0.shape)} does not match this batch "
                                f"{runner.state_shape()}; call agent.reset()")
         Xf = X.float().contiguous()
-        logits, values, attn, hT, cT = _UnrollFn.apply(runner, S, Xf, pr, pa, h0, c0, *params)
+        flat, packed = self._packed_params(runner, params)
+        logits, values, attn, hT, cT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0, *params)
         cell.prev_hidden = (hT, cT)
         if self.prev_output is None:   # Q1: the query input is created once and never updated
             self.prev_output = torch.zeros(B, self.hidden_size, device=X.device)
         return logits, values, attn
+
+    @staticmethod
+    def _packed_params(runner, params):
+        """Flat fp32 params + their packed operand layout, re-made only when a
+        parameter changed (its storage or in-place version counter: optimizer
+        steps, load_state_dict, .to()).  An actor stepping one frame at a time
+        (main_mp.py:100, test_model.py:44) then pays no per-step re-pack.  The
+        cached tensors are never written again, so graphs that saved them stay valid."""
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        cached = getattr(runner, "_pack_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1], cached[2]
+        with torch.no_grad():
+            flat = torch.cat([p.detach().reshape(-1) for p in params])
+            packed = runner.new_packed()
+            runner.pack(flat, packed)
+        runner._pack_cache = (key, flat, packed)
+        return flat, packed
 
     def _runner(self, B, T, H, W, device):
         key = (B, T, H, W, str(device), self.conv_dtype)

@@ -29,5 +29,7 @@ hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hip
 // loss.hip: REINFORCE (finish_episode) loss + logits cotangent, one workgroup per episode
 hipError_t reinforce_launch(int T, int B, int A, const float* logits, const int* actions, const float* rewards,
                             double gamma, float* loss, float* rn, float* dlogits, hipStream_t st);
+hipError_t sample_launch(int B, int A, const float* logits, uint64_t seed, unsigned long long* counter, int* actions,
+                         float* logp, float* jac, hipStream_t st);
 
 }  // namespace aaa

@@ -1128,6 +1128,16 @@ int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, 
   return AAA_OK;
 }
 
+int aaa_sample_actions(int B, int A, const float* logits, unsigned long long seed, unsigned long long* counter,
+                       int* actions, float* logp, float* dlogp_dlogits, hipStream_t stream) {
+  if (B < 1 || A < 1) return fail(AAA_E_ARG, "sample_actions: need B, A >= 1 (B=%d A=%d)", B, A);
+  if (!logits || !actions || !logp) return fail(AAA_E_ARG, "sample_actions: NULL argument");
+  int r = check_device();
+  if (r) return r;
+  HIPCHK(sample_launch(B, A, logits, seed, counter, actions, logp, dlogp_dlogits, stream));
+  return AAA_OK;
+}
+
 int aaa_linear(int M, int N, int K, const float* x, const float* w, const float* bias, float* y,
                hipStream_t stream) {
   if (M < 1 || N < 1 || K < 1 || K % 4) return fail(AAA_E_ARG, "linear: need M,N,K >= 1 and K %% 4 == 0");
