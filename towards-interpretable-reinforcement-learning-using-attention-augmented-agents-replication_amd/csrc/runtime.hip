@@ -378,6 +378,67 @@ static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, in
                               Mi, Nj, K, nsplit, st);
 }
 
+// Tail GEMMs with very few columns (the actor's B=1, T=1 step: F = 1):
+// D[i][j] = sum_k W[i][k] X[j][k], one wavefront per 4-row group, lanes split
+// K in 16-B pieces (coalesced weight rows), butterfly reduction, then the same
+// epilogue functor.  A 64x64 tile spends ~20 us on its serial K loop there;
+// this reads the weight matrix once at full width.
+constexpr int kSkinnyMaxCols = 8;
+template <class EP, int NJ>
+__global__ void __launch_bounds__(256)
+k_skinny_gemm(const float* __restrict__ W, int ldw, int Mi, const float* __restrict__ X, int ldx, int Nj, int K,
+              EP ep) {
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * 4;
+  if (i >= Mi) return;
+  float acc[4][NJ];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[r][j] = 0.f;
+  for (int k = lane * 4; k < K; k += 256) {
+    f32x4 w[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      w[r] = i + r < Mi ? *reinterpret_cast<const f32x4*>(W + (size_t)(i + r) * ldw + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j < Nj) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(X + (size_t)j * ldx + k);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r][j] += w[r][0] * x[0] + w[r][1] * x[1] + w[r][2] * x[2] + w[r][3] * x[3];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[r][j] += __shfl_xor(acc[r][j], o, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (j < Nj) ep(i, j, acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+}
+
+// Forward tail GEMM (row-major weights [Mi][K] x activations [Nj][K]): the
+// skinny kernel for <= kSkinnyMaxCols columns (AAA_SKINNY=0 disables), else head_gemm.
+template <class PA, class PB, class EP>
+static hipError_t tail_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, hipStream_t st) {
+  if (Nj <= kSkinnyMaxCols && K % 4 == 0 && pa.ld % 4 == 0 && pb.ld % 4 == 0 && env_int("AAA_SKINNY", 1)) {
+    const int blocks = cdiv(cdiv(Mi, 4), 4);
+    if (Nj == 1)
+      hipLaunchKernelGGL((k_skinny_gemm<EP, 1>), dim3(blocks), dim3(256), 0, st, pa.src, pa.ld, Mi, pb.src, pb.ld, Nj,
+                         K, ep);
+    else
+      hipLaunchKernelGGL((k_skinny_gemm<EP, kSkinnyMaxCols>), dim3(blocks), dim3(256), 0, st, pa.src, pa.ld, Mi,
+                         pb.src, pb.ld, Nj, K, ep);
+    return hipGetLastError();
+  }
+  return head_gemm<LdRows, LdRows>(pa, pb, ep, Mi, Nj, K, 1, st);
+}
+
 // Batched (off-chain) conv GEMMs on the LDS-DMA ring (env AAA_PIPE_BATCHED=0: register-staged).
 static bool pipe_batched() { return env_int("AAA_PIPE_BATCHED", 1) != 0; }
 
@@ -522,25 +583,25 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     LRf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, 512};
     LRfj::Params pb{Wf(L.ans), L.ans_ld, F};
     EpiStoreT<float> ep{Wf(L.hid1), 512, 512, F, prm + L.poff[A0B], 1};
-    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 512, F, L.ans_ld, 1, st)));
+    HIPCHK((tail_gemm(pa, pb, ep, 512, F, L.ans_ld, st)));
   }
   {  // answer_processor.2
     LRf::Params pa{prm + L.poff[A2W], 512, 256};
     LRfj::Params pb{Wf(L.hid1), 512, F};
     EpiStoreT<float> ep{Wf(L.AO), 256, 256, F, prm + L.poff[A2B], 0};
-    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 256, F, 512, 1, st)));
+    HIPCHK((tail_gemm(pa, pb, ep, 256, F, 512, st)));
   }
   {  // policy_core LSTMCell from zero state (attention.py:354-355)
     LRf::Params pa{(const float*)(pk + L.k_Wihp), 256, 1024};
     LRfj::Params pb{Wf(L.AO), 256, F};
     EpiLstmCellFwd ep{(const float*)(pk + L.k_blc), Wf(L.LG), Wf(L.LC), Wf(L.LH), F};
-    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 1024, F, 256, 1, st)));
+    HIPCHK((tail_gemm(pa, pb, ep, 1024, F, 256, st)));
   }
   {  // policy / values heads (attention.py:365-367)
     LRf::Params pa{(const float*)(pk + L.k_Whd), 256, 2 * L.A};
     LRfj::Params pb{Wf(L.LH), 256, F};
     EpiHeads ep{io->logits, io->values, (const float*)(pk + L.k_bhd), L.A, F};
-    HIPCHK((head_gemm<LdRows, LdRows>(pa, pb, ep, 2 * L.A, F, 256, 1, st)));
+    HIPCHK((tail_gemm(pa, pb, ep, 2 * L.A, F, 256, st)));
   }
   if (io->hT)
     HIPCHK(hipMemcpyAsync(io->hT, Wf(L.Hs) + (size_t)(L.T - 1) * M * 128, (size_t)M * 128 * 4,
