@@ -38,7 +38,7 @@ struct HaloCfg {
 };
 
 struct HaloParams {
-  const void* w;        // weights [Mi][9*Cin] (row stride ldw elements), tap-major k
+  const void* wt;       // weights [Mi][9*Cin] (row stride ldw elements), tap-major k
   int ldw, Mi;
   const void* x;        // pixels [F*P][cs] (element stride cs), channels coff .. coff+Cin
   int cs, coff, Cin;
@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
   const int r32 = lane & 31, hh = lane >> 5;
 
   // ---- weight tile DMA: rows i0.., k = tap*Cin + c0 + logical chunk
-  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.w, (uint32_t)((size_t)p.Mi * p.ldw * sizeof(T)));
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(p.wt, (uint32_t)((size_t)p.Mi * p.ldw * sizeof(T)));
   uint32_t avoff[PA];
 #pragma unroll
   for (int c = 0; c < PA; ++c) {
@@ -200,6 +200,12 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
     }
   }
   staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, jn, tj, pre);
+}
+
+// Whether an h x w grid with Cin channels fits tile config C.
+template <class C>
+inline bool halo_fits(int h, int w, int Cin) {
+  return C::FR * h * w <= C::BJ && C::FR * (h + 2) * (w + 2) + 1 <= C::HMAX && Cin % C::CK == 0 && Cin >= C::CK;
 }
 
 // Host launcher: Mi output rows, nframes frames of h x w pixels.  Returns

@@ -27,6 +27,7 @@
 #include "gemm.h"
 #include "loaders_b.h"
 #include "glds.h"
+#include "halo.h"
 #include "misc.h"
 #include "optim.h"
 
@@ -772,8 +773,16 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
       const T* WdT = (const T*)(pk + L.k_WdTl);
       const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
-      HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
-                             : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+      // bf16 on small grids: halo-staged conv, one frame per 64x128 tile
+      // (tools/ubench/halo_tiles: 658 vs 771 us for the ring at C3)
+      using HD = HaloCfg<__bf16, 64, 128, 64, 1, 2, 1, 176>;
+      if (std::is_same<T, __bf16>::value && halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+        const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
+        HIPCHK((launch_halo<HD>(hp, ep, s)));
+      } else {
+        HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
+                               : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+      }
     }
     if (!vision_here) return AAA_OK;
     const float* dy2 = Wf(L.dY2) + (size_t)lo * M * 64;
