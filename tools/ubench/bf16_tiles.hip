@@ -70,6 +70,10 @@ int main(int argc, char** argv) {
     FWD(256, 64, 64, 4, 1, 1, 2, "256x64 BK64 4w");
     FWD(128, 128, 64, 2, 2, 1, 3, "128x128 BK64 4w pipe3");
     FWD(128, 128, 128, 2, 2, 2, 2, "128x128 BK128 8w 2-way");
+    FWD(128, 64, 64, 4, 2, 1, 3, "128x64 BK64 8w pipe3");
+    FWD(128, 64, 64, 4, 2, 1, 4, "128x64 BK64 8w pipe4");
+    FWD(128, 128, 64, 4, 2, 1, 3, "128x128 BK64 8w pipe3");
+    FWD(256, 64, 64, 4, 1, 1, 3, "256x64 BK64 4w pipe3");
   }
   {
     const ConvGeo g = ConvGeo{512, 512, 0, h, w, h, w, 3, 1, 1, 1}.prep();
@@ -84,6 +88,10 @@ int main(int argc, char** argv) {
     BPTT(128, 64, 128, 2, 1, 2, 2, "128x64 BK128 4w 2-way");
     BPTT(128, 64, 64, 2, 2, 1, 3, "128x64 BK64 4w pipe3");
     BPTT(64, 128, 64, 2, 2, 1, 2, "64x128 BK64 4w");
+    BPTT(128, 128, 64, 2, 2, 2, 3, "128x128 BK64 8w 2-way pipe3");
+    BPTT(128, 128, 128, 2, 2, 2, 2, "128x128 BK128 8w 2-way (again)");
+    BPTT(128, 64, 64, 4, 2, 1, 3, "128x64 BK64 8w pipe3");
+    BPTT(128, 64, 64, 4, 2, 1, 4, "128x64 BK64 8w pipe4");
   }
   {
     const ConvGeo g = ConvGeo{512, 512, 0, h, w, h, w, 3, 1, 1, 1}.prep();
@@ -95,6 +103,8 @@ int main(int argc, char** argv) {
     DX(64, 256, 64, 1, 4, 1, 2, "64x256 BK64 4w");
     DX(64, 256, 64, 2, 4, 1, 2, "64x256 BK64 8w");
     DX(64, 128, 64, 1, 2, 1, 3, "64x128 BK64 2w pipe3");
+    DX(64, 128, 64, 2, 2, 1, 3, "64x128 BK64 4w pipe3");
+    DX(64, 256, 64, 2, 4, 1, 3, "64x256 BK64 8w pipe3");
   }
   {
     const ConvGeo g = ConvGeo{64, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
@@ -105,6 +115,9 @@ int main(int argc, char** argv) {
     XP(128, 128, 64, 2, 2, 1, 2, "128x128 BK64 4w");
     XP(256, 128, 64, 4, 2, 1, 2, "256x128 BK64 8w");
     XP(128, 256, 64, 2, 4, 1, 2, "128x256 BK64 8w");
+    XP(128, 128, 64, 4, 2, 1, 3, "128x128 BK64 8w pipe3");
+    XP(128, 64, 64, 4, 2, 1, 3, "128x64 BK64 8w pipe3");
+    XP(64, 64, 64, 2, 2, 1, 3, "64x64 BK64 4w pipe3");
   }
   printf("done\n");
   return 0;

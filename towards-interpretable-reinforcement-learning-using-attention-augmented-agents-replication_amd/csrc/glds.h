@@ -37,8 +37,11 @@ __device__ __forceinline__ int lds_swz(int row) {
   return (row / RPL) & (RS - 1);
 }
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, 0, 0, 0);
+// soff: wave-uniform byte offset added by the address unit (an SGPR, no VALU);
+// the range check applies to voff + soff, so kOOB lanes stay out of range
+// for any soff < 2^31.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff, int soff = 0) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, soff, 0, 0);
 }
 
 // Epilogues with a split prefetch()/finish() (EP::Pre) have their global
@@ -104,10 +107,10 @@ struct GRowsB {
       voff[c] = row < p.nrows ? (uint32_t)((row * p.ld + lc * VG) * (int)sizeof(T)) : kOOB;
     }
   }
-  __device__ __forceinline__ void issue(T* lds, int k0) const {
-    const uint32_t ko = (uint32_t)(k0 * (int)sizeof(T));
+  __device__ __forceinline__ void issue(T* lds, int k0) {
+    const int ko = __builtin_amdgcn_readfirstlane(k0 * (int)sizeof(T));
 #pragma unroll
-    for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, voff[c] + ko);
+    for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, voff[c], ko);
   }
 };
 
@@ -127,24 +130,49 @@ struct GIm2colB {
   ConvGeo g;
   int base[PER], dt[PER];
   uint64_t vmask[PER];
+  uint32_t vo[PER];     // whole-tap path: byte offset of this piece at tap ``cur`` (or kOOB)
+  int cur;              // tap vo[] holds, -1 none
+  bool whole;           // every K tile lies inside one tap (Cin % BK == 0): dt == 0
   int wofs;
   __device__ static bool ok_shape(const ConvGeo& g) { return LdIm2colB<T, T, R, BK, NT>::ok_shape(g); }
   __device__ __forceinline__ GIm2colB(const Params& p, int row0) : g(p.g) {
     rs = make_rsrc(p.src, p.src_bytes);
     wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
+    whole = g.Cin % BK == 0;
+    cur = -1;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const int ch = threadIdx.x + c * NT;
       const int lr = ch / RS, kc = ((ch % RS) ^ lds_swz<RS>(lr)) * VG, m = row0 + lr;
       im2col_setup(g, BK, m < p.nrows, m, kc, base[c], dt[c], vmask[c]);
+      vo[c] = kOOB;
     }
   }
-  __device__ __forceinline__ void issue(T* lds, int k0) const {
+  // Whole-tap tiles: the per-lane offsets change only when the tap does (every
+  // Cin / BK tiles); the channel offset ci0 is wave-uniform and goes in soff.
+  // The tap's own offset is negative for the transposed gather, so vo carries
+  // it (kOOB lanes stay kOOB), and soff = ci0 >= 0 only.
+  __device__ __forceinline__ void issue(T* lds, int k0) {
     const int tap = __builtin_amdgcn_readfirstlane((int)g.dCin.div(k0));
     const int ci0 = k0 - tap * g.Cin;
     const int ky = __builtin_amdgcn_readfirstlane((int)g.dKW.div(tap));
     const int kx = tap - ky * g.KW;
-    const int toff = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs + ci0;
+    const int tv = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs;
+    if (whole) {
+      if (tap != cur) {
+        cur = tap;
+#pragma unroll
+        for (int c = 0; c < PER; ++c) {
+          const bool v = ((uint32_t)vmask[c] >> tap) & 1u;
+          vo[c] = v ? (uint32_t)((base[c] + tv) * (int)sizeof(T)) : kOOB;
+        }
+      }
+      const int so = __builtin_amdgcn_readfirstlane(ci0 * (int)sizeof(T));
+#pragma unroll
+      for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, vo[c], so);
+      return;
+    }
+    const int toff = tv + ci0;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const bool v = (vmask[c] >> (tap + dt[c])) & 1ull;
@@ -343,10 +371,11 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     }
     const T* Ac = smem + (kt % NBUF) * STG;
     const T* Bc = Ac + AEL;
+    constexpr int S2 = (ABL & 2) ? 0 : BK / 16 / WK;
+    if constexpr (is_f32<T>::value) {
 #pragma unroll
-    for (int s2 = 0; s2 < ((ABL & 2) ? 0 : BK / 16 / WK); ++s2) {
-      const int kofs = 16 * (s2 * WK + wk) + 8 * h;
-      if constexpr (is_f32<T>::value) {
+      for (int s2 = 0; s2 < S2; ++s2) {
+        const int kofs = 16 * (s2 * WK + wk) + 8 * h;
         float af[MI][8], bfr[MJ][8];
 #pragma unroll
         for (int a = 0; a < MI; ++a) frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
@@ -359,22 +388,42 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
 #pragma unroll
             for (int b = 0; b < MJ; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
-      } else {
-        bf16x8 af[MI], bfr[MJ];
+        if constexpr (ILV) {
+          if (pf && s2 == 0) la.issue(st, kn);
+          if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+        }
+      }
+    } else {
+      // Fragments run NS-1 sub-steps ahead of the MFMAs (NS register slots,
+      // <= 32 VGPRs), so an MFMA waits only for its own reads (counted
+      // lgkmcnt) instead of a full LDS round trip per sub-step; the sched
+      // barriers stop the scheduler from sinking the reads back behind the MFMAs.
+      constexpr int NS0 = 32 / ((MI + MJ) * 4), NS = NS0 < 2 ? 2 : (NS0 > S2 ? (S2 > 0 ? S2 : 1) : NS0);
+      bf16x8 fa[NS][MI], fb[NS][MJ];
+      auto ld = [&](int s2, int slot) {
+        const int kofs = 16 * (s2 * WK + wk) + 8 * h;
 #pragma unroll
-        for (int a = 0; a < MI; ++a) af[a] = frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs);
+        for (int a = 0; a < MI; ++a) fa[slot][a] = frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs);
 #pragma unroll
-        for (int b = 0; b < MJ; ++b) bfr[b] = frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
+        for (int b = 0; b < MJ; ++b) fb[slot][b] = frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
+      };
+#pragma unroll
+      for (int s2 = 0; s2 < NS - 1; ++s2)
+        if (s2 < S2) ld(s2, s2);
+#pragma unroll
+      for (int s2 = 0; s2 < S2; ++s2) {
+        if (s2 + NS - 1 < S2) ld(s2 + NS - 1, (s2 + NS - 1) % NS);
+        __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of these MFMAs
 #pragma unroll
         for (int a = 0; a < MI; ++a)
 #pragma unroll
           for (int b = 0; b < MJ; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
-      }
-      if constexpr (ILV) {
-        constexpr int S2 = BK / 16 / WK;
-        if (pf && s2 == 0) la.issue(st, kn);
-        if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s2 % NS][a], fb[s2 % NS][b], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ILV) {
+          if (pf && s2 == 0) la.issue(st, kn);
+          if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+        }
       }
     }
   }
