@@ -175,12 +175,16 @@ def main():
     # launch = the class's algorithmic FLOP per iteration / its launches per iteration
     M = B * learner.runner.P
     F = B * T
+    # bf16 runs the x-part inside every step (runtime.hip forward_impl, AAA_FUSED_X)
+    fused_x = int(os.environ.get("AAA_FUSED_X", "1" if dtype == "bf16" else "0")) != 0
     per_iter = {
-        N.TIMER_FWD_STEP: (T - 1) * 2.0 * M * 512 * 1152,      # h-part of steps 1..T-1 (x-part batched)
+        N.TIMER_FWD_STEP: (T * 2.0 * M * 512 * 1728 if fused_x       # [x | h] parts of all T steps
+                           else (T - 1) * 2.0 * M * 512 * 1152),   # h-part of steps 1..T-1 (x-part batched)
         N.TIMER_BPTT_STEP: (T - 1) * 2.0 * M * 128 * 4608,     # dh rows of steps T-1..1
         N.TIMER_CORE_WGRAD: 2.0 * 512 * 1728 * F * learner.runner.P,
     }
-    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step (h-part)",
+    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step (x+h parts)" if fused_x else
+             "fused ConvLSTM forward step (h-part)",
              N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dh dgrad + fused gate bwd)",
              N.TIMER_CORE_WGRAD: "ConvLSTM weight-gradient GEMM"}
     per_launch = {k: per_iter[k] * args.steps / max(kt[k][1], 1) for k in kt}

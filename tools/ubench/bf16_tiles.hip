@@ -48,6 +48,25 @@ static void run(const char* what, const char* name, const bf* W, int ldw, int Mi
   printf("%-5s %-36s %8.2f us  %7.1f TF/s\n", what, name, us, flop / (us * 1e-6) / 1e12);
 }
 
+// Same launch with glds.h ablation bits: 1 no in-loop DMA, 2 no MFMA, 4 no epilogue.
+template <class C, int NB, int ABL>
+static void abl(const char* name, const bf* W, int ldw, int Mi, const bf* src, const ConvGeo& g, int M,
+                size_t src_elems, int K, float* out, double flop) {
+  using LA = GRowsB<bf, C::BI, C::BK, C::NT>;
+  using LB = GIm2colB<bf, C::BJ, C::BK, C::NT>;
+  using EP = EpiStoreT<float>;
+  EP ep{out, Mi, Mi, M, nullptr, 0};
+  dim3 grid((M + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, 1);
+  typename LA::Params pa{W, ldw, Mi};
+  typename LB::Params pb{src, g, M, (uint32_t)(src_elems * 2)};
+  const TileMap tm = tile_map(grid);
+  const float us = time_us([&] {
+    hipLaunchKernelGGL((gemm_pipe_kernel<C, LA, LB, EP, NB, ABL, false>), grid, dim3(C::NT), 0, 0, pa, pb, ep, K, K, tm);
+    CK(hipGetLastError());
+  });
+  printf("abl%d %-36s %8.2f us  %7.1f TF/s\n", ABL, name, us, flop / (us * 1e-6) / 1e12);
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 256, h = 11, w = 11, M = B * h * w;
   const int T = 20, FM = T * M;
@@ -63,6 +82,13 @@ int main(int argc, char** argv) {
 #define FWD(BI, BJ, BK, WI, WJ, WK, NB, NAME) \
     run<GemmCfg<bf, BI, BJ, BK, WI, WJ, WK>, NB>("fwd", NAME, WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl)
     FWD(128, 64, 64, 4, 2, 1, 2, "128x64 BK64 8w (current)");
+    using F0 = GemmCfg<bf, 128, 64, 64, 4, 2, 1>;
+    abl<F0, 2, 1>("fwd 128x64 no DMA", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
+    abl<F0, 2, 2>("fwd 128x64 no MFMA", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
+    abl<F0, 2, 4>("fwd 128x64 no epilogue", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
+    abl<F0, 2, 5>("fwd 128x64 no DMA, no epi", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
+    abl<F0, 2, 6>("fwd 128x64 DMA only", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
+    abl<F0, 2, 7>("fwd 128x64 nothing (barriers)", WpH, 1152, 512, xh, g, M, (size_t)2 * M * 192, 1152, out, fl);
     FWD(128, 128, 64, 2, 2, 1, 2, "128x128 BK64 4w");
     FWD(128, 128, 64, 4, 2, 1, 2, "128x128 BK64 8w");
     FWD(256, 128, 64, 4, 2, 1, 2, "256x128 BK64 8w");
@@ -85,6 +111,10 @@ int main(int argc, char** argv) {
     BPTT(128, 128, 64, 2, 2, 1, 2, "128x128 BK64 4w");
     BPTT(128, 128, 64, 4, 2, 1, 2, "128x128 BK64 8w");
     BPTT(128, 128, 128, 2, 2, 2, 2, "128x128 BK128 8w 2-way");
+    using B7 = GemmCfg<bf, 128, 128, 128, 2, 2, 2>;
+    abl<B7, 2, 1>("bptt 128x128 no DMA", WdT + 64 * 4608, 4608, 128, dz, g, M, (size_t)M * 512, 4608, out, fl);
+    abl<B7, 2, 5>("bptt 128x128 no DMA, no epi", WdT + 64 * 4608, 4608, 128, dz, g, M, (size_t)M * 512, 4608, out, fl);
+    abl<B7, 2, 6>("bptt 128x128 DMA only", WdT + 64 * 4608, 4608, 128, dz, g, M, (size_t)M * 512, 4608, out, fl);
     BPTT(128, 64, 128, 2, 1, 2, 2, "128x64 BK128 4w 2-way");
     BPTT(128, 64, 64, 2, 2, 1, 3, "128x64 BK64 4w pipe3");
     BPTT(64, 128, 64, 2, 2, 1, 2, "64x128 BK64 4w");

@@ -141,12 +141,16 @@ struct EpiConvLstmFwd {
   T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
   float* gates;        // [M][512]  in: Wx*x_t + b;  out: post-activation (i,f,c~,o)
   int Nj;              // M = B*P
+  // Fused x-part (the GEMM's K covers [x_t | h_{t-1}]): the gate bias [512]
+  // takes the place of the batched x-part, which ``gates`` then does not hold.
+  const float* bias = nullptr;
   // Inputs of one (4-row, column) group, loadable before the K loop (glds.h).
   struct Pre { f32x4 zx; float cp; };
   __device__ __forceinline__ Pre prefetch(int i, int j) const {
     Pre p{f32x4{0.f, 0.f, 0.f, 0.f}, 0.f};
     if (j < Nj && i < 512) {
-      p.zx = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
+      p.zx = bias ? *reinterpret_cast<const f32x4*>(bias + i)
+                  : *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
       p.cp = cprev[(size_t)j * 128 + (i >> 2)];
     }
     return p;

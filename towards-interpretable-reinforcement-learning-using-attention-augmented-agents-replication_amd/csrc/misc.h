@@ -43,6 +43,7 @@ template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipS
 template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);
 template <typename T> hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st);
 template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st);
+template <typename T> hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st);
 template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);

@@ -458,6 +458,18 @@ __global__ void k_pack_lstm(LstmPtrs L, T* WpX, T* WpH, float* bl) {
   }
 }
 
+// Fused-step operand (bf16 path): WpXH[n][tap*192 + c'] = W(n, tap, c'), c'
+// over [x | h], i.e. the forward step's K runs over the whole XH slot.
+template <typename T>
+__global__ void k_pack_lstm_xh(LstmPtrs L, T* WpXH) {
+  const int n = 512 * 1728;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int row = idx / 1728, k = idx - row * 1728;
+    const int tap = k / 192, cp = k - tap * 192, ky = tap / 3, kx = tap - ky * 3;
+    WpXH[idx] = (T)lstm_w(L, row, ky, kx, cp);
+  }
+}
+
 // ConvLSTM dgrad operand: WdT[c'][tap*512 + n] = W(n, tap, c'), c' over [x | h].
 template <typename T>
 __global__ void k_pack_lstm_dgradT(LstmPtrs L, T* WdT) {
@@ -709,6 +721,12 @@ hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipSt
 }
 
 template <typename T>
+hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lstm_xh<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, WpXH);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext,
                        hipStream_t st) {
   hipLaunchKernelGGL(k_gate_fwd_zx<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, cprev, gates, cnext, hout,
@@ -777,6 +795,8 @@ template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipS
 template hipError_t pack_dgradT<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t pack_dgradT<__bf16>(const __bf16*, int, int, int, __bf16*, hipStream_t);
 template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, float*, float*, hipStream_t);
+template hipError_t pack_lstm_xh<float>(const LstmPtrs&, float*, hipStream_t);
+template hipError_t pack_lstm_xh<__bf16>(const LstmPtrs&, __bf16*, hipStream_t);
 template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t);

@@ -67,7 +67,7 @@ struct Layout {
   int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
@@ -108,6 +108,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.k_WdT2 = take(4 * 32 * 256 * e);   // conv2 dgrad, 4 parity classes
   L.k_WpX = take(512 * 576 * e);
   L.k_WpH = take(512 * 1152 * e);
+  L.k_WpXH = take(512 * 1728 * e);     // [x | h] step operand (fused x-part, bf16 default)
   L.k_WdTl = take(192 * 4608 * e);
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
@@ -462,6 +463,7 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     lp.wh[g] = prm + L.poff[HI_W + 3 * g];
   }
   HIPCHK(pack_lstm<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl), st));
+  HIPCHK(pack_lstm_xh<T>(lp, (T*)(pk + L.k_WpXH), st));
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
@@ -474,10 +476,12 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
 
 // ------------------------------------------------------------- forward ----
 template <typename T>
+static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
+
+template <typename T>
 static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   using C = CfgFor<T>;
   constexpr int NT = C::NT;
-  constexpr int NTF = CF::NT;
   char* ws = (char*)io->workspace;
   const char* pk = (const char*)io->packed;
   const float* prm = io->params;
@@ -516,6 +520,24 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
   if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  // bf16: the x-part rides in each step's GEMM (K over the whole XH slot,
+  // [x_t | h_{t-1}], bias in the epilogue): no batched x-part GEMM and no
+  // fp32 x-part round trip through HBM (tools/ubench/bf16_tiles: the step's
+  // epilogue traffic, not its MFMAs, is half its time).  AAA_FUSED_X=0/1 overrides.
+  if (env_int("AAA_FUSED_X", std::is_same<T, __bf16>::value ? 1 : 0)) {
+    const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
+    const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
+    const T* WpXH = (const T*)(pk + L.k_WpXH);
+    for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
+      EpiConvLstmFwd<T> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
+                           Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
+                           Wf(L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
+      TimerScope tim(AAA_TIMER_FWD_STEP, st);
+      HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep, 512,
+                                          1728, st)));
+    }
+    return forward_tail<T>(L, io, st);
+  }
   // x-part of the ConvLSTM steps (not recurrent): Gt <- Wx * x_t + b, in
   // chunks of ``cs`` steps on the aux stream; step t waits only for its chunk.
   hipStream_t ax = aux_stream();
@@ -572,6 +594,19 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     }
     HIPCHK(e);
   }
+  return forward_tail<T>(L, io, st);
+}
+
+// Everything after the ConvLSTM: query, attention readout, answer MLP,
+// LSTMCell, heads (all batched over the T*B frames, Q1) and state outputs.
+template <typename T>
+static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
+  constexpr int NTF = CF::NT;
+  char* ws = (char*)io->workspace;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  auto Wf = [&](size_t off) { return (float*)(ws + off); };
+  const int F = L.F, P = L.P, M = L.B * L.P;
   // constant query (Q1) + fused attention readout over all T*B frames
   HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
                    io->basis, P, L.nq, Wf(L.q1), Wf(L.q2), Wf(L.Q), Wf(L.SQ), st));
