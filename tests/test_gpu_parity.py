@@ -77,7 +77,7 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
 # Every per-step tile variant of the ConvLSTM forward / BPTT GEMMs (runtime.hip
 # step_tile: 0 64x64, 1/2 split-K, 3 BK=128 split-K, 4-6 the LDS-DMA ring of
 # glds.h) must give the same answer; B=5 makes B*P = 605 pixels (ragged tiles).
-@pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 4)])
+@pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 4), (7, 7), (4, 8)])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     monkeypatch.setenv("AAA_STEP_TILE", str(fwd))
@@ -89,6 +89,20 @@ def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     else:
         ref = _oracle(T, B, conv_mode="bf16")
         _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), ref, 2e-2, f"bf16 tiles {fwd}/{bwd}: ")
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
+    """The x-part of the ConvLSTM either batched over all frames or inside each
+    forward step (AAA_FUSED_X; bf16 default fused, fp32 default batched)."""
+    monkeypatch.setenv("AAA_FUSED_X", fused)
+    T, B = 4, 3
+    if conv_dtype == "fp32":
+        _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"fused_x={fused}: ")
+    else:
+        _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
+                 f"bf16 fused_x={fused}: ")
 
 
 def test_c1_against_reference_fixture(cuda, golden):

@@ -325,8 +325,10 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 }
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
-  if (v >= 0) return (v == 7 && !bf16) ? 4 : v;   // tile 7 exists for bf16 only
-  if (bptt && bf16) return 7;
+  if (v >= 0) return (v >= 7 && !bf16) ? 4 : v;   // tiles 7, 8 exist for bf16 only
+  // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
+  // (tools/ubench/bf16_tiles at B=128: 34.6 vs 39.6 us)
+  if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 8;
   if (bptt) return out_tiles32 < 1024 ? 4 : (out_tiles32 < 1536 ? 1 : 0);   // C2: 484 tiles, 66 us (reg 71)
   return out_tiles32 < 1024 ? 5 : 4;                                          // C2: 1936 tiles, 56 us (reg 58)
 }
@@ -858,7 +860,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     // the register-staged ones leave the bias to a column sum over dZ
     const int bj = bwd_tile == 7 ? 128 : 64;
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
-                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7;
+                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8;
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     HIPCHK(gate_bwd_last<T>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
@@ -909,6 +911,11 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
           if constexpr (std::is_same<T, float>::value) e = hipErrorInvalidValue;
           else e = step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
                                                                        4608, st);
+          break;
+        case 8:   // bf16: 128x64, BK128, 2-way in-WG split-K, 4 waves (small batches)
+          if constexpr (std::is_same<T, float>::value) e = hipErrorInvalidValue;
+          else e = step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                      4608, st);
           break;
         default: e = step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
       }
