@@ -122,22 +122,29 @@ def _vision_step(P, X_t, state, mode, peep):
     return h_new, c_new, peep
 
 
-def _query(P, B, nq, hidden=256):
-    """QueryNetwork on the zero prev_output (Q1), attention.py:184-198,325-331."""
-    z = torch.zeros(B, hidden, dtype=P["query.model.0.weight"].dtype)
+def _query(P, B, nq, hidden=256, prev_output=None):
+    """QueryNetwork on prev_output (attention.py:184-198,325-331): the zero
+    tensor in the reference's reachable path (Q1), h_{t-1} in the stateful core."""
+    z = prev_output if prev_output is not None else torch.zeros(B, hidden, dtype=P["query.model.0.weight"].dtype)
     q = F.relu(F.linear(z, P["query.model.0.weight"], P["query.model.0.bias"]))
     q = F.relu(F.linear(q, P["query.model.2.weight"], P["query.model.2.bias"]))
     q = F.linear(q, P["query.model.4.weight"], P["query.model.4.bias"])
     return q.reshape(-1, nq, 72)
 
 
-def _head(P, O, S, nq, prev_reward, prev_action):
-    """Attention readout + answer MLP + zero-state LSTMCell + heads (one frame batch)."""
+def _head(P, O, S, nq, prev_reward, prev_action, core=None):
+    """Attention readout + answer MLP + LSTMCell + heads (one frame batch).
+
+    core=None: the reference's reachable path, zero-state LSTMCell and a query
+    of zeros (Q1).  core=(h, c): the stateful core -- the reference's own
+    ``else`` branch (attention.py:356-358), reached when ``agent.prev_hidden``
+    holds a tensor: Q = query(h), LSTMCell from (h, c); returns the new (h, c).
+    """
     B, h, w, _ = O.shape
     K, V = O.split([8, 120], dim=3)                                     # attention.py:319
     Sb = torch.stack([S.to(O.dtype)] * B)
     K, V = torch.cat([K, Sb], dim=3), torch.cat([V, Sb], dim=3)         # :231-232
-    Q = _query(P, B, nq)
+    Q = _query(P, B, nq, prev_output=None if core is None else core[0])
     A = torch.matmul(K, Q.transpose(2, 1).unsqueeze(1))                  # :336
     A = F.softmax(A.reshape(B, h * w, nq), dim=1).reshape(B, h, w, nq)  # :235-243
     a = torch.matmul(A.reshape(B, h * w, nq).transpose(1, 2),
@@ -154,38 +161,56 @@ def _head(P, O, S, nq, prev_reward, prev_action):
                        dim=2).squeeze(1)                                 # :343-348
     x = F.relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]))
     x = F.linear(x, P["answer_processor.2.weight"], P["answer_processor.2.bias"])
-    zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1], dtype=O.dtype)
-    hc, _ = torch._VF.lstm_cell(x, (zeros, zeros), P["policy_core.weight_ih"],
-                                P["policy_core.weight_hh"], P["policy_core.bias_ih"],
-                                P["policy_core.bias_hh"])               # :354-355 (Q1)
+    if core is None:
+        zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1], dtype=O.dtype)
+        state = (zeros, zeros)                                          # :354-355 (Q1)
+    else:
+        state = core                                                    # :356-358
+    hc, cc = torch._VF.lstm_cell(x, state, P["policy_core.weight_ih"],
+                                 P["policy_core.weight_hh"], P["policy_core.bias_ih"],
+                                 P["policy_core.bias_hh"])
     logits = F.linear(hc, P["policy_head.0.weight"], P["policy_head.0.bias"])
     values = F.linear(hc, P["values_head.0.weight"], P["values_head.0.bias"])
+    if core is not None:
+        return logits, values, A, (hc, cc)
     return logits, values, A
 
 
 def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=None,
-           state=None, S=None, conv_mode: str = "fp32", return_state: bool = False):
+           state=None, S=None, conv_mode: str = "fp32", return_state: bool = False,
+           stateful_core: bool = False, core_state=None):
     """T-step unroll from ``reset()``: X is (T, B, H, W, 3) fp32 raw pixels.
 
     Returns logits (T,B,A), values (T,B,A), attention maps (T,B,h,w,nq)
-    [, (h_T, c_T) in the reference's (B,128,w,h) layout].
+    [, (h_T, c_T) in the reference's (B,128,w,h) layout].  With
+    ``stateful_core`` the policy core carries (prev_output, prev_hidden) --
+    the reference with ``agent.prev_hidden`` set to zeros after ``reset()``
+    (attention.py:324-331, 356-358); ``core_state`` = (h, c) (B, 256) to
+    continue from, and return_state then returns ((h_T, c_T), (core_h, core_c)).
     """
-    T = X.shape[0]
+    T, B = X.shape[0], X.shape[1]
     if S is None:
         S = spatial_basis(*grid_of(X.shape[2], X.shape[3]))
     peep = None
     L, Vv, Am = [], [], []
+    core = None
+    if stateful_core:
+        dt = P["policy_core.weight_hh"].dtype
+        core = core_state if core_state is not None else (torch.zeros(B, 256, dtype=dt), torch.zeros(B, 256, dtype=dt))
     for t in range(T):
         hN, cN, peep = _vision_step(P, X[t], state, conv_mode, peep)
         state = (hN, cN)
         O = hN.transpose(1, 3)                                          # attention.py:181
         r = None if prev_reward is None else prev_reward[t]
         a = None if prev_action is None else prev_action[t]
-        lg, vl, A = _head(P, O, S, nq, r, a)
+        if stateful_core:
+            lg, vl, A, core = _head(P, O, S, nq, r, a, core)
+        else:
+            lg, vl, A = _head(P, O, S, nq, r, a)
         L.append(lg), Vv.append(vl), Am.append(A)
     out = (torch.stack(L), torch.stack(Vv), torch.stack(Am))
     if return_state:
-        return out + (state,)
+        return out + (((state, core) if stateful_core else state),)
     return out
 
 

@@ -14,10 +14,14 @@ Fixtures:
   G6  210x160 frames with the default SpatialBasis(27,20), B=1, T=2 forward
   G7  bf16-emulated reference: every nn.Conv2d rounds its GEMM operands to
       bf16 (forward x,w; dgrad dy,w; wgrad x,dy), fp32 accumulate; B=2, T=4
+  G9  stateful policy core: the reference with ``agent.prev_hidden`` set to
+      zeros after reset(), so every step takes its else branch
+      (attention.py:356-358: query from h_{t-1}, LSTMCell from (h, c));
+      B=3, T=6 with prev_reward / prev_action, fwd+bwd
 
 Weights: detinit.deterministic_params(seed=0).  Frames: detinit.frames_u8.
 Loss for G3/G4/G7: sum(logits*Gl) + sum(values*Gv), Gl/Gv = detinit.cotangent.
-Usage:  python tests/golden/gen_golden.py
+Usage:  python tests/golden/gen_golden.py [G1 G2 ...]   (default: all)
 """
 import importlib.util
 import os
@@ -64,8 +68,10 @@ def frames(T, B, H=84, W=84, seed=1234):
     return torch.from_numpy(detinit.frames_u8(seed, (T, B, H, W, 3)).astype(np.float32))
 
 
-def run(agent, X, prev_reward=None, prev_action=None, capture=False):
+def run(agent, X, prev_reward=None, prev_action=None, capture=False, stateful=False):
     agent.reset()
+    if stateful:   # reach the reference's else branch (attention.py:356-358): a policy-core state exists
+        agent.prev_hidden = torch.zeros(X.shape[1], agent.hidden_size)
     L, V, As, Rs = [], [], [], []
     orig_sm, orig_aa = ref.spatial_softmax, ref.apply_alpha
     if capture:
@@ -114,14 +120,14 @@ def g2():
             "attn": As[0].numpy(), "readout": Rs[0].numpy(), "T": 1, "B": 2}
 
 
-def fwd_bwd(T, B, scale=1.0, with_prev=False, H=84, W=84, grid=(11, 11)):
+def fwd_bwd(T, B, scale=1.0, with_prev=False, H=84, W=84, grid=(11, 11), stateful=False):
     agent = new_agent(*grid)
     X = frames(T, B, H, W) * scale
     pr = pa = None
     if with_prev:
         pr = torch.from_numpy(detinit.cotangent(77, (T, B)))
         pa = torch.from_numpy((detinit.frames_u8(78, (T, B)) % 18).astype(np.float32))
-    lg, vl, As, _ = run(agent, X, pr, pa, capture=True)
+    lg, vl, As, _ = run(agent, X, pr, pa, capture=True, stateful=stateful)
     Gl = torch.from_numpy(detinit.cotangent(2, tuple(lg.shape)))
     Gv = torch.from_numpy(detinit.cotangent(3, tuple(vl.shape)))
     loss = (lg * Gl).sum() + (vl * Gv).sum()
@@ -222,8 +228,12 @@ def g7():
 
 def main():
     jobs = {"G1": g1, "G2": g2, "G3": lambda: fwd_bwd(20, 1), "G3n": lambda: fwd_bwd(20, 1, 1 / 255.0),
-            "G4": lambda: fwd_bwd(4, 4, with_prev=True), "G5": g5, "G6": g6, "G7": g7}
+            "G4": lambda: fwd_bwd(4, 4, with_prev=True), "G5": g5, "G6": g6, "G7": g7,
+            "G9": lambda: fwd_bwd(6, 3, with_prev=True, stateful=True)}
+    only = set(sys.argv[1:])
     for name, fn in jobs.items():
+        if only and name not in only:
+            continue
         out = fn()
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **{k: np.asarray(v) for k, v in out.items()})

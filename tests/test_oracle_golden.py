@@ -86,6 +86,25 @@ def test_g4_prev_reward_action(golden):
     _check_grads(P, g, RTOL)
 
 
+def test_g9_stateful_core(golden):
+    """The oracle's stateful policy core against the reference run with
+    agent.prev_hidden = zeros (its else branch, attention.py:356-358)."""
+    g = golden("G9")
+    P = _params()
+    T, B = 6, 3
+    pr = torch.from_numpy(detinit.cotangent(77, (T, B)))
+    pa = torch.from_numpy((detinit.frames_u8(78, (T, B)) % 18).astype(np.float32))
+    lg, vl, A = ref_cpu.unroll(P, _frames(T, B), prev_reward=pr, prev_action=pa, stateful_core=True)
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    assert_close(vl.detach().numpy(), g["values"], RTOL, "values")
+    assert_close(A.detach().numpy(), g["attn"], RTOL, "attn")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, RTOL)
+    # the query MLP and weight_hh now learn (they are exactly zero-grad in the Q1 path)
+    assert float(P["query.model.0.weight"].grad.abs().max()) > 0
+    assert float(P["policy_core.weight_hh"].grad.abs().max()) > 0
+
+
 def test_g5_reinforce(golden):
     g = golden("G5")
     P = _params()
