@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 1
+#define AAA_ABI_VERSION 2
 
 enum aaa_status {
   AAA_OK = 0,
@@ -68,8 +68,15 @@ typedef struct aaa_cfg {
   int nq;       /* attention queries (reference: 4, attention.py:265)          */
   int A;        /* actions (Seaquest: 18, main_mp.py:179)                       */
   int dtype;    /* enum aaa_dtype                                             */
-  int reserved;
+  int flags;    /* AAA_FLAG_* (0: the reference's reachable path)             */
 } aaa_cfg;
+
+/* Stateful policy core: the reference's `else` branch (attention.py:356-358),
+ * taken when agent.prev_hidden holds a tensor -- the query is computed from
+ * prev_output = h_{t-1} and the LSTMCell runs from (h_{t-1}, c_{t-1}), both
+ * carried across steps (and across calls through io->core_*).  Off, the
+ * reference's reachable path: zero query input, zero-state LSTMCell (Q1). */
+#define AAA_FLAG_STATEFUL_CORE 1
 
 typedef struct aaa_io {
   /* inputs */
@@ -99,6 +106,16 @@ typedef struct aaa_io {
   /* scratch */
   void* workspace;           /* aaa_workspace_bytes(); activations saved by
                                 aaa_forward for aaa_backward live here        */
+  /* stateful policy core (AAA_FLAG_STATEFUL_CORE only; ignored otherwise):
+     (B, 256) fp32 (prev_output, prev_hidden) in, out and their grads      */
+  const float* core_h0;      /* or NULL (zeros: reset())                       */
+  const float* core_c0;      /* or NULL                                        */
+  float* core_hT;            /* or NULL                                        */
+  float* core_cT;            /* or NULL                                        */
+  const float* dcore_hT;     /* backward input or NULL                         */
+  const float* dcore_cT;     /* backward input or NULL                         */
+  float* dcore_h0;           /* backward output or NULL                        */
+  float* dcore_c0;           /* backward output or NULL                        */
 } aaa_io;
 
 /* Backward phases, in execution order (DP bucket boundaries). */

@@ -29,12 +29,14 @@ TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD = 0, 1, 2
 
 class Cfg(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int), ("T", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
-                ("nq", ctypes.c_int), ("A", ctypes.c_int), ("dtype", ctypes.c_int), ("reserved", ctypes.c_int)]
+                ("nq", ctypes.c_int), ("A", ctypes.c_int), ("dtype", ctypes.c_int), ("flags", ctypes.c_int)]
 
 
 IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action", "h0", "c0",
              "logits", "values", "attn", "hT", "cT", "dlogits", "dvalues", "dhT", "dcT",
-             "grads", "dh0", "dc0", "workspace")
+             "grads", "dh0", "dc0", "workspace",
+             "core_h0", "core_c0", "core_hT", "core_cT", "dcore_hT", "dcore_cT", "dcore_h0", "dcore_c0")
+FLAG_STATEFUL_CORE = 1
 
 
 class IO(ctypes.Structure):

@@ -20,7 +20,11 @@ chain through the ConvLSTM state so ``loss.backward()`` after an episode
 There is no CPU fallback: calling the Agent with CPU tensors raises.
 
 Added (optional) surface: ``Agent(..., grid=None | (h, w) | "auto",
-conv_dtype="fp32" | "bf16")`` and ``Agent.unroll``.
+conv_dtype="fp32" | "bf16", stateful_core=False)`` and ``Agent.unroll``.
+``stateful_core`` (or a tensor placed in ``agent.prev_hidden``, as the
+reference itself reacts to) runs the reference's otherwise unreachable else
+branch (attention.py:356-358): the query reads prev_output = h_{t-1} and the
+LSTMCell carries (prev_output, prev_hidden) across steps and calls.
 """
 from __future__ import annotations
 
@@ -143,31 +147,40 @@ class _UnrollFn(torch.autograd.Function):
     """One library forward over T steps; its backward is the hand-written BPTT."""
 
     @staticmethod
-    def forward(ctx, runner, flat, packed, S, X, pr, pa, h0, c0, *params):
+    def forward(ctx, runner, flat, packed, S, X, pr, pa, h0, c0, ch0, cc0, *params):
         ws = runner.new_workspace()
-        logits, values, attn, hT, cT = runner.forward(flat, packed, S, X, ws, pr, pa, h0, c0,
-                                                      want_attn=True, want_state=True)
+        out = runner.forward(flat, packed, S, X, ws, pr, pa, h0, c0, want_attn=True, want_state=True,
+                             core=(ch0, cc0) if runner.stateful_core else None)
+        logits, values, attn, hT, cT = out[:5]
+        chT, ccT = out[5:] if runner.stateful_core else (None, None)
         ctx.runner, ctx.flat, ctx.packed, ctx.ws, ctx.S, ctx.X = runner, flat, packed, ws, S, X
         ctx.shapes = [p.shape for p in params]
         ctx.mark_non_differentiable(attn)
-        return logits, values, attn, hT, cT
+        return logits, values, attn, hT, cT, chT, ccT
 
     @staticmethod
-    def backward(ctx, dl, dv, _dattn, dhT, dcT):
+    def backward(ctx, dl, dv, _dattn, dhT, dcT, dchT=None, dccT=None):
         r = ctx.runner
         want_state = bool(ctx.needs_input_grad[7] or ctx.needs_input_grad[8])
-        grads, dh0, dc0 = r.backward(ctx.flat, ctx.packed, ctx.S, ctx.X, ctx.ws, dl, dv, dhT, dcT,
-                                     want_state_grads=want_state)
+        if r.stateful_core:
+            want_core = bool(ctx.needs_input_grad[9] or ctx.needs_input_grad[10])
+            grads, dh0, dc0, dch0, dcc0 = r.backward(ctx.flat, ctx.packed, ctx.S, ctx.X, ctx.ws, dl, dv, dhT, dcT,
+                                                     want_state_grads=want_state, dcore=(dchT, dccT),
+                                                     want_core_grads=want_core)
+        else:
+            grads, dh0, dc0 = r.backward(ctx.flat, ctx.packed, ctx.S, ctx.X, ctx.ws, dl, dv, dhT, dcT,
+                                         want_state_grads=want_state)
+            dch0 = dcc0 = None
         ctx.ws = None
         views = [g.view(s) for g, s in zip(grads.split(r.sizes), ctx.shapes)]
-        return (None, None, None, None, None, None, None, dh0, dc0, *views)
+        return (None, None, None, None, None, None, None, dh0, dc0, dch0, dcc0, *views)
 
 
 class Agent(nn.Module):
     """Attention-augmented agent (attention.py:257-368) on the gfx950 HIP path."""
 
     def __init__(self, num_actions, hidden_size: int = 256, c_v: int = 120, c_k: int = 8, c_s: int = 64,
-                 num_queries: int = 4, *, grid=None, conv_dtype: str = "fp32"):
+                 num_queries: int = 4, *, grid=None, conv_dtype: str = "fp32", stateful_core: bool = False):
         super().__init__()
         if (hidden_size, c_v, c_k, c_s) != (256, 120, 8, 64):
             raise ValueError("hidden_size/c_v/c_k/c_s are hard-coded elsewhere in the reference "
@@ -180,6 +193,9 @@ class Agent(nn.Module):
         self.c_v, self.c_k, self.c_s, self.num_queries = c_v, c_k, c_s, num_queries
         self.num_actions = num_actions
         self.conv_dtype = conv_dtype
+        # the reference's else branch (attention.py:356-358): also taken whenever
+        # a caller puts a tensor in ``prev_hidden``, exactly as the reference does
+        self.stateful_core = bool(stateful_core)
         self.vision = VisionNetwork()
         self.query = QueryNetwork(num_queries)
         self._auto_grid = grid == "auto"
@@ -236,18 +252,28 @@ class Agent(nn.Module):
             if p.device != X.device:
                 raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
                                    f"call agent.to({X.device})")
-        runner = self._runner(B, T, H, W, X.device)
+        stateful = self.stateful_core or self.prev_hidden is not None
+        runner = self._runner(B, T, H, W, X.device, stateful)
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
         cell = self.vision.vision_lstm
         h0, c0 = cell.prev_hidden if cell.prev_hidden is not None else (None, None)
         if h0 is not None and tuple(h0.shape) != runner.state_shape():
             raise RuntimeError(f"carried ConvLSTM state {tuple(h0.shape)} does not match this batch "
                                f"{runner.state_shape()}; call agent.reset()")
+        ch0 = cc0 = None
+        if stateful:   # (prev_output, prev_hidden) of the policy core, zeros after reset()
+            ch0, cc0 = self.prev_output, self.prev_hidden
+            for name, v in (("prev_output", ch0), ("prev_hidden", cc0)):
+                if v is not None and tuple(v.shape) != (B, self.hidden_size):
+                    raise RuntimeError(f"{name} has shape {tuple(v.shape)}, expected {(B, self.hidden_size)}")
         Xf = X.float().contiguous()
         flat, packed = self._packed_params(runner, params)
-        logits, values, attn, hT, cT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0, *params)
+        logits, values, attn, hT, cT, chT, ccT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0,
+                                                                 ch0, cc0, *params)
         cell.prev_hidden = (hT, cT)
-        if self.prev_output is None:   # Q1: the query input is created once and never updated
+        if stateful:
+            self.prev_output, self.prev_hidden = chT, ccT
+        elif self.prev_output is None:   # Q1: the query input is created once and never updated
             self.prev_output = torch.zeros(B, self.hidden_size, device=X.device)
         return logits, values, attn
 
@@ -269,11 +295,12 @@ class Agent(nn.Module):
         runner._pack_cache = (key, flat, packed)
         return flat, packed
 
-    def _runner(self, B, T, H, W, device):
-        key = (B, T, H, W, str(device), self.conv_dtype)
+    def _runner(self, B, T, H, W, device, stateful=False):
+        key = (B, T, H, W, str(device), self.conv_dtype, bool(stateful))
         r = self._runners.get(key)
         if r is None:
-            r = UnrollRunner(B, T, H, W, self.num_queries, self.num_actions, self.conv_dtype, device)
+            r = UnrollRunner(B, T, H, W, self.num_queries, self.num_actions, self.conv_dtype, device,
+                             stateful_core=stateful)
             self._runners[key] = r
         return r
 

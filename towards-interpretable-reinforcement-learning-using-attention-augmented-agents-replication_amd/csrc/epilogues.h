@@ -283,6 +283,77 @@ struct EpiLstmCellFwd {
   }
 };
 
+// Stateful policy core (the reference's else branch, attention.py:356-358):
+// LSTMCell from (h_{t-1}, c_{t-1}), D = [W_ih | W_hh] x [answer | h_{t-1}].
+// Writes the gate activations, c_t and h_t into the state slots and h_t into
+// the next step's GEMM operand row (cols 256..511 of its [answer | h] row).
+struct EpiLstmCellFwdS {
+  const float* bias;   // [1024] interleaved b_ih + b_hh
+  float* gates;        // [B][1024]
+  const float* cprev;  // [B][256] c_{t-1}
+  float* cout;         // [B][256] c_t
+  float* hout;         // [B][256] h_t
+  float* hnext;        // [B][512] next step's operand rows (+256 applied by the caller), or null
+  int Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 1024) return;
+    const int u = i >> 2;
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + i);
+    const float gi = sigm_acc(v0 + b[0]), gf = sigm_acc(v1 + b[1]);
+    const float gc = tanhf(v2 + b[2]), go = sigm_acc(v3 + b[3]);
+    const float c = gf * cprev[(size_t)j * 256 + u] + gi * gc;
+    const float h = go * tanhf(c);
+    cout[(size_t)j * 256 + u] = c;
+    hout[(size_t)j * 256 + u] = h;
+    if (hnext) hnext[(size_t)j * 512 + u] = h;
+    *reinterpret_cast<f32x4*>(gates + (size_t)j * 1024 + i) = f32x4{gi, gf, gc, go};
+  }
+};
+
+// Its backward: dh = heads' dgrad (the GEMM, rows = units u..u+3) + the carry
+// from step t+1 (dhc); the cell-state carry dcc is read and replaced by the
+// carry for t-1.
+struct EpiLstmCellBwdS {
+  const float* gates;  // [B][1024]
+  const float* cprev;  // [B][256] c_{t-1}
+  const float* ccur;   // [B][256] c_t
+  const float* dhc;    // [B][256] dh carried from t+1
+  float* dcc;          // [B][256] dc carry (in/out)
+  float* dgates;       // [B][1024]
+  int Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= 256) return;
+    const float v[4] = {v0, v1, v2, v3};
+    const f32x4 cv = *reinterpret_cast<const f32x4*>(ccur + (size_t)j * 256 + i);
+    const f32x4 cp = *reinterpret_cast<const f32x4*>(cprev + (size_t)j * 256 + i);
+    const f32x4 hc = *reinterpret_cast<const f32x4*>(dhc + (size_t)j * 256 + i);
+    f32x4 dc = *reinterpret_cast<const f32x4*>(dcc + (size_t)j * 256 + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 1024 + 4 * (i + e));
+      float d = dc[e], di, df, dcg, dout;
+      gate_bwd(v[e] + hc[e], g, cp[e], cv[e], d, di, df, dcg, dout);
+      dc[e] = d;
+      *reinterpret_cast<f32x4*>(dgates + (size_t)j * 1024 + 4 * (i + e)) = f32x4{di, df, dcg, dout};
+    }
+    *reinterpret_cast<f32x4*>(dcc + (size_t)j * 256 + i) = dc;
+  }
+};
+
+// out[j*ld + i] = v + add[j*ld_add + i]  (two gradient paths into one tensor)
+struct EpiStoreAddT {
+  float* out;
+  const float* add;
+  int ld, ld_add, Mi, Nj;
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    const float v[4] = {v0, v1, v2, v3};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i + e < Mi) out[(size_t)j * ld + i + e] = v[e] + add[(size_t)j * ld_add + i + e];
+  }
+};
+
 // dh from the heads' dgrad (rows = units u..u+3) -> d(gates) of the zero-state cell.
 struct EpiLstmCellBwd {
   const float* gates;  // [F][1024]

@@ -18,19 +18,28 @@ struct F32Pack {
   const float *a0w, *wih, *bih, *bhh, *pw, *vw, *pb, *vb;
   float *W1p, *Wihp, *blc, *Whd, *bhd;
   int ans_in, ans_ld, A, ldy;
+  const float* whh = nullptr;   // stateful core: also pack [W_ih | W_hh] into Wihhp
+  float* Wihhp = nullptr;
 };
 struct F32Unpack {
   const float *gW1p, *gWihp, *gblc, *gWhd, *gbhd;
   float *a0w, *wih, *bih, *bhh, *pw, *vw, *pb, *vb;
   int ans_in, ans_ld, A;
+  const float* gWihhp = nullptr;   // stateful core: W_ih and W_hh grads from [1024][512]
+  float* whh = nullptr;
 };
 
 hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
                      const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st);
+// qs: per-frame query stride in floats (0 = one query for all frames, Q1);
+// SQ == NULL computes the basis half of the logits per frame.  addq adds the
+// answer row's Q-column gradient (dAns[f][184*nq ...]) into dQp.
 hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
-                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st);
+                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
+                    int qs = 0);
 hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
-                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st);
+                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs = 0,
+                    int addq = 0);
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st);

@@ -71,7 +71,7 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // and the answer row [a_0..a_nq-1 | Q_0..Q_nq-1 | r | a_prev | 0-pad].
 template <int NQ>
 __global__ void __launch_bounds__(256)
-k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q,
+k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
            int P, float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -79,7 +79,8 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   float* Qs = sm + P * NQ;     // NQ*72
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
-  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Q[i];
+  const float* Qf = Q + (size_t)f * qs;   // qs = 0: one query for every frame (Q1)
+  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Qf[i];
   __syncthreads();
   for (int idx = tid; idx < P * NQ; idx += 256) {
     const int p = idx / NQ, q = idx - (idx / NQ) * NQ;
@@ -88,7 +89,17 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     const float* qq = Qs + q * 72;
     float s = k0[0] * qq[0] + k0[1] * qq[1] + k0[2] * qq[2] + k0[3] * qq[3] +
               k1[0] * qq[4] + k1[1] * qq[5] + k1[2] * qq[6] + k1[3] * qq[7];
-    L[idx] = s + SQ[idx];
+    if (SQ) {
+      s += SQ[idx];
+    } else {   // per-frame query: the basis half of the logit here
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(S + p * 64);
+#pragma unroll 4
+      for (int c = 0; c < 16; ++c) {
+        const f32x4 v = s4[c];
+        s += v[0] * qq[8 + 4 * c] + v[1] * qq[9 + 4 * c] + v[2] * qq[10 + 4 * c] + v[3] * qq[11 + 4 * c];
+      }
+    }
+    L[idx] = s;
   }
   __syncthreads();
   for (int q = wave; q < NQ; q += 4) {
@@ -141,8 +152,8 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
 // this frame's contribution to dQ.
 template <int NQ>
 __global__ void __launch_bounds__(128 * NQ)
-k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q,
-           const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int P,
+k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
+           const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
            float* __restrict__ dO, float* __restrict__ dQp) {
   constexpr int NT = 128 * NQ;     // thread (q, p0): head q, grid positions p0, p0+128, ...
   constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT; LDS < 64 KB at P=441, NQ=8)
@@ -157,7 +168,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   const float* O = Hs + (size_t)f * P * 128;
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
-  for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[i];
+  for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
   __syncthreads();
   // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S]: one thread per (p, q),
   // q uniform per 128 threads (da reads broadcast), rows of V as float4.
@@ -230,6 +241,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     float acc = 0.f;
 #pragma unroll 4
     for (int g = 0; g < G; ++g) acc += red[g * NQ * 72 + i];
+    if (addq) acc += dAns[(size_t)f * da_ld + NQ * 184 + i];   // the answer row's copy of Q (stateful core)
     dQp[(size_t)f * NQ * 72 + i] = acc;
   }
 }
@@ -500,9 +512,16 @@ __global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gat
 
 __global__ void k_pack_f32(F32Pack p) {
   const int n1 = 512 * p.ans_ld, n2 = 1024 * 256, n3 = 1024, n4 = p.ldy * 256, n5 = p.ldy;
-  const int tot = n1 + n2 + n3 + n4 + n5;
+  const int n6 = p.Wihhp ? 1024 * 512 : 0;
+  const int tot = n1 + n2 + n3 + n4 + n5 + n6;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
     int i = idx;
+    if (i >= n1 + n2 + n3 + n4 + n5) {   // [W_ih | W_hh] rows 4u+g (stateful core)
+      i -= n1 + n2 + n3 + n4 + n5;
+      const int row = i >> 9, k = i & 511, u = row >> 2, g = row & 3;
+      p.Wihhp[i] = k < 256 ? p.wih[(size_t)(g * 256 + u) * 256 + k] : p.whh[(size_t)(g * 256 + u) * 256 + k - 256];
+      continue;
+    }
     if (i < n1) {
       const int o = i / p.ans_ld, k = i - o * p.ans_ld;
       p.W1p[i] = k < p.ans_in ? p.a0w[(size_t)o * p.ans_in + k] : 0.f;
@@ -590,7 +609,12 @@ __global__ void k_unpack_f32(F32Unpack p) {
     i -= n1;
     if (i < n2) {
       const int row = i >> 8, k = i & 255, g = row >> 8, u = row & 255;
-      p.wih[i] = p.gWihp[(size_t)(4 * u + g) * 256 + k];
+      if (p.gWihhp) {   // stateful core: W_ih | W_hh from one [1024][512] gradient
+        p.wih[i] = p.gWihhp[(size_t)(4 * u + g) * 512 + k];
+        p.whh[i] = p.gWihhp[(size_t)(4 * u + g) * 512 + 256 + k];
+      } else {
+        p.wih[i] = p.gWihp[(size_t)(4 * u + g) * 256 + k];
+      }
       continue;
     }
     i -= n2;
@@ -633,20 +657,25 @@ hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const fl
 }
 
 hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
-                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st) {
+                    const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
+                    int qs) {
   const size_t sh = (size_t)(P * nq + nq * 72) * sizeof(float);
-  if (nq == 4) hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, SQ, pr, pa, P, Am, ans, ans_ld);
-  else if (nq == 8) hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, SQ, pr, pa, P, Am, ans, ans_ld);
+  if (nq == 4)
+    hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
+  else if (nq == 8)
+    hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
-                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st) {
+                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs, int addq) {
   const int G = 7;   // k_attn_bwd's dQ position groups
   const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72) * sizeof(float);
-  if (nq == 4) hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(512), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
-  else if (nq == 8) hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(1024), sh, st, Hs, S, Q, Am, dAns, da_ld, P, dO, dQp);
+  if (nq == 4)
+    hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(512), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
+  else if (nq == 8)
+    hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(1024), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -735,7 +764,7 @@ hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, fl
 }
 
 hipError_t pack_f32(const F32Pack& p, hipStream_t st) {
-  long n = 512L * p.ans_ld + 1024L * 256 + 1024 + (long)p.ldy * 256 + p.ldy;
+  long n = 512L * p.ans_ld + 1024L * 256 + 1024 + (long)p.ldy * 256 + p.ldy + (p.Wihhp ? 1024L * 512 : 0);
   hipLaunchKernelGGL(k_pack_f32, dim3(nblk(n)), dim3(256), 0, st, p);
   return hipGetLastError();
 }

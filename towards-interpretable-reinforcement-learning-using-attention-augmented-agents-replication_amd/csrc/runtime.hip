@@ -65,12 +65,15 @@ enum PIdx {
 
 struct Layout {
   int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
+  int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_Wihhp, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
+  // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
+  size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
 };
 
 static int build_layout(const aaa_cfg* c, Layout& L) {
@@ -79,13 +82,16 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   if (c->nq != 4 && c->nq != 8) return fail(AAA_E_ARG, "nq must be 4 or 8 (got %d)", c->nq);
   if (c->A < 1 || c->A > 256) return fail(AAA_E_ARG, "A out of range (%d)", c->A);
   if (c->dtype != AAA_F32 && c->dtype != AAA_BF16) return fail(AAA_E_ARG, "bad dtype %d", c->dtype);
+  if (c->flags & ~AAA_FLAG_STATEFUL_CORE) return fail(AAA_E_ARG, "unknown flags 0x%x", c->flags);
+  L.sc = (c->flags & AAA_FLAG_STATEFUL_CORE) != 0;
   L.B = c->B; L.T = c->T; L.F = c->B * c->T; L.H = c->H; L.W = c->W;
   L.H1 = conv_out(c->H, 8, 4, 1); L.W1 = conv_out(c->W, 8, 4, 1);
   L.h = conv_out(L.H1, 4, 2, 2); L.w = conv_out(L.W1, 4, 2, 2);
   if (L.H1 < 1 || L.W1 < 1 || L.h < 1 || L.w < 1) return fail(AAA_E_ARG, "frame %dx%d too small", c->H, c->W);
   L.P1 = L.H1 * L.W1; L.P = L.h * L.w;
   L.nq = c->nq; L.A = c->A; L.dt = c->dtype; L.esz = c->dtype == AAA_BF16 ? 2 : 4;
-  L.qd = 72 * L.nq; L.da = 184 * L.nq; L.ans_in = 256 * L.nq + 2;
+  // dAns columns: the readout part, plus the query copy when Q depends on the state
+  L.qd = 72 * L.nq; L.da = (L.sc ? 256 : 184) * L.nq; L.ans_in = 256 * L.nq + 2;
   L.ans_ld = (L.ans_in + 7) / 8 * 8;
   L.ldy = (2 * L.A + 3) / 4 * 4;
   const size_t shp[NPARAM] = {
@@ -116,6 +122,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.k_blc = take(1024 * 4);
   L.k_Whd = take((size_t)L.ldy * 256 * 4);
   L.k_bhd = take((size_t)L.ldy * 4);
+  L.k_Wihhp = take(L.sc ? 1024 * 512 * 4 : 0);   // [W_ih | W_hh], rows 4u+g
   L.packed = p;
   // workspace
   p = 0;
@@ -149,6 +156,21 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.dZp = take((size_t)L.T * ((M + 31) / 32) * 512 * 4);  // gate-bias partials per (step, column tile)
   L.dY2 = take(F * P * 64 * 4);
   L.dY1 = take(F * L.P1 * 32 * 4);
+  {
+    const size_t sc = L.sc ? 1 : 0, B = L.B;
+    L.CH = take(sc * (L.T + 1) * B * 256 * 4);
+    L.CC = take(sc * (L.T + 1) * B * 256 * 4);
+    L.AOX = take(sc * F * 512 * 4);
+    L.Qf = take(sc * F * L.qd * 4);
+    L.q1s = take(sc * F * 128 * 4);
+    L.q2s = take(sc * F * L.qd * 4);
+    L.dAOX = take(sc * F * 512 * 4);
+    L.dQf = take(sc * F * L.qd * 4);
+    L.dq2s = take(sc * F * L.qd * 4);
+    L.dq1s = take(sc * F * 128 * 4);
+    L.dhc = take(sc * B * 256 * 4);
+    L.dcc = take(sc * B * 256 * 4);
+  }
   // zero-initialised (atomic) accumulation region: one memset covers it
   L.dQs = take((size_t)L.qd * 4);
   L.gWp1 = take(32 * 256 * 4);
@@ -160,6 +182,7 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.gblc = take(1024 * 4);
   L.gWhd = take((size_t)L.ldy * 256 * 4);
   L.gbhd = take((size_t)L.ldy * 4);
+  L.gWihhp = take(L.sc ? 1024 * 512 * 4 : 0);
   L.ws = p;
   return AAA_OK;
 }
@@ -472,6 +495,10 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
   fp.W1p = (float*)(pk + L.k_W1p); fp.Wihp = (float*)(pk + L.k_Wihp); fp.blc = (float*)(pk + L.k_blc);
   fp.Whd = (float*)(pk + L.k_Whd); fp.bhd = (float*)(pk + L.k_bhd);
   fp.ans_in = L.ans_in; fp.ans_ld = L.ans_ld; fp.A = L.A; fp.ldy = L.ldy;
+  if (L.sc) {
+    fp.whh = prm + L.poff[WHH];
+    fp.Wihhp = (float*)(pk + L.k_Wihhp);
+  }
   HIPCHK(pack_f32(fp, st));
   return AAA_OK;
 }
@@ -599,6 +626,82 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   return forward_tail<T>(L, io, st);
 }
 
+// Stateful policy core (AAA_FLAG_STATEFUL_CORE; the reference's else branch,
+// attention.py:324-331, 356-358): per step t, over the B frames of that step,
+//   Q_t = QueryNetwork(h_{t-1}) -> attention readout with the per-frame Q_t ->
+//   answer MLP -> LSTMCell([answer | h_{t-1}], c_{t-1}) -> (h_t, c_t).
+// State slots CH/CC[t] hold (h, c) entering step t (slot 0 = io->core_*0 or
+// zeros); the LSTMCell epilogue also writes h_t into step t+1's [answer | h]
+// GEMM row, so each step is five small GEMMs and one attention launch.  The
+// heads then run batched over all frames on CH[1..T].
+static int forward_tail_stateful(const Layout& L, const aaa_io* io, hipStream_t st) {
+  constexpr int NTF = CF::NT;
+  char* ws = (char*)io->workspace;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  auto Wf = [&](size_t off) { return (float*)(ws + off); };
+  const int B = L.B, P = L.P, qd = L.qd;
+  const size_t sB = (size_t)B * 256 * 4;
+  float *CH = Wf(L.CH), *CC = Wf(L.CC), *AOX = Wf(L.AOX);
+  if (io->core_h0) HIPCHK(hipMemcpyAsync(CH, io->core_h0, sB, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(CH, 0, sB, st));
+  if (io->core_c0) HIPCHK(hipMemcpyAsync(CC, io->core_c0, sB, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(CC, 0, sB, st));
+  HIPCHK(hipMemcpy2DAsync(AOX + 256, 512 * 4, CH, 256 * 4, 256 * 4, B, hipMemcpyDeviceToDevice, st));
+  using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
+  using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
+  for (int t = 0; t < L.T; ++t) {
+    const size_t f0 = (size_t)t * B;
+    float* q1 = Wf(L.q1s) + f0 * 128;
+    float* q2 = Wf(L.q2s) + f0 * qd;
+    float* Qt = Wf(L.Qf) + f0 * qd;
+    {  // QueryNetwork(prev_output = h_{t-1}) (attention.py:184-198, 331)
+      LRf::Params pa{prm + L.poff[Q0W], 256, 128};
+      LRfj::Params pb{CH + f0 * 256, 256, B};
+      EpiStoreT<float> ep{q1, 128, 128, B, prm + L.poff[Q0B], 1};
+      HIPCHK((tail_gemm(pa, pb, ep, 128, B, 256, st)));
+    }
+    {
+      LRf::Params pa{prm + L.poff[Q2W], 128, qd};
+      LRfj::Params pb{q1, 128, B};
+      EpiStoreT<float> ep{q2, qd, qd, B, prm + L.poff[Q2B], 1};
+      HIPCHK((tail_gemm(pa, pb, ep, qd, B, 128, st)));
+    }
+    {
+      LRf::Params pa{prm + L.poff[Q4W], qd, qd};
+      LRfj::Params pb{q2, qd, B};
+      EpiStoreT<float> ep{Qt, qd, qd, B, prm + L.poff[Q4B], 0};
+      HIPCHK((tail_gemm(pa, pb, ep, qd, B, qd, st)));
+    }
+    // attention readout with this step's per-frame queries (basis logits in-kernel)
+    HIPCHK(attn_fwd(Wf(L.Hs) + f0 * P * 128, io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
+                    io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
+                    Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
+    {  // answer_processor.0 + ReLU
+      LRf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, 512};
+      LRfj::Params pb{Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, B};
+      EpiStoreT<float> ep{Wf(L.hid1) + f0 * 512, 512, 512, B, prm + L.poff[A0B], 1};
+      HIPCHK((tail_gemm(pa, pb, ep, 512, B, L.ans_ld, st)));
+    }
+    {  // answer_processor.2 -> the answer half of this step's [answer | h_{t-1}] rows
+      LRf::Params pa{prm + L.poff[A2W], 512, 256};
+      LRfj::Params pb{Wf(L.hid1) + f0 * 512, 512, B};
+      EpiStoreT<float> ep{AOX + f0 * 512, 512, 256, B, prm + L.poff[A2B], 0};
+      HIPCHK((tail_gemm(pa, pb, ep, 256, B, 512, st)));
+    }
+    {  // policy_core LSTMCell from (h_{t-1}, c_{t-1}) (attention.py:356-358)
+      LRf::Params pa{(const float*)(pk + L.k_Wihhp), 512, 1024};
+      LRfj::Params pb{AOX + f0 * 512, 512, B};
+      EpiLstmCellFwdS ep{(const float*)(pk + L.k_blc), Wf(L.LG) + f0 * 1024, CC + f0 * 256, CC + (f0 + B) * 256,
+                         CH + (f0 + B) * 256, t + 1 < L.T ? AOX + (f0 + B) * 512 + 256 : nullptr, B};
+      HIPCHK((tail_gemm(pa, pb, ep, 1024, B, 512, st)));
+    }
+  }
+  if (io->attn)
+    HIPCHK(hipMemcpyAsync(io->attn, Wf(L.Am), (size_t)L.F * P * L.nq * 4, hipMemcpyDeviceToDevice, st));
+  return AAA_OK;
+}
+
 // Everything after the ConvLSTM: query, attention readout, answer MLP,
 // LSTMCell, heads (all batched over the T*B frames, Q1) and state outputs.
 template <typename T>
@@ -609,6 +712,10 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
   const float* prm = io->params;
   auto Wf = [&](size_t off) { return (float*)(ws + off); };
   const int F = L.F, P = L.P, M = L.B * L.P;
+  if (L.sc) {   // stateful core: the tail runs step by step
+    const int rc = forward_tail_stateful(L, io, st);
+    if (rc) return rc;
+  } else {
   // constant query (Q1) + fused attention readout over all T*B frames
   HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
                    io->basis, P, L.nq, Wf(L.q1), Wf(L.q2), Wf(L.Q), Wf(L.SQ), st));
@@ -635,9 +742,12 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     EpiLstmCellFwd ep{(const float*)(pk + L.k_blc), Wf(L.LG), Wf(L.LC), Wf(L.LH), F};
     HIPCHK((tail_gemm(pa, pb, ep, 1024, F, 256, st)));
   }
-  {  // policy / values heads (attention.py:365-367)
+  }
+  {  // policy / values heads (attention.py:365-367), batched over all frames
+    using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
+    using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
     LRf::Params pa{(const float*)(pk + L.k_Whd), 256, 2 * L.A};
-    LRfj::Params pb{Wf(L.LH), 256, F};
+    LRfj::Params pb{L.sc ? Wf(L.CH) + (size_t)L.B * 256 : Wf(L.LH), 256, F};
     EpiHeads ep{io->logits, io->values, (const float*)(pk + L.k_bhd), L.A, F};
     HIPCHK((tail_gemm(pa, pb, ep, 2 * L.A, F, 256, st)));
   }
@@ -646,6 +756,12 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
                           hipMemcpyDeviceToDevice, st));
   if (io->cT)
     HIPCHK(hipMemcpyAsync(io->cT, Wf(L.Cst) + (size_t)L.T * M * 128, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  if (L.sc && io->core_hT)
+    HIPCHK(hipMemcpyAsync(io->core_hT, Wf(L.CH) + (size_t)L.T * L.B * 256, (size_t)L.B * 256 * 4,
+                          hipMemcpyDeviceToDevice, st));
+  if (L.sc && io->core_cT)
+    HIPCHK(hipMemcpyAsync(io->core_cT, Wf(L.CC) + (size_t)L.T * L.B * 256, (size_t)L.B * 256 * 4,
+                          hipMemcpyDeviceToDevice, st));
   return AAA_OK;
 }
 
@@ -688,6 +804,113 @@ static int conv1_wgrad(const Layout& L, const float* dy1, const T* xp, int frame
 }
 
 // ------------------------------------------------------------ backward ----
+// Stateful policy core, backward of the tail (phase HEAD): the dgrad chain runs
+// step by step from t = T-1 (the carries dh, dc of the core state flow through
+// the LSTMCell's W_hh and the query MLP into step t-1); every weight gradient
+// is then one batched GEMM over all frames from the saved per-step operands.
+static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t st) {
+  constexpr int NTF = CF::NT;
+  char* ws = (char*)io->workspace;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  float* grads = io->grads;
+  auto Wf = [&](size_t off) { return (float*)(ws + off); };
+  const int F = L.F, P = L.P, B = L.B, qd = L.qd, da = L.da;
+  using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
+  using LTf = LdRowsT<float, float, CF::BI, CF::BK, NTF>;
+  using LTfj = LdRowsT<float, float, CF::BJ, CF::BK, NTF>;
+  float *CH = Wf(L.CH), *CC = Wf(L.CC), *AOX = Wf(L.AOX), *dAOX = Wf(L.dAOX), *dhc = Wf(L.dhc), *dcc = Wf(L.dcc);
+  const size_t sB = (size_t)B * 256 * 4;
+  if (io->dcore_hT) HIPCHK(hipMemcpyAsync(dhc, io->dcore_hT, sB, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(dhc, 0, sB, st));
+  if (io->dcore_cT) HIPCHK(hipMemcpyAsync(dcc, io->dcore_cT, sB, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(dcc, 0, sB, st));
+  for (int t = L.T - 1; t >= 0; --t) {
+    const size_t f0 = (size_t)t * B;
+    {  // heads dgrad + dh carry -> LSTMCell backward from (c_{t-1}, c_t), dc carry
+      LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
+      LRfj::Params pb{Wf(L.dY) + f0 * L.ldy, L.ldy, B};
+      EpiLstmCellBwdS ep{Wf(L.LG) + f0 * 1024, CC + f0 * 256, CC + (f0 + B) * 256, dhc, dcc, Wf(L.dLG) + f0 * 1024, B};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, B, L.ldy, 1, st)));
+    }
+    {  // [d answer | d h_{t-1} (recurrent part)] = [W_ih | W_hh]^T dgates
+      LTf::Params pa{(const float*)(pk + L.k_Wihhp), 512, 512};
+      LRfj::Params pb{Wf(L.dLG) + f0 * 1024, 1024, B};
+      EpiStoreT<float> ep{dAOX + f0 * 512, 512, 512, B, nullptr, 0};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 512, B, 1024, 1, st)));
+    }
+    {  // answer_processor.2 dgrad fused with the ReLU backward
+      LTf::Params pa{prm + L.poff[A2W], 512, 512};
+      LRfj::Params pb{dAOX + f0 * 512, 512, B};
+      EpiReluBwdT ep{Wf(L.dH1) + f0 * 512, Wf(L.hid1) + f0 * 512, 512, 512, 512, B};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 512, B, 256, 1, st)));
+    }
+    {  // answer_processor.0 dgrad: readout and query columns of the answer row
+      LTf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, da};
+      LRfj::Params pb{Wf(L.dH1) + f0 * 512, 512, B};
+      EpiStoreT<float> ep{Wf(L.dAns) + f0 * da, da, da, B, nullptr, 0};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, da, B, 512, 1, st)));
+    }
+    // readout / softmax / logits backward with this step's queries; dQ gets
+    // the logits path plus the answer row's copy of Q
+    HIPCHK(attn_bwd(Wf(L.Hs) + f0 * P * 128, io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
+                    Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1));
+    {  // query MLP backward to its input h_{t-1}
+      LTf::Params pa{prm + L.poff[Q4W], qd, qd};
+      LRfj::Params pb{Wf(L.dQf) + f0 * qd, qd, B};
+      EpiReluBwdT ep{Wf(L.dq2s) + f0 * qd, Wf(L.q2s) + f0 * qd, qd, qd, qd, B};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, qd, B, qd, 1, st)));
+    }
+    {
+      LTf::Params pa{prm + L.poff[Q2W], 128, 128};
+      LRfj::Params pb{Wf(L.dq2s) + f0 * qd, qd, B};
+      EpiReluBwdT ep{Wf(L.dq1s) + f0 * 128, Wf(L.q1s) + f0 * 128, 128, 128, 128, B};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 128, B, qd, 1, st)));
+    }
+    {  // dh_{t-1} = W0^T dq1 (query path) + W_hh^T dgates (recurrent path)
+      LTf::Params pa{prm + L.poff[Q0W], 256, 256};
+      LRfj::Params pb{Wf(L.dq1s) + f0 * 128, 128, B};
+      EpiStoreAddT ep{dhc, dAOX + f0 * 512 + 256, 256, 512, 256, B};
+      HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, B, 128, 1, st)));
+    }
+  }
+  if (io->dcore_h0) HIPCHK(hipMemcpyAsync(io->dcore_h0, dhc, sB, hipMemcpyDeviceToDevice, st));
+  if (io->dcore_c0) HIPCHK(hipMemcpyAsync(io->dcore_c0, dcc, sB, hipMemcpyDeviceToDevice, st));
+  // weight gradients, batched over all T*B frames
+  auto wgrad = [&](const float* dA, int lda, int Mi, const float* X, int ldx, int Nj, float* out, int ldo) -> int {
+    LTf::Params pa{dA, lda, Mi};
+    LTfj::Params pb{X, ldx, Nj};
+    EpiStore<true> ep{out, ldo, Mi, Nj};
+    HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, Mi, Nj, F, wgrad_splits(cdiv(Mi, 64) * cdiv(Nj, 64), F, CF::BK),
+                                        st)));
+    return AAA_OK;
+  };
+  int rc;
+  if ((rc = wgrad(Wf(L.dY), L.ldy, L.ldy, CH + (size_t)B * 256, 256, 256, Wf(L.gWhd), 256))) return rc;
+  HIPCHK(colsum(Wf(L.dY), L.ldy, F, L.ldy, Wf(L.gbhd), st));
+  if ((rc = wgrad(Wf(L.dLG), 1024, 1024, AOX, 512, 512, Wf(L.gWihhp), 512))) return rc;
+  HIPCHK(colsum(Wf(L.dLG), 1024, F, 1024, Wf(L.gblc), st));
+  if ((rc = wgrad(dAOX, 512, 256, Wf(L.hid1), 512, 512, grads + L.poff[A2W], 512))) return rc;
+  HIPCHK(colsum(dAOX, 512, F, 256, grads + L.poff[A2B], st));
+  if ((rc = wgrad(Wf(L.dH1), 512, 512, Wf(L.ans), L.ans_ld, L.ans_ld, Wf(L.gW1p), L.ans_ld))) return rc;
+  HIPCHK(colsum(Wf(L.dH1), 512, F, 512, grads + L.poff[A0B], st));
+  if ((rc = wgrad(Wf(L.dQf), qd, qd, Wf(L.q2s), qd, qd, grads + L.poff[Q4W], qd))) return rc;
+  HIPCHK(colsum(Wf(L.dQf), qd, F, qd, grads + L.poff[Q4B], st));
+  if ((rc = wgrad(Wf(L.dq2s), qd, qd, Wf(L.q1s), 128, 128, grads + L.poff[Q2W], 128))) return rc;
+  HIPCHK(colsum(Wf(L.dq2s), qd, F, qd, grads + L.poff[Q2B], st));
+  if ((rc = wgrad(Wf(L.dq1s), 128, 128, CH, 256, 256, grads + L.poff[Q0W], 256))) return rc;
+  HIPCHK(colsum(Wf(L.dq1s), 128, F, 128, grads + L.poff[Q0B], st));
+  F32Unpack up;
+  up.gW1p = Wf(L.gW1p); up.gWihp = Wf(L.gWihp); up.gblc = Wf(L.gblc); up.gWhd = Wf(L.gWhd); up.gbhd = Wf(L.gbhd);
+  up.a0w = grads + L.poff[A0W]; up.wih = grads + L.poff[WIH]; up.bih = grads + L.poff[BIH];
+  up.bhh = grads + L.poff[BHH]; up.pw = grads + L.poff[PW]; up.vw = grads + L.poff[VW];
+  up.pb = grads + L.poff[PB]; up.vb = grads + L.poff[VB];
+  up.ans_in = L.ans_in; up.ans_ld = L.ans_ld; up.A = L.A;
+  up.gWihhp = Wf(L.gWihhp); up.whh = grads + L.poff[WHH];
+  HIPCHK(unpack_f32(up, st));
+  return AAA_OK;
+}
+
 template <typename T>
 static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st) {
   using C = CfgFor<T>;
@@ -708,6 +931,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
     HIPCHK(hipMemsetAsync(ws + L.dQs, 0, L.ws - L.dQs, st));
     HIPCHK(concat_dy(F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
+    if (L.sc) {
+      const int rc = head_backward_stateful(L, io, st);
+      if (rc) return rc;
+    } else {
     {  // heads dgrad fused with the zero-state LSTMCell backward
       LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
       LRfj::Params pb{Wf(L.dY), L.ldy, F};
@@ -774,6 +1001,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     up.pb = grads + L.poff[PB]; up.vb = grads + L.poff[VB];
     up.ans_in = L.ans_in; up.ans_ld = L.ans_ld; up.A = L.A;
     HIPCHK(unpack_f32(up, st));
+    }
   }
 
   // Off-chain backward work for the steps [lo, hi): weight/bias grads of the

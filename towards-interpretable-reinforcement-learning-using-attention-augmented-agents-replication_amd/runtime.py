@@ -15,14 +15,16 @@ from . import _native as N
 
 class UnrollRunner:
     def __init__(self, B: int, T: int, H: int, W: int, nq: int = 4, A: int = 18,
-                 dtype: str = "fp32", device=None):
+                 dtype: str = "fp32", device=None, stateful_core: bool = False):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
         self.lib = N.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
-        self.cfg = N.Cfg(B, T, H, W, nq, A, N.BF16 if dtype == "bf16" else N.F32, 0)
+        self.stateful_core = bool(stateful_core)
+        self.cfg = N.Cfg(B, T, H, W, nq, A, N.BF16 if dtype == "bf16" else N.F32,
+                         N.FLAG_STATEFUL_CORE if stateful_core else 0)
         self.B, self.T, self.H, self.W, self.nq, self.A, self.dtype = B, T, H, W, nq, A, dtype
         self.h, self.w = N.grid(H, W)
         self.P = self.h * self.w
@@ -56,7 +58,10 @@ class UnrollRunner:
         return io
 
     def forward(self, flat_params, packed, basis, frames, workspace, prev_reward=None, prev_action=None,
-                h0=None, c0=None, want_attn=True, want_state=False):
+                h0=None, c0=None, want_attn=True, want_state=False, core=None):
+        """Returns (logits, values, attn, hT, cT); a stateful-core runner also
+        returns the core state (core_hT, core_cT) (B, 256), starting from
+        ``core`` = (h0, c0) or zeros."""
         T, B, A = self.T, self.B, self.A
         dev = self.device
         self._check_frames(frames)
@@ -68,14 +73,24 @@ class UnrollRunner:
         # keep converted inputs alive until the launches are enqueued
         keep = dict(prev_reward=_f32(prev_reward, (T, B)), prev_action=_f32(prev_action, (T, B)),
                     h0=_f32(h0, self.state_shape()), c0=_f32(c0, self.state_shape()))
+        extra = {}
+        if self.stateful_core:
+            ch0, cc0 = core if core is not None else (None, None)
+            extra = dict(core_h0=_f32(ch0, (B, 256)), core_c0=_f32(cc0, (B, 256)),
+                         core_hT=torch.empty(B, 256, device=dev), core_cT=torch.empty(B, 256, device=dev))
         io = self._io(params=flat_params, packed=packed, basis=basis, frames=frames,
-                      logits=logits, values=values, attn=attn, hT=hT, cT=cT, workspace=workspace, **keep)
+                      logits=logits, values=values, attn=attn, hT=hT, cT=cT, workspace=workspace, **keep, **extra)
         N.check(self.lib.aaa_forward(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(dev)), "forward")
+        if self.stateful_core:
+            return logits, values, attn, hT, cT, extra["core_hT"], extra["core_cT"]
         return logits, values, attn, hT, cT
 
     def backward(self, flat_params, packed, basis, frames, workspace, dlogits, dvalues=None, dhT=None,
-                 dcT=None, grads=None, want_state_grads=False, phases=N.BWD_ALL):
+                 dcT=None, grads=None, want_state_grads=False, phases=N.BWD_ALL, dcore=None, want_core_grads=False):
+        """Returns (grads, dh0, dc0); a stateful-core runner also returns the
+        core-state grads (dcore_h0, dcore_c0) when ``want_core_grads``."""
         dev = self.device
+        B = self.B
         if grads is None:
             grads = torch.empty(self.n_params, device=dev)
         dh0 = torch.empty(self.state_shape(), device=dev) if want_state_grads else None
@@ -83,10 +98,18 @@ class UnrollRunner:
         keep = dict(dlogits=_f32(dlogits, (self.T, self.B, self.A)),
                     dvalues=_f32(dvalues, (self.T, self.B, self.A)),
                     dhT=_f32(dhT, self.state_shape()), dcT=_f32(dcT, self.state_shape()))
+        extra = {}
+        if self.stateful_core:
+            dch, dcc = dcore if dcore is not None else (None, None)
+            extra = dict(dcore_hT=_f32(dch, (B, 256)), dcore_cT=_f32(dcc, (B, 256)),
+                         dcore_h0=torch.empty(B, 256, device=dev) if want_core_grads else None,
+                         dcore_c0=torch.empty(B, 256, device=dev) if want_core_grads else None)
         io = self._io(params=flat_params, packed=packed, basis=basis, frames=frames, workspace=workspace,
-                      grads=grads, dh0=dh0, dc0=dc0, **keep)
+                      grads=grads, dh0=dh0, dc0=dc0, **keep, **extra)
         N.check(self.lib.aaa_backward(ctypes.byref(self.cfg), ctypes.byref(io), phases, N.stream_ptr(dev)),
                 "backward")
+        if self.stateful_core:
+            return grads, dh0, dc0, extra["dcore_h0"], extra["dcore_c0"]
         return grads, dh0, dc0
 
     def _check_frames(self, frames):
