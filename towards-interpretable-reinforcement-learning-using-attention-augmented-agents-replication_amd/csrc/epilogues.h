@@ -1,6 +1,7 @@
 // GEMM epilogues.  Each is called once per (4 consecutive rows i..i+3, column j)
 // of the D tile with the fp32 accumulators; it owns its bounds checks.
 #pragma once
+#include <type_traits>
 #include "common.h"
 
 namespace aaa {
@@ -130,27 +131,45 @@ __device__ __forceinline__ void gate_bwd(float dh, const f32x4& g, float cprev, 
   dc = dcc * gf;
 }
 
+// Gate-activation storage: fp32, or fp16 on the bf16 path (values in (-1, 1),
+// 2^-11 relative; the backward's only use of them), half the bytes of the
+// step epilogues' largest stream.
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 load_gates(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 load_gates(const _Float16* p) {
+  const f16x4 h = *reinterpret_cast<const f16x4*>(p);
+  return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+}
+__device__ __forceinline__ void store_gates(float* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void store_gates(_Float16* p, const f32x4& v) {
+  *reinterpret_cast<f16x4*>(p) = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+}
+
 // ConvLSTM forward step epilogue: D[n = 4ch+g][m] = Wh*h_{t-1}; the x-part
 // (Wx*x_t + b, batched over all frames beforehand) is read from ``gates``
 // and overwritten in place with the activations.
-template <typename T>
+template <typename T, typename GT = float>
 struct EpiConvLstmFwd {
   const float* cprev;  // [M][128]  c_{t-1}
   float* cnext;        // [M][128]  c_t
   float* hout;         // [M][128]  h_t (fp32, attention input)
   T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
-  float* gates;        // [M][512]  in: Wx*x_t + b;  out: post-activation (i,f,c~,o)
+  GT* gates;           // [M][512]  in: Wx*x_t + b (fp32 only);  out: post-activation (i,f,c~,o)
   int Nj;              // M = B*P
   // Fused x-part (the GEMM's K covers [x_t | h_{t-1}]): the gate bias [512]
-  // takes the place of the batched x-part, which ``gates`` then does not hold.
+  // takes the place of the batched x-part, which ``gates`` then does not hold
+  // (and must not: an fp16 gate buffer only ever holds activations).
   const float* bias = nullptr;
   // Inputs of one (4-row, column) group, loadable before the K loop (glds.h).
   struct Pre { f32x4 zx; float cp; };
   __device__ __forceinline__ Pre prefetch(int i, int j) const {
     Pre p{f32x4{0.f, 0.f, 0.f, 0.f}, 0.f};
     if (j < Nj && i < 512) {
-      p.zx = bias ? *reinterpret_cast<const f32x4*>(bias + i)
-                  : *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
+      if constexpr (std::is_same<GT, float>::value)
+        p.zx = bias ? *reinterpret_cast<const f32x4*>(bias + i)
+                    : *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + i);
+      else
+        p.zx = *reinterpret_cast<const f32x4*>(bias + i);
       p.cp = cprev[(size_t)j * 128 + (i >> 2)];
     }
     return p;
@@ -163,7 +182,7 @@ struct EpiConvLstmFwd {
     cnext[(size_t)j * 128 + ch] = c;
     hout[(size_t)j * 128 + ch] = h;
     xhnext[(size_t)j * 192 + 64 + ch] = (T)h;
-    *reinterpret_cast<f32x4*>(gates + (size_t)j * 512 + i) = f32x4{gi, gf, gc, go};
+    store_gates(gates + (size_t)j * 512 + i, f32x4{gi, gf, gc, go});
   }
   __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
     finish(i, j, v0, v1, v2, v3, prefetch(i, j));
@@ -181,10 +200,10 @@ struct EpiConvLstmFwd {
 // the bias gradient then needs only a column sum over T x (column tiles) rows
 // instead of a pass over the whole dZ tensor, and it is taken before dz is
 // rounded to TZ (the reference sums fp32 gradients).
-template <typename TZ>
+template <typename TZ, typename GT = float>
 struct EpiConvLstmBwd {
   float* dx;            // [M][64]  dY2 slot t
-  const float* gates;   // [M][512] slot t-1
+  const GT* gates;      // [M][512] slot t-1
   const float* cprev;   // [M][128] c_{t-2}
   const float* ccur;    // [M][128] c_{t-1}
   const float* dO;      // [M][128] attention-path grad of h_{t-1}
@@ -208,7 +227,7 @@ struct EpiConvLstmBwd {
     p.cc = *reinterpret_cast<const f32x4*>(ccur + (size_t)j * 128 + ch);
     p.dcv = *reinterpret_cast<const f32x4*>(dC + (size_t)j * 128 + ch);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) p.g[e] = *reinterpret_cast<const f32x4*>(gates + (size_t)j * 512 + 4 * (ch + e));
+    for (int e = 0; e < 4; ++e) p.g[e] = load_gates(gates + (size_t)j * 512 + 4 * (ch + e));
     return p;
   }
   __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre& p,

@@ -44,8 +44,8 @@ hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int an
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st);
 template <typename TI> hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st);
-template <typename TZ>
-hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const float* gates, const float* cprev,
+template <typename TZ, typename GT>
+hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const GT* gates, const float* cprev,
                          const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);

@@ -305,10 +305,10 @@ __global__ void k_colsum(const TI* __restrict__ X, int ld, int M, int N, int row
 // One workgroup per tile of ``bj`` pixels (the BPTT GEMM's column tile), 128
 // channels x 4 pixel lanes; dz is stored as TZ and, when ``part`` is set, the
 // tile's fp32 gate-bias partials go to part[tile][512] (EpiConvLstmBwd::flush).
-template <typename TZ>
+template <typename TZ, typename GT>
 __global__ void __launch_bounds__(512)
 k_gate_bwd_last(int M, int bj, const float* __restrict__ dO, const float* __restrict__ dhT,
-                const float* __restrict__ gates, const float* __restrict__ cprev, const float* __restrict__ ccur,
+                const GT* __restrict__ gates, const float* __restrict__ cprev, const float* __restrict__ ccur,
                 float* dC, TZ* dz, float* part) {
   __shared__ f32x4 red[4][128];
   const int ch = threadIdx.x & 127, sl = threadIdx.x >> 7;
@@ -318,7 +318,7 @@ k_gate_bwd_last(int M, int bj, const float* __restrict__ dO, const float* __rest
   for (int m = m0 + sl; m < m1; m += 4) {
     const size_t idx = (size_t)m * 128 + ch;
     const float dh = dO[idx] + (dhT ? dhT[idx] : 0.f);
-    const f32x4 g = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
+    const f32x4 g = load_gates(gates + (size_t)m * 512 + 4 * ch);
     float dc = dC[idx], di, df, dcg, dout;
     gate_bwd(dh, g, cprev[idx], ccur[idx], dc, di, df, dcg, dout);
     dC[idx] = dc;
@@ -711,11 +711,11 @@ hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st)
   return hipGetLastError();
 }
 
-template <typename TZ>
-hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const float* gates, const float* cprev,
+template <typename TZ, typename GT>
+hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const GT* gates, const float* cprev,
                          const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st) {
-  hipLaunchKernelGGL(k_gate_bwd_last<TZ>, dim3((M + bj - 1) / bj), dim3(512), 0, st, M, bj, dO, dhT, gates, cprev,
-                     ccur, dC, dz, part);
+  hipLaunchKernelGGL((k_gate_bwd_last<TZ, GT>), dim3((M + bj - 1) / bj), dim3(512), 0, st, M, bj, dO, dhT, gates,
+                     cprev, ccur, dC, dz, part);
   return hipGetLastError();
 }
 
@@ -807,10 +807,14 @@ hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st) {
 }
 template hipError_t colsum<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t colsum<__bf16>(const __bf16*, int, int, int, float*, hipStream_t);
-template hipError_t gate_bwd_last<float>(int, int, const float*, const float*, const float*, const float*, const float*,
-                                         float*, float*, float*, hipStream_t);
-template hipError_t gate_bwd_last<__bf16>(int, int, const float*, const float*, const float*, const float*,
-                                          const float*, float*, __bf16*, float*, hipStream_t);
+template hipError_t gate_bwd_last<float, float>(int, int, const float*, const float*, const float*, const float*,
+                                                const float*, float*, float*, float*, hipStream_t);
+template hipError_t gate_bwd_last<__bf16, float>(int, int, const float*, const float*, const float*, const float*,
+                                                 const float*, float*, __bf16*, float*, hipStream_t);
+template hipError_t gate_bwd_last<float, _Float16>(int, int, const float*, const float*, const _Float16*,
+                                                   const float*, const float*, float*, float*, float*, hipStream_t);
+template hipError_t gate_bwd_last<__bf16, _Float16>(int, int, const float*, const float*, const _Float16*,
+                                                    const float*, const float*, float*, __bf16*, float*, hipStream_t);
 template hipError_t frames_rgbx<float>(int, int, int, const float*, float*, hipStream_t);
 template hipError_t frames_rgbx<__bf16>(int, int, int, const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t);

@@ -356,6 +356,17 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
   return out_tiles32 < 1024 ? 5 : 4;                                          // C2: 1936 tiles, 56 us (reg 58)
 }
 
+// fp16 gate-activation storage (halves the step epilogues' largest stream):
+// bf16 operands, fused x-part (the gate buffer then holds activations only)
+// and the bf16 BPTT tiles 7/8.  AAA_GATES_F16=0 keeps fp32.  Forward and
+// backward evaluate this identically (same env, same shapes).
+static bool fused_x(int dt) { return env_int("AAA_FUSED_X", dt == AAA_BF16 ? 1 : 0) != 0; }
+static bool gates_f16(int dt, int M) {
+  if (dt != AAA_BF16 || !fused_x(dt) || !env_int("AAA_GATES_F16", 1)) return false;
+  const int bt = step_tile((long)(128 / 32) * ((M + 31) / 32), "AAA_BPTT_TILE", true, true);
+  return bt == 7 || bt == 8;
+}
+
 // Whether the LDS-DMA ring can run tile config CK (every wave issues the same DMA count).
 template <class CK>
 constexpr bool pipe_even() {
@@ -553,18 +564,24 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   // [x_t | h_{t-1}], bias in the epilogue): no batched x-part GEMM and no
   // fp32 x-part round trip through HBM (tools/ubench/bf16_tiles: the step's
   // epilogue traffic, not its MFMAs, is half its time).  AAA_FUSED_X=0/1 overrides.
-  if (env_int("AAA_FUSED_X", std::is_same<T, __bf16>::value ? 1 : 0)) {
+  if (fused_x(L.dt)) {
     const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
     const T* WpXH = (const T*)(pk + L.k_WpXH);
-    for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
-      EpiConvLstmFwd<T> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
-                           Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
-                           Wf(L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
-      TimerScope tim(AAA_TIMER_FWD_STEP, st);
-      HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep, 512,
-                                          1728, st)));
-    }
+    auto steps = [&](auto gtag) -> int {
+      using GT = decltype(gtag);
+      for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
+        EpiConvLstmFwd<T, GT> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
+                                 Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
+                                 (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
+        TimerScope tim(AAA_TIMER_FWD_STEP, st);
+        HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
+                                            512, 1728, st)));
+      }
+      return AAA_OK;
+    };
+    const int rc = gates_f16(L.dt, M) ? steps(_Float16{}) : steps(float{});
+    if (rc) return rc;
     return forward_tail<T>(L, io, st);
   }
   // x-part of the ConvLSTM steps (not recurrent): Gt <- Wx * x_t + b, in
@@ -1091,9 +1108,18 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                       (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8;
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
-    HIPCHK(gate_bwd_last<T>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
-                            Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128, Wf(L.dC),
-                            Wt(L.dZ) + (size_t)t1 * M * 512, part ? part + (size_t)t1 * ntj * 512 : nullptr, st));
+    const bool g16 = gates_f16(L.dt, M);
+    if (g16)
+      HIPCHK((gate_bwd_last<T, _Float16>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT,
+                                         (const _Float16*)(ws + L.Gt) + (size_t)t1 * M * 512,
+                                         Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128,
+                                         Wf(L.dC), Wt(L.dZ) + (size_t)t1 * M * 512,
+                                         part ? part + (size_t)t1 * ntj * 512 : nullptr, st)));
+    else
+      HIPCHK((gate_bwd_last<T, float>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT, Wf(L.Gt) + (size_t)t1 * M * 512,
+                                      Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128,
+                                      Wf(L.dC), Wt(L.dZ) + (size_t)t1 * M * 512,
+                                      part ? part + (size_t)t1 * ntj * 512 : nullptr, st)));
     const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * L.esz);  // one step slice of dZ
     const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
     int done_hi = L.T;   // chunks [lo, done_hi) not yet issued
@@ -1113,40 +1139,51 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       const bool prev = t > 0;
       if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
-      EpiConvLstmBwd<T> ep{nullptr,
-                           prev ? Wf(L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
-                           prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
-                           Wf(L.Cst) + (size_t)t * M * 128,
-                           prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
-                           Wf(L.dC),
-                           prev ? Wt(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
-                           prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64,
-                           part && prev ? part + (size_t)(t - 1) * ntj * 512 : nullptr};
       const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st);
-      using EB = EpiConvLstmBwd<T>;
-      hipError_t e;
-      switch (bwd_tile) {
-        case 1: e = step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 2: e = step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 3: e = step_gemm<CfgK4BFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 4:   // 3-stage ring, DMA interleaved with the MFMAs (tools/ubench/step_ablate: 57.9 vs 59.4 us)
-          e = step_gemm<CfgK4BFor<T>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
-          break;
-        case 5: e = step_gemm<CfgK4For<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 6: e = step_gemm<C, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-        case 7:   // bf16: 128x128, BK128, 2-way in-WG split-K (tools/ubench/bf16_tiles: 48 vs 53-60 us at C3)
-          if constexpr (std::is_same<T, float>::value) e = hipErrorInvalidValue;
-          else e = step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+      auto step = [&](auto gtag) -> hipError_t {
+        using GT = decltype(gtag);
+        using EB = EpiConvLstmBwd<T, GT>;
+        EB ep{nullptr,
+              prev ? (const GT*)(ws + L.Gt) + (size_t)(t - 1) * M * 512 : nullptr,
+              prev ? Wf(L.Cst) + (size_t)(t - 1) * M * 128 : nullptr,
+              Wf(L.Cst) + (size_t)t * M * 128,
+              prev ? Wf(L.dO) + (size_t)(t - 1) * M * 128 : nullptr,
+              Wf(L.dC),
+              prev ? Wt(L.dZ) + (size_t)(t - 1) * M * 512 : nullptr,
+              prev ? nullptr : io->dh0, prev ? 1 : 0, M, 64,
+              part && prev ? part + (size_t)(t - 1) * ntj * 512 : nullptr};
+        if constexpr (!std::is_same<GT, float>::value) {   // fp16 gates: the bf16 tiles only (gates_f16)
+          if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
+          else if (bwd_tile == 7)
+            return step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                        4608, st);
+          else
+            return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
                                                                        4608, st);
-          break;
-        case 8:   // bf16: 128x64, BK128, 2-way in-WG split-K, 4 waves (small batches)
-          if constexpr (std::is_same<T, float>::value) e = hipErrorInvalidValue;
-          else e = step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
-                                                                      4608, st);
-          break;
-        default: e = step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st); break;
-      }
+        } else {
+          switch (bwd_tile) {
+            case 1: return step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+            case 2: return step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+            case 3: return step_gemm<CfgK4BFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+            case 4:   // 3-stage ring, DMA interleaved with the MFMAs (tools/ubench/step_ablate: 57.9 vs 59.4 us)
+              return step_gemm<CfgK4BFor<T>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                       4608, st);
+            case 5: return step_gemm<CfgK4For<T>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+            case 6: return step_gemm<C, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+            case 7:   // bf16: 128x128, BK128, 2-way in-WG split-K (tools/ubench/bf16_tiles: 48 vs 53-60 us at C3)
+              if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
+                                                                              128, 4608, st);
+            case 8:   // bf16: 128x64, BK128, 2-way in-WG split-K, 4 waves (small batches)
+              if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
+                                                                             128, 4608, st);
+            default: return step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
+          }
+        }
+      };
+      const hipError_t e = g16 ? step(_Float16{}) : step(float{});
       HIPCHK(e);
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
