@@ -54,6 +54,30 @@ def flop_per_frame(H, W, nq, A=18):
     return 3 * fwd - c1
 
 
+def attention_hbm(ka, B, T, P, nq, steps):
+    """Achieved HBM GB/s of the fused attention readout kernels:
+    algorithmic bytes per frame (fp32) -- forward reads the ConvLSTM output O
+    (128 ch) and writes the attention map and the answer row; backward reads O,
+    the map and the answer grad, writes dO and dQ -- times the frames per launch."""
+    import attention  # noqa: F401
+    from aaa_amd import _native as N
+    ans_ld = (256 * nq + 2 + 7) // 8 * 8
+    per_frame = {N.TIMER_ATTN_FWD: 4 * (128 * P + nq * P + ans_ld),
+                 N.TIMER_ATTN_BWD: 4 * (2 * 128 * P + nq * P + 184 * nq + 72 * nq)}
+    names = {N.TIMER_ATTN_FWD: "attention readout fwd (softmax over P, fused)",
+             N.TIMER_ATTN_BWD: "attention readout bwd"}
+    out = {}
+    for k, (ms, n) in ka.items():
+        if n == 0:
+            continue
+        per_launch = per_frame[k] * B * T * steps / n
+        avg_s = ms / n * 1e-3
+        gbps = per_launch / avg_s / 1e9
+        out[names[k]] = {"avg_us": round(avg_s * 1e6, 2), "launches": n, "bytes_per_launch": round(per_launch),
+                         "achieved_GBps": round(gbps, 1), "peak_GBps": 8000.0, "frac": round(gbps / 8000.0, 4)}
+    return out
+
+
 def cpu_baseline(cfg):
     """Time the CPU oracle (the reference op sequence, oracle/ref_cpu.py) on the host."""
     import numpy as np
@@ -162,6 +186,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kt = {k: N.timing_read(k) for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
+    ka = {k: N.timing_read(k) for k in (N.TIMER_ATTN_FWD, N.TIMER_ATTN_BWD)}
     N.timing_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -213,6 +238,7 @@ def main():
         "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
                          "frac": round(value * fpf / world / 1e12 / peak, 4)},
         "kernels": kernels,
+        "hbm_kernels": attention_hbm(ka, B, T, learner.runner.P, nq, args.steps),
     }
     # fused Adam (excluded from the metric, which stops at
     # ready gradients): HBM-bound, 28 B per parameter (p, g, m, v read; p, m, v written)

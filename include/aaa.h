@@ -163,7 +163,9 @@ enum aaa_timer {
   AAA_TIMER_FWD_STEP = 0,    /* fused ConvLSTM forward step (one per t)          */
   AAA_TIMER_BPTT_STEP = 1,   /* ConvLSTM dgrad + fused gate backward (one per t) */
   AAA_TIMER_CORE_WGRAD = 2,  /* ConvLSTM weight-gradient GEMM over all frames    */
-  AAA_TIMER_N = 3
+  AAA_TIMER_ATTN_FWD = 3,    /* fused spatial-softmax attention readout (HBM)    */
+  AAA_TIMER_ATTN_BWD = 4,    /* its backward (HBM)                               */
+  AAA_TIMER_N = 5
 };
 int aaa_timing_enable(int on);
 int aaa_timing_read(int kind, double* total_ms, long* launches);

@@ -24,7 +24,7 @@ EXPORTS = (
     "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
     "aaa_adam_step", "aaa_reinforce", "aaa_sample_actions",
 )
-TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD = 0, 1, 2
+TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
 
 
 class Cfg(ctypes.Structure):

@@ -69,40 +69,56 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // logits A[p][q] = K[p]·Q[q] with K = [O[:8] | S], softmax over the P grid
 // positions (spatial_softmax), readout a[q] = sum_p A[p][q] [O[8:] | S][p],
 // and the answer row [a_0..a_nq-1 | Q_0..Q_nq-1 | r | a_prev | 0-pad].
+// HBM-bound: the frame's O rows are read once, 16 B per lane, each row's
+// 480 B of V by consecutive lanes (readout: 46 four-column groups x 5
+// position slices, slices summed through LDS).
+constexpr int kAttnFwdThreads = 256;
+constexpr int kAttnSlices = 5;          // position slices of the readout (46 * 5 = 230 threads)
 template <int NQ>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kAttnFwdThreads)
 k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
            int P, float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* L = sm;               // P*NQ
-  float* Qs = sm + P * NQ;     // NQ*72
+  float* L = sm;                         // P*NQ
+  float* Qs = L + P * NQ;                // NQ*72
+  float* red = Qs + NQ * 72;             // kAttnSlices * NQ * 184
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
   const float* Qf = Q + (size_t)f * qs;   // qs = 0: one query for every frame (Q1)
-  for (int i = tid; i < NQ * 72; i += 256) Qs[i] = Qf[i];
+  for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) Qs[i] = Qf[i];
   __syncthreads();
-  for (int idx = tid; idx < P * NQ; idx += 256) {
-    const int p = idx / NQ, q = idx - (idx / NQ) * NQ;
+  // logits: one thread per position, all NQ queries (its 8 key channels read once)
+  for (int p = tid; p < P; p += kAttnFwdThreads) {
     const f32x4 k0 = *reinterpret_cast<const f32x4*>(O + p * 128);
     const f32x4 k1 = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
-    const float* qq = Qs + q * 72;
-    float s = k0[0] * qq[0] + k0[1] * qq[1] + k0[2] * qq[2] + k0[3] * qq[3] +
-              k1[0] * qq[4] + k1[1] * qq[5] + k1[2] * qq[6] + k1[3] * qq[7];
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float* qq = Qs + q * 72;
+      acc[q] = k0[0] * qq[0] + k0[1] * qq[1] + k0[2] * qq[2] + k0[3] * qq[3] +
+               k1[0] * qq[4] + k1[1] * qq[5] + k1[2] * qq[6] + k1[3] * qq[7];
+    }
     if (SQ) {
-      s += SQ[idx];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] += SQ[p * NQ + q];
     } else {   // per-frame query: the basis half of the logit here
       const f32x4* s4 = reinterpret_cast<const f32x4*>(S + p * 64);
 #pragma unroll 4
       for (int c = 0; c < 16; ++c) {
         const f32x4 v = s4[c];
-        s += v[0] * qq[8 + 4 * c] + v[1] * qq[9 + 4 * c] + v[2] * qq[10 + 4 * c] + v[3] * qq[11 + 4 * c];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float* qq = Qs + q * 72 + 8 + 4 * c;
+          acc[q] += v[0] * qq[0] + v[1] * qq[1] + v[2] * qq[2] + v[3] * qq[3];
+        }
       }
     }
-    L[idx] = s;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) L[p * NQ + q] = acc[q];
   }
   __syncthreads();
-  for (int q = wave; q < NQ; q += 4) {
+  for (int q = wave; q < NQ; q += kAttnFwdThreads / 64) {
     float m = -INFINITY;
     for (int p = lane; p < P; p += 64) m = fmaxf(m, L[p * NQ + q]);
     m = wave_max(m);
@@ -117,29 +133,36 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
   }
   __syncthreads();
-  float* arow = ans + (size_t)f * ans_ld;
-  for (int c = tid; c < 184; c += 256) {
-    float acc[NQ];
+  // readout: thread (column group g of 4, position slice sl)
+  if (tid < 46 * kAttnSlices) {
+    const int g = tid % 46, sl = tid / 46;
+    float acc[NQ][4];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-    if (c < 120) {
-      for (int p = 0; p < P; ++p) {
-        const float v = O[p * 128 + 8 + c];
+    for (int q = 0; q < NQ; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
+    const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
+    const int ld = g < 30 ? 128 : 64;
+    for (int p = sl; p < P; p += kAttnSlices) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] += L[p * NQ + q] * v;
-      }
-    } else {
-      for (int p = 0; p < P; ++p) {
-        const float v = S[p * 64 + c - 120];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] += L[p * NQ + q] * v;
+      for (int q = 0; q < NQ; ++q) {
+        const float a = L[p * NQ + q];
+        acc[q][0] += a * v[0]; acc[q][1] += a * v[1]; acc[q][2] += a * v[2]; acc[q][3] += a * v[3];
       }
     }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) arow[q * 184 + c] = acc[q];
+    for (int q = 0; q < NQ; ++q)
+      *reinterpret_cast<f32x4*>(red + (sl * NQ + q) * 184 + 4 * g) = f32x4{acc[q][0], acc[q][1], acc[q][2], acc[q][3]};
   }
-  for (int i = tid; i < NQ * 72; i += 256) arow[NQ * 184 + i] = Qs[i];
-  for (int i = NQ * 256 + tid; i < ans_ld; i += 256) {
+  __syncthreads();
+  float* arow = ans + (size_t)f * ans_ld;
+  for (int i = tid; i < NQ * 184; i += kAttnFwdThreads) {
+    float v = 0.f;
+#pragma unroll
+    for (int sl = 0; sl < kAttnSlices; ++sl) v += red[sl * NQ * 184 + i];
+    arow[i] = v;
+  }
+  for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) arow[NQ * 184 + i] = Qs[i];
+  for (int i = NQ * 256 + tid; i < ans_ld; i += kAttnFwdThreads) {
     float v = 0.f;
     if (i == NQ * 256) v = pr ? pr[f] : 0.f;
     else if (i == NQ * 256 + 1) v = pa ? pa[f] : 0.f;
@@ -147,56 +170,63 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   }
 }
 
+constexpr int kAttnChunk = 32;   // positions per staged V chunk (attention backward)
+constexpr int kVld = 188;        // its row pitch in floats (184 + 4: 16-B aligned rows, spread banks)
+
 // Backward of the readout / softmax / logits for one frame: from da (the
 // answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
-// this frame's contribution to dQ.
+// this frame's dQ (logits path, plus the answer row's Q columns when addq).
 template <int NQ>
-__global__ void __launch_bounds__(128 * NQ)
+__global__ void __launch_bounds__(512)
 k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
            float* __restrict__ dO, float* __restrict__ dQp) {
-  constexpr int NT = 128 * NQ;     // thread (q, p0): head q, grid positions p0, p0+128, ...
-  constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT; LDS < 64 KB at P=441, NQ=8)
+  constexpr int NT = 512, NW = NT / 64;
+  constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* A = sm;                 // P*NQ
   float* dA = A + P * NQ;        // P*NQ  (becomes dlogits)
   float* da = dA + P * NQ;       // NQ*184
   float* Qs = da + NQ * 184;     // NQ*72
-  float* ss = Qs + NQ * 72;      // NQ (padded to 4)
-  float* red = ss + 4 * ((NQ + 3) / 4);   // G*NQ*72
+  float* ss = Qs + NQ * 72;      // NQ (padded to 8)
+  float* red = ss + 8;           // G*NQ*72
+  float* Vc = red + G * NQ * 72; // kAttnChunk * kVld
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
   for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
   __syncthreads();
-  // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S]: one thread per (p, q),
-  // q uniform per 128 threads (da reads broadcast), rows of V as float4.
-  {
-    const int q = tid >> 7;
-    const float* dq = da + q * 184;
-    for (int p = tid & 127; p < P; p += 128) {
-      const f32x4* o4 = reinterpret_cast<const f32x4*>(O + p * 128 + 8);
-      const f32x4* s4 = reinterpret_cast<const f32x4*>(S + p * 64);
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll 6
-      for (int c = 0; c < 30; ++c) {
-        const f32x4 v = o4[c];
-        a0 += dq[4 * c] * v[0] + dq[4 * c + 1] * v[1];
-        a1 += dq[4 * c + 2] * v[2] + dq[4 * c + 3] * v[3];
-      }
-#pragma unroll 4
-      for (int c = 0; c < 16; ++c) {
-        const f32x4 v = s4[c];
-        a0 += dq[120 + 4 * c] * v[0] + dq[121 + 4 * c] * v[1];
-        a1 += dq[122 + 4 * c] * v[2] + dq[123 + 4 * c] * v[3];
-      }
-      dA[p * NQ + q] = a0 + a1;
+  // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S], in chunks of
+  // kAttnChunk positions: the chunk's V rows are staged in LDS by consecutive
+  // threads (16 B each, coalesced rows), then thread (p, q) takes its dot
+  // product from LDS (no cross-lane reductions).
+  for (int p0 = 0; p0 < P; p0 += kAttnChunk) {
+    const int np = min(kAttnChunk, P - p0);
+    for (int i = tid; i < np * 46; i += NT) {
+      const int pp = i / 46, g = i - pp * 46, p = p0 + pp;
+      const f32x4 v = g < 30 ? *reinterpret_cast<const f32x4*>(O + p * 128 + 8 + 4 * g)
+                             : *reinterpret_cast<const f32x4*>(S + p * 64 + 4 * (g - 30));
+      *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = v;
     }
+    __syncthreads();
+    for (int i = tid; i < np * NQ; i += NT) {
+      const int pp = i / NQ, q = i - pp * NQ;
+      const f32x4* vr = reinterpret_cast<const f32x4*>(Vc + pp * kVld);
+      const f32x4* dr = reinterpret_cast<const f32x4*>(da + q * 184);
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll 2
+      for (int g = 0; g < 46; ++g) {
+        const f32x4 v = vr[g], d = dr[g];
+        a0 += v[0] * d[0] + v[1] * d[1];
+        a1 += v[2] * d[2] + v[3] * d[3];
+      }
+      dA[(p0 + pp) * NQ + q] = a0 + a1;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   // softmax backward: dlogit = A (dA - sum_p A dA)
-  for (int q = wave; q < NQ; q += NT / 64) {
+  for (int q = wave; q < NQ; q += NW) {
     float s = 0.f;
     for (int p = lane; p < P; p += 64) s += A[p * NQ + q] * dA[p * NQ + q];
     s = wave_sum(s);
@@ -208,18 +238,27 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     dA[i] = A[i] * (dA[i] - ss[q]);
   }
   __syncthreads();
+  // dO: 16 B per thread, rows written by consecutive threads
   float* dOf = dO + (size_t)f * P * 128;
-  for (int i = tid; i < P * 128; i += NT) {
-    const int p = i >> 7, c = i & 127;
-    float acc = 0.f;
-    if (c < 8) {
+  for (int i = tid; i < P * 32; i += NT) {
+    const int p = i >> 5, c4 = (i & 31) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c4 < 8) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc += dA[p * NQ + q] * Qs[q * 72 + c];
+      for (int q = 0; q < NQ; ++q) {
+        const float d = dA[p * NQ + q];
+        const float* qq = Qs + q * 72 + c4;
+        acc[0] += d * qq[0]; acc[1] += d * qq[1]; acc[2] += d * qq[2]; acc[3] += d * qq[3];
+      }
     } else {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc += A[p * NQ + q] * da[q * 184 + c - 8];
+      for (int q = 0; q < NQ; ++q) {
+        const float a = A[p * NQ + q];
+        const float* dd = da + q * 184 + c4 - 8;
+        acc[0] += a * dd[0]; acc[1] += a * dd[1]; acc[2] += a * dd[2]; acc[3] += a * dd[3];
+      }
     }
-    dOf[i] = acc;
+    *reinterpret_cast<f32x4*>(dOf + p * 128 + c4) = acc;
   }
   // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] | S]: G position groups,
   // every loaded K element feeds all NQ heads, partials reduced through LDS.
@@ -659,11 +698,13 @@ hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const fl
 hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
                     const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
                     int qs) {
-  const size_t sh = (size_t)(P * nq + nq * 72) * sizeof(float);
+  const size_t sh = (size_t)(P * nq + nq * 72 + kAttnSlices * nq * 184) * sizeof(float);
   if (nq == 4)
-    hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(256), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
+    hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans,
+                       ans_ld);
   else if (nq == 8)
-    hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(256), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
+    hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans,
+                       ans_ld);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -671,11 +712,16 @@ hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float
 hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
                     int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs, int addq) {
   const int G = 7;   // k_attn_bwd's dQ position groups
-  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72) * sizeof(float);
-  if (nq == 4)
-    hipLaunchKernelGGL(k_attn_bwd<4>, dim3(F), dim3(512), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
-  else if (nq == 8)
-    hipLaunchKernelGGL(k_attn_bwd<8>, dim3(F), dim3(1024), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
+  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72 + kAttnChunk * kVld) * sizeof(float);
+  if (sh > 160 * 1024) return hipErrorInvalidValue;
+  auto launch = [&](auto kern) {
+    if (sh > 64 * 1024)   // large grids (168x168: P = 441, nq = 8) use more than the default 64 KiB
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sh);
+    hipLaunchKernelGGL(kern, dim3(F), dim3(512), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
+  };
+  if (nq == 4) launch(k_attn_bwd<4>);
+  else if (nq == 8) launch(k_attn_bwd<8>);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

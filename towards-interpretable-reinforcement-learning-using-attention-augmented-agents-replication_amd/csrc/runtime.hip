@@ -691,9 +691,12 @@ static int forward_tail_stateful(const Layout& L, const aaa_io* io, hipStream_t 
       HIPCHK((tail_gemm(pa, pb, ep, qd, B, qd, st)));
     }
     // attention readout with this step's per-frame queries (basis logits in-kernel)
-    HIPCHK(attn_fwd(Wf(L.Hs) + f0 * P * 128, io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
-                    io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
-                    Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
+    {
+      TimerScope tim(AAA_TIMER_ATTN_FWD, st);
+      HIPCHK(attn_fwd(Wf(L.Hs) + f0 * P * 128, io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
+                      io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
+                      Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
+    }
     {  // answer_processor.0 + ReLU
       LRf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, 512};
       LRfj::Params pb{Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, B};
@@ -736,8 +739,11 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
   // constant query (Q1) + fused attention readout over all T*B frames
   HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
                    io->basis, P, L.nq, Wf(L.q1), Wf(L.q2), Wf(L.Q), Wf(L.SQ), st));
-  HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
-                  Wf(L.ans), L.ans_ld, st));
+  {
+    TimerScope tim(AAA_TIMER_ATTN_FWD, st);
+    HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
+                    Wf(L.ans), L.ans_ld, st));
+  }
   if (io->attn) HIPCHK(hipMemcpyAsync(io->attn, Wf(L.Am), (size_t)F * P * L.nq * 4, hipMemcpyDeviceToDevice, st));
   using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
   using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
@@ -870,8 +876,11 @@ static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t
     }
     // readout / softmax / logits backward with this step's queries; dQ gets
     // the logits path plus the answer row's copy of Q
-    HIPCHK(attn_bwd(Wf(L.Hs) + f0 * P * 128, io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
-                    Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1));
+    {
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st);
+      HIPCHK(attn_bwd(Wf(L.Hs) + f0 * P * 128, io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
+                      Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1));
+    }
     {  // query MLP backward to its input h_{t-1}
       LTf::Params pa{prm + L.poff[Q4W], qd, qd};
       LRfj::Params pb{Wf(L.dQf) + f0 * qd, qd, B};
@@ -1006,7 +1015,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       HIPCHK(colsum(Wf(L.dH1), 512, F, 512, grads + L.poff[A0B], st));
     }
     // attention readout / softmax / logits backward, then the query MLP
-    HIPCHK(attn_bwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq, Wf(L.dO), Wf(L.dQp), st));
+    {
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st);
+      HIPCHK(attn_bwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq, Wf(L.dO), Wf(L.dQp), st));
+    }
     HIPCHK(colsum(Wf(L.dQp), L.qd, F, L.qd, Wf(L.dQs), st));
     HIPCHK(query_bwd(Wf(L.dQs), grads + L.poff[A0B], prm + L.poff[A0W], L.ans_in, L.nq, prm + L.poff[Q2W],
                      prm + L.poff[Q4W], Wf(L.q1), Wf(L.q2), grads + L.poff[Q4W], grads + L.poff[Q4B],
