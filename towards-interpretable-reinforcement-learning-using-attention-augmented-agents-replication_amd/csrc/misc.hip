@@ -72,8 +72,8 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // HBM-bound: the frame's O rows are read once, 16 B per lane, each row's
 // 480 B of V by consecutive lanes (readout: 46 four-column groups x 5
 // position slices, slices summed through LDS).
-constexpr int kAttnFwdThreads = 256;
-constexpr int kAttnSlices = 5;          // position slices of the readout (46 * 5 = 230 threads)
+constexpr int kAttnFwdThreads = 512;
+constexpr int kAttnSlices = 11;         // position slices of the readout (46 * 11 = 506 threads)
 template <int NQ>
 __global__ void __launch_bounds__(kAttnFwdThreads)
 k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
@@ -141,6 +141,7 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     for (int q = 0; q < NQ; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
     const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
     const int ld = g < 30 ? 128 : 64;
+#pragma unroll 4
     for (int p = sl; p < P; p += kAttnSlices) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
 #pragma unroll
