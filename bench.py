@@ -201,7 +201,7 @@ def main():
     M = B * learner.runner.P
     F = B * T
     # bf16 runs the x-part inside every step (runtime.hip forward_impl, AAA_FUSED_X)
-    fused_x = int(os.environ.get("AAA_FUSED_X", "1" if dtype == "bf16" else "0")) != 0
+    fused_x = int(os.environ.get("AAA_FUSED_X", "1" if dtype == "bf16" or M <= 1024 else "0")) != 0
     per_iter = {
         N.TIMER_FWD_STEP: (T * 2.0 * M * 512 * 1728 if fused_x       # [x | h] parts of all T steps
                            else (T - 1) * 2.0 * M * 512 * 1152),   # h-part of steps 1..T-1 (x-part batched)

@@ -29,8 +29,9 @@ struct F32Unpack {
   float* whh = nullptr;
 };
 
-hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
-                     const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st);
+hipError_t query_pack(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4, int nq,
+                      float* q1, float* q2, float* Q, hipStream_t st);
+hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hipStream_t st);
 // qs: per-frame query stride in floats (0 = one query for all frames, Q1);
 // SQ == NULL computes the basis half of the logits per frame.  addq adds the
 // answer row's Q-column gradient (dAns[f][184*nq ...]) into dQp.

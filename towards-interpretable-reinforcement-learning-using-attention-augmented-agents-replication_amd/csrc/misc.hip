@@ -684,14 +684,19 @@ static inline int nblk(long n, int bs = 256) {
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
-hipError_t query_fwd(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4,
-                     const float* S, int P, int nq, float* q1, float* q2, float* Q, float* SQ, hipStream_t st) {
+hipError_t query_pack(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4, int nq,
+                      float* q1, float* q2, float* Q, hipStream_t st) {
   // QueryNetwork on the always-zero prev_output (attention.py:184-198, 325-331; Q1):
-  // q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4.
+  // q1 = relu(b0), q2 = relu(W2 q1 + b2), Q = W4 q2 + b4 -- a function of the
+  // weights alone, so it is computed when they are packed, not per forward.
   const int qd = 72 * nq;
   hipLaunchKernelGGL(k_query_layer, dim3((qd + 3) / 4), dim3(256), 0, st, W2, 128, b0, 1, b2, 1, qd, q2, q1);
   hipLaunchKernelGGL(k_query_layer, dim3((qd + 3) / 4), dim3(256), 0, st, W4, qd, q2, 0, b4, 0, qd, Q,
                      (float*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hipStream_t st) {
   hipLaunchKernelGGL(k_query_sq, dim3((P + 3) / 4), dim3(256), 0, st, S, Q, P, nq, SQ);
   return hipGetLastError();
 }

@@ -68,8 +68,8 @@ struct Layout {
   int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_Wihhp, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
-  size_t Xp, Y1, XH, Hs, Cst, Gt, q1, q2, Q, SQ, Am, ans, hid1, AO, LG, LC, LH;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
   // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
@@ -123,6 +123,9 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.k_Whd = take((size_t)L.ldy * 256 * 4);
   L.k_bhd = take((size_t)L.ldy * 4);
   L.k_Wihhp = take(L.sc ? 1024 * 512 * 4 : 0);   // [W_ih | W_hh], rows 4u+g
+  L.k_q1 = take(128 * 4);                          // the constant query (Q1) and its activations
+  L.k_q2 = take((size_t)L.qd * 4);
+  L.k_Q = take((size_t)L.qd * 4);
   L.packed = p;
   // workspace
   p = 0;
@@ -133,9 +136,6 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.Hs = take(F * P * 128 * 4);
   L.Cst = take((size_t)(L.T + 1) * M * 128 * 4);
   L.Gt = take(F * P * 512 * 4);
-  L.q1 = take(128 * 4);
-  L.q2 = take((size_t)L.qd * 4);
-  L.Q = take((size_t)L.qd * 4);
   L.SQ = take(P * L.nq * 4);
   L.Am = take(F * P * L.nq * 4);
   L.ans = take(F * L.ans_ld * 4);
@@ -360,9 +360,12 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
 // bf16 operands, fused x-part (the gate buffer then holds activations only)
 // and the bf16 BPTT tiles 7/8.  AAA_GATES_F16=0 keeps fp32.  Forward and
 // backward evaluate this identically (same env, same shapes).
-static bool fused_x(int dt) { return env_int("AAA_FUSED_X", dt == AAA_BF16 ? 1 : 0) != 0; }
+// The x-part rides in the step GEMM for bf16 and for small steps (M = B*P
+// pixels; the actor's B = 1: one launch instead of two latency-bound ones);
+// fp32 at C2 (M = 3872) keeps the batched x-part (measured 5.02 vs 5.09 ms).
+static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
 static bool gates_f16(int dt, int M) {
-  if (dt != AAA_BF16 || !fused_x(dt) || !env_int("AAA_GATES_F16", 1)) return false;
+  if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
   const int bt = step_tile((long)(128 / 32) * ((M + 31) / 32), "AAA_BPTT_TILE", true, true);
   return bt == 7 || bt == 8;
 }
@@ -511,6 +514,8 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     fp.Wihhp = (float*)(pk + L.k_Wihhp);
   }
   HIPCHK(pack_f32(fp, st));
+  HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
+                    (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
   return AAA_OK;
 }
 
@@ -564,7 +569,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   // [x_t | h_{t-1}], bias in the epilogue): no batched x-part GEMM and no
   // fp32 x-part round trip through HBM (tools/ubench/bf16_tiles: the step's
   // epilogue traffic, not its MFMAs, is half its time).  AAA_FUSED_X=0/1 overrides.
-  if (fused_x(L.dt)) {
+  if (fused_x(L.dt, M)) {
     const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
     const T* WpXH = (const T*)(pk + L.k_WpXH);
@@ -737,11 +742,11 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     if (rc) return rc;
   } else {
   // constant query (Q1) + fused attention readout over all T*B frames
-  HIPCHK(query_fwd(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B],
-                   io->basis, P, L.nq, Wf(L.q1), Wf(L.q2), Wf(L.Q), Wf(L.SQ), st));
+  const float* Qc = (const float*)(pk + L.k_Q);
+  HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
   {
     TimerScope tim(AAA_TIMER_ATTN_FWD, st);
-    HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
+    HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
                     Wf(L.ans), L.ans_ld, st));
   }
   if (io->attn) HIPCHK(hipMemcpyAsync(io->attn, Wf(L.Am), (size_t)F * P * L.nq * 4, hipMemcpyDeviceToDevice, st));
@@ -1017,11 +1022,13 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     // attention readout / softmax / logits backward, then the query MLP
     {
       TimerScope tim(AAA_TIMER_ATTN_BWD, st);
-      HIPCHK(attn_bwd(Wf(L.Hs), io->basis, Wf(L.Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq, Wf(L.dO), Wf(L.dQp), st));
+      HIPCHK(attn_bwd(Wf(L.Hs), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
+                      Wf(L.dO), Wf(L.dQp), st));
     }
     HIPCHK(colsum(Wf(L.dQp), L.qd, F, L.qd, Wf(L.dQs), st));
     HIPCHK(query_bwd(Wf(L.dQs), grads + L.poff[A0B], prm + L.poff[A0W], L.ans_in, L.nq, prm + L.poff[Q2W],
-                     prm + L.poff[Q4W], Wf(L.q1), Wf(L.q2), grads + L.poff[Q4W], grads + L.poff[Q4B],
+                     prm + L.poff[Q4W], (const float*)(pk + L.k_q1), (const float*)(pk + L.k_q2), grads + L.poff[Q4W],
+                     grads + L.poff[Q4B],
                      grads + L.poff[Q2W], grads + L.poff[Q2B], grads + L.poff[Q0B], st));
     F32Unpack up;
     up.gW1p = Wf(L.gW1p); up.gWihp = Wf(L.gWihp); up.gblc = Wf(L.gblc); up.gWhd = Wf(L.gWhd); up.gbhd = Wf(L.gbhd);
