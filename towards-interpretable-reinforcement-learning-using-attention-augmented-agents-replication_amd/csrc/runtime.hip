@@ -556,6 +556,10 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     if constexpr (32 % C::BK == 0) {   // LDS-DMA ring (tools/ubench/conv_cfg: 62 vs 67 us)
       HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Wt(L.Y1), g, F * P,
                                  (uint32_t)((size_t)F * L.P1 * 32 * L.esz), ep, 64, 512, st)));
+    } else if (pipe_batched()) {   // bf16: a BK=32 ring, one 4x4 tap row's 32 channels per K tile
+      HIPCHK((step_gemm<GemmCfg<T, 64, 128, 32, 2, 2>, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Wt(L.Y1), g,
+                                                           F * P, (uint32_t)((size_t)F * L.P1 * 32 * L.esz), ep, 64,
+                                                           512, st)));
     } else {
       using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
       HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P}, ep, 64, F * P, 512, 1, st)));
@@ -1080,6 +1084,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       if (std::is_same<T, __bf16>::value && halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
         const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
         HIPCHK((launch_halo<HD>(hp, ep, s)));
+      } else if (std::is_same<T, __bf16>::value && pipe_batched()) {
+        // larger grids (21x21 at 168x168): 64x128 on a 3-stage ring (bf16_tiles at C3: 643 vs 716 us for 64x64)
+        HIPCHK((step_gemm<GemmCfg<T, 64, 128, 64, 2, 2>, true, T, T, EpiStoreT<float>, 3>(WdT, 4608, 64, dz, g, rows,
+                                                                                          zb, ep, 64, 4608, s)));
       } else {
         HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
                                : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
