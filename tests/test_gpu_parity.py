@@ -225,6 +225,17 @@ def test_c2_full_size_vs_oracle(cuda):
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B, dtype=torch.float64), RTOL, "C2 ")
 
 
+@pytest.mark.parametrize("B", [128, 256])
+def test_c3_c4_full_size_bf16_vs_emulated_oracle(cuda, B):
+    """Configs 3 (B=256) and 4's per-GPU shape (B=128), T=20, on the bf16 path in
+    full -- fused x-part, fp16 gate storage, both bf16 BPTT tiles, the halo dx --
+    against the bf16-emulated oracle at the bf16 tolerance (2e-2)."""
+    T = 20
+    torch.set_num_threads(16)
+    _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
+             f"B={B} bf16 ")
+
+
 def test_repeat_is_deterministic_enough(cuda):
     """Two identical runs agree (atomics may reorder fp32 sums: ~1e-6)."""
     a = _run_unroll(_agent(cuda), 3, 4, cuda)
