@@ -51,6 +51,90 @@ struct EpiStoreParity {
   }
 };
 
+// Bias partials of a conv-input gradient for the LDS-staged epilogues
+// (glds.h/halo.h: Pre/Acc/flush): every thread sums the fp32 values of its
+// fixed 4-row group, the workgroup reduces them through LDS and adds one
+// atomic per channel -- the bias gradient is the column sum of the fp32
+// gradient (as the reference's autograd takes it) even where the gradient
+// itself is stored rounded to the next GEMM's operand type.
+struct BiasAcc {
+  struct Pre {};
+  struct Acc { float s[4]; };
+  __device__ __forceinline__ Pre prefetch(int, int) const { return {}; }
+  template <int G4, int NT>
+  __device__ __forceinline__ void flush_to(const Acc& acc, float* red, int i0, int Mi, float* bg) const {
+    static_assert(NT % G4 == 0, "fixed row group per thread");
+    constexpr int NS = NT / G4;
+    const int r4 = threadIdx.x % G4, sl = threadIdx.x / G4;
+    *reinterpret_cast<f32x4*>(red + (sl * G4 + r4) * 4) = f32x4{acc.s[0], acc.s[1], acc.s[2], acc.s[3]};
+    __syncthreads();
+    for (int c = threadIdx.x; c < G4 * 4; c += NT) {
+      float t = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < NS; ++k) t += red[k * G4 * 4 + c];
+      if (i0 + c < Mi) atomicAdd(bg + i0 + c, t);
+    }
+  }
+};
+
+// out[j*ld + i..i+3] = (OT)v (a conv-input gradient stored in the operand type
+// of the GEMMs that read it) and bg[i] += sum_j v (its conv's bias gradient).
+template <typename OT>
+struct EpiStoreBiasT : BiasAcc {
+  OT* out;
+  int ld, Mi, Nj;
+  float* bg;
+  EpiStoreBiasT(OT* o, int l, int mi, int nj, float* b) : out(o), ld(l), Mi(mi), Nj(nj), bg(b) {}
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre&,
+                                         Acc* acc = nullptr) const {
+    if (j >= Nj || i >= Mi) return;
+    store4(out + (size_t)j * ld + i, v0, v1, v2, v3);
+    if (acc) { acc->s[0] += v0; acc->s[1] += v1; acc->s[2] += v2; acc->s[3] += v3; }
+  }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;   // unstaged kernels: per-element bias atomics
+    store4(out + (size_t)j * ld + i, v0, v1, v2, v3);
+    atomicAdd(bg + i, v0); atomicAdd(bg + i + 1, v1); atomicAdd(bg + i + 2, v2); atomicAdd(bg + i + 3, v3);
+  }
+  template <int G4, int NT>
+  __device__ __forceinline__ void flush(const Acc& acc, float* red, int i0, int) const {
+    flush_to<G4, NT>(acc, red, i0, Mi, bg);
+  }
+};
+
+// The stride-2 dgrad parity class of EpiStoreParity, stored in OT, with the
+// bias partials of BiasAcc (conv1's bias gradient from dY1).
+template <typename OT>
+struct EpiStoreParityBias : BiasAcc {
+  OT* out;             // [F][H1][W1][C]
+  int C, Nj, Ha, Wa, H1, W1, py, px;
+  uint64_t mHW, mW;
+  float* bg;
+  EpiStoreParityBias(OT* o, int c, int nj, int ha, int wa, int h1, int w1, int py_, int px_, uint64_t mhw, uint64_t mw,
+                     float* b)
+      : out(o), C(c), Nj(nj), Ha(ha), Wa(wa), H1(h1), W1(w1), py(py_), px(px_), mHW(mhw), mW(mw), bg(b) {}
+  __device__ __forceinline__ OT* at(int i, int j) const {
+    const int f = (int)(((uint64_t)j * mHW) >> 32), r = j - f * Ha * Wa;
+    const int a = (int)(((uint64_t)r * mW) >> 32), b = r - a * Wa;
+    return out + ((size_t)(f * H1 + 2 * a + py) * W1 + 2 * b + px) * C + i;
+  }
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre&,
+                                         Acc* acc = nullptr) const {
+    if (j >= Nj || i >= C) return;
+    store4(at(i, j), v0, v1, v2, v3);
+    if (acc) { acc->s[0] += v0; acc->s[1] += v1; acc->s[2] += v2; acc->s[3] += v3; }
+  }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= C) return;
+    store4(at(i, j), v0, v1, v2, v3);
+    atomicAdd(bg + i, v0); atomicAdd(bg + i + 1, v1); atomicAdd(bg + i + 2, v2); atomicAdd(bg + i + 3, v3);
+  }
+  template <int G4, int NT>
+  __device__ __forceinline__ void flush(const Acc& acc, float* red, int i0, int) const {
+    flush_to<G4, NT>(acc, red, i0, C, bg);
+  }
+};
+
 // dx[j*ld + i] = v * (mask[j*ldm + i] > 0)   (ReLU backward through a saved output)
 struct EpiReluBwdT {
   float* out;

@@ -154,8 +154,8 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.dC = take(M * 128 * 4);
   L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
   L.dZp = take((size_t)L.T * ((M + 31) / 32) * 512 * 4);  // gate-bias partials per (step, column tile)
-  L.dY2 = take(F * P * 64 * 4);
-  L.dY1 = take(F * L.P1 * 32 * 4);
+  L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
+  L.dY1 = take(F * L.P1 * 32 * e);
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -800,7 +800,29 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
 // conv2 dgrad (stride 2, k4, pad 2) as four parity-class 2x2 convs over dY2:
 // output pixel (2a+py, 2b+px) only receives taps ky = py + 2(1-ty), kx = px + 2(1-tx).
 template <typename T>
-static int conv2_dgrad(const Layout& L, const char* pk, const float* dy2, float* dy1, int frames, hipStream_t s) {
+static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, int frames, float* gbias,
+                       hipStream_t s) {
+  if constexpr (!std::is_same<T, float>::value) {
+    // bf16: dY2 is already bf16 -> the LDS-DMA ring, dY1 stored bf16, conv1's
+    // bias gradient summed from the fp32 values in the epilogue
+    using CP = GemmCfg<T, 32, 128, 64, 1, 4>;
+    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
+    for (int cls = 0; cls < 4; ++cls) {
+      const int py = cls >> 1, px = cls & 1;
+      const int Ha = (L.H1 - py + 1) / 2, Wa = (L.W1 - px + 1) / 2;
+      if (Ha <= 0 || Wa <= 0) continue;
+      const int rows = frames * Ha * Wa;
+      EpiStoreParityBias<T> ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
+                               ((1ull << 32) + Wa - 1) / Wa, gbias};
+      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreParityBias<T>, 2>(
+          typename PA::Params{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32},
+          typename PB::Params{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
+                              (uint32_t)((size_t)frames * L.P * 64 * L.esz)},
+          ep, 32, rows, 256, 1, s)));
+    }
+    return AAA_OK;
+  }
   using C3 = Cfg32For<T>;
   using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
   using LB = LdIm2colB<float, T, C3::BJ, C3::BK, C3::NT>;
@@ -810,9 +832,9 @@ static int conv2_dgrad(const Layout& L, const char* pk, const float* dy2, float*
     if (Ha <= 0 || Wa <= 0) continue;
     const int rows = frames * Ha * Wa;
     typename LA::Params pa{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32};
-    typename LB::Params pb{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
+    typename LB::Params pb{(const float*)dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
                            (uint32_t)((size_t)frames * L.P * 64 * 4)};
-    EpiStoreParity ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
+    EpiStoreParity ep{(float*)dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
                       ((1ull << 32) + Wa - 1) / Wa};
     HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows, 256, 1, s)));
   }
@@ -821,9 +843,9 @@ static int conv2_dgrad(const Layout& L, const char* pk, const float* dy2, float*
 
 // conv1 weight gradient over RGBx frames (Cin 4; the 4th channel's grad is dropped on unpack)
 template <typename T>
-static int conv1_wgrad(const Layout& L, const float* dy1, const T* xp, int frames, float* gW, hipStream_t s) {
+static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, float* gW, hipStream_t s) {
   using C3 = Cfg32For<T>;
-  using LA = LdRowsTB<float, T, C3::BI, C3::BK, C3::NT>;
+  using LA = LdRowsTB<T, T, C3::BI, C3::BK, C3::NT>;
   using LB = LdIm2colTB<T, T, C3::BJ, C3::BK, C3::NT>;   // bf16 chunks = 2 taps x 4 ch, in-bounds (bordered image)
   const int rows1 = frames * L.P1;
   typename LA::Params pa{dy1, 32, 32, rows1};
@@ -1073,32 +1095,38 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       if (rc) return rc;
     }
     {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
-      // 64x64 tiles (64x128 measured slower: occupancy)
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
-      EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
       const T* WdT = (const T*)(pk + L.k_WdTl);
       const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
-      // bf16 on small grids: halo-staged conv, one frame per 64x128 tile
-      // (tools/ubench/halo_tiles: 658 vs 771 us for the ring at C3)
-      using HD = HaloCfg<__bf16, 64, 128, 64, 1, 2, 1, 176>;
-      if (std::is_same<T, __bf16>::value && halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
-        const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
-        HIPCHK((launch_halo<HD>(hp, ep, s)));
-      } else if (std::is_same<T, __bf16>::value && pipe_batched()) {
-        // larger grids (21x21 at 168x168): 64x128 on a 3-stage ring (bf16_tiles at C3: 643 vs 716 us for 64x64)
-        HIPCHK((step_gemm<GemmCfg<T, 64, 128, 64, 2, 2>, true, T, T, EpiStoreT<float>, 3>(WdT, 4608, 64, dz, g, rows,
-                                                                                          zb, ep, 64, 4608, s)));
-      } else {
+      if constexpr (std::is_same<T, float>::value) {
+        // 64x64 tiles (64x128 measured slower: occupancy)
+        EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
         HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
                                : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+      } else {
+        // bf16: dY2 stored bf16 (its readers round it to bf16 anyway), conv2's
+        // bias gradient summed from the fp32 values in the epilogue
+        EpiStoreBiasT<T> ep{Wt(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
+        // small grids: halo-staged conv, one frame per 64x128 tile
+        // (tools/ubench/halo_tiles: 658 vs 771 us for the ring at C3)
+        using HD = HaloCfg<__bf16, 64, 128, 64, 1, 2, 1, 176>;
+        if (halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+          const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
+          HIPCHK((launch_halo<HD>(hp, ep, s)));
+        } else {
+          // larger grids (21x21 at 168x168): 64x128 on a 3-stage ring (bf16_tiles at C3: 643 vs 716 us for 64x64)
+          HIPCHK((step_gemm<GemmCfg<T, 64, 128, 64, 2, 2>, true, T, T, EpiStoreBiasT<T>, 3>(WdT, 4608, 64, dz, g, rows,
+                                                                                            zb, ep, 64, 4608, s)));
+        }
       }
     }
     if (!vision_here) return AAA_OK;
-    const float* dy2 = Wf(L.dY2) + (size_t)lo * M * 64;
-    float* dy1 = Wf(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
+    const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
+    T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
     const int rows1 = F1 * L.P1;
+    constexpr bool f32 = std::is_same<T, float>::value;   // fp32: bias grads by column sums
     {  // conv2 wgrad / bias
-      using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
+      using LA = LdRowsTB<T, T, C::BI, C::BK, NT>;
       using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
       typename LA::Params pa{dy2, 64, 64, rows};
       typename LB::Params pb{Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(),
@@ -1106,13 +1134,13 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
       const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
-      HIPCHK(colsum(dy2, 64, rows, 64, grads + L.poff[C1B], s));
+      if (f32) HIPCHK(colsum(dy2, 64, rows, 64, grads + L.poff[C1B], s));
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
-      int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, s);
+      int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
       if (!rc) rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
       if (rc) return rc;
-      HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
+      if (f32) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
     return AAA_OK;
   };
@@ -1231,21 +1259,22 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   if (phases & AAA_BWD_VISION) {
     if (!vision_here) {   // VISION alone: its chunk work over all frames, here
       const int rows = F * P, rows1 = F * L.P1;
+      constexpr bool f32 = std::is_same<T, float>::value;
       {
-        using LA = LdRowsTB<float, T, C::BI, C::BK, NT>;
+        using LA = LdRowsTB<T, T, C::BI, C::BK, NT>;
         using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
-        typename LA::Params pa{Wf(L.dY2), 64, 64, rows};
+        typename LA::Params pa{Wt(L.dY2), 64, 64, rows};
         typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
                                (uint32_t)((size_t)rows1 * 32 * L.esz)};
         EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
         HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(cdiv(512, C::BJ), rows, C::BK), st)));
-        HIPCHK(colsum(Wf(L.dY2), 64, rows, 64, grads + L.poff[C1B], st));
+        if (f32) HIPCHK(colsum(Wt(L.dY2), 64, rows, 64, grads + L.poff[C1B], st));
       }
       {
-        int rc = conv2_dgrad<T>(L, pk, Wf(L.dY2), Wf(L.dY1), F, st);
-        if (!rc) rc = conv1_wgrad<T>(L, Wf(L.dY1), Wt(L.Xp), F, Wf(L.gWp1), st);
+        int rc = conv2_dgrad<T>(L, pk, Wt(L.dY2), Wt(L.dY1), F, grads + L.poff[C0B], st);
+        if (!rc) rc = conv1_wgrad<T>(L, Wt(L.dY1), Wt(L.Xp), F, Wf(L.gWp1), st);
         if (rc) return rc;
-        HIPCHK(colsum(Wf(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
+        if (f32) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
     }
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
