@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
   const double flop = 2.0 * M * 128 * 4608;
   {  // BPTT step: D[128][M] = WdT[64:192] x gather(dz)
     const ConvGeo g = ConvGeo{512, 512, 0, h, w, h, w, 3, 1, 1, 1}.prep();
-    EpiConvLstmBwd ep{nullptr, gates, cprev, ccur, dO, dC, dzo, nullptr, 1, M, 64};
+    EpiConvLstmBwd<float> ep{nullptr, gates, cprev, ccur, dO, dC, dzo, nullptr, 1, M, 64};
     using LA = GRowsB<float, K4B::BI, K4B::BK, K4B::NT>;
     using LB = GIm2colB<float, K4B::BJ, K4B::BK, K4B::NT>;
     typename LA::Params pa{WdT, 4608, 128};
@@ -65,16 +65,16 @@ int main(int argc, char** argv) {
       const float us = time_us([&] { hipLaunchKernelGGL(kern, grid, dim3(K4B::NT), 0, 0, pa, pb, ep, 4608, 4608, tile_map(grid)); });
       printf("bptt %-34s %8.2f us  %6.1f TF/s\n", name, us, flop / (us * 1e-6) / 1e12);
     };
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 0>, "pipe3 full");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 2, 0>, "pipe2 full");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 2, 0, true>, "pipe2 interleaved DMA");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 0, true>, "pipe3 interleaved DMA");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 1>, "pipe3 no-loop-DMA");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 2>, "pipe3 no-MFMA");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 4>, "pipe3 no-epilogue");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 3>, "pipe3 skeleton (no DMA, no MFMA)");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 7>, "pipe3 skeleton, no epilogue");
-    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd, 3, 5>, "pipe3 MFMA only (no DMA, no epi)");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 0>, "pipe3 full");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 2, 0>, "pipe2 full");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 2, 0, true>, "pipe2 interleaved DMA");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 0, true>, "pipe3 interleaved DMA");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 1>, "pipe3 no-loop-DMA");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 2>, "pipe3 no-MFMA");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 4>, "pipe3 no-epilogue");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 3>, "pipe3 skeleton (no DMA, no MFMA)");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 7>, "pipe3 skeleton, no epilogue");
+    run(gemm_pipe_kernel<K4B, LA, LB, EpiConvLstmBwd<float>, 3, 5>, "pipe3 MFMA only (no DMA, no epi)");
   }
   {  // forward step: D[512][M] = WpH x gather(h_{t-1}) + fused gates
     const ConvGeo g = ConvGeo{128, 192, 64, h, w, h, w, 3, 1, 1, 0}.prep();
@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
   }
   {  // BPTT alternatives
     const ConvGeo g = ConvGeo{512, 512, 0, h, w, h, w, 3, 1, 1, 1}.prep();
-    EpiConvLstmBwd ep{nullptr, gates, cprev, ccur, dO, dC, dzo, nullptr, 1, M, 64};
+    EpiConvLstmBwd<float> ep{nullptr, gates, cprev, ccur, dO, dC, dzo, nullptr, 1, M, 64};
     auto run = [&](auto cfg, auto nbuf, auto ilv, const char* name) {
       using C = decltype(cfg);
       constexpr int NB = decltype(nbuf)::value;
@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
       using LA = GRowsB<float, C::BI, C::BK, C::NT>;
       using LB = GIm2colB<float, C::BJ, C::BK, C::NT>;
       const float us = time_us([&] {
-        CK((launch_pipe<C, LA, LB, EpiConvLstmBwd, NB, IL>(typename LA::Params{WdT, 4608, 128},
+        CK((launch_pipe<C, LA, LB, EpiConvLstmBwd<float>, NB, IL>(typename LA::Params{WdT, 4608, 128},
                                                             typename LB::Params{dz, g, M, (uint32_t)((size_t)M * 2048)},
                                                             ep, 128, M, 4608, 1, 0)));
       });

@@ -335,8 +335,8 @@ template <typename T> using CfgSFor = std::conditional_t<std::is_same<T, float>:
 // Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE override):
 //   0 64x64 BK32 | 1 32x64 BK64 2-way in-WG split-K | 2 ... 4-way | 3 32x64 BK128 4-way
 //   (forward: 3 = 64x64 BK64) | 4-6 the same shapes on the LDS-DMA ring of glds.h
-//   (forward 4 = 64x64, 5 = 32x64 split-K, 6 = 64x64 BK64; BPTT 4 = 32x64 BK128
-//   4-way, 5 = BK64 4-way, 6 = 64x64).  The default picks by how many 32x32
+//   (forward 4 = 128x64 8 waves, 5 = 32x64 split-K, 6 = 64x64 BK64; BPTT 4 = 32x64 BK128
+//   4-way, 5 = BK64 4-way, 6 = 64x64, 9 = 64x32 BK128 4-way).  The default picks by how many 32x32
 //   output tiles the step has, i.e. how many waves it can feed; measured on C2.
 static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
@@ -348,12 +348,14 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 }
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
-  if (v >= 0) return (v >= 7 && !bf16) ? 4 : v;   // tiles 7, 8 exist for bf16 only
+  if (v >= 0) return ((v == 7 || v == 8) && !bf16) || (v == 9 && !bptt) ? 4 : v;   // 7, 8: bf16 only; 9: BPTT only
   // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
   // (tools/ubench/bf16_tiles at B=128: 34.6 vs 39.6 us)
   if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 8;
-  if (bptt) return out_tiles32 < 1024 ? 4 : (out_tiles32 < 1536 ? 1 : 0);   // C2: 484 tiles, 66 us (reg 71)
-  return out_tiles32 < 1024 ? 5 : 4;                                          // C2: 1936 tiles, 56 us (reg 58)
+  // fp32 (C2: 484 BPTT / 1936 forward tiles): 64x32 BPTT 54.6 vs 55.9 us for 32x64; 64x64 BK64
+  // forward 47.9 vs 51.9 us for BK32 (bench.py kernel table, AAA_*_TILE A/B)
+  if (bptt) return out_tiles32 < 1024 ? 9 : (out_tiles32 < 1536 ? 1 : 0);
+  return out_tiles32 < 1024 ? 5 : 6;
 }
 
 // fp16 gate-activation storage (halves the step epilogues' largest stream):
@@ -577,6 +579,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
     const T* WpXH = (const T*)(pk + L.k_WpXH);
+    const int ftile = env_int("AAA_FUSED_TILE", 4);   // 4: 128x64 8 waves, 7: 64x64 4 waves
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
       for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
@@ -584,8 +587,12 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                                  Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
                                  (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
         TimerScope tim(AAA_TIMER_FWD_STEP, st);
-        HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
-                                            512, 1728, st)));
+        if (ftile == 7)
+          HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
+                                             512, 1728, st)));
+        else
+          HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
+                                              512, 1728, st)));
       }
       return AAA_OK;
     };
@@ -639,7 +646,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     switch (fwd_tile) {
       case 1: case 2: e = step_gemm<CfgKFor<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 3: e = step_gemm<Cfg64For<T>, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
-      case 4:   // 128x64, 8 waves (tools/ubench/step_ablate: 45.8 vs 47.4 us for 64x64)
+      case 4:   // 128x64, 8 waves
         e = step_gemm<CfgSFor<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st);
         break;
       case 7: e = step_gemm<C, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
@@ -1158,9 +1165,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
     // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
     // the register-staged ones leave the bias to a column sum over dZ
-    const int bj = bwd_tile == 7 ? 128 : 64;
+    const int bj = bwd_tile == 7 ? 128 : (bwd_tile == 9 ? 32 : 64);
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
-                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8;
+                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 ||
+                      (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>());
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
@@ -1234,6 +1242,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
               if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
               else return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
                                                                              128, 4608, st);
+            case 9:   // 64x32, BK128, 4-way in-WG split-K, 3-stage ring, interleaved DMA
+              return step_gemm<GemmCfg<T, 64, 32, 128, 2, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                          dz_bytes, ep, 128, 4608, st);
             default: return step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
           }
         }
