@@ -105,6 +105,22 @@ def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
                  f"bf16 fused_x={fused}: ")
 
 
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "6", "7"])
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_lstm_wgrad_ring_variants(cuda, monkeypatch, mode, conv_dtype):
+    """ConvLSTM weight gradient on the LDS-DMA ring with transposed fragment
+    reads (AAA_WGRAD_PIPE 1-7: tile shape / ring depth / DMA issue variants; bf16 default 6) or the
+    register-staged GEMM (0).  T*B*121 = 7744 pixels: a whole number of K tiles,
+    which the ring requires (the 1728 im2col columns are 13.5 tiles: ragged)."""
+    monkeypatch.setenv("AAA_WGRAD_PIPE", mode)
+    T, B = 4, 16
+    if conv_dtype == "fp32":
+        _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"wgrad pipe {mode}: ")
+    else:
+        _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
+                 f"bf16 wgrad pipe {mode}: ")
+
+
 def test_c1_against_reference_fixture(cuda, golden):
     """Config 1 (B=1, T=20) against the fixture made by the reference itself."""
     g = golden("G3")

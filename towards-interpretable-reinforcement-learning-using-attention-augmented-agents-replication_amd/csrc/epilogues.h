@@ -167,6 +167,11 @@ struct EpiStore {
   }
 };
 
+// Split-K weight gradients on the LDS-DMA ring: atomics from the accumulators.
+struct EpiAtomicD : EpiStore<true> {
+  static constexpr bool kDirect = true;
+};
+
 // Policy / value heads: rows o < A -> logits, A <= o < 2A -> values (+bias).
 struct EpiHeads {
   float* logits;

@@ -1,4 +1,5 @@
-// LDS-DMA pipelined variant of the MFMA GEMM for k-contiguous operands.
+// LDS-DMA pipelined variant of the MFMA GEMM (k-contiguous operands, and
+// row-contiguous ones whose k runs over pixels: GRowsT / GIm2colT).
 //
 // Operands go global -> LDS with `buffer_load_dwordx4 ... lds` (no VGPR
 // staging, no ds_write pass).  NBUF LDS stages form a ring: at K tile kt the
@@ -52,6 +53,11 @@ template <class EP, bool> struct pre_of { using type = int; };
 template <class EP> struct pre_of<EP, true> { using type = typename EP::Pre; };
 // Epilogues with a per-thread accumulator (EP::Acc) get it passed to finish()
 // and reduced by EP::flush<G4, NT>() after the epilogue (e.g. bias partials).
+// Epilogues marked kDirect (split-K weight-gradient atomics) run straight from
+// the accumulators: lanes of a 32-lane half own 32 consecutive columns of one
+// row, so each atomic instruction covers a contiguous 128-B run of the output.
+template <class EP, class = void> struct is_direct : std::false_type {};
+template <class EP> struct is_direct<EP, std::enable_if_t<EP::kDirect>> : std::true_type {};
 template <class EP, class = void> struct has_acc : std::false_type {};
 template <class EP> struct has_acc<EP, std::void_t<typename EP::Acc>> : std::true_type {};
 template <class EP, bool> struct acc_of { using type = int; };
@@ -198,6 +204,149 @@ __device__ __forceinline__ bf16x8 frag_sw(const __bf16* t, int r, int kofs) {
   return *reinterpret_cast<const bf16x8*>(t + r * BK + (((kofs >> 3) ^ g) << 3));
 }
 
+// Row-contiguous (RC) stages: k-rows of R elements, [BK][R], for operands whose
+// k runs over pixels (weight gradients).  The fragment reads are transposed
+// (bf16: ds_read_b64_tr_b16, a 32-lane half reading 4 k-rows x 4 slots; f32:
+// ds_read_b32 down a column), so the slot XOR spreads each aligned 4-row
+// group over the 256-B bank line: rows sharing a line (16/RS of them) keep
+// their offset, the next 4 groups of lines rotate by 4 slots.
+template <int RS>
+__device__ __forceinline__ int lds_swz_rc(int k) {
+  if constexpr (RS < 8) {
+    return 0;
+  } else {
+    constexpr int RPL = RS >= 16 ? 1 : 16 / RS;
+    return 4 * ((k / RPL) & (RS / 4 - 1));
+  }
+}
+
+// Transposed rows: element (row, k) at src[k*ld + row] (activation gradients,
+// k = pixel), staged RC.  Rows >= nrows and k >= ktotal land as zeros.
+template <typename T, int R, int BK, int NT>
+struct GRowsT {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(T);
+  static constexpr int RS = R / VG;
+  static constexpr int NCH = BK * RS;
+  static constexpr int PER = NCH / NT;
+  static constexpr int ELEMS = R * BK;
+  static_assert(NCH % NT == 0, "every wave must issue the same number of DMA pieces");
+  struct Params { const T* src; int ld; int nrows; int ktotal; };
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t voff[PER];
+  int wofs, rowbytes;
+  __device__ __forceinline__ GRowsT(const Params& p, int row0) {
+    rs = make_rsrc(p.src, (uint32_t)((size_t)p.ktotal * p.ld * sizeof(T)));
+    rowbytes = p.ld * (int)sizeof(T);
+    wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      const int kr = ch / RS, row = row0 + ((ch % RS) ^ lds_swz_rc<RS>(kr)) * VG;
+      voff[c] = row < p.nrows ? (uint32_t)((kr * p.ld + row) * (int)sizeof(T)) : kOOB;
+    }
+  }
+  __device__ __forceinline__ void issue(T* lds, int k0) { issue_part(lds, k0, 0, 1); }
+  // pieces c with c % nparts == part (part, nparts compile-time after unrolling)
+  __device__ __forceinline__ void issue_part(T* lds, int k0, int part, int nparts) {
+    const int ko = __builtin_amdgcn_readfirstlane(k0 * rowbytes);
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (c % nparts == part) dma16(rs, lds + c * NT * VG + wofs, voff[c], ko);
+  }
+};
+
+// Weight-gradient gather, staged RC: row = (tap, ci) fixed per piece, k =
+// output pixel (forward geometry, as LdIm2colTB).  Cin % VG == 0.  Pixels
+// past the source's frames fall outside src_bytes and land as zeros.
+template <typename T, int R, int BK, int NT>
+struct GIm2colT {
+  static constexpr bool KC = false;
+  static constexpr int VG = 16 / (int)sizeof(T);
+  static constexpr int RS = R / VG;
+  static constexpr int NCH = BK * RS;
+  static constexpr int PER = NCH / NT;
+  static constexpr int ELEMS = R * BK;
+  static_assert(NCH % NT == 0, "every wave must issue the same number of DMA pieces");
+  struct Params { const T* src; ConvGeo g; int nrows; uint32_t src_bytes; };
+  __amdgpu_buffer_rsrc_t rs;
+  ConvGeo g;
+  int kr[PER], ky[PER], kx[PER], toff[PER];
+  int wofs;
+  __device__ static bool ok_shape(const ConvGeo& g) { return g.Cin % VG == 0 && !g.transposed; }
+  __device__ __forceinline__ GIm2colT(const Params& p, int row0) : g(p.g) {
+    rs = make_rsrc(p.src, p.src_bytes);
+    wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int ch = threadIdx.x + c * NT;
+      kr[c] = ch / RS;
+      const int kp = row0 + ((ch % RS) ^ lds_swz_rc<RS>(kr[c])) * VG;
+      const bool ok = kp < p.nrows;
+      const int kq = ok ? kp : 0;
+      const int tap = (int)g.dCin.div(kq), ci = kq - tap * g.Cin;
+      ky[c] = ok ? (int)g.dKW.div(tap) : -100000;   // invalid rows never pass the bounds test
+      kx[c] = tap - (int)g.dKW.div(tap) * g.KW;
+      toff[c] = (ky[c] * g.Win + kx[c]) * g.cs + ci + g.coff;
+    }
+  }
+  __device__ __forceinline__ void issue(T* lds, int k0) { issue_part(lds, k0, 0, 1); }
+  __device__ __forceinline__ void issue_part(T* lds, int k0, int part, int nparts) {
+    const int hw = g.Hout * g.Wout;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      if (c % nparts != part) continue;
+      const int m = k0 + kr[c];
+      const int f = (int)g.dHW.div(m), pix = m - f * hw;
+      const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
+      const int iy0 = oy * g.stride - g.pad, ix0 = ox * g.stride - g.pad;
+      const int iy = iy0 + ky[c], ix = ix0 + kx[c];
+      const bool v = (unsigned)iy < (unsigned)g.Hin && (unsigned)ix < (unsigned)g.Win;
+      const int off = ((f * g.Hin + iy0) * g.Win + ix0) * g.cs + toff[c];
+      dma16(rs, lds + c * NT * VG + wofs, v ? (uint32_t)(off * (int)sizeof(T)) : kOOB);
+    }
+  }
+};
+
+// Fragments from an RC stage (same lane -> (row, k) map as frag_sw).
+template <int R>
+__device__ __forceinline__ void frag_rc(const float* t, int r, int kofs, float (&a)[8]) {
+  constexpr int RS = R / 4;
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = kofs + kk;
+    a[kk] = t[k * R + (((r >> 2) ^ lds_swz_rc<RS>(k)) << 2) + (r & 3)];
+  }
+}
+template <int R>
+__device__ __forceinline__ bf16x8 frag_rc(const __bf16* t, int r, int kofs) {
+  // two transpose reads: in each 16-lane group (rows c0..c0+15 of one h) lane
+  // 4q+p addresses k-row kofs+q (+4), rows c0+4p..+3, and receives row
+  // c0 + (lane & 15) of the 4 k-rows
+  constexpr int RS = R / 8;
+  const int li = (int)(threadIdx.x & 15), q = li >> 2, p = li & 3;
+  const int lc = (r - li + 4 * p) >> 3, e = 4 * (p & 1);
+  const int k0 = kofs + q, k1 = k0 + 4;
+  const __bf16* a0 = t + k0 * R + ((lc ^ lds_swz_rc<RS>(k0)) << 3) + e;
+  const __bf16* a1 = t + k1 * R + ((lc ^ lds_swz_rc<RS>(k1)) << 3) + e;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(a0)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(a1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// Dispatch on the loader's stage layout.
+template <class LD, int R, int BK>
+__device__ __forceinline__ void frag_any(const float* t, int r, int kofs, float (&a)[8]) {
+  if constexpr (LD::KC) frag_sw<BK>(t, r, kofs, a);
+  else frag_rc<R>(t, r, kofs, a);
+}
+template <class LD, int R, int BK>
+__device__ __forceinline__ bf16x8 frag_any(const __bf16* t, int r, int kofs) {
+  if constexpr (LD::KC) return frag_sw<BK>(t, r, kofs);
+  else return frag_rc<R>(t, r, kofs);
+}
+
 // Epilogue work split: the tile's (4-row group, column) items, G4 row groups
 // per column, NPT items per thread.  Items with a split prefetch() (EP::Pre)
 // keep at most PD of them in registers: the first PD are requested before the
@@ -297,10 +446,11 @@ __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32
 
 // ABL (diagnostic builds only, tools/ubench): bit 0 = no in-loop DMA, bit 1 =
 // no MFMA, bit 2 = no epilogue.  Production launches use ABL = 0.
-// ILV: issue the next tile's DMA between the MFMA groups of this tile (A
-// pieces after the first 16-deep k step, B after the last) instead of all at
-// once after the barrier, so the DMA issue overlaps MFMA execution.
-template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, bool ILV = false>
+// ILV: issue the next tile's DMA between the MFMA groups of this tile instead
+// of all at once after the barrier, so the DMA issue overlaps MFMA execution:
+// 1 = A pieces after the first 16-deep k step, B after the last; 2 = every
+// loader's pieces spread evenly over the k steps (loaders with issue_part).
+template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, int ILV = 0>
 __global__ void __launch_bounds__(C::NT)
 gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
   using T = typename C::type;
@@ -313,7 +463,9 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   // ONE shared array for everything (a second __shared__ object can make the
   // compiler drain vmcnt before the fragment reads).
   constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
-  constexpr int EPI_T = (int)((WK * BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
+  constexpr bool DIRECT = is_direct<EP>::value;
+  static_assert(!DIRECT || WK == 1, "direct epilogue: no in-WG split-K");
+  constexpr int EPI_T = DIRECT ? 0 : (int)((WK * BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STG > EPI_T ? NBUF * STG : EPI_T];
   static_assert(!has_acc<EP>::value || C::NT * 16 * sizeof(float) <= sizeof(smem),
                 "accumulator reduction does not fit in LDS");
@@ -378,9 +530,9 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
         const int kofs = 16 * (s2 * WK + wk) + 8 * h;
         float af[MI][8], bfr[MJ][8];
 #pragma unroll
-        for (int a = 0; a < MI; ++a) frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+        for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
 #pragma unroll
-        for (int b = 0; b < MJ; ++b) frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+        for (int b = 0; b < MJ; ++b) frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
@@ -388,9 +540,14 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
 #pragma unroll
             for (int b = 0; b < MJ; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
-        if constexpr (ILV) {
+        if constexpr (ILV == 1) {
           if (pf && s2 == 0) la.issue(st, kn);
           if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+        } else if constexpr (ILV == 2) {
+          if (pf) {
+            la.issue_part(st, kn, s2, S2);
+            lb.issue_part(st + AEL, kn, s2, S2);
+          }
         }
       }
     } else {
@@ -403,9 +560,9 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       auto ld = [&](int s2, int slot) {
         const int kofs = 16 * (s2 * WK + wk) + 8 * h;
 #pragma unroll
-        for (int a = 0; a < MI; ++a) fa[slot][a] = frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs);
+        for (int a = 0; a < MI; ++a) fa[slot][a] = frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs);
 #pragma unroll
-        for (int b = 0; b < MJ; ++b) fb[slot][b] = frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
+        for (int b = 0; b < MJ; ++b) fb[slot][b] = frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
       };
 #pragma unroll
       for (int s2 = 0; s2 < NS - 1; ++s2)
@@ -420,9 +577,14 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
           for (int b = 0; b < MJ; ++b)
             acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s2 % NS][a], fb[s2 % NS][b], acc[a][b], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (ILV) {
+        if constexpr (ILV == 1) {
           if (pf && s2 == 0) la.issue(st, kn);
           if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
+        } else if constexpr (ILV == 2) {
+          if (pf) {
+            la.issue_part(st, kn, s2, S2);
+            lb.issue_part(st + AEL, kn, s2, S2);
+          }
         }
       }
     }
@@ -433,11 +595,22 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     return;
   }
   AAA_STAMP(2);
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          ep(i0 + wi * WTI + a * 32 + 8 * g + 4 * h, j0 + wj * WTJ + b * 32 + r32, acc[a][b][4 * g],
+             acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+    return;
+  }
   staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, BJ, tj, pre);
   AAA_STAMP(3);
 }
 
-template <class C, class LA, class LB, class EP, int NBUF = 2, bool ILV = false>
+template <class C, class LA, class LB, class EP, int NBUF = 2, int ILV = 0>
 inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep, int Mi,
                               int Nj, int K, int nsplit, hipStream_t st) {
   if (Mi <= 0 || Nj <= 0 || K <= 0) return hipSuccess;

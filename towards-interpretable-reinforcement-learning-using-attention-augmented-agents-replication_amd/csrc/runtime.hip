@@ -1095,7 +1095,58 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
       return AAA_OK;
     };
-    {
+    // LDS-DMA ring with transposed fragment reads for both operands (k = pixel)
+    // and the split-K atomics straight from the accumulators
+    auto wgrad_lstm_pipe = [&](auto cfg, auto nbuf, auto ilv) -> int {
+      using CW = decltype(cfg);
+      constexpr int NB = decltype(nbuf)::value, IL = decltype(ilv)::value;
+      using LA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
+      using LB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
+      typename LA::Params pa{dz, 512, 512, rows};
+      typename LB::Params pb{Wt(L.XH) + (size_t)lo * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(),
+                             1728, (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)};
+      EpiAtomicD ep{{Wf(L.gWpl), 1728, 512, 1728}};
+      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
+      TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+      // split-K over pixels: about one resident wave of workgroups (fewer
+      // passes of the output's atomics than the register path's ~1024)
+      const int wgs = env_int("AAA_WGRAD_WGS", 256);
+      const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
+      HIPCHK((launch_pipe<CW, LA, LB, EpiAtomicD, NB, IL>(pa, pb, ep, 512, 1728, rows, ns, s)));
+      return AAA_OK;
+    };
+    // bf16 default: 256x256 (8 waves of 128x64), BK=32 in a 4-deep ring with the
+    // DMA pieces spread over the k steps (tools/ubench/wgrad_ablate at C3: 1163 us
+    // vs 1296 for BK=64 in a 2-deep ring and 1400 for the register-staged GEMM)
+    constexpr int WBK = std::is_same<T, float>::value ? 32 : 64;
+    // (not on the aux stream: its 128 KB of LDS would keep the chain's step kernels off the CU)
+    const int wpipe = rows % WBK == 0 ? env_int("AAA_WGRAD_PIPE", std::is_same<T, float>::value || s != st ? 0 : 6) : 0;
+    if (wpipe) {
+      using I0 = std::integral_constant<int, 0>;
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      int rc;
+      switch (wpipe) {
+        case 2: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
+        case 3:   // 8 waves of 128x64 (fp32: spills, so 256x128)
+          if constexpr (std::is_same<T, float>::value) rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{});
+          else rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, WBK, 2, 4>{}, I2{}, I0{});
+          break;
+        case 4: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 256, WBK, 2, 2>{}, I2{}, I0{}); break;
+        case 5: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I3{}, I0{}); break;
+        case 6:   // bf16: 8 waves, BK=32, 4-deep ring, spread DMA issue
+        case 7:   // bf16: the same in a 3-deep ring
+          if constexpr (std::is_same<T, float>::value)
+            rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
+          else if (wpipe == 6)
+            rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, std::integral_constant<int, 4>{}, I2{});
+          else
+            rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, I3{}, I2{});
+          break;
+        default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
+      }
+      if (rc) return rc;
+    } else {
       // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
       const int wide = env_int("AAA_AUX_WIDE", s == st ? 1 : 0);
       const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
