@@ -69,16 +69,21 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // logits A[p][q] = K[p]·Q[q] with K = [O[:8] | S], softmax over the P grid
 // positions (spatial_softmax), readout a[q] = sum_p A[p][q] [O[8:] | S][p],
 // and the answer row [a_0..a_nq-1 | Q_0..Q_nq-1 | r | a_prev | 0-pad].
-// HBM-bound: the frame's O rows are read once, 16 B per lane, each row's
-// 480 B of V by consecutive lanes (readout: 46 four-column groups x 5
-// position slices, slices summed through LDS).
+// HBM-bound: every load of the frame is issued before the first wait -- the
+// key channels by the logit threads (one position each) and the first
+// kAttnPre positions of each readout thread's V slice straight into
+// registers -- so the frame's O rows stream in as one burst (no load phase
+// behind the softmax).  Readout thread (g, sl): 4-column group g of the 184
+// V columns (46 groups, 16 B per lane, consecutive lanes along a row),
+// position slice sl of 11; slices summed through LDS.
 constexpr int kAttnFwdThreads = 512;
 constexpr int kAttnSlices = 11;         // position slices of the readout (46 * 11 = 506 threads)
-template <int NQ>
-__global__ void __launch_bounds__(kAttnFwdThreads)
+template <int NQ, int PRE>
+__global__ void __launch_bounds__(kAttnFwdThreads) __attribute__((amdgpu_waves_per_eu(PRE > 0 || NQ > 4 ? 4 : 8)))
 k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
            int P, float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
+  constexpr int kAttnPre = PRE;   // V positions per readout thread loaded before the first wait
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* L = sm;                         // P*NQ
   float* Qs = L + P * NQ;                // NQ*72
@@ -86,12 +91,30 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
   const float* Qf = Q + (size_t)f * qs;   // qs = 0: one query for every frame (Q1)
+  // the first logit position's keys, then this thread's V slice head
+  f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0;
+  if (tid < P) {
+    k0 = *reinterpret_cast<const f32x4*>(O + tid * 128);
+    k1 = *reinterpret_cast<const f32x4*>(O + tid * 128 + 4);
+  }
+  const bool rd = tid < 46 * kAttnSlices;
+  const int g = tid % 46, sl = tid / 46;
+  const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
+  const int ld = g < 30 ? 128 : 64;
+  f32x4 pre[kAttnPre > 0 ? kAttnPre : 1];
+#pragma unroll
+  for (int i = 0; i < kAttnPre; ++i) {
+    const int p = sl + i * kAttnSlices;
+    pre[i] = rd && p < P ? *reinterpret_cast<const f32x4*>(src + (size_t)p * ld) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) Qs[i] = Qf[i];
   __syncthreads();
   // logits: one thread per position, all NQ queries (its 8 key channels read once)
   for (int p = tid; p < P; p += kAttnFwdThreads) {
-    const f32x4 k0 = *reinterpret_cast<const f32x4*>(O + p * 128);
-    const f32x4 k1 = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
+    if (p != tid) {
+      k0 = *reinterpret_cast<const f32x4*>(O + p * 128);
+      k1 = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
+    }
     float acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -133,16 +156,25 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
   }
   __syncthreads();
-  // readout: thread (column group g of 4, position slice sl)
-  if (tid < 46 * kAttnSlices) {
-    const int g = tid % 46, sl = tid / 46;
+  // readout: the prefetched head of the slice, then the rest (large grids)
+  if (rd) {
     float acc[NQ][4];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
-    const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
-    const int ld = g < 30 ? 128 : 64;
+#pragma unroll
+    for (int i = 0; i < kAttnPre; ++i) {
+      const int p = sl + i * kAttnSlices;
+      if (p < P) {
+        const f32x4 v = pre[i];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float a = L[p * NQ + q];
+          acc[q][0] += a * v[0]; acc[q][1] += a * v[1]; acc[q][2] += a * v[2]; acc[q][3] += a * v[3];
+        }
+      }
+    }
 #pragma unroll 4
-    for (int p = sl; p < P; p += kAttnSlices) {
+    for (int p = sl + kAttnPre * kAttnSlices; p < P; p += kAttnSlices) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -159,7 +191,7 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   for (int i = tid; i < NQ * 184; i += kAttnFwdThreads) {
     float v = 0.f;
 #pragma unroll
-    for (int sl = 0; sl < kAttnSlices; ++sl) v += red[sl * NQ * 184 + i];
+    for (int s2 = 0; s2 < kAttnSlices; ++s2) v += red[s2 * NQ * 184 + i];
     arow[i] = v;
   }
   for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) arow[NQ * 184 + i] = Qs[i];
@@ -705,12 +737,15 @@ hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float
                     const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
                     int qs) {
   const size_t sh = (size_t)(P * nq + nq * 72 + kAttnSlices * nq * 184) * sizeof(float);
-  if (nq == 4)
-    hipLaunchKernelGGL(k_attn_fwd<4>, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans,
-                       ans_ld);
-  else if (nq == 8)
-    hipLaunchKernelGGL(k_attn_fwd<8>, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans,
-                       ans_ld);
+  // register prefetch of the V slice only on large grids (many positions per
+  // slice): at 84x84 (11 per slice) the registers cost more occupancy than the
+  // early loads buy (C3: 118 vs 104 us; 168x168, C5: 217 vs 275 us)
+  const bool pre = P > 2 * kAttnSlices * 11;
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
+  };
+  if (nq == 4) pre ? launch(k_attn_fwd<4, 8>) : launch(k_attn_fwd<4, 0>);
+  else if (nq == 8) pre ? launch(k_attn_fwd<8, 8>) : launch(k_attn_fwd<8, 0>);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -809,10 +809,10 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
 template <typename T>
 static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, int frames, float* gbias,
                        hipStream_t s) {
-  if constexpr (!std::is_same<T, float>::value) {
-    // bf16: dY2 is already bf16 -> the LDS-DMA ring, dY1 stored bf16, conv1's
-    // bias gradient summed from the fp32 values in the epilogue
-    using CP = GemmCfg<T, 32, 128, 64, 1, 4>;
+  if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
+    // the LDS-DMA ring (dY2 is already in T), dY1 stored in T, conv1's bias
+    // gradient summed from the fp32 values in the epilogue (no column-sum pass)
+    using CP = GemmCfg<T, 32, 128, std::is_same<T, float>::value ? 32 : 64, 1, 4>;
     using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
     using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
     for (int cls = 0; cls < 4; ++cls) {
@@ -830,6 +830,8 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     }
     return AAA_OK;
   }
+  // register-staged fallback (fp32 only: dY2's loader converts from fp32)
+  if constexpr (!std::is_same<T, float>::value) return fail(AAA_E_ARG, "AAA_CONV2_DGRAD_RING=0 needs fp32");
   using C3 = Cfg32For<T>;
   using LA = LdRowsB<T, T, C3::BI, C3::BK, C3::NT>;
   using LB = LdIm2colB<float, T, C3::BJ, C3::BK, C3::NT>;
@@ -1157,10 +1159,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       const T* WdT = (const T*)(pk + L.k_WdTl);
       const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
       if constexpr (std::is_same<T, float>::value) {
-        // 64x64 tiles (64x128 measured slower: occupancy)
-        EpiStoreT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, nullptr, 0};
-        HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)
-                               : step_gemm<CfgFor<T>, false>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+        // 64x64 tiles (64x128 measured slower: occupancy); conv2's bias
+        // gradient summed from the tile in the epilogue (no column-sum pass)
+        EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
+        HIPCHK((pipe_batched()
+                    ? step_gemm<CfgFor<T>, true, T, T, EpiStoreBiasT<float>>(WdT, 4608, 64, dz, g, rows, zb, ep, 64,
+                                                                             4608, s)
+                    : step_gemm<CfgFor<T>, false, T, T, EpiStoreBiasT<float>>(WdT, 4608, 64, dz, g, rows, zb, ep, 64,
+                                                                              4608, s)));
       } else {
         // bf16: dY2 stored bf16 (its readers round it to bf16 anyway), conv2's
         // bias gradient summed from the fp32 values in the epilogue
@@ -1182,7 +1188,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
     T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
     const int rows1 = F1 * L.P1;
-    constexpr bool f32 = std::is_same<T, float>::value;   // fp32: bias grads by column sums
+    constexpr bool f32 = std::is_same<T, float>::value;   // fp32 with AAA_CONV2_DGRAD_RING=0: conv1 bias by a column sum
     {  // conv2 wgrad / bias
       using LA = LdRowsTB<T, T, C::BI, C::BK, NT>;
       using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
@@ -1192,13 +1198,12 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
       const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
       HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
-      if (f32) HIPCHK(colsum(dy2, 64, rows, 64, grads + L.poff[C1B], s));
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
       int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
       if (!rc) rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
       if (rc) return rc;
-      if (f32) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
+      if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
     return AAA_OK;
   };
@@ -1330,13 +1335,12 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
                                (uint32_t)((size_t)rows1 * 32 * L.esz)};
         EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
         HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(cdiv(512, C::BJ), rows, C::BK), st)));
-        if (f32) HIPCHK(colsum(Wt(L.dY2), 64, rows, 64, grads + L.poff[C1B], st));
       }
       {
         int rc = conv2_dgrad<T>(L, pk, Wt(L.dY2), Wt(L.dY1), F, grads + L.poff[C0B], st);
         if (!rc) rc = conv1_wgrad<T>(L, Wt(L.dY1), Wt(L.Xp), F, Wf(L.gWp1), st);
         if (rc) return rc;
-        if (f32) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
+        if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
     }
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
