@@ -10,6 +10,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Workgroup barrier that drains only the LDS counter: global loads issued
+// before it stay in flight (a __syncthreads fence would wait for them).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -226,37 +229,56 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   float* Vc = red + G * NQ * 72; // kAttnChunk * kVld
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
+  // V chunk pieces of this thread (16 B each, consecutive threads along a row),
+  // loaded into registers one chunk AHEAD of its LDS staging: chunk c+1's
+  // loads are in flight while chunk c's dot products run (the barriers below
+  // drain only the LDS counter), so the frame's V rows stream in behind the
+  // compute instead of one exposed load latency per chunk.
+  constexpr int VPT = (kAttnChunk * 46 + NT - 1) / NT;
+  f32x4 vr[VPT];
+  auto vload = [&](int p0) {
+    const int nv = min(kAttnChunk, P - p0) * 46;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      // one unconditional load from a selected address (a load per branch
+      // would serialise them on the shared destination registers, and a
+      // select on the loaded value would wait for it right here)
+      const int i = tid + j * NT, pp = i / 46, g = i - pp * 46, p = p0 + pp;
+      const bool ok = i < nv;
+      const float* src = !ok ? S : (g < 30 ? O + p * 128 + 8 + 4 * g : S + p * 64 + 4 * (g - 30));
+      vr[j] = *reinterpret_cast<const f32x4*>(src);   // unused when !ok (the staging skips it)
+    }
+  };
+  vload(0);
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
   for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
-  __syncthreads();
   // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S], in chunks of
-  // kAttnChunk positions: the chunk's V rows are staged in LDS by consecutive
-  // threads (16 B each, coalesced rows), then thread (p, q) takes its dot
+  // kAttnChunk positions staged in LDS, then thread (p, q) takes its dot
   // product from LDS (no cross-lane reductions).
   for (int p0 = 0; p0 < P; p0 += kAttnChunk) {
     const int np = min(kAttnChunk, P - p0);
-    for (int i = tid; i < np * 46; i += NT) {
-      const int pp = i / 46, g = i - pp * 46, p = p0 + pp;
-      const f32x4 v = g < 30 ? *reinterpret_cast<const f32x4*>(O + p * 128 + 8 + 4 * g)
-                             : *reinterpret_cast<const f32x4*>(S + p * 64 + 4 * (g - 30));
-      *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = v;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int i = tid + j * NT, pp = i / 46, g = i - pp * 46;
+      if (i < np * 46) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = vr[j];
     }
-    __syncthreads();
+    lds_barrier();
+    if (p0 + kAttnChunk < P) vload(p0 + kAttnChunk);
     for (int i = tid; i < np * NQ; i += NT) {
       const int pp = i / NQ, q = i - pp * NQ;
-      const f32x4* vr = reinterpret_cast<const f32x4*>(Vc + pp * kVld);
+      const f32x4* vrow = reinterpret_cast<const f32x4*>(Vc + pp * kVld);
       const f32x4* dr = reinterpret_cast<const f32x4*>(da + q * 184);
       float a0 = 0.f, a1 = 0.f;
 #pragma unroll 2
       for (int g = 0; g < 46; ++g) {
-        const f32x4 v = vr[g], d = dr[g];
+        const f32x4 v = vrow[g], d = dr[g];
         a0 += v[0] * d[0] + v[1] * d[1];
         a1 += v[2] * d[2] + v[3] * d[3];
       }
       dA[(p0 + pp) * NQ + q] = a0 + a1;
     }
-    __syncthreads();
+    lds_barrier();
   }
   // softmax backward: dlogit = A (dA - sum_p A dA)
   for (int q = wave; q < NQ; q += NW) {
@@ -300,8 +322,13 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     float acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    // K = [O[:8] | S] column c: one strided address stream per thread, loads
+    // unrolled so several are in flight (not one latency per position)
+    const float* kp = c < 8 ? O + c : S + c - 8;
+    const int kld = c < 8 ? 128 : 64;
+#pragma unroll 8
     for (int p = g; p < P; p += G) {
-      const float k = c < 8 ? O[p * 128 + c] : S[p * 64 + c - 8];
+      const float k = kp[p * kld];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] += dA[p * NQ + q] * k;
     }
