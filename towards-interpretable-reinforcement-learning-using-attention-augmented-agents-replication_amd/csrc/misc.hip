@@ -1,6 +1,9 @@
 // Non-GEMM kernels of the attention-agent path: constant query MLP, fused
 // spatial-softmax attention readout (fwd/bwd), column reductions, the last
 // BPTT gate step, and parameter (un)packing.
+#include <cstdlib>
+#include <type_traits>
+
 #include "misc.h"
 
 namespace aaa {
@@ -80,8 +83,8 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // V columns (46 groups, 16 B per lane, consecutive lanes along a row),
 // position slice sl of 11; slices summed through LDS.
 constexpr int kAttnFwdThreads = 512;
-constexpr int kAttnSlices = 11;         // position slices of the readout (46 * 11 = 506 threads)
-template <int NQ, int PRE>
+constexpr int kAttnSlices = 11;         // default position slices of the readout (46 * 11 = 506 threads)
+template <int NQ, int PRE, int SL = kAttnSlices>
 __global__ void __launch_bounds__(kAttnFwdThreads) __attribute__((amdgpu_waves_per_eu(PRE > 0 || NQ > 4 ? 4 : 8)))
 k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
@@ -90,44 +93,51 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* L = sm;                         // P*NQ
   float* Qs = L + P * NQ;                // NQ*72
-  float* red = Qs + NQ * 72;             // kAttnSlices * NQ * 184
+  float* red = Qs + NQ * 72;             // SL * NQ * 184
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
   const float* Qf = Q + (size_t)f * qs;   // qs = 0: one query for every frame (Q1)
+  // the queries first (their LDS copy below then waits only for them), then
   // the first logit position's keys, then this thread's V slice head
-  f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0;
-  if (tid < P) {
-    k0 = *reinterpret_cast<const f32x4*>(O + tid * 128);
-    k1 = *reinterpret_cast<const f32x4*>(O + tid * 128 + 4);
-  }
-  const bool rd = tid < 46 * kAttnSlices;
+  static_assert(NQ * 72 <= 2 * kAttnFwdThreads, "two query elements per thread");
+  const int qi1 = min(tid + kAttnFwdThreads, NQ * 72 - 1);
+  const float qv0 = Qf[min(tid, NQ * 72 - 1)], qv1 = Qf[qi1];
+  // position tid's keys and (constant query) basis logits: unconditional
+  // loads from a clamped valid position, used only when tid < P
+  const int p0 = min(tid, P - 1);
+  f32x4 k0 = *reinterpret_cast<const f32x4*>(O + p0 * 128);
+  f32x4 k1 = *reinterpret_cast<const f32x4*>(O + p0 * 128 + 4);
+  f32x4 sq[NQ / 4];
+#pragma unroll
+  for (int j = 0; j < NQ / 4; ++j)
+    sq[j] = SQ ? *reinterpret_cast<const f32x4*>(SQ + p0 * NQ + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool rd = tid < 46 * SL;
   const int g = tid % 46, sl = tid / 46;
   const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
   const int ld = g < 30 ? 128 : 64;
   f32x4 pre[kAttnPre > 0 ? kAttnPre : 1];
 #pragma unroll
   for (int i = 0; i < kAttnPre; ++i) {
-    const int p = sl + i * kAttnSlices;
-    pre[i] = rd && p < P ? *reinterpret_cast<const f32x4*>(src + (size_t)p * ld) : f32x4{0.f, 0.f, 0.f, 0.f};
+    // unconditional load from a valid address (a select on the loaded value
+    // would wait for it here); positions past P are skipped at their use
+    const int p = min(sl + i * SL, P - 1);
+    pre[i] = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
   }
-  for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) Qs[i] = Qf[i];
+  if (tid < NQ * 72) Qs[tid] = qv0;
+  if (tid + kAttnFwdThreads < NQ * 72) Qs[tid + kAttnFwdThreads] = qv1;
   __syncthreads();
   // logits: one thread per position, all NQ queries (its 8 key channels read once)
-  for (int p = tid; p < P; p += kAttnFwdThreads) {
-    if (p != tid) {
-      k0 = *reinterpret_cast<const f32x4*>(O + p * 128);
-      k1 = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
-    }
+  auto logits = [&](int p, const f32x4& ka, const f32x4& kb, const f32x4* sqp) {
     float acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const float* qq = Qs + q * 72;
-      acc[q] = k0[0] * qq[0] + k0[1] * qq[1] + k0[2] * qq[2] + k0[3] * qq[3] +
-               k1[0] * qq[4] + k1[1] * qq[5] + k1[2] * qq[6] + k1[3] * qq[7];
+      acc[q] = ka[0] * qq[0] + ka[1] * qq[1] + ka[2] * qq[2] + ka[3] * qq[3] +
+               kb[0] * qq[4] + kb[1] * qq[5] + kb[2] * qq[6] + kb[3] * qq[7];
     }
     if (SQ) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[q] += SQ[p * NQ + q];
+      for (int q = 0; q < NQ; ++q) acc[q] += sqp[q / 4][q % 4];
     } else {   // per-frame query: the basis half of the logit here
       const f32x4* s4 = reinterpret_cast<const f32x4*>(S + p * 64);
 #pragma unroll 4
@@ -142,6 +152,16 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) L[p * NQ + q] = acc[q];
+  };
+  if (tid < P) logits(tid, k0, k1, sq);
+  for (int p = tid + kAttnFwdThreads; p < P; p += kAttnFwdThreads) {   // grids past 512 positions
+    const f32x4 ka = *reinterpret_cast<const f32x4*>(O + p * 128);
+    const f32x4 kb = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
+    f32x4 sp[NQ / 4];
+#pragma unroll
+    for (int j = 0; j < NQ / 4; ++j)
+      sp[j] = SQ ? *reinterpret_cast<const f32x4*>(SQ + p * NQ + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    logits(p, ka, kb, sp);
   }
   __syncthreads();
   for (int q = wave; q < NQ; q += kAttnFwdThreads / 64) {
@@ -166,7 +186,7 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     for (int q = 0; q < NQ; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
 #pragma unroll
     for (int i = 0; i < kAttnPre; ++i) {
-      const int p = sl + i * kAttnSlices;
+      const int p = sl + i * SL;
       if (p < P) {
         const f32x4 v = pre[i];
 #pragma unroll
@@ -177,7 +197,7 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
       }
     }
 #pragma unroll 4
-    for (int p = sl + kAttnPre * kAttnSlices; p < P; p += kAttnSlices) {
+    for (int p = sl + kAttnPre * SL; p < P; p += SL) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -194,7 +214,7 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   for (int i = tid; i < NQ * 184; i += kAttnFwdThreads) {
     float v = 0.f;
 #pragma unroll
-    for (int s2 = 0; s2 < kAttnSlices; ++s2) v += red[s2 * NQ * 184 + i];
+    for (int s2 = 0; s2 < SL; ++s2) v += red[s2 * NQ * 184 + i];
     arow[i] = v;
   }
   for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) arow[NQ * 184 + i] = Qs[i];
@@ -763,16 +783,30 @@ hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hi
 hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
                     const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
                     int qs) {
-  const size_t sh = (size_t)(P * nq + nq * 72 + kAttnSlices * nq * 184) * sizeof(float);
   // register prefetch of the V slice only on large grids (many positions per
   // slice): at 84x84 (11 per slice) the registers cost more occupancy than the
   // early loads buy (C3: 118 vs 104 us; 168x168, C5: 217 vs 275 us)
-  const bool pre = P > 2 * kAttnSlices * 11;
+  static const int pre_env = getenv("AAA_ATTN_PRE") ? atoi(getenv("AAA_ATTN_PRE")) : -1;   // A/B override
+  static const int sl_env = getenv("AAA_ATTN_SLICES") ? atoi(getenv("AAA_ATTN_SLICES")) : -1;
+  const bool pre = pre_env >= 0 ? pre_env != 0 : P > 2 * kAttnSlices * 11;
+  const int sl = sl_env > 0 ? sl_env : kAttnSlices;
+  const size_t sh = (size_t)(P * nq + nq * 72 + sl * nq * 184) * sizeof(float);
+  if (sh > 160 * 1024) return hipErrorInvalidValue;
   auto launch = [&](auto kern) {
+    if (sh > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sh);
     hipLaunchKernelGGL(kern, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
   };
-  if (nq == 4) pre ? launch(k_attn_fwd<4, 8>) : launch(k_attn_fwd<4, 0>);
-  else if (nq == 8) pre ? launch(k_attn_fwd<8, 8>) : launch(k_attn_fwd<8, 0>);
+  auto go = [&](auto slc) {
+    constexpr int SL = decltype(slc)::value;
+    if (nq == 4) pre ? launch(k_attn_fwd<4, 8, SL>) : launch(k_attn_fwd<4, 0, SL>);
+    else if (nq == 8) pre ? launch(k_attn_fwd<8, 8, SL>) : launch(k_attn_fwd<8, 0, SL>);
+  };
+  if (nq != 4 && nq != 8) return hipErrorInvalidValue;
+  if (sl == 8) go(std::integral_constant<int, 8>{});
+  else if (sl == 5) go(std::integral_constant<int, 5>{});
+  else if (sl == kAttnSlices) go(std::integral_constant<int, kAttnSlices>{});
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
