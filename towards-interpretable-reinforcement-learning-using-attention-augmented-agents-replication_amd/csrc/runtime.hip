@@ -348,13 +348,19 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 }
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
-  if (v >= 0) return ((v == 7 || v == 8) && !bf16) || (v == 9 && !bptt) ? 4 : v;   // 7, 8: bf16 only; 9: BPTT only
+  if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
+    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16;
+    const bool fwd_only = v == 14 || v == 17 || v == 18;
+    return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
+  }
   // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
   // (tools/ubench/bf16_tiles at B=128: 34.6 vs 39.6 us)
   if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 8;
-  // fp32 (C2: 484 BPTT / 1936 forward tiles): 64x32 BPTT 54.6 vs 55.9 us for 32x64; 64x64 BK64
-  // forward 47.9 vs 51.9 us for BK32 (bench.py kernel table, AAA_*_TILE A/B)
-  if (bptt) return out_tiles32 < 1024 ? 9 : (out_tiles32 < 1536 ? 1 : 0);
+  // fp32 (C2: 484 BPTT / 1936 forward tiles): 32x32 BK64 4-way BPTT on a 3-stage ring, two WGs
+  // per CU whose barriers are not in step (51.6 vs 54.4 us for 64x32 BK128, 54.6 vs 55.9 for
+  // 32x64); 64x64 BK64 forward 47.4 us (32x64 / 32x32 / 64x32 split-K rings: 52-55 us)
+  // (bench.py kernel table, tools/ab_bptt.sh)
+  if (bptt) return out_tiles32 < 1024 ? 16 : (out_tiles32 < 1536 ? 1 : 0);
   return out_tiles32 < 1024 ? 5 : 6;
 }
 
@@ -652,6 +658,22 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
       case 7: e = step_gemm<C, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 5: e = step_gemm<CfgKFor<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
       case 6: e = step_gemm<Cfg64For<T>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
+      case 12:   // 32x64 BK64, 2-way in-WG split-K, 3-stage ring
+        e = step_gemm<CfgKFor<T>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512,
+                                                                          1152, st);
+        break;
+      case 14:   // 32x32 BK64, 4-way in-WG split-K, 3-stage ring
+        e = step_gemm<GemmCfg<T, 32, 32, 64, 1, 1, 4>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M,
+                                                                                              xh_bytes, ep, 512, 1152, st);
+        break;
+      case 17:   // 64x32 BK64, 2-way in-WG split-K, 3-stage ring
+        e = step_gemm<GemmCfg<T, 64, 32, 64, 2, 1, 2>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M,
+                                                                                              xh_bytes, ep, 512, 1152, st);
+        break;
+      case 18:   // 64x64 BK64, 2x2 waves, 3-stage ring
+        e = step_gemm<Cfg64For<T>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512,
+                                                                           1152, st);
+        break;
       default: e = step_gemm<C, false>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st); break;
     }
     HIPCHK(e);
@@ -1221,10 +1243,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
     // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
     // the register-staged ones leave the bias to a column sum over dZ
-    const int bj = bwd_tile == 7 ? 128 : (bwd_tile == 9 ? 32 : 64);
+    const int bj = bwd_tile == 7 ? 128 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64);
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
                       (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 ||
-                      (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>());
+                      (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>()) ||
+                      (bwd_tile == 10 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 4>>()) ||
+                      ((bwd_tile == 11 || bwd_tile == 12 || bwd_tile == 16) && pipe_even<GemmCfg<T, 32, 32, 64, 1, 1, 4>>()) ||
+                      (bwd_tile == 13 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 8>>()) ||
+                      (bwd_tile == 15 && pipe_even<GemmCfg<T, 64, 32, 64, 2, 1, 4>>());
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
@@ -1301,6 +1327,24 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
             case 9:   // 64x32, BK128, 4-way in-WG split-K, 3-stage ring, interleaved DMA
               return step_gemm<GemmCfg<T, 64, 32, 128, 2, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
                                                                                           dz_bytes, ep, 128, 4608, st);
+            case 10:   // 32x32, BK128, 4-way in-WG split-K, 2-stage ring (2 WGs per CU, desynchronised barriers)
+              return step_gemm<GemmCfg<T, 32, 32, 128, 1, 1, 4>, true, T, T, EB, 2, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                         dz_bytes, ep, 128, 4608, st);
+            case 11:   // 32x32, BK64, 4-way in-WG split-K, 3-stage ring
+              return step_gemm<GemmCfg<T, 32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                        dz_bytes, ep, 128, 4608, st);
+            case 12:   // 32x32, BK64, 4-way in-WG split-K, 4-stage ring
+              return step_gemm<GemmCfg<T, 32, 32, 64, 1, 1, 4>, true, T, T, EB, 4, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                        dz_bytes, ep, 128, 4608, st);
+            case 13:   // 32x32, BK128, 8-way in-WG split-K (8 waves), 2-stage ring
+              return step_gemm<GemmCfg<T, 32, 32, 128, 1, 1, 8>, true, T, T, EB, 2, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                         dz_bytes, ep, 128, 4608, st);
+            case 15:   // 64x32, BK64, 4-way in-WG split-K, 3-stage ring
+              return step_gemm<GemmCfg<T, 64, 32, 64, 2, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                        dz_bytes, ep, 128, 4608, st);
+            case 16:   // 32x32, BK64, 4-way in-WG split-K, 3-stage ring, DMA issued before the MFMAs
+              return step_gemm<GemmCfg<T, 32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, false>(WdTh, 4608, 128, dzt, g, M,
+                                                                                         dz_bytes, ep, 128, 4608, st);
             default: return step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
           }
         }
