@@ -406,13 +406,27 @@ static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const 
 
 // Small GEMMs of the head (F = T*B rows; answer MLP, LSTMCell, policy/value
 // heads): 64x64 tiles leave most CUs idle, so below ~192 tiles use the 32x64
-// tile (twice the workgroups).  AAA_HEAD_TILE=1 forces 64x64, =2 forces 32x64.
+// tile with a 4-way in-WG split-K (8 waves per WG: the serial K loop of these
+// long-K, few-tile GEMMs is what they wait on; C2 4.487 -> 4.414 ms per
+// iteration vs the plain 32x64 tile, tools/ab_head.sh).  AAA_HEAD_TILE=1 forces
+// 64x64, =2 the plain 32x64, =3/4/5 the 2-way / 4-way / 4-way BK128 split-K tiles.
 template <template <typename, typename, int, int, int> class LA_,
           template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
 static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, int nsplit,
                             hipStream_t st) {
   const int mode = env_int("AAA_HEAD_TILE", 0);
   const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
+  auto splitk = [&](auto cfg) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
+    using C = decltype(cfg);
+    using A = LA_<float, float, C::BI, C::BK, C::NT>;
+    using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+    return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
+                                ep, Mi, Nj, K, nsplit, st);
+  };
+  if (mode == 3) return splitk(CFK{});
+  if (mode == 4) return splitk(CFK4{});
+  if (mode == 5) return splitk(CFK4B{});
+  if (mode == 0 && tiles < 192) return splitk(CFK4{});
   if (mode == 1 || (mode == 0 && tiles >= 192)) {
     using C = CF;
     using A = LA_<float, float, C::BI, C::BK, C::NT>;
