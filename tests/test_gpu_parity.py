@@ -107,6 +107,21 @@ def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
                  f"bf16 fused_x={fused}: ")
 
 
+# Every tile of the fused [x | h] forward step (runtime.hip AAA_FUSED_TILE: 4 128x64 8 waves,
+# 7 64x64, 8/10 3-stage rings, 9 128x128 4 waves (bf16 default), 11 2-way split-K, 12 128x64 4 waves).
+@pytest.mark.parametrize("tile", ["4", "7", "8", "9", "10", "11", "12"])
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
+    monkeypatch.setenv("AAA_FUSED_X", "1")
+    monkeypatch.setenv("AAA_FUSED_TILE", tile)
+    T, B = 3, 5
+    if conv_dtype == "fp32":
+        _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"fused tile {tile}: ")
+    else:
+        _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
+                 f"bf16 fused tile {tile}: ")
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "6", "7"])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_lstm_wgrad_ring_variants(cuda, monkeypatch, mode, conv_dtype):

@@ -599,7 +599,11 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
     const T* WpXH = (const T*)(pk + L.k_WpXH);
-    const int ftile = env_int("AAA_FUSED_TILE", 4);   // 4: 128x64 8 waves, 7: 64x64 4 waves
+    // bf16: 128x128 tiles of 4 waves (64x64 per wave: twice the MFMA work per
+    // fragment read of the 128x64 8-wave tile) -- C3 94.7 -> 81-83 us, C4 51.5 ->
+    // 44.6 us, C5 90.7 -> 78.6-79.5 us per step (tools/ab_fused.sh); fp32 (only
+    // small M, e.g. the B=1 actor, fuses the x-part): 128x64 8 waves.
+    const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
       for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
@@ -607,9 +611,23 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                                  Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
                                  (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
         TimerScope tim(AAA_TIMER_FWD_STEP, st);
+        using EF = EpiConvLstmFwd<T, GT>;
+        const T* xht = Wt(L.XH) + (size_t)t * M * 192;
         if (ftile == 7)
-          HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
-                                             512, 1728, st)));
+          HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+        else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring
+          HIPCHK((step_gemm<CfgSFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+        else if (ftile == 9)   // 128x128, 4 waves of 64x64
+          HIPCHK((step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
+                                                                   st)));
+        else if (ftile == 10)   // 64x64, 4 waves, 3-stage ring
+          HIPCHK((step_gemm<CfgFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+        else if (ftile == 11)   // 64x64, 2-way in-WG split-K (8 waves), BK64 (K = 1728 = 27 x 64)
+          HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
+                                                                    st)));
+        else if (ftile == 12)   // 128x64, 2x2 waves of 64x32
+          HIPCHK((step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
+                                                                  st)));
         else
           HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
                                               512, 1728, st)));
