@@ -349,7 +349,8 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
   if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
-    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16;
+    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || v >= 19;
+    if (v >= 19 && !bf16) return 4;   // 19-21: bf16 BPTT tiles (fp16 gate storage)
     const bool fwd_only = v == 14 || v == 17 || v == 18;
     return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
   }
@@ -375,7 +376,7 @@ static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF1
 static bool gates_f16(int dt, int M) {
   if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
   const int bt = step_tile((long)(128 / 32) * ((M + 31) / 32), "AAA_BPTT_TILE", true, true);
-  return bt == 7 || bt == 8;
+  return bt == 7 || bt == 8 || bt >= 19;
 }
 
 // Whether the LDS-DMA ring can run tile config CK (every wave issues the same DMA count).
@@ -1275,9 +1276,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
     // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
     // the register-staged ones leave the bias to a column sum over dZ
-    const int bj = bwd_tile == 7 ? 128 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64);
+    const int bj = bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64));
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
-                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 ||
+                      (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 || bwd_tile >= 19 ||
                       (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>()) ||
                       (bwd_tile == 10 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 4>>()) ||
                       ((bwd_tile == 11 || bwd_tile == 12 || bwd_tile == 16) && pipe_even<GemmCfg<T, 32, 32, 64, 1, 1, 4>>()) ||
@@ -1335,6 +1336,15 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
           else if (bwd_tile == 7)
             return step_gemm<GemmCfg<T, 128, 128, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
                                                                         4608, st);
+          else if (bwd_tile == 19)   // 128x128, 4 waves of 64x64, BK64
+            return step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608,
+                                                                    st);
+          else if (bwd_tile == 20)   // the same on a 3-stage ring
+            return step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
+                                                                                      dz_bytes, ep, 128, 4608, st);
+          else if (bwd_tile == 21)   // 128x64, 4 waves of 64x32, BK64
+            return step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608,
+                                                                   st);
           else
             return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
                                                                        4608, st);
