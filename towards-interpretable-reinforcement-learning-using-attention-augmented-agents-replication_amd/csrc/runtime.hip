@@ -350,13 +350,15 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
   const int v = env_int(env, -1);
   if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
     const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || v >= 19;
-    if (v >= 19 && !bf16) return 4;   // 19-21: bf16 BPTT tiles (fp16 gate storage)
+    if (v >= 19 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
     const bool fwd_only = v == 14 || v == 17 || v == 18;
     return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
   }
   // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
   // (tools/ubench/bf16_tiles at B=128: 34.6 vs 39.6 us)
-  if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 8;
+  // below that, 128x64 with a 4-way in-WG split-K (8 waves; C4: 50.0 vs 52.5 us for the 4-wave
+  // 2-way tile 8, tools/ab_bptt_bf16.sh)
+  if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 22;
   // fp32 (C2: 484 BPTT / 1936 forward tiles): 32x32 BK64 4-way BPTT on a 3-stage ring, two WGs
   // per CU whose barriers are not in step (51.6 vs 54.4 us for 64x32 BK128, 54.6 vs 55.9 for
   // 32x64); 64x64 BK64 forward 47.4 us (32x64 / 32x32 / 64x32 split-K rings: 52-55 us)
@@ -1276,7 +1278,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
     // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
     // the register-staged ones leave the bias to a column sum over dZ
-    const int bj = bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64));
+    const int bj = bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 || bwd_tile == 22 || bwd_tile == 23 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64));
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
                       (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 || bwd_tile >= 19 ||
                       (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>()) ||
@@ -1342,6 +1344,15 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
           else if (bwd_tile == 20)   // the same on a 3-stage ring
             return step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
                                                                                       dz_bytes, ep, 128, 4608, st);
+          else if (bwd_tile == 22)   // 128x64, BK128, 4-way in-WG split-K (8 waves)
+            return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 4>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                       4608, st);
+          else if (bwd_tile == 23)   // 64x64, BK128, 2-way in-WG split-K (8 waves)
+            return step_gemm<GemmCfg<T, 64, 64, 128, 2, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                      4608, st);
+          else if (bwd_tile == 24)   // 64x32, BK128, 4-way in-WG split-K (8 waves)
+            return step_gemm<GemmCfg<T, 64, 32, 128, 2, 1, 4>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
+                                                                      4608, st);
           else if (bwd_tile == 21)   // 128x64, 4 waves of 64x32, BK64
             return step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608,
                                                                    st);
@@ -1349,6 +1360,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
             return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128,
                                                                        4608, st);
         } else {
+          // tiles 19-24 other than 22 exist for fp16 gate storage only: fail loudly, never fall back
+          if (bwd_tile >= 19 && bwd_tile != 22) return hipErrorInvalidValue;
           switch (bwd_tile) {
             case 1: return step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
             case 2: return step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
@@ -1365,6 +1378,10 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
             case 8:   // bf16: 128x64, BK128, 2-way in-WG split-K, 4 waves (small batches)
               if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
               else return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 2>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
+                                                                             128, 4608, st);
+            case 22:   // bf16 with fp32 gate storage (AAA_FUSED_X=0 / AAA_GATES_F16=0): the default small-batch tile
+              if constexpr (std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfg<T, 128, 64, 128, 2, 1, 4>, true>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep,
                                                                              128, 4608, st);
             case 9:   // 64x32, BK128, 4-way in-WG split-K, 3-stage ring, interleaved DMA
               return step_gemm<GemmCfg<T, 64, 32, 128, 2, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g, M,
