@@ -655,8 +655,18 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     const T* WpX = (const T*)(pk + L.k_WpX);
     const T* xs0 = Wt(L.XH) + (size_t)lo * M * 192;
     const uint32_t xb = (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz);
-    HIPCHK((pipe_batched() ? step_gemm<CfgFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)
-                           : step_gemm<CfgFor<T>, false>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)));
+    using EX = EpiStoreT<float>;
+    switch (pipe_batched() ? env_int("AAA_XPART_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
+      case -1: HIPCHK((step_gemm<CfgFor<T>, false>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+      case 1: HIPCHK((step_gemm<Cfg64For<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+      case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, EX, 3, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+      case 3: HIPCHK((step_gemm<CfgJFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+      case 4: HIPCHK((step_gemm<CfgSFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+      case 5:
+        HIPCHK((step_gemm<GemmCfg<T, 128, 128, 32, 2, 2>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)));
+        break;
+      default: HIPCHK((step_gemm<CfgFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+    }
     return AAA_OK;
   };
   hipEvent_t xev[64];
@@ -1219,11 +1229,18 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         // 64x64 tiles (64x128 measured slower: occupancy); conv2's bias
         // gradient summed from the tile in the epilogue (no column-sum pass)
         EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
-        HIPCHK((pipe_batched()
-                    ? step_gemm<CfgFor<T>, true, T, T, EpiStoreBiasT<float>>(WdT, 4608, 64, dz, g, rows, zb, ep, 64,
-                                                                             4608, s)
-                    : step_gemm<CfgFor<T>, false, T, T, EpiStoreBiasT<float>>(WdT, 4608, 64, dz, g, rows, zb, ep, 64,
-                                                                              4608, s)));
+        using ED = EpiStoreBiasT<float>;
+        switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
+          case -1: HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+          case 1: HIPCHK((step_gemm<Cfg64For<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+          case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED, 3, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+          case 3: HIPCHK((step_gemm<CfgJFor<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+          case 4:   // 64x64, 2-way in-WG split-K (8 waves), BK64
+            HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608,
+                                                                                s)));
+            break;
+          default: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+        }
       } else {
         // bf16: dY2 stored bf16 (its readers round it to bf16 anyway), conv2's
         // bias gradient summed from the fp32 values in the epilogue
