@@ -80,7 +80,7 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
 # B=5 makes B*P = 605 pixels (ragged tiles).
 @pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 4), (7, 7), (4, 8), (4, 9),
                                      (6, 10), (6, 11), (12, 12), (14, 13), (17, 15), (18, 16),
-                                     (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24)])
+                                     (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24), (25, 16), (26, 16)])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     monkeypatch.setenv("AAA_STEP_TILE", str(fwd))

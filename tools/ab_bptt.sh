@@ -10,5 +10,5 @@ run() {  # name env...
   python -c "import json;d=json.loads(open('$O/ab_${c}_$n.json').read().strip().splitlines()[-1]);k=d['kernels'];print('$c $n',d['value'],[(n[:20],v['avg_us']) for n,v in k.items()])"
 }
 run default
-for t in 12 14 17 18; do run fwd$t AAA_STEP_TILE=$t; done
-for t in 11 12 13 15 16; do run bptt$t AAA_BPTT_TILE=$t; done
+for t in 25 26; do run fwd$t AAA_STEP_TILE=$t; done
+run default2

@@ -349,9 +349,9 @@ static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unl
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
   if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
-    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || v >= 19;
-    if (v >= 19 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
-    const bool fwd_only = v == 14 || v == 17 || v == 18;
+    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || (v >= 19 && v <= 24);
+    if (v >= 19 && v <= 24 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
+    const bool fwd_only = v == 14 || v == 17 || v == 18 || v == 25 || v == 26;
     return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
   }
   // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
@@ -714,6 +714,12 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
       case 17:   // 64x32 BK64, 2-way in-WG split-K, 3-stage ring
         e = step_gemm<GemmCfg<T, 64, 32, 64, 2, 1, 2>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M,
                                                                                               xh_bytes, ep, 512, 1152, st);
+        break;
+      case 25:   // 64x64 BK64, 2-way in-WG split-K (8 waves), 2-stage ring
+        e = step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st);
+        break;
+      case 26:   // 64x64 BK128, 2-way in-WG split-K (8 waves), 2-stage ring
+        e = step_gemm<GemmCfg<T, 64, 64, 128, 2, 2, 2>, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512, 1152, st);
         break;
       case 18:   // 64x64 BK64, 2x2 waves, 3-stage ring
         e = step_gemm<Cfg64For<T>, true, T, T, EpiConvLstmFwd<T>, 3, true>(WpH, 1152, 512, xh, g, M, xh_bytes, ep, 512,
