@@ -55,6 +55,8 @@ template <typename T> hipError_t pack_dgradT(const T* Wp, int Cout, int taps, in
 template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st);
 template <typename T> hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st);
 template <typename T>
+hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T* WpXH, hipStream_t st);
+template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);
 template <typename T> hipError_t frames_rgbx(int F, int H, int W, const float* x, T* y, hipStream_t st);

@@ -612,6 +612,36 @@ __global__ void k_pack_lstm_dgradT(LstmPtrs L, T* WdT) {
   }
 }
 
+// All four ConvLSTM weight layouts in one launch (x-part, h-part, dgrad
+// transpose, fused [x | h]): the same element maps as the three kernels above,
+// one grid-stride pass over their concatenated index ranges.
+template <typename T>
+__global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T* WpXH) {
+  const int nx = 512 * 576, nh = 512 * 1152, nd = 192 * 4608, nf = 512 * 1728;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nx + nh + nd + nf; idx += gridDim.x * blockDim.x) {
+    int i = idx;
+    if (i < nx) {
+      const int row = i / 576, k = i - row * 576;
+      const int tap = k / 64, ci = k - tap * 64, ky = tap / 3, kx = tap - ky * 3;
+      WpX[i] = (T)lstm_w(L, row, ky, kx, ci);
+      if (k == 0) bl[row] = L.bx[row & 3][row >> 2];
+    } else if ((i -= nx) < nh) {
+      const int row = i / 1152, k = i - row * 1152;
+      const int tap = k / 128, ci = k - tap * 128, ky = tap / 3, kx = tap - ky * 3;
+      WpH[i] = (T)lstm_w(L, row, ky, kx, 64 + ci);
+    } else if ((i -= nh) < nd) {
+      const int cp = i / 4608, r = i - cp * 4608;
+      const int tap = r >> 9, row = r & 511, ky = tap / 3, kx = tap - ky * 3;
+      WdT[i] = (T)lstm_w(L, row, ky, kx, cp);
+    } else {
+      i -= nd;
+      const int row = i / 1728, k = i - row * 1728;
+      const int tap = k / 192, cp = k - tap * 192, ky = tap / 3, kx = tap - ky * 3;
+      WpXH[i] = (T)lstm_w(L, row, ky, kx, cp);
+    }
+  }
+}
+
 // Step 0 from a zero state: the gates come from the batched x-part alone.
 template <typename T>
 __global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gates, float* cnext, float* hout,
@@ -898,6 +928,13 @@ hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipSt
 }
 
 template <typename T>
+hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T* WpXH, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_lstm_all<T>, dim3(nblk(512L * 576 + 512L * 1152 + 192L * 4608 + 512L * 1728)), dim3(256), 0,
+                     st, L, WpX, WpH, bl, WdT, WpXH);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st) {
   hipLaunchKernelGGL(k_pack_lstm_xh<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, WpXH);
   return hipGetLastError();
@@ -977,6 +1014,8 @@ template hipError_t pack_dgradT<float>(const float*, int, int, int, float*, hipS
 template hipError_t pack_dgradT<__bf16>(const __bf16*, int, int, int, __bf16*, hipStream_t);
 template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, float*, float*, hipStream_t);
 template hipError_t pack_lstm_xh<float>(const LstmPtrs&, float*, hipStream_t);
+template hipError_t pack_lstm_all<float>(const LstmPtrs&, float*, float*, float*, float*, float*, hipStream_t);
+template hipError_t pack_lstm_all<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, __bf16*, hipStream_t);
 template hipError_t pack_lstm_xh<__bf16>(const LstmPtrs&, __bf16*, hipStream_t);
 template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);

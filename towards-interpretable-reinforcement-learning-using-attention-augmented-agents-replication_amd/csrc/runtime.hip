@@ -526,8 +526,8 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     lp.bx[g] = prm + L.poff[XI_B + 3 * g];
     lp.wh[g] = prm + L.poff[HI_W + 3 * g];
   }
-  HIPCHK(pack_lstm<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl), st));
-  HIPCHK(pack_lstm_xh<T>(lp, (T*)(pk + L.k_WpXH), st));
+  HIPCHK(pack_lstm_all<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl),
+                          (T*)(pk + L.k_WpXH), st));
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
