@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 2
+#define AAA_ABI_VERSION 3
 
 enum aaa_status {
   AAA_OK = 0,
@@ -235,6 +235,81 @@ int aaa_conv2d_nhwc_wgrad(const aaa_conv_desc* d, const float* x, const float* d
 /* C[m][n] = sum_k A[m][k] * Bw[n][k] (+ bias[n]) -- torch.nn.functional.linear */
 int aaa_linear(int M, int N, int K, const float* x, const float* w, const float* bias, float* y,
                hipStream_t stream);
+
+/* ---- component entry points ----
+ * One reference module each, on caller-owned buffers, through the kernels
+ * aaa_forward / aaa_backward run for that module.  They back the drop-in's
+ * standalone ConvLSTMCell.forward / VisionNetwork.forward and let each piece
+ * be checked in isolation.  Layout convention (Q3): the reference's NCHW
+ * tensors (B, C, a, b) of the vision core are passed NHWC as
+ * x.permute(0, 3, 2, 1) = (B, b, a, C); for the Agent's vision core that is
+ * (B, h, w, C) with (h, w) the grid of an H x W frame. */
+
+/* ConvLSTMCell(64, 128, 3) at one step (attention.py:110-126, zero
+ * peepholes :132-141).  cell_params: the cell's 12 state_dict tensors fp32,
+ * concatenated in state_dict order (W{x,h}{i,f,c,o} as in attention.py:39-102:
+ * Wxi.weight, Wxi.bias, Whi.weight, Wxf.weight, ...; 885,248 floats) -- a
+ * contiguous slice of aaa_param_layout's params.  x (B,h,w,64); h0, c0, h1,
+ * c1 (B,h,w,128); h0/c0 NULL = the zero state of init_hidden (:142-149).
+ * The workspace keeps the step's activations for aaa_convlstm_cell_bwd. */
+typedef struct aaa_cell_desc {
+  int B, h, w, dtype;
+} aaa_cell_desc;
+size_t aaa_convlstm_packed_bytes(const aaa_cell_desc* d);
+size_t aaa_convlstm_workspace_bytes(const aaa_cell_desc* d);
+int aaa_convlstm_pack(const aaa_cell_desc* d, const float* cell_params, void* packed, hipStream_t stream);
+int aaa_convlstm_cell_fwd(const aaa_cell_desc* d, const void* packed, const float* x, const float* h0,
+                          const float* c0, float* h1, float* c1, void* workspace, hipStream_t stream);
+/* Backward through the matching forward's workspace: dh1/dc1 (NULL = 0) ->
+ * dx (B,h,w,64), dh0, dc0 (each NULL = not wanted) and, when cell_grads is
+ * set, the 12 parameter gradients (overwritten) in cell_params' layout. */
+int aaa_convlstm_cell_bwd(const aaa_cell_desc* d, const void* packed, const float* dh1, const float* dc1, float* dx,
+                          float* dh0, float* dc0, float* cell_grads, void* workspace, hipStream_t stream);
+
+/* VisionNetwork.vision_cnn (attention.py:155-170) applied to X.transpose(1,3)
+ * (:179): frames (N,H,W,3) fp32 -> y2 (N,h,w,64) (= the reference's output
+ * permuted (0,3,2,1)), y1 (N,H1,W1,32) the conv1 output (NULL = not wanted).
+ * cnn_params: vision_cnn.{0,1}.{weight,bias} fp32 in state_dict order (39,008
+ * floats, the head of aaa_param_layout's params). */
+typedef struct aaa_cnn_desc {
+  int N, H, W, dtype;
+} aaa_cnn_desc;
+size_t aaa_vision_cnn_packed_bytes(const aaa_cnn_desc* d);
+size_t aaa_vision_cnn_workspace_bytes(const aaa_cnn_desc* d);
+int aaa_vision_cnn_pack(const aaa_cnn_desc* d, const float* cnn_params, void* packed, hipStream_t stream);
+int aaa_vision_cnn_fwd(const aaa_cnn_desc* d, const float* cnn_params, const void* packed, const float* frames,
+                       float* y1, float* y2, void* workspace, hipStream_t stream);
+/* dy2 (N,h,w,64) -> the four parameter gradients (overwritten, cnn_params'
+ * layout) and dy1 (N,H1,W1,32) (NULL = not wanted); frames get no gradient. */
+int aaa_vision_cnn_bwd(const aaa_cnn_desc* d, const void* packed, const float* dy2, float* dy1, float* cnn_grads,
+                       void* workspace, hipStream_t stream);
+
+/* Attention readout of F frames (attention.py:319-348: K/V split + spatial
+ * basis, logits K.Q, spatial_softmax :235-243, apply_alpha :246-254, answer
+ * assembly): O (F,h,w,128) the vision output, S (h,w,64), Q (nq,72) shared by
+ * every frame (q_stride 0, the reference's constant query) or (F,nq,72)
+ * (q_stride nq*72), prev_reward/prev_action (F) or NULL (zeros) ->
+ * attn (F,h,w,nq) and answer (F, 256nq+2) = [a_0..a_{nq-1} (184 each) |
+ * Q_0..Q_{nq-1} (72 each) | r | a_prev], the reference's ``answer`` before
+ * answer_processor. */
+int aaa_attn_fwd(int F, int h, int w, int nq, const float* O, const float* S, const float* Q, int q_stride,
+                 const float* prev_reward, const float* prev_action, float* attn, float* answer, hipStream_t stream);
+/* Its backward from danswer (F, 256nq+2): dO (F,h,w,128) and dQ (F,nq,72) per
+ * frame (logits path + the answer's Q columns; sum over F for a shared Q). */
+int aaa_attn_bwd(int F, int h, int w, int nq, const float* O, const float* S, const float* Q, int q_stride,
+                 const float* attn, const float* danswer, float* dO, float* dQ, hipStream_t stream);
+
+/* ---- index-arithmetic self-checks (host only, no device needed) ----
+ * Every pixel / tap / tile index in the kernels is divided by a runtime
+ * constant through one multiply-shift divider (csrc/common.h FastDiv).
+ * aaa_fastdiv_check runs the divider for d on every dividend n in [lo, hi)
+ * (hi <= 2^31, the divider's whole domain) against the exact quotient and
+ * returns the number of mismatches in *mismatches.  aaa_divisor_log(1, ...)
+ * starts recording every divisor the runtime builds for its launches;
+ * aaa_divisor_log(-1, out, cap) copies them out; aaa_divisor_log(0, ...)
+ * copies, stops and clears.  Returns the number recorded. */
+int aaa_fastdiv_check(unsigned d, unsigned lo, unsigned hi, unsigned long long* mismatches);
+int aaa_divisor_log(int enable, unsigned* out, int cap);
 
 #ifdef __cplusplus
 }

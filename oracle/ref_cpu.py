@@ -24,9 +24,14 @@ Parity pinning: tests/test_oracle_golden.py checks this restatement against
 fixtures produced by importing the reference itself (tests/golden/gen_golden.py).
 
 ``conv_mode='bf16'`` is the bf16-emulated oracle (SURVEY.md §8c G7 analogue):
-every convolution rounds its GEMM operands to bf16 exactly where the HIP
-kernels do (forward: activation and weight; dgrad: output-gradient and weight;
-wgrad: activation and output-gradient) and accumulates in fp32.
+every convolution rounds its GEMM operands to bf16 where the HIP kernels do
+(forward: activation and weight; dgrad: output-gradient and weight; wgrad:
+activation and output-gradient) and accumulates in fp32, and the ConvLSTM
+backward reads the gate activations rounded to fp16, as the HIP bf16 path
+stores them (``gate_store``).  What it does not emulate: the order of the fp32
+accumulations (MFMA tiles, split-K atomics) and the HIP path's bf16 rounding
+of conv1's bordered input image (exact for raw 0..255 pixels) -- so the HIP
+bf16 path matches it to ~1e-3, well inside the 2e-2 criterion, not bit for bit.
 """
 from __future__ import annotations
 
@@ -36,7 +41,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
-__all__ = ["spatial_basis", "unroll", "reinforce_loss", "grid_of", "tensor_params"]
+__all__ = ["spatial_basis", "unroll", "reinforce_loss", "grid_of", "tensor_params", "vision_cnn", "convlstm_cell",
+           "attention_readout"]
 
 
 def grid_of(H: int, W: int):
@@ -95,31 +101,72 @@ def _conv(mode, x, w, b, stride, pad):
     return F.conv2d(x, w, b, stride=stride, padding=pad)
 
 
-def _vision_step(P, X_t, state, mode, peep):
-    """Encoder + one ConvLSTM step in the reference's transposed orientation."""
+def vision_cnn(P, X_t, mode="fp32"):
+    """VisionNetwork.vision_cnn on X.transpose(1,3) (attention.py:155-170, 179):
+    frames (B,H,W,3) -> (B,64,w,h) in the reference's transposed orientation."""
     x = X_t.transpose(1, 3)                                            # attention.py:179
     y = _conv(mode, x, P["vision.vision_cnn.0.weight"], P["vision.vision_cnn.0.bias"], 4, 1)
-    y = _conv(mode, y, P["vision.vision_cnn.1.weight"], P["vision.vision_cnn.1.bias"], 2, 2)
+    return _conv(mode, y, P["vision.vision_cnn.1.weight"], P["vision.vision_cnn.1.bias"], 2, 2)
+
+
+class _GateCellF16(torch.autograd.Function):
+    """Cell update of attention.py:119-123 (zero peepholes) whose backward reads
+    the gate activations rounded to fp16 -- the HIP bf16 path stores them so
+    (csrc/epilogues.h store_gates / gate_bwd); the forward and the cell state
+    stay fp32, and tanh(c) is recomputed from the fp32 c, as there."""
+
+    @staticmethod
+    def forward(ctx, zi, zf, zc, zo, c):
+        gi, gf, gc, go = torch.sigmoid(zi), torch.sigmoid(zf), torch.tanh(zc), torch.sigmoid(zo)
+        c_new = gf * c + gi * gc
+        h_new = go * torch.tanh(c_new)
+        r = [g.to(torch.float16).to(g.dtype) for g in (gi, gf, gc, go)]
+        ctx.save_for_backward(*r, c, c_new)
+        return h_new, c_new
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        gi, gf, gc, go, c, c_new = ctx.saved_tensors
+        tc = torch.tanh(c_new)
+        dcc = dc + dh * go * (1 - tc * tc)
+        return (dcc * gc * (1 - gi) * gi, dcc * c * (1 - gf) * gf, dcc * gi * (1 - gc * gc),
+                dh * tc * (1 - go) * go, dcc * gf)
+
+
+def convlstm_cell(P, x, state, mode="fp32", peep=None, gate_store="fp32"):
+    """One ConvLSTMCell step (attention.py:110-126) on the reference's NCHW input
+    x (B,64,a,b); state (h, c) (B,128,a,b) or None (zeros, :111-115, 142-149).
+    Returns (h, c, peep).  gate_store="fp16" (bf16 mode only) emulates the HIP
+    bf16 path's fp16 storage of the gate activations for the backward."""
     if state is None:
-        B, _, a, b = y.shape
-        h = torch.zeros(B, 128, a, b, dtype=y.dtype)
-        c = torch.zeros(B, 128, a, b, dtype=y.dtype)
+        B, _, a, b = x.shape
+        h = torch.zeros(B, 128, a, b, dtype=x.dtype)
+        c = torch.zeros(B, 128, a, b, dtype=x.dtype)
     else:
         h, c = state
     if peep is None:                                                     # Q2: zero, lazily sized
-        peep = torch.zeros(1, 128, y.shape[2], y.shape[3], dtype=y.dtype)
+        peep = torch.zeros(1, 128, x.shape[2], x.shape[3], dtype=x.dtype)
 
     def gate(g):
         L = "vision.vision_lstm."
-        return (_conv(mode, y, P[L + f"Wx{g}.weight"], P[L + f"Wx{g}.bias"], 1, 1)
+        return (_conv(mode, x, P[L + f"Wx{g}.weight"], P[L + f"Wx{g}.bias"], 1, 1)
                 + _conv(mode, h, P[L + f"Wh{g}.weight"], None, 1, 1))
 
+    if gate_store == "fp16":
+        assert not bool(peep.count_nonzero()), "fp16 gate emulation assumes the reference's zero peepholes"
+        h_new, c_new = _GateCellF16.apply(gate("i"), gate("f"), gate("c"), gate("o"), c)
+        return h_new, c_new, peep
     gi = torch.sigmoid(gate("i") + c * peep)                            # attention.py:119
     gf = torch.sigmoid(gate("f") + c * peep)                            # :120
     c_new = gf * c + gi * torch.tanh(gate("c"))                         # :121
     go = torch.sigmoid(gate("o") + c_new * peep)                        # :122
     h_new = go * torch.tanh(c_new)                                      # :123
     return h_new, c_new, peep
+
+
+def _vision_step(P, X_t, state, mode, peep, gate_store="fp32"):
+    """Encoder + one ConvLSTM step in the reference's transposed orientation."""
+    return convlstm_cell(P, vision_cnn(P, X_t, mode), state, mode, peep, gate_store)
 
 
 def _query(P, B, nq, hidden=256, prev_output=None):
@@ -132,19 +179,15 @@ def _query(P, B, nq, hidden=256, prev_output=None):
     return q.reshape(-1, nq, 72)
 
 
-def _head(P, O, S, nq, prev_reward, prev_action, core=None):
-    """Attention readout + answer MLP + LSTMCell + heads (one frame batch).
-
-    core=None: the reference's reachable path, zero-state LSTMCell and a query
-    of zeros (Q1).  core=(h, c): the stateful core -- the reference's own
-    ``else`` branch (attention.py:356-358), reached when ``agent.prev_hidden``
-    holds a tensor: Q = query(h), LSTMCell from (h, c); returns the new (h, c).
-    """
+def attention_readout(O, S, Q, prev_reward=None, prev_action=None):
+    """K/V split + spatial basis, logits, spatial_softmax, apply_alpha and the
+    answer assembly (attention.py:319-348, 235-254) for one frame batch:
+    O (B,h,w,128), S (h,w,64), Q (B,nq,72) -> A (B,h,w,nq), answer (B, 256nq+2)."""
     B, h, w, _ = O.shape
+    nq = Q.shape[1]
     K, V = O.split([8, 120], dim=3)                                     # attention.py:319
     Sb = torch.stack([S.to(O.dtype)] * B)
     K, V = torch.cat([K, Sb], dim=3), torch.cat([V, Sb], dim=3)         # :231-232
-    Q = _query(P, B, nq, prev_output=None if core is None else core[0])
     A = torch.matmul(K, Q.transpose(2, 1).unsqueeze(1))                  # :336
     A = F.softmax(A.reshape(B, h * w, nq), dim=1).reshape(B, h, w, nq)  # :235-243
     a = torch.matmul(A.reshape(B, h * w, nq).transpose(1, 2),
@@ -159,6 +202,20 @@ def _head(P, O, S, nq, prev_reward, prev_action, core=None):
         act = prev_action.to(O.dtype).reshape(B, 1, 1)
     answer = torch.cat(torch.chunk(a, nq, dim=1) + torch.chunk(Q, nq, dim=1) + (r, act),
                        dim=2).squeeze(1)                                 # :343-348
+    return A, answer
+
+
+def _head(P, O, S, nq, prev_reward, prev_action, core=None):
+    """Attention readout + answer MLP + LSTMCell + heads (one frame batch).
+
+    core=None: the reference's reachable path, zero-state LSTMCell and a query
+    of zeros (Q1).  core=(h, c): the stateful core -- the reference's own
+    ``else`` branch (attention.py:356-358), reached when ``agent.prev_hidden``
+    holds a tensor: Q = query(h), LSTMCell from (h, c); returns the new (h, c).
+    """
+    B = O.shape[0]
+    Q = _query(P, B, nq, prev_output=None if core is None else core[0])
+    A, answer = attention_readout(O, S, Q, prev_reward, prev_action)
     x = F.relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]))
     x = F.linear(x, P["answer_processor.2.weight"], P["answer_processor.2.bias"])
     if core is None:
@@ -178,7 +235,7 @@ def _head(P, O, S, nq, prev_reward, prev_action, core=None):
 
 def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=None,
            state=None, S=None, conv_mode: str = "fp32", return_state: bool = False,
-           stateful_core: bool = False, core_state=None):
+           stateful_core: bool = False, core_state=None, gate_store=None):
     """T-step unroll from ``reset()``: X is (T, B, H, W, 3) fp32 raw pixels.
 
     Returns logits (T,B,A), values (T,B,A), attention maps (T,B,h,w,nq)
@@ -189,6 +246,8 @@ def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=
     continue from, and return_state then returns ((h_T, c_T), (core_h, core_c)).
     """
     T, B = X.shape[0], X.shape[1]
+    if gate_store is None:   # the HIP path's default: fp16 gate activations on the bf16 path
+        gate_store = "fp16" if conv_mode == "bf16" else "fp32"
     if S is None:
         S = spatial_basis(*grid_of(X.shape[2], X.shape[3]))
     peep = None
@@ -198,7 +257,7 @@ def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=
         dt = P["policy_core.weight_hh"].dtype
         core = core_state if core_state is not None else (torch.zeros(B, 256, dtype=dt), torch.zeros(B, 256, dtype=dt))
     for t in range(T):
-        hN, cN, peep = _vision_step(P, X[t], state, conv_mode, peep)
+        hN, cN, peep = _vision_step(P, X[t], state, conv_mode, peep, gate_store)
         state = (hN, cN)
         O = hN.transpose(1, 3)                                          # attention.py:181
         r = None if prev_reward is None else prev_reward[t]

@@ -123,8 +123,11 @@ def test_policy_episode_matches_oracle(cuda, T):
             assert float(g.abs().max()) == 0.0, n
 
 
-def test_packed_weights_follow_parameter_updates(cuda):
-    """The per-runner packed-weight cache re-packs after an in-place update."""
+@pytest.mark.parametrize("optim", ["torch", "aaa"])
+def test_packed_weights_follow_parameter_updates(cuda, optim):
+    """The per-runner packed-weight cache re-packs after an in-place update --
+    also after the fused aaa_amd.optim.Adam, which writes the parameters through
+    raw pointers and bumps their version counters itself."""
     params = detinit.deterministic_params(0, 18, 4)
     agent = attention.Agent(18, grid=(11, 11))
     detinit.load_into(agent, params)
@@ -135,7 +138,8 @@ def test_packed_weights_follow_parameter_updates(cuda):
     agent.reset()
     l1, _ = agent(x)
     assert torch.equal(l0, l1)
-    opt = torch.optim.Adam(agent.parameters(), lr=1e-2)
+    from aaa_amd.optim import Adam as FusedAdam
+    opt = (torch.optim.Adam if optim == "torch" else FusedAdam)(agent.parameters(), lr=1e-2)
     (l1.sum()).backward()
     opt.step()
     agent.reset()

@@ -81,6 +81,18 @@ def test_adam_on_agent_after_backward(cuda):
         err = float((p.detach().cpu() - r.detach()).abs().max())
         assert err <= 1e-6 * max(float(r.detach().abs().max()), 1e-30) + 1e-9, (n, err)
     assert torch.equal(ag.policy_core.weight_hh.detach(), before["policy_core.weight_hh"])
+    # the next forward runs on the updated weights (the fused step bumps the
+    # parameters' version counters, so the packed-weight cache re-packs)
+    fresh = attention.Agent(18, grid=(11, 11))
+    fresh.load_state_dict(ag.state_dict())
+    fresh.to(cuda)
+    ag.reset()
+    fresh.reset()
+    with torch.no_grad():
+        l_next, _, _ = ag.unroll(X)
+        l_fresh, _, _ = fresh.unroll(X)
+    assert torch.equal(l_next, l_fresh)
+    assert not torch.equal(l_next, lg.detach())
 
 
 def test_adam_flat_matches_torch(cuda):

@@ -128,12 +128,26 @@ def test_g6_default_basis_210x160(golden):
 
 
 def test_g7_bf16_emulation(golden):
+    """G7 = the reference with its convs' operands rounded to bf16 (fp32 gates)."""
+    g = golden("G7")
+    P = _params()
+    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16", gate_store="fp32")
+    assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, 1e-4)
+
+
+def test_fp16_gate_storage_emulation_is_a_small_backward_perturbation(golden):
+    """The bf16 oracle's default also rounds the stored gate activations to fp16
+    (the HIP bf16 path's storage).  That changes only the backward, by the
+    fp16 rounding of the gates (2^-11 relative): forward identical to G7,
+    gradients within 1e-2 of it (measured ~1.4e-3; the HIP criterion is 2e-2)."""
     g = golden("G7")
     P = _params()
     lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16")
     assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
     _loss_backward(P, lg, vl)
-    _check_grads(P, g, 1e-4)
+    _check_grads(P, g, 1e-2)
 
 
 def test_quirks_q1_zero_grads(golden):

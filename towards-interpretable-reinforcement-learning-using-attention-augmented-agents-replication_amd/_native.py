@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
+ABI_VERSION = 3   # include/aaa.h AAA_ABI_VERSION
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 
 # Every symbol include/aaa.h declares (checked by tests/test_native_abi.py).
@@ -22,7 +23,10 @@ EXPORTS = (
     "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
     "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
     "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
-    "aaa_adam_step", "aaa_reinforce", "aaa_sample_actions",
+    "aaa_adam_step", "aaa_reinforce", "aaa_sample_actions", "aaa_fastdiv_check", "aaa_divisor_log",
+    "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
+    "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
+    "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
 )
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
 
@@ -47,6 +51,14 @@ class AdamHP(ctypes.Structure):
     _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("amsgrad", ctypes.c_int),
                 ("maximize", ctypes.c_int)]
+
+
+class CellDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "h", "w", "dtype")]
+
+
+class CnnDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("N", "H", "W", "dtype")]
 
 
 class ConvDesc(ctypes.Structure):
@@ -89,12 +101,35 @@ def load(path: str = LIB_PATH):
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
             "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
+            "aaa_convlstm_packed_bytes": (S, [ctypes.POINTER(CellDesc)]),
+            "aaa_convlstm_workspace_bytes": (S, [ctypes.POINTER(CellDesc)]),
+            "aaa_convlstm_pack": (I, [ctypes.POINTER(CellDesc), P, P, P]),
+            "aaa_convlstm_cell_fwd": (I, [ctypes.POINTER(CellDesc), P, P, P, P, P, P, P, P]),
+            "aaa_convlstm_cell_bwd": (I, [ctypes.POINTER(CellDesc), P, P, P, P, P, P, P, P, P]),
+            "aaa_vision_cnn_packed_bytes": (S, [ctypes.POINTER(CnnDesc)]),
+            "aaa_vision_cnn_workspace_bytes": (S, [ctypes.POINTER(CnnDesc)]),
+            "aaa_vision_cnn_pack": (I, [ctypes.POINTER(CnnDesc), P, P, P]),
+            "aaa_vision_cnn_fwd": (I, [ctypes.POINTER(CnnDesc), P, P, P, P, P, P, P]),
+            "aaa_vision_cnn_bwd": (I, [ctypes.POINTER(CnnDesc), P, P, P, P, P, P]),
+            "aaa_attn_fwd": (I, [I, I, I, I, P, P, P, I, P, P, P, P, P]),
+            "aaa_attn_bwd": (I, [I, I, I, I, P, P, P, I, P, P, P, P, P]),
+            "aaa_fastdiv_check": (I, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_ulonglong)]),
+            "aaa_divisor_log": (I, [I, ctypes.POINTER(ctypes.c_uint), I]),
         }
+        ab_override = "AAA_LIB" in os.environ
+        missing = [name for name in sig if not hasattr(lib, name)]
+        if missing and not ab_override:
+            raise RuntimeError(f"aaa: {path} does not export {missing}; it is older than these bindings -- "
+                               f"rebuild it (make -C {os.path.join(_HERE, 'csrc')})")
         for name, (res, args) in sig.items():
-            if not hasattr(lib, name):   # an older build (A/B runs); calling it raises AttributeError
+            if name in missing:   # only with an explicit AAA_LIB (A/B runs of an older build)
                 continue
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
+        abi = lib.aaa_abi_version()
+        if abi != ABI_VERSION and not ab_override:
+            raise RuntimeError(f"aaa: {path} has ABI version {abi}, these bindings expect {ABI_VERSION}; "
+                               f"rebuild it (make -C {os.path.join(_HERE, 'csrc')})")
         _lib = lib
         return lib
 
@@ -129,6 +164,21 @@ def param_layout(cfg: Cfg):
     sizes = (ctypes.c_size_t * 34)()
     check(load().aaa_param_layout(ctypes.byref(cfg), ctypes.byref(total), offs, sizes), "param_layout")
     return total.value, list(offs), list(sizes)
+
+
+def fastdiv_check(d: int, lo: int = 0, hi: int = 1 << 31) -> int:
+    """Mismatches of the kernels' divider for d over every dividend in [lo, hi) (host)."""
+    bad = ctypes.c_ulonglong()
+    check(load().aaa_fastdiv_check(d, lo, hi, ctypes.byref(bad)), "fastdiv_check")
+    return bad.value
+
+
+def divisor_log(enable: int = -1):
+    """Divisors the runtime built since recording started (enable: 1 start, 0 stop+clear, -1 read)."""
+    n = load().aaa_divisor_log(-1, None, 0)
+    buf = (ctypes.c_uint * max(n, 1))()
+    n = load().aaa_divisor_log(enable, buf, n)
+    return sorted(set(buf[:n]))
 
 
 def timing_enable(on: bool = True) -> None:

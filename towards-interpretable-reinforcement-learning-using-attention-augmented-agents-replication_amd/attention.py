@@ -4,14 +4,15 @@ Same class names, constructor signatures, attributes and state_dict keys as
 the reference ``attention.py``, so ``main_mp.py`` /
 ``test_model.py`` and saved checkpoints work unchanged:
 
-  ConvLSTMCell   attention.py:7-149      (parameter container; fused into Agent)
-  VisionNetwork  attention.py:152-181    (parameter container; fused into Agent)
+  ConvLSTMCell   attention.py:7-149      (aaa_convlstm_cell_fwd/bwd; fused into Agent's unroll)
+  VisionNetwork  attention.py:152-181    (aaa_vision_cnn_fwd/bwd + the cell; fused into Agent's unroll)
   QueryNetwork   attention.py:184-198
   SpatialBasis   attention.py:201-232
   spatial_softmax / apply_alpha  attention.py:235-254
   Agent          attention.py:257-368
 
-``Agent.forward`` (one step, state carried in ``vision.vision_lstm.prev_hidden``)
+``Agent.forward`` (one step, state carried in ``vision.vision_lstm.prev_hidden`` in
+the reference's (B, 128, w, h) layout -- a permuted view of the kernels' NHWC state)
 and the added ``Agent.unroll`` (T steps in one call) run entirely in the gfx950
 kernels of libaaa.so through one ``torch.autograd.Function`` per call; the
 Function's backward is the hand-written BPTT, and consecutive per-step calls
@@ -40,12 +41,82 @@ __all__ = ["ConvLSTMCell", "VisionNetwork", "QueryNetwork", "SpatialBasis", "spa
            "apply_alpha", "Agent"]
 
 
-class ConvLSTMCell(nn.Module):
-    """Zero-peephole ConvLSTM cell parameters (attention.py:7-149).
+def _no_cpu(t, what):
+    if not t.is_cuda:
+        raise RuntimeError(f"aaa: {what} runs only on the MI355X HIP path; move it and its inputs to a ROCm GPU "
+                           f"(there is no CPU fallback)")
 
-    The cell math runs fused inside Agent's HIP kernels; ``prev_hidden`` holds
-    the carried (h, c) state as (B, h, w, hidden) NHWC device tensors.
+
+def _packed_cache(owner, params, dtype, pack):
+    """(flat fp32 params, packed operands) of ``params``, re-made only when a
+    parameter changed (storage or in-place version: optimizer steps,
+    load_state_dict, .to()).  The cached tensors are never written again."""
+    key = (dtype,) + tuple((p.data_ptr(), p._version) for p in params)
+    cached = getattr(owner, "_pack_cache", None)
+    if cached is not None and cached[0] == key:
+        return cached[1], cached[2]
+    with torch.no_grad():
+        flat = torch.cat([p.detach().reshape(-1) for p in params])
+        packed = pack(flat)
+    owner._pack_cache = (key, flat, packed)
+    return flat, packed
+
+
+class _CellFn(torch.autograd.Function):
+    """One ConvLSTM step (aaa_convlstm_cell_fwd); backward = aaa_convlstm_cell_bwd."""
+
+    @staticmethod
+    def forward(ctx, runner, packed, x, h0, c0, *params):
+        h1, c1, ws = runner.forward(packed, x, h0, c0)
+        ctx.runner, ctx.packed, ctx.ws = runner, packed, ws
+        ctx.shapes = [p.shape for p in params]
+        ctx.has_state = (h0 is not None, c0 is not None)
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh1, dc1):
+        need = ctx.needs_input_grad
+        dx, dh0, dc0, grads = ctx.runner.backward(
+            ctx.packed, ctx.ws, dh1, dc1, want_dx=need[2], want_dh0=need[3] and ctx.has_state[0],
+            want_dc0=need[4] and ctx.has_state[1], want_grads=any(need[5:]))
+        ctx.ws = None
+        views = ([g.view(s) for g, s in zip(grads.split([int(torch.Size(s).numel()) for s in ctx.shapes]),
+                                            ctx.shapes)] if grads is not None else [None] * len(ctx.shapes))
+        return (None, None, dx, dh0, dc0, *views)
+
+
+class _CnnFn(torch.autograd.Function):
+    """VisionNetwork.vision_cnn over N frames (aaa_vision_cnn_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, runner, flat, packed, X, *params):
+        y2, _, ws = runner.forward(flat, packed, X)
+        ctx.runner, ctx.packed, ctx.ws = runner, packed, ws
+        ctx.shapes = [p.shape for p in params]
+        return y2
+
+    @staticmethod
+    def backward(ctx, dy2):
+        grads, _ = ctx.runner.backward(ctx.packed, ctx.ws, dy2)
+        ctx.ws = None
+        views = [g.view(s) for g, s in zip(grads.split([int(torch.Size(s).numel()) for s in ctx.shapes]), ctx.shapes)]
+        return (None, None, None, None, *views)
+
+
+class ConvLSTMCell(nn.Module):
+    """Zero-peephole ConvLSTM cell (attention.py:7-149) on the HIP path.
+
+    ``forward(x)`` takes the reference's (B, C, a, b) input and returns
+    ``(h, c)`` (B, hidden, a, b), carrying them in ``prev_hidden`` exactly as
+    attention.py:110-126 does (``reset()`` clears it; the zero peepholes
+    ``Wci/Wcf/Wco`` are created on the first zero-state step, :132-141, and
+    are not parameters).  The eight gate convs, the gate math and the cell
+    update are one MFMA implicit-GEMM launch with a fused epilogue
+    (aaa_convlstm_cell_fwd); the backward is aaa_convlstm_cell_bwd.  Inside
+    ``Agent`` the same kernels run fused over the whole unroll.
     """
+
+    conv_dtype = "fp32"
 
     def __init__(self, input_channels, hidden_channels, kernel_size):
         super().__init__()
@@ -64,21 +135,92 @@ class ConvLSTMCell(nn.Module):
         self.Wcf = None
         self.Wco = None
         self.prev_hidden = None
+        self._runners = {}
+        self._own_peepholes = None
 
     def forward(self, x):
-        raise NotImplementedError(
-            "ConvLSTMCell runs fused inside Agent.forward / Agent.unroll on the MI355X HIP path")
+        _no_cpu(x, "ConvLSTMCell")
+        if x.dim() != 4 or x.shape[1] != self.input_channels:
+            raise ValueError(f"ConvLSTMCell expects (B, {self.input_channels}, H, W), got {tuple(x.shape)}")
+        h, c = self.step_nhwc(x.permute(0, 3, 2, 1))
+        return h.permute(0, 3, 2, 1), c.permute(0, 3, 2, 1)
+
+    def step_nhwc(self, x):
+        """One step on x (B, b, a, C) = the reference input permuted (0, 3, 2, 1);
+        returns (h, c) in that layout and keeps prev_hidden in the reference's."""
+        if (self.input_channels, self.hidden_channels, self.kernel_size) != (64, 128, 3):
+            raise NotImplementedError("the HIP cell implements ConvLSTMCell(64, 128, 3), the reference's only "
+                                      "instance (attention.py:171-173)")
+        B, b, a, _ = x.shape
+        if self.prev_hidden is None:
+            h0 = c0 = None                       # init_hidden: zeros (attention.py:111-115, 142-149)
+            self._peepholes(a, b, x.device)
+        else:
+            h, c = self.prev_hidden
+            if tuple(h.shape) != (B, self.hidden_channels, a, b) or tuple(c.shape) != tuple(h.shape):
+                raise RuntimeError(f"prev_hidden is {tuple(h.shape)}, this input needs "
+                                   f"{(B, self.hidden_channels, a, b)}; call reset()")
+            h0, c0 = h.permute(0, 3, 2, 1), c.permute(0, 3, 2, 1)
+        self._check_peepholes(a, b)
+        params = list(self.parameters())
+        r = self._runner(B, b, a, x.device)
+        _, packed = _packed_cache(self, params, self.conv_dtype, r.pack)
+        h1, c1 = _CellFn.apply(r, packed, x.float().contiguous(), h0, c0, *params)
+        self.prev_hidden = (h1.permute(0, 3, 2, 1), c1.permute(0, 3, 2, 1))
+        return h1, c1
 
     def reset(self):
         self.prev_hidden = None
 
     def init_hidden(self, batch_size, hidden, height, width, device):
-        z = torch.zeros(batch_size, height, width, hidden, device=device)
+        """The reference's zero state (attention.py:131-149), (B, hidden, height, width)."""
+        self._peepholes(height, width, device)
+        z = torch.zeros(batch_size, hidden, height, width, device=device)
         return z, z.clone()
+
+    # -- internals ----------------------------------------------------------
+    def _runner(self, B, h, w, device):
+        from .runtime import CellRunner
+        key = (B, h, w, str(device), self.conv_dtype)
+        r = self._runners.get(key)
+        if r is None:
+            r = self._runners[key] = CellRunner(B, h, w, self.conv_dtype, device)
+        return r
+
+    def _peepholes(self, height, width, device):
+        if self.Wci is None:   # created once, sized by the first input; never cleared (Q2)
+            self.Wci, self.Wcf, self.Wco = (torch.zeros(1, self.hidden_channels, height, width, device=device)
+                                            for _ in range(3))
+            self._own_peepholes = (self.Wci, self.Wcf, self.Wco)
+
+    def _check_peepholes(self, a, b):
+        """The kernels drop the c * W_c* terms, exact for the reference's zero
+        peepholes; a later input of another size fails there as in the
+        reference (``c * self.Wci`` does not broadcast)."""
+        if self.Wci is None:
+            return
+        if tuple(self.Wci.shape[2:]) != (a, b):
+            raise RuntimeError(f"The size of tensor a ({b}) must match the size of tensor b ({self.Wci.shape[3]}) "
+                               f"at non-singleton dimension 3 (the zero peepholes Wci/Wcf/Wco were sized "
+                               f"{tuple(self.Wci.shape[2:])} by the first input, attention.py:132-141)")
+        if self._own_peepholes is None or any(p is not q for p, q in zip((self.Wci, self.Wcf, self.Wco),
+                                                                           self._own_peepholes)):
+            if any(bool(p.count_nonzero()) for p in (self.Wci, self.Wcf, self.Wco)):
+                raise NotImplementedError("non-zero peepholes: the reference's are constant zeros (attention.py:"
+                                          "132-141) and the HIP cell drops the c * W_c* terms")
+            self._own_peepholes = (self.Wci, self.Wcf, self.Wco)
 
 
 class VisionNetwork(nn.Module):
-    """conv 8/4/1 -> conv 4/2/2 (no activation) -> ConvLSTM (attention.py:152-181)."""
+    """conv 8/4/1 -> conv 4/2/2 (no activation) -> ConvLSTM (attention.py:152-181).
+
+    ``forward(X)`` (B, H, W, 3) -> O (B, h, w, 128), the reference's
+    ``O.transpose(1, 3)``, with the cell state carried in
+    ``vision_lstm.prev_hidden``: the encoder is aaa_vision_cnn_fwd, the cell
+    aaa_convlstm_cell_fwd (both with hand-written backwards).
+    """
+
+    conv_dtype = "fp32"
 
     def __init__(self):
         super().__init__()
@@ -87,13 +229,30 @@ class VisionNetwork(nn.Module):
             nn.Conv2d(in_channels=32, out_channels=64, kernel_size=(4, 4), stride=2, padding=2),
         )
         self.vision_lstm = ConvLSTMCell(input_channels=64, hidden_channels=128, kernel_size=3)
+        self._runners = {}
 
     def reset(self):
         self.vision_lstm.reset()
 
     def forward(self, X):
-        raise NotImplementedError(
-            "VisionNetwork runs fused inside Agent.forward / Agent.unroll on the MI355X HIP path")
+        _no_cpu(X, "VisionNetwork")
+        if X.dim() != 4 or X.shape[3] != 3:
+            raise ValueError(f"VisionNetwork expects (B, H, W, 3) frames, got {tuple(X.shape)}")
+        if X.requires_grad:
+            raise NotImplementedError("frame gradients are not computed on the HIP path (the reference's frames "
+                                      "are data, main_mp.py:53)")
+        B, H, W, _ = X.shape
+        from .runtime import CnnRunner
+        key = (B, H, W, str(X.device), self.conv_dtype)
+        r = self._runners.get(key)
+        if r is None:
+            r = self._runners[key] = CnnRunner(B, H, W, self.conv_dtype, X.device)
+        params = list(self.vision_cnn.parameters())
+        flat, packed = _packed_cache(self, params, self.conv_dtype, r.pack)
+        y = _CnnFn.apply(r, flat, packed, X.float().contiguous(), *params)   # (B, h, w, 64)
+        self.vision_lstm.conv_dtype = self.conv_dtype
+        O, _ = self.vision_lstm.step_nhwc(y)
+        return O
 
 
 class QueryNetwork(nn.Module):
@@ -197,6 +356,7 @@ class Agent(nn.Module):
         # a caller puts a tensor in ``prev_hidden``, exactly as the reference does
         self.stateful_core = bool(stateful_core)
         self.vision = VisionNetwork()
+        self.vision.conv_dtype = self.vision.vision_lstm.conv_dtype = conv_dtype
         self.query = QueryNetwork(num_queries)
         self._auto_grid = grid == "auto"
         self.spatial = SpatialBasis(*grid) if isinstance(grid, (tuple, list)) else SpatialBasis()
@@ -256,10 +416,17 @@ class Agent(nn.Module):
         runner = self._runner(B, T, H, W, X.device, stateful)
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
         cell = self.vision.vision_lstm
-        h0, c0 = cell.prev_hidden if cell.prev_hidden is not None else (None, None)
-        if h0 is not None and tuple(h0.shape) != runner.state_shape():
-            raise RuntimeError(f"carried ConvLSTM state {tuple(h0.shape)} does not match this batch "
-                               f"{runner.state_shape()}; call agent.reset()")
+        # prev_hidden holds the reference's (B, 128, w, h) tensors (attention.py:125); the
+        # kernels' NHWC (B, h, w, 128) is their permute(0, 3, 2, 1) -- a view, no copy
+        if cell.prev_hidden is None:
+            h0 = c0 = None
+            cell._peepholes(runner.w, runner.h, X.device)      # init_hidden's lazy zero peepholes (Q2)
+        else:
+            h0, c0 = (s.permute(0, 3, 2, 1) for s in cell.prev_hidden)
+            if tuple(h0.shape) != runner.state_shape() or tuple(c0.shape) != runner.state_shape():
+                raise RuntimeError(f"carried ConvLSTM state {tuple(cell.prev_hidden[0].shape)} does not match this "
+                                   f"batch {(B, 128, runner.w, runner.h)}; call agent.reset()")
+        cell._check_peepholes(runner.w, runner.h)
         ch0 = cc0 = None
         if stateful:   # (prev_output, prev_hidden) of the policy core, zeros after reset()
             ch0, cc0 = self.prev_output, self.prev_hidden
@@ -270,7 +437,7 @@ class Agent(nn.Module):
         flat, packed = self._packed_params(runner, params)
         logits, values, attn, hT, cT, chT, ccT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0,
                                                                  ch0, cc0, *params)
-        cell.prev_hidden = (hT, cT)
+        cell.prev_hidden = (hT.permute(0, 3, 2, 1), cT.permute(0, 3, 2, 1))
         if stateful:
             self.prev_output, self.prev_hidden = chT, ccT
         elif self.prev_output is None:   # Q1: the query input is created once and never updated

@@ -4,6 +4,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
 namespace aaa {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -35,5 +39,46 @@ __device__ __forceinline__ void lds_store_chunk(T* dst, const u32x4& raw) {
 }
 
 template <typename T> __device__ __forceinline__ T to_t(float x) { return (T)x; }
+
+// Host-side log of every divisor the runtime builds (aaa_debug_divisors): the
+// tests re-check each one over the whole dividend range of FastDiv.
+struct DivisorLog {
+  std::mutex mu;
+  bool on = false;
+  std::vector<uint32_t> seen;
+};
+inline DivisorLog& divisor_log() {
+  static DivisorLog g;
+  return g;
+}
+inline void note_divisor(uint32_t d) {
+  DivisorLog& g = divisor_log();
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (g.on && std::find(g.seen.begin(), g.seen.end(), d) == g.seen.end()) g.seen.push_back(d);
+}
+
+// Division by a runtime constant d in [1, 2^31), exact for EVERY dividend
+// 0 <= n < 2^31 (all indices here are non-negative ints): with l = ceil(log2 d),
+// s = 31 + l and m = ceil(2^s / d), 2^s <= m*d < 2^s + 2^l, so n*m / 2^s
+// exceeds n/d by less than 1/d and floor(n*m / 2^s) = floor(n/d)
+// (Granlund & Montgomery 1994, Thm 4.2 with N = 31).  m < 2^32 and
+// n*m < 2^63: one 32x32->64 multiply and a shift.  (The round-1 divider,
+// m = ceil(2^32/d) >> 32, was exact only while n*d < 2^32 -- false for conv1's
+// 5.38 M pixel rows at 168x168.)
+struct FastDiv {
+  uint32_t d, m, s;
+  __host__ __device__ FastDiv() : d(1), m(1u << 31), s(31) {}
+  __host__ explicit FastDiv(uint32_t dd) : d(dd ? dd : 1) {
+    uint32_t l = 0;
+    while (l < 31 && (1ull << l) < d) ++l;
+    s = 31 + l;
+    m = (uint32_t)(((1ull << s) + d - 1) / d);
+    note_divisor(d);
+  }
+  __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((uint64_t)n * m) >> s);
+  }
+};
+
 
 }  // namespace aaa

@@ -41,11 +41,11 @@ struct EpiStoreT {
 struct EpiStoreParity {
   float* out;          // [F][H1][W1][C]
   int C, Nj, Ha, Wa, H1, W1, py, px;
-  uint64_t mHW, mW;    // magic divisors for Ha*Wa and Wa (FastDiv)
+  FastDiv dHW, dW;     // Ha*Wa and Wa
   __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
     if (j >= Nj || i >= C) return;
-    const int f = (int)(((uint64_t)j * mHW) >> 32), r = j - f * Ha * Wa;
-    const int a = (int)(((uint64_t)r * mW) >> 32), b = r - a * Wa;
+    const int f = (int)dHW.div((uint32_t)j), r = j - f * Ha * Wa;
+    const int a = (int)dW.div((uint32_t)r), b = r - a * Wa;
     float* o = out + ((size_t)(f * H1 + 2 * a + py) * W1 + 2 * b + px) * C + i;
     *reinterpret_cast<f32x4*>(o) = f32x4{v0, v1, v2, v3};
   }
@@ -108,14 +108,14 @@ template <typename OT>
 struct EpiStoreParityBias : BiasAcc {
   OT* out;             // [F][H1][W1][C]
   int C, Nj, Ha, Wa, H1, W1, py, px;
-  uint64_t mHW, mW;
+  FastDiv dHW, dW;
   float* bg;
-  EpiStoreParityBias(OT* o, int c, int nj, int ha, int wa, int h1, int w1, int py_, int px_, uint64_t mhw, uint64_t mw,
-                     float* b)
-      : out(o), C(c), Nj(nj), Ha(ha), Wa(wa), H1(h1), W1(w1), py(py_), px(px_), mHW(mhw), mW(mw), bg(b) {}
+  EpiStoreParityBias(OT* o, int c, int nj, int ha, int wa, int h1, int w1, int py_, int px_, float* b)
+      : out(o), C(c), Nj(nj), Ha(ha), Wa(wa), H1(h1), W1(w1), py(py_), px(px_), dHW((uint32_t)(ha * wa)),
+        dW((uint32_t)wa), bg(b) {}
   __device__ __forceinline__ OT* at(int i, int j) const {
-    const int f = (int)(((uint64_t)j * mHW) >> 32), r = j - f * Ha * Wa;
-    const int a = (int)(((uint64_t)r * mW) >> 32), b = r - a * Wa;
+    const int f = (int)dHW.div((uint32_t)j), r = j - f * Ha * Wa;
+    const int a = (int)dW.div((uint32_t)r), b = r - a * Wa;
     return out + ((size_t)(f * H1 + 2 * a + py) * W1 + 2 * b + px) * C + i;
   }
   __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre&,

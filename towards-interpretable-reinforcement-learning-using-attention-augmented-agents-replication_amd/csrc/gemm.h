@@ -124,17 +124,6 @@ struct LdRowsT {
   }
 };
 
-// Division by a runtime constant as one 32x32->64 multiply: q = (n * m) >> 32
-// with m = ceil(2^32 / d).  Exact whenever n * d < 2^32, which holds for every
-// index divided here (pixels * frames < 2^26, k < 2^16).
-struct FastDiv {
-  uint32_t d;
-  uint64_t m;
-  __host__ __device__ FastDiv() : d(1), m(1ull << 32) {}
-  __host__ __device__ explicit FastDiv(uint32_t dd) : d(dd), m(((1ull << 32) + dd - 1) / dd) {}
-  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (uint32_t)(((uint64_t)n * m) >> 32); }
-};
-
 // Convolution geometry shared by the im2col loaders.  NHWC input with pixel
 // stride ``cs`` elements and channel offset ``coff``; k = (ky*KW + kx)*Cin + ci.
 struct ConvGeo {

@@ -50,10 +50,9 @@ hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const
                          const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
+template <typename T> hipError_t cell_xh(int M, const float* x, const float* h, T* xh, hipStream_t st);
+template <typename TI, typename TO> hipError_t cast(long n, const TI* src, TO* dst, hipStream_t st);
 template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);
-template <typename T> hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st);
-template <typename T> hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st);
-template <typename T> hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st);
 template <typename T>
 hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T* WpXH, hipStream_t st);
 template <typename T>

@@ -478,6 +478,25 @@ __global__ void k_state_to_xh(int M, const float* h0, T* xh) {
   }
 }
 
+// XH slot <- [x (64) | h (128)] of the standalone ConvLSTM cell (h NULL: the
+// zero state of init_hidden, attention.py:142-149).
+template <typename T>
+__global__ void k_cell_xh(int M, const float* __restrict__ x, const float* __restrict__ h, T* xh) {
+  const int n = M * 192;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
+    const int m = idx / 192, c = idx - m * 192;
+    const float v = c < 64 ? x[(size_t)m * 64 + c] : (h ? h[(size_t)m * 128 + c - 64] : 0.f);
+    xh[idx] = (T)v;
+  }
+}
+
+// dst[i] = (TO) src[i]
+template <typename TI, typename TO>
+__global__ void k_cast(long n, const TI* __restrict__ src, TO* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = (TO)(float)src[i];
+}
+
 // ------------------------------------------------------------- packing ----
 // Conv weight in the reference's (Cout, Cin, kx, ky) orientation (Q3) ->
 // [Cout][(ky*K + kx)*Cin + ci].
@@ -550,16 +569,6 @@ __global__ void k_unpack_conv1_rgbx(const float* __restrict__ g, float* dst) {
   }
 }
 
-// WdT[ci][tap*Cout + co] = Wp[co][tap*Cin + ci]
-template <typename T>
-__global__ void k_pack_dgradT(const T* __restrict__ Wp, int Cout, int taps, int Cin, T* WdT) {
-  const int n = Cin * taps * Cout;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int ci = idx / (taps * Cout), r = idx - ci * (taps * Cout);
-    const int tap = r / Cout, co = r - tap * Cout;
-    WdT[idx] = Wp[(size_t)co * taps * Cin + tap * Cin + ci];
-  }
-}
 
 // ConvLSTM weight (gate g, channel ch) for tap (ky,kx) and input channel ci of
 // [x (64) | h (128)], in the reference's (Cout, Cin, kx, ky) orientation (Q3).
@@ -569,52 +578,13 @@ __device__ __forceinline__ float lstm_w(const LstmPtrs& L, int row, int ky, int 
                  : L.wh[g][((size_t)(ch * 128 + ci - 64) * 3 + kx) * 3 + ky];
 }
 
-// ConvLSTM forward operands, row n = 4*ch + gate: x-part [512][9*64] (batched
-// over all frames) and h-part [512][9*128] (the recurrent step); biases
-// interleaved the same way.
-template <typename T>
-__global__ void k_pack_lstm(LstmPtrs L, T* WpX, T* WpH, float* bl) {
-  const int nx = 512 * 576, nh = 512 * 1152;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nx + nh; idx += gridDim.x * blockDim.x) {
-    if (idx < nx) {
-      const int row = idx / 576, k = idx - row * 576;
-      const int tap = k / 64, ci = k - tap * 64, ky = tap / 3, kx = tap - ky * 3;
-      WpX[idx] = (T)lstm_w(L, row, ky, kx, ci);
-      if (k == 0) bl[row] = L.bx[row & 3][row >> 2];
-    } else {
-      const int i = idx - nx, row = i / 1152, k = i - row * 1152;
-      const int tap = k / 128, ci = k - tap * 128, ky = tap / 3, kx = tap - ky * 3;
-      WpH[i] = (T)lstm_w(L, row, ky, kx, 64 + ci);
-    }
-  }
-}
-
-// Fused-step operand (bf16 path): WpXH[n][tap*192 + c'] = W(n, tap, c'), c'
-// over [x | h], i.e. the forward step's K runs over the whole XH slot.
-template <typename T>
-__global__ void k_pack_lstm_xh(LstmPtrs L, T* WpXH) {
-  const int n = 512 * 1728;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int row = idx / 1728, k = idx - row * 1728;
-    const int tap = k / 192, cp = k - tap * 192, ky = tap / 3, kx = tap - ky * 3;
-    WpXH[idx] = (T)lstm_w(L, row, ky, kx, cp);
-  }
-}
-
-// ConvLSTM dgrad operand: WdT[c'][tap*512 + n] = W(n, tap, c'), c' over [x | h].
-template <typename T>
-__global__ void k_pack_lstm_dgradT(LstmPtrs L, T* WdT) {
-  const int n = 192 * 4608;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int cp = idx / 4608, r = idx - cp * 4608;
-    const int tap = r >> 9, row = r & 511, ky = tap / 3, kx = tap - ky * 3;
-    WdT[idx] = (T)lstm_w(L, row, ky, kx, cp);
-  }
-}
-
-// All four ConvLSTM weight layouts in one launch (x-part, h-part, dgrad
-// transpose, fused [x | h]): the same element maps as the three kernels above,
-// one grid-stride pass over their concatenated index ranges.
+// All four ConvLSTM weight layouts in one launch, row n = 4*ch + gate (gate
+// interleaved; biases the same way), one grid-stride pass over their
+// concatenated index ranges:
+//   x-part  WpX[n][tap*64 + ci]      (batched x-part GEMM over all frames)
+//   h-part  WpH[n][tap*128 + ci]     (the recurrent step)
+//   dgrad   WdT[c'][tap*512 + n]     (c' over [x | h]: dx and dh of the BPTT)
+//   fused   WpXH[n][tap*192 + c']    (the step GEMM whose K covers the whole XH slot)
 template <typename T>
 __global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T* WpXH) {
   const int nx = 512 * 576, nh = 512 * 1152, nd = 192 * 4608, nf = 512 * 1728;
@@ -909,23 +879,25 @@ hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st) {
 }
 
 template <typename T>
+hipError_t cell_xh(int M, const float* x, const float* h, T* xh, hipStream_t st) {
+  hipLaunchKernelGGL(k_cell_xh<T>, dim3(nblk((long)M * 192)), dim3(256), 0, st, M, x, h, xh);
+  return hipGetLastError();
+}
+
+template <typename TI, typename TO>
+hipError_t cast(long n, const TI* src, TO* dst, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL((k_cast<TI, TO>), dim3(nblk(n)), dim3(256), 0, st, n, src, dst);
+  return hipGetLastError();
+}
+
+template <typename T>
 hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st) {
   hipLaunchKernelGGL(k_pack_conv<T>, dim3(nblk((long)Cout * Cin * K * K)), dim3(256), 0, st, w, Cout, Cin, K, dst);
   return hipGetLastError();
 }
 
-template <typename T>
-hipError_t pack_dgradT(const T* Wp, int Cout, int taps, int Cin, T* WdT, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_dgradT<T>, dim3(nblk((long)Cout * taps * Cin)), dim3(256), 0, st, Wp, Cout, taps, Cin, WdT);
-  return hipGetLastError();
-}
 
-template <typename T>
-hipError_t pack_lstm(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_lstm<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, WpX, WpH, bl);
-  hipLaunchKernelGGL(k_pack_lstm_dgradT<T>, dim3(nblk(192L * 4608)), dim3(256), 0, st, L, WdT);
-  return hipGetLastError();
-}
 
 template <typename T>
 hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T* WpXH, hipStream_t st) {
@@ -934,11 +906,6 @@ hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T
   return hipGetLastError();
 }
 
-template <typename T>
-hipError_t pack_lstm_xh(const LstmPtrs& L, T* WpXH, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_lstm_xh<T>, dim3(nblk(512L * 1728)), dim3(256), 0, st, L, WpXH);
-  return hipGetLastError();
-}
 
 template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext,
@@ -1006,18 +973,17 @@ template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t)
 template hipError_t pack_conv2_classes<__bf16>(const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv1_rgbx<float>(const float*, float*, hipStream_t);
 template hipError_t pack_conv1_rgbx<__bf16>(const float*, __bf16*, hipStream_t);
+template hipError_t cell_xh<float>(int, const float*, const float*, float*, hipStream_t);
+template hipError_t cell_xh<__bf16>(int, const float*, const float*, __bf16*, hipStream_t);
+template hipError_t cast<float, __bf16>(long, const float*, __bf16*, hipStream_t);
+template hipError_t cast<__bf16, float>(long, const __bf16*, float*, hipStream_t);
+template hipError_t cast<float, float>(long, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<float>(int, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<__bf16>(int, const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);
-template hipError_t pack_dgradT<float>(const float*, int, int, int, float*, hipStream_t);
-template hipError_t pack_dgradT<__bf16>(const __bf16*, int, int, int, __bf16*, hipStream_t);
-template hipError_t pack_lstm<float>(const LstmPtrs&, float*, float*, float*, float*, hipStream_t);
-template hipError_t pack_lstm_xh<float>(const LstmPtrs&, float*, hipStream_t);
 template hipError_t pack_lstm_all<float>(const LstmPtrs&, float*, float*, float*, float*, float*, hipStream_t);
 template hipError_t pack_lstm_all<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, __bf16*, hipStream_t);
-template hipError_t pack_lstm_xh<__bf16>(const LstmPtrs&, __bf16*, hipStream_t);
-template hipError_t pack_lstm<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t);
 

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -66,6 +67,7 @@ enum PIdx {
 struct Layout {
   int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
   int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
+  int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
@@ -76,7 +78,11 @@ struct Layout {
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
 };
 
-static int build_layout(const aaa_cfg* c, Layout& L) {
+static int check_ranges(Layout& L, int min_frames);
+
+// min_frames: the frames one launch must be able to address (a step's B for
+// the unroll; 1 for the frame-independent vision encoder entries).
+static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   if (!c) return fail(AAA_E_ARG, "cfg is NULL");
   if (c->B < 1 || c->T < 1) return fail(AAA_E_ARG, "B and T must be >= 1 (B=%d T=%d)", c->B, c->T);
   if (c->nq != 4 && c->nq != 8) return fail(AAA_E_ARG, "nq must be 4 or 8 (got %d)", c->nq);
@@ -184,6 +190,37 @@ static int build_layout(const aaa_cfg* c, Layout& L) {
   L.gbhd = take((size_t)L.ldy * 4);
   L.gWihhp = take(L.sc ? 1024 * 512 * 4 : 0);
   L.ws = p;
+  return check_ranges(L, min_frames > 0 ? min_frames : L.B);
+}
+
+// The GEMM loaders address their operands through buffer descriptors with
+// 32-bit byte offsets whose out-of-range sentinel is kOOB = 2^31, and index
+// rows with int.  The whole-batch conv GEMMs (conv1/conv2 over all frames, the
+// weight gradients, dx) therefore run in chunks of at most ``fchunk`` frames
+// whose operands stay below 2 GiB (one HBM-sized batch is several launches,
+// not a wrapped offset); the per-step GEMMs address one step.  A shape whose
+// single step does not fit, or whose activations exceed the int element range,
+// is refused (AAA_E_ARG) -- split the batch over ranks or calls.
+static int check_ranges(Layout& L, int min_frames) {
+  const size_t lim = size_t(1) << 31, F = (size_t)L.F, e = (size_t)L.esz;
+  const size_t per_frame = std::max({(size_t)(L.H + 2) * (L.W + 2) * 4 * e,   // bordered frames (conv1 operand)
+                                     (size_t)L.P1 * 32 * e,                 // Y1 / dY1
+                                     (size_t)L.P * 512 * e,                 // dZ
+                                     (size_t)L.P * 192 * e,                 // XH
+                                     (size_t)L.P * 64 * e,                  // dY2
+                                     (size_t)L.H * L.W * 3 * 4});           // input frames
+  const size_t fc = (lim - 1) / per_frame;
+  if (fc < (size_t)min_frames)
+    return fail(AAA_E_ARG, "B=%d %dx%d: one step's operands (%zu bytes) exceed the 2 GiB a buffer descriptor "
+                "addresses; split the batch (data-parallel ranks or several calls)", L.B, L.H, L.W,
+                per_frame * min_frames);
+  L.fchunk = (int)std::min(fc, F);
+  const size_t elems[] = {F * L.P * 512, F * L.P * 128, F * (size_t)L.ans_ld, F * 1024, F * (size_t)L.P1 * 32,
+                          F * (size_t)L.H * L.W * 3};
+  for (size_t n : elems)
+    if (n >= lim)
+      return fail(AAA_E_ARG, "B=%d T=%d %dx%d: a %zu-element activation exceeds the int index range; split the batch",
+                  L.B, L.T, L.H, L.W, n);
   return AAA_OK;
 }
 
@@ -342,9 +379,11 @@ static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
-static int chunk_steps(int T) {   // steps per off-chain chunk (whole unroll unless overlapping)
-  const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : T);
-  return std::max(1, std::min(c, T));
+// Steps per off-chain chunk: the whole unroll unless overlapping, and never
+// more than the frames one launch may address (Layout::fchunk).
+static int chunk_steps(const Layout& L) {
+  const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : L.T);
+  return std::max(1, std::min({c, L.T, L.fchunk / L.B}));
 }
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
@@ -514,6 +553,36 @@ static int wgrad_splits(int tiles, int K, int BK) {
   return std::min(s, maxs);
 }
 
+// One fused ConvLSTM forward step (attention.py:110-126): D[512][M] = WpXH x
+// im2col([x_t | h_{t-1}]) (K = 9*192), gate math and cell update in the
+// epilogue ``ep``.  Tile: AAA_FUSED_TILE, default bf16 128x128 of 4 waves
+// (64x64 per wave; tools/ab_fused.sh), fp32 (small M only, e.g. the B=1 actor
+// and the standalone cell) 128x64 of 8 waves.
+template <typename T, typename GT>
+static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const EpiConvLstmFwd<T, GT>& ep,
+                      hipStream_t st) {
+  using EF = EpiConvLstmFwd<T, GT>;
+  const ConvGeo g = ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
+  const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
+  const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
+  TimerScope tim(AAA_TIMER_FWD_STEP, st);
+  if (ftile == 7)
+    HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring
+    HIPCHK((step_gemm<CfgSFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 9)   // 128x128, 4 waves of 64x64
+    HIPCHK((step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 10)   // 64x64, 4 waves, 3-stage ring
+    HIPCHK((step_gemm<CfgFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 11)   // 64x64, 2-way in-WG split-K (8 waves), BK64 (K = 1728 = 27 x 64)
+    HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 12)   // 128x64, 2x2 waves of 64x32
+    HIPCHK((step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else
+    HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  return AAA_OK;
+}
+
 // ------------------------------------------------------------- packing ----
 template <typename T>
 static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
@@ -544,6 +613,64 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
   return AAA_OK;
 }
 
+// Vision encoder over F frames (VisionNetwork.vision_cnn, attention.py:155-170,
+// on X.transpose(1,3), :179 -- Q3): frames (F,H,W,3) -> zero-bordered RGBx
+// image Xp -> conv 8/4/1 -> Y1 (F,H1,W1,32) -> conv 4/2/2 -> out (F,h,w,64) at
+// row pitch out_ld (the ConvLSTM operand slots, or a plain output), no
+// activation in between.  Packed conv weights at L.k_Wp1 / L.k_Wp2, biases
+// from the flat params (state_dict order: the vision tensors come first).
+template <typename T, typename OT>
+static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float* prm, const float* frames, T* Xp, T* Y1,
+                      OT* out, int out_ld, hipStream_t st) {
+  using C = CfgFor<T>;
+  constexpr int NT = C::NT;
+  const int P = L.P;
+  {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
+    HIPCHK(frames_rgbx<T>(F, L.H, L.W, frames, Xp, st));
+    // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
+    constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
+    using CP = GemmCfg<T, 32, 128, BKc, 1, 4>;
+    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
+    EpiStoreT<T> ep{Y1, 32, 32, F * L.P1, prm + L.poff[C0B], 0};
+    HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
+        typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
+        typename PB::Params{Xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
+                            (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
+        ep, 32, F * L.P1, 256, 1, st)));
+  }
+  {  // conv2 (attention.py:163-169): Y1 -> out
+    using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
+    typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};
+    const ConvGeo g = ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep();
+    EpiStoreT<OT> ep{out, out_ld, 64, F * P, prm + L.poff[C1B], 0};
+    const uint32_t y1b = (uint32_t)((size_t)F * L.P1 * 32 * L.esz);
+    if constexpr (32 % C::BK == 0) {   // LDS-DMA ring (tools/ubench/conv_cfg: 62 vs 67 us)
+      HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g, F * P, y1b, ep, 64, 512, st)));
+    } else if (pipe_batched()) {   // bf16: a BK=32 ring, one 4x4 tap row's 32 channels per K tile
+      HIPCHK((step_gemm<GemmCfg<T, 64, 128, 32, 2, 2>, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g,
+                                                           F * P, y1b, ep, 64, 512, st)));
+    } else {
+      using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
+      HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Y1, g, F * P}, ep, 64, F * P, 512, 1, st)));
+    }
+  }
+  return AAA_OK;
+}
+
+template <typename T, typename OT>
+static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const float* frames, T* Xp, T* Y1,
+                      OT* out, int out_ld, hipStream_t st) {
+  for (int f0 = 0; f0 < F; f0 += L.fchunk) {   // descriptor-sized frame chunks (check_ranges)
+    const int n = std::min(L.fchunk, F - f0);
+    const int rc = vision_fwd_chunk<T, OT>(L, n, pk, prm, frames + (size_t)f0 * L.H * L.W * 3,
+                                           Xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, Y1 + (size_t)f0 * L.P1 * 32,
+                                           out + (size_t)f0 * L.P * out_ld, out_ld, st);
+    if (rc) return rc;
+  }
+  return AAA_OK;
+}
+
 // ------------------------------------------------------------- forward ----
 template <typename T>
 static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
@@ -551,44 +678,16 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
 template <typename T>
 static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   using C = CfgFor<T>;
-  constexpr int NT = C::NT;
   char* ws = (char*)io->workspace;
   const char* pk = (const char*)io->packed;
   const float* prm = io->params;
   auto Wf = [&](size_t off) { return (float*)(ws + off); };
   auto Wt = [&](size_t off) { return (T*)(ws + off); };
-  const int F = L.F, P = L.P, M = L.B * L.P;
+  const int F = L.F, M = L.B * L.P;
 
-  {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
-    HIPCHK(frames_rgbx<T>(F, L.H, L.W, io->frames, Wt(L.Xp), st));
-    // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
-    constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
-    using CP = GemmCfg<T, 32, 128, BKc, 1, 4>;
-    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
-    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
-    EpiStoreT<T> ep{Wt(L.Y1), 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
-        typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
-        typename PB::Params{Wt(L.Xp), ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
-                            (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
-        ep, 32, F * L.P1, 256, 1, st)));
-  }
-  {  // conv2 (attention.py:163-169): Y1 -> XH[:, :, 0:64] for all T slots
-    using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
-    typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};
-    const ConvGeo g = ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep();
-    EpiStoreT<T> ep{Wt(L.XH), 192, 64, F * P, prm + L.poff[C1B], 0};
-    if constexpr (32 % C::BK == 0) {   // LDS-DMA ring (tools/ubench/conv_cfg: 62 vs 67 us)
-      HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Wt(L.Y1), g, F * P,
-                                 (uint32_t)((size_t)F * L.P1 * 32 * L.esz), ep, 64, 512, st)));
-    } else if (pipe_batched()) {   // bf16: a BK=32 ring, one 4x4 tap row's 32 channels per K tile
-      HIPCHK((step_gemm<GemmCfg<T, 64, 128, 32, 2, 2>, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Wt(L.Y1), g,
-                                                           F * P, (uint32_t)((size_t)F * L.P1 * 32 * L.esz), ep, 64,
-                                                           512, st)));
-    } else {
-      using LB = LdIm2col<T, T, C::BJ, C::BK, NT, true>;
-      HIPCHK((launch_gemm<C, LA, LB>(pa, typename LB::Params{Wt(L.Y1), g, F * P}, ep, 64, F * P, 512, 1, st)));
-    }
+  {  // conv1 + conv2 over all T*B frames -> XH[:, :, 0:64] of every slot
+    const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st);
+    if (rc) return rc;
   }
   // initial state (reset(): zeros, attention.py:142-149) or carried state
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
@@ -599,41 +698,19 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   // fp32 x-part round trip through HBM (tools/ubench/bf16_tiles: the step's
   // epilogue traffic, not its MFMAs, is half its time).  AAA_FUSED_X=0/1 overrides.
   if (fused_x(L.dt, M)) {
-    const ConvGeo g = ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
-    const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * L.esz);
     const T* WpXH = (const T*)(pk + L.k_WpXH);
     // bf16: 128x128 tiles of 4 waves (64x64 per wave: twice the MFMA work per
     // fragment read of the 128x64 8-wave tile) -- C3 94.7 -> 81-83 us, C4 51.5 ->
     // 44.6 us, C5 90.7 -> 78.6-79.5 us per step (tools/ab_fused.sh); fp32 (only
     // small M, e.g. the B=1 actor, fuses the x-part): 128x64 8 waves.
-    const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
       for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
         EpiConvLstmFwd<T, GT> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
                                  Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
                                  (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
-        TimerScope tim(AAA_TIMER_FWD_STEP, st);
-        using EF = EpiConvLstmFwd<T, GT>;
-        const T* xht = Wt(L.XH) + (size_t)t * M * 192;
-        if (ftile == 7)
-          HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
-        else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring
-          HIPCHK((step_gemm<CfgSFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
-        else if (ftile == 9)   // 128x128, 4 waves of 64x64
-          HIPCHK((step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
-                                                                   st)));
-        else if (ftile == 10)   // 64x64, 4 waves, 3-stage ring
-          HIPCHK((step_gemm<CfgFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
-        else if (ftile == 11)   // 64x64, 2-way in-WG split-K (8 waves), BK64 (K = 1728 = 27 x 64)
-          HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
-                                                                    st)));
-        else if (ftile == 12)   // 128x64, 2x2 waves of 64x32
-          HIPCHK((step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728,
-                                                                  st)));
-        else
-          HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, Wt(L.XH) + (size_t)t * M * 192, g, M, xh_bytes, ep,
-                                              512, 1728, st)));
+        const int rc = fused_step<T, GT>(WpXH, Wt(L.XH) + (size_t)t * M * 192, L.h, L.w, M, ep, st);
+        if (rc) return rc;
       }
       return AAA_OK;
     };
@@ -644,7 +721,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   // x-part of the ConvLSTM steps (not recurrent): Gt <- Wx * x_t + b, in
   // chunks of ``cs`` steps on the aux stream; step t waits only for its chunk.
   hipStream_t ax = aux_stream();
-  const int cs = chunk_steps(L.T);
+  const int cs = chunk_steps(L);
   hipStream_t xs = ax ? ax : st;
   if (ax) HIPCHK(stream_order(st, ax));
   auto xpart = [&](int lo, int hi) -> int {
@@ -893,8 +970,7 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
       const int Ha = (L.H1 - py + 1) / 2, Wa = (L.W1 - px + 1) / 2;
       if (Ha <= 0 || Wa <= 0) continue;
       const int rows = frames * Ha * Wa;
-      EpiStoreParityBias<T> ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
-                               ((1ull << 32) + Wa - 1) / Wa, gbias};
+      EpiStoreParityBias<T> ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, gbias};
       HIPCHK((launch_pipe<CP, PA, PB, EpiStoreParityBias<T>, 2>(
           typename PA::Params{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32},
           typename PB::Params{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
@@ -916,10 +992,27 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     typename LA::Params pa{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32};
     typename LB::Params pb{(const float*)dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
                            (uint32_t)((size_t)frames * L.P * 64 * 4)};
-    EpiStoreParity ep{(float*)dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, ((1ull << 32) + Ha * Wa - 1) / (Ha * Wa),
-                      ((1ull << 32) + Wa - 1) / Wa};
+    EpiStoreParity ep{(float*)dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, FastDiv((uint32_t)(Ha * Wa)),
+                      FastDiv((uint32_t)Wa)};
     HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, rows, 256, 1, s)));
   }
+  return AAA_OK;
+}
+
+// conv2 weight gradient over ``frames`` frames: gW[64][(ky*4+kx)*32 + ci] +=
+// dY2^T x im2col(Y1) (k = output pixel), split-K atomics into a zeroed gW.
+template <typename T>
+static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, float* gW, hipStream_t s) {
+  using C = CfgFor<T>;
+  using LA = LdRowsTB<T, T, C::BI, C::BK, C::NT>;
+  using LB = LdIm2colTB<T, T, C::BJ, C::BK, C::NT>;
+  const int rows = frames * L.P;
+  typename LA::Params pa{dy2, 64, 64, rows};
+  typename LB::Params pb{y1, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
+                         (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
+  EpiStore<true> ep{gW, 512, 64, 512};
+  const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
+  HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
   return AAA_OK;
 }
 
@@ -936,6 +1029,104 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
   EpiStore<true> ep{gW, 256, 32, 256};
   const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
   HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
+  return AAA_OK;
+}
+
+// All 8 ConvLSTM weight gradients of ``rows`` pixels at once (attention.py:39-102
+// as used at :119-122): gW[512 = 4ch+gate][1728 = tap*192 + c'] += dZ^T x
+// im2col(XH) with k = pixel, accumulated (split-K atomics) into a zeroed gW.
+// ``aux``: issued on the low-priority overlap stream.
+template <typename T>
+static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipStream_t s, bool aux) {
+  const uint32_t xh_bytes = (uint32_t)((size_t)rows * 192 * sizeof(T));
+  auto wgrad_lstm = [&](auto cfg) -> int {   // all 8 ConvLSTM weight grads: D[512][1728] += dZ^T * im2col(XH)
+    using CW = decltype(cfg);
+    using LA = LdRowsTB<T, T, CW::BI, CW::BK, CW::NT>;
+    using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
+    typename LA::Params pa{dz, 512, 512, rows};
+    typename LB::Params pb{xh, ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep(),
+                           1728, xh_bytes};
+    EpiStore<true> ep{gW, 1728, 512, 1728};
+    const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+    HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
+    return AAA_OK;
+  };
+  // LDS-DMA ring with transposed fragment reads for both operands (k = pixel)
+  // and the split-K atomics straight from the accumulators
+  auto wgrad_lstm_pipe = [&](auto cfg, auto nbuf, auto ilv) -> int {
+    using CW = decltype(cfg);
+    constexpr int NB = decltype(nbuf)::value, IL = decltype(ilv)::value;
+    using LA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
+    using LB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
+    typename LA::Params pa{dz, 512, 512, rows};
+    typename LB::Params pb{xh, ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep(),
+                           1728, xh_bytes};
+    EpiAtomicD ep{{gW, 1728, 512, 1728}};
+    const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+    // split-K over pixels: about one resident wave of workgroups (fewer
+    // passes of the output's atomics than the register path's ~1024)
+    const int wgs = env_int("AAA_WGRAD_WGS", 256);
+    const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
+    HIPCHK((launch_pipe<CW, LA, LB, EpiAtomicD, NB, IL>(pa, pb, ep, 512, 1728, rows, ns, s)));
+    return AAA_OK;
+  };
+  // bf16 default: 256x256 (8 waves of 128x64), BK=32 in a 4-deep ring with the
+  // DMA pieces spread over the k steps (tools/ubench/wgrad_ablate at C3: 1163 us
+  // vs 1296 for BK=64 in a 2-deep ring and 1400 for the register-staged GEMM)
+  constexpr int WBK = std::is_same<T, float>::value ? 32 : 64;
+  // (not on the aux stream: its 128 KB of LDS would keep the chain's step kernels off the CU)
+  const int wpipe = rows % WBK == 0 ? env_int("AAA_WGRAD_PIPE", std::is_same<T, float>::value || aux ? 0 : 6) : 0;
+  if (wpipe) {
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    int rc;
+    switch (wpipe) {
+      case 2: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
+      case 3:   // 8 waves of 128x64 (fp32: spills, so 256x128)
+        if constexpr (std::is_same<T, float>::value) rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{});
+        else rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, WBK, 2, 4>{}, I2{}, I0{});
+        break;
+      case 4: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 256, WBK, 2, 2>{}, I2{}, I0{}); break;
+      case 5: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I3{}, I0{}); break;
+      case 6:   // bf16: 8 waves, BK=32, 4-deep ring, spread DMA issue
+      case 7:   // bf16: the same in a 3-deep ring
+        if constexpr (std::is_same<T, float>::value)
+          rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
+        else if (wpipe == 6)
+          rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, std::integral_constant<int, 4>{}, I2{});
+        else
+          rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, I3{}, I2{});
+        break;
+      default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
+    }
+    if (rc) return rc;
+  } else {
+    // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
+    const int wide = env_int("AAA_AUX_WIDE", aux ? 0 : 1);
+    const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
+    if (rc) return rc;
+  }
+  return AAA_OK;
+}
+
+// Vision encoder backward over F frames in descriptor-sized chunks: conv2
+// weight grad (gW2 +=), conv2 dgrad -> dY1 with conv1's bias grad (gb1 +=),
+// conv1 weight grad (gW1 +=); accumulators zeroed by the caller.
+template <typename T>
+static int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, const T* xp, T* dy1, int F,
+                      float* gW2, float* gW1, float* gb1, hipStream_t s) {
+  for (int f0 = 0; f0 < F; f0 += L.fchunk) {
+    const int n = std::min(L.fchunk, F - f0);
+    const T* d2 = dy2 + (size_t)f0 * L.P * 64;
+    T* d1 = dy1 + (size_t)f0 * L.P1 * 32;
+    int rc = conv2_wgrad<T>(L, d2, y1 + (size_t)f0 * L.P1 * 32, n, gW2, s);
+    if (!rc) rc = conv2_dgrad<T>(L, pk, d2, d1, n, gb1, s);
+    if (!rc) rc = conv1_wgrad<T>(L, d1, xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, n, gW1, s);
+    if (rc) return rc;
+  }
   return AAA_OK;
 }
 
@@ -1053,7 +1244,6 @@ static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t
 template <typename T>
 static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st) {
   using C = CfgFor<T>;
-  constexpr int NT = C::NT;
   constexpr int NTF = CF::NT;
   char* ws = (char*)io->workspace;
   const char* pk = (const char*)io->packed;
@@ -1157,74 +1347,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int rows = (hi - lo) * M;                       // pixels of these frames
     const int F1 = (hi - lo) * L.B;                       // frames
     const T* dz = Wt(L.dZ) + (size_t)lo * M * 512;
-    auto wgrad_lstm = [&](auto cfg) -> int {   // all 8 ConvLSTM weight grads: D[512][1728] += dZ^T * im2col(XH)
-      using CW = decltype(cfg);
-      using LA = LdRowsTB<T, T, CW::BI, CW::BK, CW::NT>;
-      using LB = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
-      typename LA::Params pa{dz, 512, 512, rows};
-      typename LB::Params pb{Wt(L.XH) + (size_t)lo * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(),
-                             1728, (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)};
-      EpiStore<true> ep{Wf(L.gWpl), 1728, 512, 1728};
-      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-      TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
-      HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
-      return AAA_OK;
-    };
-    // LDS-DMA ring with transposed fragment reads for both operands (k = pixel)
-    // and the split-K atomics straight from the accumulators
-    auto wgrad_lstm_pipe = [&](auto cfg, auto nbuf, auto ilv) -> int {
-      using CW = decltype(cfg);
-      constexpr int NB = decltype(nbuf)::value, IL = decltype(ilv)::value;
-      using LA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
-      using LB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
-      typename LA::Params pa{dz, 512, 512, rows};
-      typename LB::Params pb{Wt(L.XH) + (size_t)lo * M * 192, ConvGeo{192, 192, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep(),
-                             1728, (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz)};
-      EpiAtomicD ep{{Wf(L.gWpl), 1728, 512, 1728}};
-      const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-      TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
-      // split-K over pixels: about one resident wave of workgroups (fewer
-      // passes of the output's atomics than the register path's ~1024)
-      const int wgs = env_int("AAA_WGRAD_WGS", 256);
-      const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
-      HIPCHK((launch_pipe<CW, LA, LB, EpiAtomicD, NB, IL>(pa, pb, ep, 512, 1728, rows, ns, s)));
-      return AAA_OK;
-    };
-    // bf16 default: 256x256 (8 waves of 128x64), BK=32 in a 4-deep ring with the
-    // DMA pieces spread over the k steps (tools/ubench/wgrad_ablate at C3: 1163 us
-    // vs 1296 for BK=64 in a 2-deep ring and 1400 for the register-staged GEMM)
-    constexpr int WBK = std::is_same<T, float>::value ? 32 : 64;
-    // (not on the aux stream: its 128 KB of LDS would keep the chain's step kernels off the CU)
-    const int wpipe = rows % WBK == 0 ? env_int("AAA_WGRAD_PIPE", std::is_same<T, float>::value || s != st ? 0 : 6) : 0;
-    if (wpipe) {
-      using I0 = std::integral_constant<int, 0>;
-      using I2 = std::integral_constant<int, 2>;
-      using I3 = std::integral_constant<int, 3>;
-      int rc;
-      switch (wpipe) {
-        case 2: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
-        case 3:   // 8 waves of 128x64 (fp32: spills, so 256x128)
-          if constexpr (std::is_same<T, float>::value) rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I2{}, I0{});
-          else rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, WBK, 2, 4>{}, I2{}, I0{});
-          break;
-        case 4: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 256, WBK, 2, 2>{}, I2{}, I0{}); break;
-        case 5: rc = wgrad_lstm_pipe(GemmCfg<T, 256, 128, WBK, 2, 2>{}, I3{}, I0{}); break;
-        case 6:   // bf16: 8 waves, BK=32, 4-deep ring, spread DMA issue
-        case 7:   // bf16: the same in a 3-deep ring
-          if constexpr (std::is_same<T, float>::value)
-            rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
-          else if (wpipe == 6)
-            rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, std::integral_constant<int, 4>{}, I2{});
-          else
-            rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, I3{}, I2{});
-          break;
-        default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
-      }
-      if (rc) return rc;
-    } else {
-      // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
-      const int wide = env_int("AAA_AUX_WIDE", s == st ? 1 : 0);
-      const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
+    {
+      const int rc = lstm_wgrad<T>(dz, Wt(L.XH) + (size_t)lo * M * 192, rows, L.h, L.w, Wf(L.gWpl), s, s != st);
       if (rc) return rc;
     }
     {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
@@ -1269,15 +1393,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
     const int rows1 = F1 * L.P1;
     constexpr bool f32 = std::is_same<T, float>::value;   // fp32 with AAA_CONV2_DGRAD_RING=0: conv1 bias by a column sum
-    {  // conv2 wgrad / bias
-      using LA = LdRowsTB<T, T, C::BI, C::BK, NT>;
-      using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
-      typename LA::Params pa{dy2, 64, 64, rows};
-      typename LB::Params pb{Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(),
-                             512, (uint32_t)((size_t)rows1 * 32 * L.esz)};
-      EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
-      const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
-      HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
+    {  // conv2 wgrad
+      const int rc = conv2_wgrad<T>(L, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, F1, Wf(L.gWp2), s);
+      if (rc) return rc;
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
       int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
@@ -1291,7 +1409,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   if (phases & AAA_BWD_CORE) {
     hipStream_t ax = aux_stream();
     hipStream_t os = ax ? ax : st;     // stream for the off-chain chunks
-    const int cs = chunk_steps(L.T);
+    const int cs = chunk_steps(L);
     // ConvLSTM BPTT, t = T-1 .. 0
     if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
@@ -1451,20 +1569,11 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
 
   if (phases & AAA_BWD_VISION) {
     if (!vision_here) {   // VISION alone: its chunk work over all frames, here
-      const int rows = F * P, rows1 = F * L.P1;
+      const int rows1 = F * L.P1;
       constexpr bool f32 = std::is_same<T, float>::value;
       {
-        using LA = LdRowsTB<T, T, C::BI, C::BK, NT>;
-        using LB = LdIm2colTB<T, T, C::BJ, C::BK, NT>;
-        typename LA::Params pa{Wt(L.dY2), 64, 64, rows};
-        typename LB::Params pb{Wt(L.Y1), ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
-                               (uint32_t)((size_t)rows1 * 32 * L.esz)};
-        EpiStore<true> ep{Wf(L.gWp2), 512, 64, 512};
-        HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(cdiv(512, C::BJ), rows, C::BK), st)));
-      }
-      {
-        int rc = conv2_dgrad<T>(L, pk, Wt(L.dY2), Wt(L.dY1), F, grads + L.poff[C0B], st);
-        if (!rc) rc = conv1_wgrad<T>(L, Wt(L.dY1), Wt(L.Xp), F, Wf(L.gWp1), st);
+        const int rc = vision_bwd<T>(L, pk, Wt(L.dY2), Wt(L.Y1), Wt(L.Xp), Wt(L.dY1), F, Wf(L.gWp2), Wf(L.gWp1),
+                                     grads + L.poff[C0B], st);
         if (rc) return rc;
         if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
@@ -1472,6 +1581,195 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
     HIPCHK(unpack_conv1_rgbx(Wf(L.gWp1), grads + L.poff[C0W], st));
   }
+  return AAA_OK;
+}
+
+// ------------------------------------------------------ component entries --
+// One reference module per entry, on caller-owned buffers,
+// through the same kernels aaa_forward / aaa_backward run for that module.
+
+// ConvLSTMCell(64, 128, 3) at one step (attention.py:110-126): packed weights
+// (the four ConvLSTM layouts of pack_lstm_all) and the workspace that carries
+// the forward's saved activations to the backward.
+struct CellLayout {
+  int B, h, w, M, dt, esz;
+  size_t k_WpX, k_WpH, k_WdTl, k_bl, k_WpXH, packed;
+  size_t XH, Cst, Hs, Gt, dZ, dC, dO, dX, gW, gb, ws;
+};
+
+static int cell_layout(const aaa_cell_desc* d, CellLayout& C) {
+  if (!d) return fail(AAA_E_ARG, "cell desc is NULL");
+  if (d->B < 1 || d->h < 1 || d->w < 1) return fail(AAA_E_ARG, "cell: need B, h, w >= 1");
+  if (d->dtype != AAA_F32 && d->dtype != AAA_BF16) return fail(AAA_E_ARG, "cell: bad dtype %d", d->dtype);
+  const size_t M = (size_t)d->B * d->h * d->w, e = d->dtype == AAA_BF16 ? 2 : 4;
+  if (M * 512 * 4 >= (size_t(1) << 31))   // dZ / gates: buffer descriptors and int indices
+    return fail(AAA_E_ARG, "cell: B*h*w = %zu pixels is above the 2 GiB descriptor range; split the batch", M);
+  C.B = d->B; C.h = d->h; C.w = d->w; C.M = (int)M; C.dt = d->dtype; C.esz = (int)e;
+  size_t p = 0;
+  auto take = [&](size_t bytes) { size_t r = p; p = al256(p + bytes); return r; };
+  C.k_WpX = take(512 * 576 * e);
+  C.k_WpH = take(512 * 1152 * e);
+  C.k_WdTl = take(192 * 4608 * e);
+  C.k_bl = take(512 * 4);
+  C.k_WpXH = take(512 * 1728 * e);
+  C.packed = p;
+  p = 0;
+  C.XH = take(2 * M * 192 * e);
+  C.Cst = take(2 * M * 128 * 4);
+  C.Hs = take(M * 128 * 4);
+  C.Gt = take(M * 512 * 4);
+  C.dZ = take(M * 512 * e);
+  C.dC = take(M * 128 * 4);
+  C.dO = take(M * 128 * 4);
+  C.dX = take(M * 64 * 4);
+  C.gW = take(512 * 1728 * 4);
+  C.gb = take(512 * 4);
+  C.ws = p;
+  return AAA_OK;
+}
+
+// the cell's 12 state_dict tensors, concatenated in state_dict order
+// (Wx{g}.weight (128,64,3,3), Wx{g}.bias (128), Wh{g}.weight (128,128,3,3) for g = i, f, c, o)
+constexpr size_t kCellGate = 128 * 64 * 9 + 128 + 128 * 128 * 9;
+template <typename P, typename Ptrs>
+static void cell_ptrs(P* base, Ptrs& lp) {
+  for (int g = 0; g < 4; ++g) {
+    lp.wx[g] = base + g * kCellGate;
+    lp.bx[g] = base + g * kCellGate + 128 * 64 * 9;
+    lp.wh[g] = base + g * kCellGate + 128 * 64 * 9 + 128;
+  }
+}
+
+template <typename T>
+static int cell_fwd_impl(const CellLayout& C, const char* pk, const float* x, const float* h0, const float* c0,
+                         float* h1, float* c1, char* ws, hipStream_t st) {
+  const int M = C.M;
+  T* xh = (T*)(ws + C.XH);
+  float* cst = (float*)(ws + C.Cst);
+  HIPCHK(cell_xh<T>(M, x, h0, xh, st));
+  if (c0) HIPCHK(hipMemcpyAsync(cst, c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(cst, 0, (size_t)M * 128 * 4, st));
+  auto run = [&](auto gtag) -> int {
+    using GT = decltype(gtag);
+    EpiConvLstmFwd<T, GT> ep{cst, cst + (size_t)M * 128, (float*)(ws + C.Hs), xh + (size_t)M * 192,
+                             (GT*)(ws + C.Gt), M, (const float*)(pk + C.k_bl)};
+    return fused_step<T, GT>((const T*)(pk + C.k_WpXH), xh, C.h, C.w, M, ep, st);
+  };
+  const int rc = gates_f16(C.dt, M) ? run(_Float16{}) : run(float{});
+  if (rc) return rc;
+  if (h1) HIPCHK(hipMemcpyAsync(h1, ws + C.Hs, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  if (c1) HIPCHK(hipMemcpyAsync(c1, cst + (size_t)M * 128, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  return AAA_OK;
+}
+
+template <typename T>
+static int cell_bwd_impl(const CellLayout& C, const char* pk, const float* dh1, const float* dc1, float* dx,
+                         float* dh0, float* dc0, float* grads, char* ws, hipStream_t st) {
+  const int M = C.M;
+  const T* xh = (const T*)(ws + C.XH);
+  const float* cst = (const float*)(ws + C.Cst);
+  float* dC = (float*)(ws + C.dC);
+  T* dZ = (T*)(ws + C.dZ);
+  if (dc1) HIPCHK(hipMemcpyAsync(dC, dc1, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  else HIPCHK(hipMemsetAsync(dC, 0, (size_t)M * 128 * 4, st));
+  const float* dh = dh1;
+  if (!dh) {
+    HIPCHK(hipMemsetAsync(ws + C.dO, 0, (size_t)M * 128 * 4, st));
+    dh = (const float*)(ws + C.dO);
+  }
+  auto run = [&](auto gtag) -> int {
+    using GT = decltype(gtag);
+    // gate backward (dz of the four gates, dc carry -> dc0)
+    HIPCHK((gate_bwd_last<T, GT>(M, 64, dh, nullptr, (const GT*)(ws + C.Gt), cst, cst + (size_t)M * 128, dC, dZ,
+                                 nullptr, st)));
+    // [dx | dh0] = W^T dz: the dgrad of all eight gate convs into [x | h] in one GEMM
+    EpiConvLstmBwd<T, GT> ep{dx ? dx : (float*)(ws + C.dX), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             dh0, 0, M, 0, nullptr};
+    const ConvGeo g = ConvGeo{512, 512, 0, C.h, C.w, C.h, C.w, 3, 1, 1, 1}.prep();
+    HIPCHK((step_gemm<CfgFor<T>, false>((const T*)(pk + C.k_WdTl), 4608, 192, (const T*)dZ, g, M,
+                                         (uint32_t)((size_t)M * 512 * C.esz), ep, 192, 4608, st)));
+    return AAA_OK;
+  };
+  int rc = gates_f16(C.dt, M) ? run(_Float16{}) : run(float{});
+  if (rc) return rc;
+  if (dc0) HIPCHK(hipMemcpyAsync(dc0, dC, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  if (grads) {   // weight grads (all 8 convs, one GEMM over the pixels) and the gate biases
+    float* gW = (float*)(ws + C.gW);
+    float* gb = (float*)(ws + C.gb);
+    HIPCHK(hipMemsetAsync(gW, 0, (size_t)512 * 1728 * 4, st));
+    HIPCHK(hipMemsetAsync(gb, 0, 512 * 4, st));
+    if ((rc = lstm_wgrad<T>(dZ, xh, M, C.h, C.w, gW, st, false))) return rc;
+    HIPCHK(colsum<T>(dZ, 512, M, 512, gb, st));
+    LstmGrads lg;
+    cell_ptrs(grads, lg);
+    HIPCHK(unpack_lstm(gW, gb, lg, st));
+  }
+  return AAA_OK;
+}
+
+// VisionNetwork.vision_cnn over N frames: a Layout with B = N, T = 1 gives the
+// geometry and the packed-weight offsets (the conv weights are the first three
+// packed layouts, the vision params the first four state_dict tensors).
+struct CnnLayout {
+  Layout L;
+  size_t Xp, Y1, dY2, dY1, gW1, gW2, ws;
+};
+
+static int cnn_layout(const aaa_cnn_desc* d, CnnLayout& C) {
+  if (!d) return fail(AAA_E_ARG, "cnn desc is NULL");
+  if (d->N < 1) return fail(AAA_E_ARG, "cnn: need N >= 1");
+  const aaa_cfg cfg{d->N, 1, d->H, d->W, 4, 18, d->dtype, 0};
+  int r = build_layout(&cfg, C.L, 1);
+  if (r) return r;
+  const Layout& L = C.L;
+  const size_t F = L.F, e = L.esz;
+  size_t p = 0;
+  auto take = [&](size_t bytes) { size_t q = p; p = al256(p + bytes); return q; };
+  C.Xp = take(F * (L.H + 2) * (L.W + 2) * 4 * e);
+  C.Y1 = take(F * L.P1 * 32 * e);
+  C.dY2 = take(F * L.P * 64 * e);
+  C.dY1 = take(F * L.P1 * 32 * e);
+  C.gW1 = take(32 * 256 * 4);
+  C.gW2 = take(64 * 512 * 4);
+  C.ws = p;
+  return AAA_OK;
+}
+
+template <typename T>
+static int cnn_pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
+  HIPCHK(pack_conv1_rgbx<T>(prm + L.poff[C0W], (T*)(pk + L.k_Wp1), st));
+  HIPCHK(pack_conv<T>(prm + L.poff[C1W], 64, 32, 4, (T*)(pk + L.k_Wp2), st));
+  HIPCHK(pack_conv2_classes<T>(prm + L.poff[C1W], (T*)(pk + L.k_WdT2), st));
+  return AAA_OK;
+}
+
+template <typename T>
+static int cnn_bwd_impl(const CnnLayout& CL, const char* pk, const float* dy2, float* dy1, float* grads, char* ws,
+                        hipStream_t st) {
+  const Layout& L = CL.L;
+  const int N = L.F;
+  const T* dy2t;
+  if constexpr (std::is_same<T, float>::value) {
+    dy2t = dy2;
+  } else {
+    HIPCHK((cast<float, T>((long)N * L.P * 64, dy2, (T*)(ws + CL.dY2), st)));
+    dy2t = (const T*)(ws + CL.dY2);
+  }
+  float* gW1 = (float*)(ws + CL.gW1);
+  float* gW2 = (float*)(ws + CL.gW2);
+  T* dY1 = (T*)(ws + CL.dY1);
+  HIPCHK(hipMemsetAsync(grads, 0, L.poff[XI_W] * 4, st));
+  HIPCHK(hipMemsetAsync(gW1, 0, 32 * 256 * 4, st));
+  HIPCHK(hipMemsetAsync(gW2, 0, 64 * 512 * 4, st));
+  HIPCHK(colsum<float>(dy2, 64, N * L.P, 64, grads + L.poff[C1B], st));   // conv2 bias (fp32 grads)
+  const int rc = vision_bwd<T>(L, pk, dy2t, (const T*)(ws + CL.Y1), (const T*)(ws + CL.Xp), dY1, N, gW2, gW1,
+                               grads + L.poff[C0B], st);
+  if (rc) return rc;
+  if (std::is_same<T, float>::value && !env_int("AAA_CONV2_DGRAD_RING", 1))
+    HIPCHK(colsum(dY1, 32, N * L.P1, 32, grads + L.poff[C0B], st));
+  HIPCHK(unpack_conv(gW2, 64, 32, 4, grads + L.poff[C1W], st));
+  HIPCHK(unpack_conv1_rgbx(gW1, grads + L.poff[C0W], st));
+  if (dy1) HIPCHK((cast<T, float>((long)N * L.P1 * 32, dY1, dy1, st)));
   return AAA_OK;
 }
 
@@ -1560,6 +1858,49 @@ using namespace aaa;
 extern "C" {
 
 int aaa_abi_version(void) { return AAA_ABI_VERSION; }
+
+int aaa_fastdiv_check(unsigned d, unsigned lo, unsigned hi, unsigned long long* mismatches) {
+  if (!mismatches || d == 0 || d >= (1u << 31) || hi > (1u << 31) || lo > hi)
+    return fail(AAA_E_ARG, "fastdiv_check: need 1 <= d < 2^31 and lo <= hi <= 2^31");
+  const FastDiv fd(d);
+  // exhaustive over [lo, hi): split over host threads; the exact quotient is
+  // carried incrementally (no hardware division in the loop)
+  const unsigned nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<unsigned long long> bad(nthr, 0);
+  std::vector<std::thread> th;
+  const unsigned long long span = hi - lo, per = (span + nthr - 1) / nthr;
+  for (unsigned t = 0; t < nthr; ++t) {
+    th.emplace_back([&, t]() {
+      const unsigned long long a = lo + std::min(span, t * per), b = lo + std::min(span, (t + 1) * per);
+      if (a >= b) return;
+      uint32_t q = (uint32_t)(a / d), r = (uint32_t)(a % d);
+      unsigned long long nb = 0;
+      for (unsigned long long n = a; n < b; ++n) {
+        nb += fd.div((uint32_t)n) != q;
+        if (++r == d) { r = 0; ++q; }
+      }
+      bad[t] = nb;
+    });
+  }
+  for (auto& x : th) x.join();
+  unsigned long long tot = 0;
+  for (auto v : bad) tot += v;
+  *mismatches = tot;
+  return AAA_OK;
+}
+
+int aaa_divisor_log(int enable, unsigned* out, int cap) {
+  DivisorLog& g = divisor_log();
+  std::lock_guard<std::mutex> lk(g.mu);
+  const int n = (int)g.seen.size();
+  if (out)
+    for (int i = 0; i < std::min(n, cap); ++i) out[i] = g.seen[i];
+  if (enable >= 0) {   // -1: read only
+    g.on = enable != 0;
+    if (!g.on) g.seen.clear();
+  }
+  return n;
+}
 
 const char* aaa_last_error(void) { return g_err.c_str(); }
 
@@ -1678,6 +2019,10 @@ static int check_conv(const aaa_conv_desc* d) {
   if (d->Hout != conv_out(d->Hin, d->KH, d->stride, d->pad) || d->Wout != conv_out(d->Win, d->KW, d->stride, d->pad))
     return fail(AAA_E_ARG, "Hout/Wout inconsistent with Hin/Win/K/stride/pad");
   if ((d->KH * d->KW * d->Cin) % 4 || d->Cout % 4) return fail(AAA_E_ARG, "KH*KW*Cin and Cout must be multiples of 4");
+  // buffer descriptors span the whole input / output gradient (32-bit byte offsets, kOOB = 2^31)
+  const size_t lim = size_t(1) << 31;
+  if ((size_t)d->N * d->Hin * d->Win * d->Cin * 4 >= lim || (size_t)d->N * d->Hout * d->Wout * d->Cout * 4 >= lim)
+    return fail(AAA_E_ARG, "conv tensors must stay below 2 GiB (split N)");
   return check_device();
 }
 
@@ -1760,6 +2105,158 @@ int aaa_sample_actions(int B, int A, const float* logits, unsigned long long see
   int r = check_device();
   if (r) return r;
   HIPCHK(sample_launch(B, A, logits, seed, counter, actions, logp, dlogp_dlogits, stream));
+  return AAA_OK;
+}
+
+// ---- component entries (include/aaa.h) ----
+size_t aaa_convlstm_packed_bytes(const aaa_cell_desc* d) {
+  CellLayout C;
+  return cell_layout(d, C) ? 0 : C.packed;
+}
+
+size_t aaa_convlstm_workspace_bytes(const aaa_cell_desc* d) {
+  CellLayout C;
+  return cell_layout(d, C) ? 0 : C.ws;
+}
+
+int aaa_convlstm_pack(const aaa_cell_desc* d, const float* cell_params, void* packed, hipStream_t stream) {
+  CellLayout C;
+  int r = cell_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!cell_params || !packed) return fail(AAA_E_ARG, "convlstm_pack: NULL argument");
+  if (!aligned16(packed)) return fail(AAA_E_ALIGN, "packed must be 16-byte aligned");
+  LstmPtrs lp;
+  cell_ptrs(cell_params, lp);
+  char* pk = (char*)packed;
+  if (C.dt == AAA_BF16)
+    HIPCHK(pack_lstm_all<__bf16>(lp, (__bf16*)(pk + C.k_WpX), (__bf16*)(pk + C.k_WpH), (__bf16*)(pk + C.k_WdTl),
+                                 (float*)(pk + C.k_bl), (__bf16*)(pk + C.k_WpXH), stream));
+  else
+    HIPCHK(pack_lstm_all<float>(lp, (float*)(pk + C.k_WpX), (float*)(pk + C.k_WpH), (float*)(pk + C.k_WdTl),
+                                (float*)(pk + C.k_bl), (float*)(pk + C.k_WpXH), stream));
+  return AAA_OK;
+}
+
+int aaa_convlstm_cell_fwd(const aaa_cell_desc* d, const void* packed, const float* x, const float* h0,
+                          const float* c0, float* h1, float* c1, void* workspace, hipStream_t stream) {
+  CellLayout C;
+  int r = cell_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!packed || !x || !workspace) return fail(AAA_E_ARG, "convlstm_cell_fwd: packed/x/workspace must be set");
+  const void* ptrs[] = {packed, x, h0, c0, h1, c1, workspace};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(AAA_E_ALIGN, "buffers must be 16-byte aligned");
+  return C.dt == AAA_BF16 ? cell_fwd_impl<__bf16>(C, (const char*)packed, x, h0, c0, h1, c1, (char*)workspace, stream)
+                          : cell_fwd_impl<float>(C, (const char*)packed, x, h0, c0, h1, c1, (char*)workspace, stream);
+}
+
+int aaa_convlstm_cell_bwd(const aaa_cell_desc* d, const void* packed, const float* dh1, const float* dc1, float* dx,
+                          float* dh0, float* dc0, float* cell_grads, void* workspace, hipStream_t stream) {
+  CellLayout C;
+  int r = cell_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!packed || !workspace) return fail(AAA_E_ARG, "convlstm_cell_bwd: packed/workspace must be set");
+  const void* ptrs[] = {packed, dh1, dc1, dx, dh0, dc0, cell_grads, workspace};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(AAA_E_ALIGN, "buffers must be 16-byte aligned");
+  return C.dt == AAA_BF16
+             ? cell_bwd_impl<__bf16>(C, (const char*)packed, dh1, dc1, dx, dh0, dc0, cell_grads, (char*)workspace, stream)
+             : cell_bwd_impl<float>(C, (const char*)packed, dh1, dc1, dx, dh0, dc0, cell_grads, (char*)workspace, stream);
+}
+
+size_t aaa_vision_cnn_packed_bytes(const aaa_cnn_desc* d) {
+  CnnLayout C;
+  return cnn_layout(d, C) ? 0 : C.L.k_WpX;   // the first three packed layouts
+}
+
+size_t aaa_vision_cnn_workspace_bytes(const aaa_cnn_desc* d) {
+  CnnLayout C;
+  return cnn_layout(d, C) ? 0 : C.ws;
+}
+
+int aaa_vision_cnn_pack(const aaa_cnn_desc* d, const float* cnn_params, void* packed, hipStream_t stream) {
+  CnnLayout C;
+  int r = cnn_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!cnn_params || !packed) return fail(AAA_E_ARG, "vision_cnn_pack: NULL argument");
+  if (!aligned16(packed)) return fail(AAA_E_ALIGN, "packed must be 16-byte aligned");
+  return C.L.dt == AAA_BF16 ? cnn_pack_impl<__bf16>(C.L, cnn_params, (char*)packed, stream)
+                            : cnn_pack_impl<float>(C.L, cnn_params, (char*)packed, stream);
+}
+
+int aaa_vision_cnn_fwd(const aaa_cnn_desc* d, const float* cnn_params, const void* packed, const float* frames,
+                       float* y1, float* y2, void* workspace, hipStream_t stream) {
+  CnnLayout C;
+  int r = cnn_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!cnn_params || !packed || !frames || !y2 || !workspace)
+    return fail(AAA_E_ARG, "vision_cnn_fwd: cnn_params/packed/frames/y2/workspace must be set");
+  const void* ptrs[] = {packed, frames, y1, y2, workspace};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(AAA_E_ALIGN, "buffers must be 16-byte aligned");
+  const Layout& L = C.L;
+  char* ws = (char*)workspace;
+  auto run = [&](auto tag) -> int {
+    using T = decltype(tag);
+    int rc = vision_fwd<T, float>(L, L.F, (const char*)packed, cnn_params, frames, (T*)(ws + C.Xp), (T*)(ws + C.Y1),
+                                  y2, 64, stream);
+    if (rc) return rc;
+    if (y1) HIPCHK((cast<T, float>((long)L.F * L.P1 * 32, (const T*)(ws + C.Y1), y1, stream)));
+    return AAA_OK;
+  };
+  return L.dt == AAA_BF16 ? run(__bf16{}) : run(float{});
+}
+
+int aaa_vision_cnn_bwd(const aaa_cnn_desc* d, const void* packed, const float* dy2, float* dy1, float* cnn_grads,
+                       void* workspace, hipStream_t stream) {
+  CnnLayout C;
+  int r = cnn_layout(d, C);
+  if (r) return r;
+  if ((r = check_device())) return r;
+  if (!packed || !dy2 || !cnn_grads || !workspace)
+    return fail(AAA_E_ARG, "vision_cnn_bwd: packed/dy2/cnn_grads/workspace must be set");
+  const void* ptrs[] = {packed, dy2, dy1, cnn_grads, workspace};
+  for (const void* p : ptrs)
+    if (p && !aligned16(p)) return fail(AAA_E_ALIGN, "buffers must be 16-byte aligned");
+  return C.L.dt == AAA_BF16
+             ? cnn_bwd_impl<__bf16>(C, (const char*)packed, dy2, dy1, cnn_grads, (char*)workspace, stream)
+             : cnn_bwd_impl<float>(C, (const char*)packed, dy2, dy1, cnn_grads, (char*)workspace, stream);
+}
+
+static int check_attn(int F, int h, int w, int nq, int q_stride) {
+  if (F < 1 || h < 1 || w < 1) return fail(AAA_E_ARG, "attn: need F, h, w >= 1");
+  if (nq != 4 && nq != 8) return fail(AAA_E_ARG, "attn: nq must be 4 or 8 (got %d)", nq);
+  if (q_stride != 0 && q_stride != nq * 72) return fail(AAA_E_ARG, "attn: q_stride must be 0 or nq*72");
+  if ((size_t)F * h * w * 128 >= (size_t(1) << 31)) return fail(AAA_E_ARG, "attn: F*h*w too large; split F");
+  return check_device();
+}
+
+int aaa_attn_fwd(int F, int h, int w, int nq, const float* O, const float* S, const float* Q, int q_stride,
+                 const float* prev_reward, const float* prev_action, float* attn, float* answer, hipStream_t stream) {
+  int r = check_attn(F, h, w, nq, q_stride);
+  if (r) return r;
+  if (!O || !S || !Q || !attn || !answer) return fail(AAA_E_ARG, "attn_fwd: O/S/Q/attn/answer must be set");
+  if (!aligned16(O) || !aligned16(S)) return fail(AAA_E_ALIGN, "O and S must be 16-byte aligned");
+  TimerScope tim(AAA_TIMER_ATTN_FWD, stream);
+  HIPCHK(attn_fwd(O, S, Q, nullptr, prev_reward, prev_action, F, h * w, nq, attn, answer, 256 * nq + 2, stream,
+                  q_stride));
+  return AAA_OK;
+}
+
+int aaa_attn_bwd(int F, int h, int w, int nq, const float* O, const float* S, const float* Q, int q_stride,
+                 const float* attn, const float* danswer, float* dO, float* dQ, hipStream_t stream) {
+  int r = check_attn(F, h, w, nq, q_stride);
+  if (r) return r;
+  if (!O || !S || !Q || !attn || !danswer || !dO || !dQ)
+    return fail(AAA_E_ARG, "attn_bwd: O/S/Q/attn/danswer/dO/dQ must be set");
+  if (!aligned16(O) || !aligned16(S) || !aligned16(dO)) return fail(AAA_E_ALIGN, "O, S, dO must be 16-byte aligned");
+  TimerScope tim(AAA_TIMER_ATTN_BWD, stream);
+  HIPCHK(attn_bwd(O, S, Q, attn, danswer, 256 * nq + 2, F, h * w, nq, dO, dQ, stream, q_stride, 1));
   return AAA_OK;
 }
 

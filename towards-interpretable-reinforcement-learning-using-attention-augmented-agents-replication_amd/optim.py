@@ -15,6 +15,7 @@ from __future__ import annotations
 from collections import defaultdict
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _native as N
 
@@ -83,7 +84,18 @@ class Adam(torch.optim.Optimizer):
             for step, (ps, gs, ms, vs, xs) in by_step.items():
                 N.adam_step(hp, step, ps, gs, ms, vs, xs if amsgrad else None,
                             stream=N.stream_ptr(ps[0].device))
+                _bump_versions(ps)
         return loss
+
+
+def _bump_versions(ps) -> None:
+    """The kernel writes the parameters through raw pointers, which autograd's
+    version counters do not see; bump them as an in-place torch op would, so
+    every cache keyed on (data_ptr, _version) -- Agent's packed weights,
+    GraphActor's re-pack check -- sees the update (and autograd still catches
+    a stale saved parameter)."""
+    for p in ps:
+        increment_version(p)
 
 
 def adam_flat_(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
@@ -91,3 +103,4 @@ def adam_flat_(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor,
     """Adam over one flat fp32 buffer (the Learner's state_dict-ordered params): one launch."""
     hp = N.AdamHP(float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0, 0)
     N.adam_step(hp, step, [params], [grads], [exp_avg], [exp_avg_sq], None, stream=N.stream_ptr(params.device))
+    _bump_versions([params])

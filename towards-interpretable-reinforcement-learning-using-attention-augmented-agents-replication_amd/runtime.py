@@ -127,3 +127,99 @@ def _f32(t, shape):
     if t.dtype != torch.float32:
         t = t.float()
     return t.contiguous()
+
+
+class CellRunner:
+    """ConvLSTMCell(64, 128, 3) steps of one (B, h, w) shape on the C ABI
+    (aaa_convlstm_*; attention.py:110-126).  Tensors are NHWC: the reference's
+    (B, C, a, b) permuted (0, 3, 2, 1)."""
+
+    def __init__(self, B: int, h: int, w: int, dtype: str = "fp32", device=None):
+        self.lib = N.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
+        self.B, self.h, self.w, self.dtype = B, h, w, dtype
+        self.desc = N.CellDesc(B, h, w, N.BF16 if dtype == "bf16" else N.F32)
+        self.pk_bytes = self.lib.aaa_convlstm_packed_bytes(ctypes.byref(self.desc))
+        self.ws_bytes = self.lib.aaa_convlstm_workspace_bytes(ctypes.byref(self.desc))
+        if not self.pk_bytes or not self.ws_bytes:
+            N.check(-1, "convlstm layout")
+
+    def pack(self, cell_flat):
+        packed = torch.empty(self.pk_bytes, dtype=torch.uint8, device=self.device)
+        N.check(self.lib.aaa_convlstm_pack(ctypes.byref(self.desc), N.ptr(cell_flat), N.ptr(packed),
+                                           N.stream_ptr(self.device)), "convlstm_pack")
+        return packed
+
+    def forward(self, packed, x, h0=None, c0=None):
+        """x (B,h,w,64), h0/c0 (B,h,w,128) or None -> (h1, c1, workspace)."""
+        shp = (self.B, self.h, self.w, 128)
+        x = _f32(x, (self.B, self.h, self.w, 64))
+        h0, c0 = _f32(h0, shp), _f32(c0, shp)
+        ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        h1 = torch.empty(shp, device=self.device)
+        c1 = torch.empty(shp, device=self.device)
+        N.check(self.lib.aaa_convlstm_cell_fwd(ctypes.byref(self.desc), N.ptr(packed), N.ptr(x), N.ptr(h0), N.ptr(c0),
+                                               N.ptr(h1), N.ptr(c1), N.ptr(ws), N.stream_ptr(self.device)),
+                "convlstm_cell_fwd")
+        return h1, c1, ws
+
+    def backward(self, packed, ws, dh1=None, dc1=None, want_dx=True, want_dh0=True, want_dc0=True,
+                 want_grads=True):
+        shp = (self.B, self.h, self.w, 128)
+        dh1, dc1 = _f32(dh1, shp), _f32(dc1, shp)
+        dev = self.device
+        dx = torch.empty(self.B, self.h, self.w, 64, device=dev) if want_dx else None
+        dh0 = torch.empty(shp, device=dev) if want_dh0 else None
+        dc0 = torch.empty(shp, device=dev) if want_dc0 else None
+        grads = torch.empty(4 * (128 * 64 * 9 + 128 + 128 * 128 * 9), device=dev) if want_grads else None
+        N.check(self.lib.aaa_convlstm_cell_bwd(ctypes.byref(self.desc), N.ptr(packed), N.ptr(dh1), N.ptr(dc1),
+                                               N.ptr(dx), N.ptr(dh0), N.ptr(dc0), N.ptr(grads), N.ptr(ws),
+                                               N.stream_ptr(dev)), "convlstm_cell_bwd")
+        return dx, dh0, dc0, grads
+
+
+class CnnRunner:
+    """VisionNetwork.vision_cnn over N frames (aaa_vision_cnn_*; attention.py:155-170
+    on X.transpose(1,3)): frames (N,H,W,3) -> (N,h,w,64) NHWC."""
+
+    def __init__(self, N_: int, H: int, W: int, dtype: str = "fp32", device=None):
+        self.lib = N.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
+        self.N, self.H, self.W, self.dtype = N_, H, W, dtype
+        self.h, self.w = N.grid(H, W)
+        self.H1, self.W1 = (H + 2 - 8) // 4 + 1, (W + 2 - 8) // 4 + 1
+        self.desc = N.CnnDesc(N_, H, W, N.BF16 if dtype == "bf16" else N.F32)
+        self.pk_bytes = self.lib.aaa_vision_cnn_packed_bytes(ctypes.byref(self.desc))
+        self.ws_bytes = self.lib.aaa_vision_cnn_workspace_bytes(ctypes.byref(self.desc))
+        if not self.pk_bytes or not self.ws_bytes:
+            N.check(-1, "vision_cnn layout")
+
+    def pack(self, cnn_flat):
+        packed = torch.empty(self.pk_bytes, dtype=torch.uint8, device=self.device)
+        N.check(self.lib.aaa_vision_cnn_pack(ctypes.byref(self.desc), N.ptr(cnn_flat), N.ptr(packed),
+                                             N.stream_ptr(self.device)), "vision_cnn_pack")
+        return packed
+
+    def forward(self, cnn_flat, packed, frames, want_y1=False):
+        """-> (y2 (N,h,w,64), y1 (N,H1,W1,32) or None, workspace)."""
+        frames = _f32(frames, (self.N, self.H, self.W, 3))
+        ws = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        y2 = torch.empty(self.N, self.h, self.w, 64, device=self.device)
+        y1 = torch.empty(self.N, self.H1, self.W1, 32, device=self.device) if want_y1 else None
+        N.check(self.lib.aaa_vision_cnn_fwd(ctypes.byref(self.desc), N.ptr(cnn_flat), N.ptr(packed), N.ptr(frames),
+                                            N.ptr(y1), N.ptr(y2), N.ptr(ws), N.stream_ptr(self.device)),
+                "vision_cnn_fwd")
+        return y2, y1, ws
+
+    def backward(self, packed, ws, dy2, want_dy1=False):
+        """-> (flat grads of the 4 vision_cnn tensors (39,008), dy1 or None)."""
+        dy2 = _f32(dy2, (self.N, self.h, self.w, 64))
+        grads = torch.empty(32 * 3 * 64 + 32 + 64 * 32 * 16 + 64, device=self.device)
+        dy1 = torch.empty(self.N, self.H1, self.W1, 32, device=self.device) if want_dy1 else None
+        N.check(self.lib.aaa_vision_cnn_bwd(ctypes.byref(self.desc), N.ptr(packed), N.ptr(dy2), N.ptr(dy1),
+                                            N.ptr(grads), N.ptr(ws), N.stream_ptr(self.device)), "vision_cnn_bwd")
+        return grads, dy1
