@@ -54,37 +54,46 @@ def flop_per_frame(H, W, nq, A=18):
     return 3 * fwd - c1
 
 
-def attention_hbm(ka, B, T, P, nq, steps):
+def attention_hbm(ka):
     """Achieved HBM GB/s of the fused attention readout kernels:
-    algorithmic bytes per frame (fp32) -- forward reads the ConvLSTM output O
-    (128 ch) and writes the attention map and the answer row; backward reads O,
-    the map and the answer grad, writes dO and dQ -- times the frames per launch."""
-    import attention  # noqa: F401
+    the library's algorithmic bytes of each launch (forward reads the ConvLSTM
+    output O and writes the attention map and answer row; backward reads O, the
+    map and the answer grad, writes dO and dQ) over its event-timed duration."""
     from aaa_amd import _native as N
-    ans_ld = (256 * nq + 2 + 7) // 8 * 8
-    per_frame = {N.TIMER_ATTN_FWD: 4 * (128 * P + nq * P + ans_ld),
-                 N.TIMER_ATTN_BWD: 4 * (2 * 128 * P + nq * P + 184 * nq + 72 * nq)}
     names = {N.TIMER_ATTN_FWD: "attention readout fwd (softmax over P, fused)",
              N.TIMER_ATTN_BWD: "attention readout bwd"}
     out = {}
-    for k, (ms, n) in ka.items():
-        if n == 0:
+    for k, v in ka.items():
+        if v["launches"] == 0:
             continue
-        per_launch = per_frame[k] * B * T * steps / n
-        avg_s = ms / n * 1e-3
+        per_launch = v["work"] / v["launches"]
+        avg_s = v["ms"] / v["launches"] * 1e-3
         gbps = per_launch / avg_s / 1e9
-        out[names[k]] = {"avg_us": round(avg_s * 1e6, 2), "launches": n, "bytes_per_launch": round(per_launch),
-                         "achieved_GBps": round(gbps, 1), "peak_GBps": 8000.0, "frac": round(gbps / 8000.0, 4)}
+        out[names[k]] = {"avg_us": round(avg_s * 1e6, 2), "launches": v["launches"], "bytes_per_launch": round(per_launch),
+                         "achieved_GBps": round(gbps, 1), "peak_GBps": 8000.0, "frac": round(gbps / 8000.0, 4),
+                         "variant": v["variant"]}
     return out
 
 
+def _cpu_threads():
+    """Host threads for the CPU baseline: every CPU in this process's affinity
+    mask, capped by OMP_NUM_THREADS when the box sets it (the
+    GPU box's CPU share is 16 threads per GPU; its affinity mask shows the
+    whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff), aff
+
+
 def cpu_baseline(cfg):
-    """Time the CPU oracle (the reference op sequence, oracle/ref_cpu.py) on the host."""
+    """Time the CPU oracle (the reference op sequence, oracle/ref_cpu.py) on the
+    host: the bench config's shape (B capped at 32) for ~10 s of whole
+    iterations, and config 1 (BASELINE.json configs[0]: B=1, T=20) for ~5 s."""
     import numpy as np
     import torch
     from oracle import ref_cpu
     from aaa_amd import detinit
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, aff = _cpu_threads()
     torch.set_num_threads(cores)
     T, nq = cfg["T"], cfg["nq"]
     B = min(cfg["B"], 32)
@@ -92,32 +101,42 @@ def cpu_baseline(cfg):
     mode = "bf16" if cfg["dtype"] == "bf16" else "fp32"
     P = ref_cpu.tensor_params(detinit.deterministic_params(0, 18, nq))
 
-    def it(Tn, Bn):
+    def it(Tn, Bn, Hn, Wn, md):
         for p in P.values():
             p.grad = None
-        X = torch.from_numpy(detinit.frames_u8(1234, (Tn, Bn, H, W, 3)).astype(np.float32))
-        lg, vl, _ = ref_cpu.unroll(P, X, nq=nq, conv_mode=mode)
+        X = torch.from_numpy(detinit.frames_u8(1234, (Tn, Bn, Hn, Wn, 3)).astype(np.float32))
+        lg, vl, _ = ref_cpu.unroll(P, X, nq=nq, conv_mode=md)
         Gl = torch.from_numpy(detinit.cotangent(2, tuple(lg.shape)))
         Gv = torch.from_numpy(detinit.cotangent(3, tuple(vl.shape)))
         ((lg * Gl).sum() + (vl * Gv).sum()).backward()
 
-    it(2, 2)   # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:                      # bounded sample: whole iterations, >= ~10 s of CPU work
-        it(T, B)
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= 10.0 or n >= 50:
-            break
+    def timed(Tn, Bn, Hn, Wn, md, budget):
+        n, t0 = 0, time.perf_counter()
+        while True:                      # bounded sample of whole iterations
+            it(Tn, Bn, Hn, Wn, md)
+            n += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget or n >= 50:
+                return n, dt
+
+    it(2, 2, H, W, mode)   # warm-up
+    n, dt = timed(T, B, H, W, mode, 10.0)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": round(n * B * T / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{n} iterations of oracle/ref_cpu.py (reference op sequence, torch CPU {mode}), "
-                      f"B={B} x T={T}, {H}x{W}, nq={nq}, {dt:.1f} s on {cores} threads ({model})"}
+    out = {"value": round(n * B * T / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+           "sample": f"{n} iterations of oracle/ref_cpu.py (reference op sequence, torch CPU {mode}), "
+                     f"B={B} x T={T}, {H}x{W}, nq={nq}, {dt:.1f} s on {cores} threads ({model}; "
+                     f"affinity mask {aff} CPUs, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})"}
+    if nq == 4:   # config 1 (BASELINE.json configs[0]): the reference's CPU-runnable case, fp32
+        it(2, 1, 84, 84, "fp32")
+        n1, dt1 = timed(20, 1, 84, 84, "fp32", 5.0)
+        out["c1"] = {"value": round(n1 * 20 / dt1, 3), "unit": "frames/s", "ms_per_iteration": round(dt1 / n1 * 1e3, 1),
+                     "sample": f"{n1} iterations of B=1 x T=20, 84x84, fp32, fwd+bwd, {dt1:.1f} s on {cores} threads"}
+    return out
 
 
 def pmc_traffic(config, dtype, world, kernel):
@@ -158,11 +177,12 @@ def main():
     from aaa_amd.learner import Learner
     from aaa_amd.parallel import init_from_env
 
-    rank, world, local = init_from_env("nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)            # before the process group: RCCL binds this rank to its GPU
+    dev = torch.device("cuda", local)
+    rank, world, local = init_from_env("nccl", device=dev)
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     B, T, H, W, nq, dtype = cfg["B"], cfg["T"], cfg["H"], cfg["W"], cfg["nq"], cfg["dtype"]
     A = 18
     learner = Learner(B, T, H, W, nq, A, dtype, dev)
@@ -186,15 +206,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        last = i == args.steps - 1
         if timed and i == args.steps - timed:
             N.timing_enable(True)
-        learner.step(frames, dl, dv, overlap=not args.no_overlap)
+        learner.step(frames, dl, dv, overlap=not args.no_overlap, comm_timing=last and world > 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kt = {k: N.timing_read(k) for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
-    ka = {k: N.timing_read(k) for k in (N.TIMER_ATTN_FWD, N.TIMER_ATTN_BWD)}
+    kt = {k: N.timing_stats(k) for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
+    ka = {k: N.timing_stats(k) for k in (N.TIMER_ATTN_FWD, N.TIMER_ATTN_BWD)}
     N.timing_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -209,32 +230,24 @@ def main():
                               "steps": args.steps, "ms_per_step": round(ms, 3), "kernel_timing": False}), flush=True)
         return
 
-    # roofline of the dominant kernel class (largest total device time); work per
-    # launch = the class's algorithmic FLOP per iteration / its launches per iteration
-    M = B * learner.runner.P
-    F = B * T
-    # bf16 runs the x-part inside every step (runtime.hip forward_impl, AAA_FUSED_X)
-    fused_x = int(os.environ.get("AAA_FUSED_X", "1" if dtype == "bf16" or M <= 1024 else "0")) != 0
-    per_iter = {
-        N.TIMER_FWD_STEP: (T * 2.0 * M * 512 * 1728 if fused_x       # [x | h] parts of all T steps
-                           else (T - 1) * 2.0 * M * 512 * 1152),   # h-part of steps 1..T-1 (x-part batched)
-        N.TIMER_BPTT_STEP: (T - 1) * 2.0 * M * 128 * 4608,     # dh rows of steps T-1..1
-        N.TIMER_CORE_WGRAD: 2.0 * 512 * 1728 * F * learner.runner.P,
-    }
-    names = {N.TIMER_FWD_STEP: "fused ConvLSTM forward step (x+h parts)" if fused_x else
-             "fused ConvLSTM forward step (h-part)",
-             N.TIMER_BPTT_STEP: "ConvLSTM BPTT step (dh dgrad + fused gate bwd)",
+    # roofline of the dominant kernel class (largest total device time): the
+    # library accounts each launch's algorithmic FLOP and names the variant it
+    # dispatched (aaa_timing_stats), so nothing here re-derives its dispatch
+    names = {N.TIMER_FWD_STEP: "ConvLSTM forward step", N.TIMER_BPTT_STEP: "ConvLSTM BPTT step",
              N.TIMER_CORE_WGRAD: "ConvLSTM weight-gradient GEMM"}
-    per_launch = {k: per_iter[k] * timed / max(kt[k][1], 1) for k in kt}
-    dom = max(kt, key=lambda k: kt[k][0])
-    tot_ms, launches = kt[dom]
-    avg_ms = tot_ms / max(launches, 1)
+    dom = max(kt, key=lambda k: kt[k]["ms"])
+    d = kt[dom]
+    avg_ms = d["ms"] / max(d["launches"], 1)
+    per_launch = d["work"] / max(d["launches"], 1)
     peak = PEAK_TFLOPS[dtype]
-    achieved = per_launch[dom] / (avg_ms * 1e-3) / 1e12
+    achieved = per_launch / (avg_ms * 1e-3) / 1e12
     fpf = flop_per_frame(H, W, nq)
-    kernels = {names[k]: {"avg_us": round(v[0] / max(v[1], 1) * 1e3, 2), "launches": v[1],
-                          "tflops": round(per_launch[k] / (v[0] / max(v[1], 1) * 1e-3) / 1e12, 2)}
-               for k, v in kt.items()}
+    kernels = {names[k]: {"avg_us": round(v["ms"] / max(v["launches"], 1) * 1e3, 2), "launches": v["launches"],
+                          "flop_per_launch": v["work"] / max(v["launches"], 1),
+                          "tflops": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12, 2),
+                          "frac": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12 / peak, 4),
+                          "variant": v["variant"]}
+               for k, v in kt.items() if v["launches"]}
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -244,16 +257,20 @@ def main():
                 "architecture, uniform[-1,1) logits/values cotangents",
         "config": {"workload": cfg["desc"], "global_batch": B * world, "seq_len": T, "frame": f"{H}x{W}",
                    "heads": nq, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": names[dom], "achieved": round(achieved, 2), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+        "roofline": {"bound": "mfma", "kernel": names[dom], "variant": d["variant"], "achieved": round(achieved, 2),
+                     "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      **pmc_traffic(args.config, dtype, world, names[dom]),
-                     "flop_per_launch": per_launch[dom], "avg_launch_us": round(avg_ms * 1e3, 2),
-                     "timed_launches": launches, "timing": "HIP events around each launch of the last timed step"},
+                     "flop_per_launch": per_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
+                     "timed_launches": d["launches"], "timing": "HIP events around each launch of the last timed step"},
         "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
                          "frac": round(value * fpf / world / 1e12 / peak, 4)},
         "kernels": kernels,
-        "hbm_kernels": attention_hbm(ka, B, T, learner.runner.P, nq, timed),
+        "hbm_kernels": attention_hbm(ka),
     }
+    if world > 1:   # RCCL gradient all-reduce of the last timed step, per bucket
+        out["comm"] = {**learner.comm_stats(), "backend": dist.get_backend(),
+                       "note": "allreduce_ms: RCCL time per bucket on the comm stream; exposed_ms: comm still "
+                               "running after the last backward phase finished (the part not overlapped)"}
     # fused Adam (excluded from the metric, which stops at
     # ready gradients): HBM-bound, 28 B per parameter (p, g, m, v read; p, m, v written)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -169,6 +169,17 @@ enum aaa_timer {
 };
 int aaa_timing_enable(int on);
 int aaa_timing_read(int kind, double* total_ms, long* launches);
+/* The same read with the roofline inputs the runtime knows: the summed
+ * algorithmic work of those launches (FLOP for the MFMA classes 0-2: 2*M*N*K
+ * of each GEMM; bytes for the HBM classes 3-4: the fp32 tensors each frame
+ * must move) and the kernel variant (tile / ring) dispatched last. */
+typedef struct aaa_timer_stats {
+  double total_ms;
+  long launches;
+  double work;
+  char variant[96];
+} aaa_timer_stats;
+int aaa_timing_stats(int kind, aaa_timer_stats* out);
 
 /* ---- optimizer ----
  * One fused multi-tensor Adam step with torch.optim.Adam semantics (the

@@ -39,8 +39,10 @@ def main():
     for overlap in (True, False):
         lr = Learner(b, T, 84, 84, 4, A, dtype, dev)
         lr.step(X[:, rows].contiguous().to(dev), Gl[:, rows].contiguous().to(dev), Gv[:, rows].contiguous().to(dev),
-                overlap=overlap)
+                overlap=overlap, comm_timing=True)
         torch.cuda.synchronize()
+        cs = lr.comm_stats()
+        assert len(cs["buckets"]) == 3 and all(x["allreduce_ms"] >= 0 for x in cs["buckets"]), cs
         if rank == 0:   # single-process reference over the whole batch, same weights
             r = UnrollRunner(Bt, T, 84, 84, 4, A, dtype, dev)
             pk, ws = r.new_packed(), r.new_workspace()

@@ -14,13 +14,15 @@ import json
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
-from pmcsum import load  # noqa: E402
+from pmcsum import derived, load  # noqa: E402
 
-# kernel class (bench.py names) -> all substrings that must appear in the kernel name
+# kernel class (bench.py names) -> alternatives, each a list of substrings that
+# must all appear in the kernel name (fp32 register-staged / bf16 LDS-DMA ring)
 CLASSES = {
-    "ConvLSTM BPTT step (dh dgrad + fused gate bwd)": ["EpiConvLstmBwd"],
-    "fused ConvLSTM forward step (h-part)": ["EpiConvLstmFwd"],
-    "ConvLSTM weight-gradient GEMM": ["128, 128, 32", "LdIm2colTB", "EpiStore<true>"],
+    "ConvLSTM BPTT step": [["EpiConvLstmBwd"]],
+    "ConvLSTM forward step": [["EpiConvLstmFwd"]],
+    "ConvLSTM weight-gradient GEMM": [["128, 128, 32", "LdIm2colTB", "EpiStore<true>"], ["GIm2colT", "EpiAtomicD"],
+                                      ["GIm2colT", "EpiWgrad"]],
 }
 
 
@@ -29,17 +31,19 @@ def main():
     acc = load(d)
     res = {}
     for cls, subs in CLASSES.items():
-        fetch, write, n = [], [], 0
+        vals = {}
         for k, cs in acc.items():
-            if all(s in k for s in subs):
-                fetch += cs.get("FETCH_SIZE", [])
-                write += cs.get("WRITE_SIZE", [])
-        if not fetch or not write:
+            if any(all(s in k for s in alt) for alt in subs):
+                for c, v in cs.items():
+                    vals.setdefault(c, []).extend(v)
+        if not vals.get("FETCH_SIZE") or not vals.get("WRITE_SIZE"):
             continue
-        f = sum(fetch) / len(fetch) * 1024.0
-        w = sum(write) / len(write) * 1024.0
+        mean = {c: sum(v) / len(v) for c, v in vals.items()}
+        f, w = mean["FETCH_SIZE"] * 1024.0, mean["WRITE_SIZE"] * 1024.0
         res[cls] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes_per_launch": 2.0 * f + w,
-                    "dispatches": len(fetch), "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)"}
+                    "dispatches": len(vals["FETCH_SIZE"]), "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)",
+                    **{k: round(v, 4) for k, v in derived(mean).items()},
+                    "counters_per_dispatch": {c: v for c, v in mean.items() if c not in ("FETCH_SIZE", "WRITE_SIZE")}}
     json.dump({"source": d, "classes": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -8,6 +8,10 @@ passes, plus derived ratios when their inputs are present:
   wait%   = SQ_WAIT_ANY / SQ_WAVE_CYCLES          (parked on s_waitcnt / barrier)
   stall%  = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES     (issue stalls: MFMA RAW, pipe busy)
   active% = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES
+  mfma%   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
+            (busy cycles are summed over every SIMD; GRBM_GUI_ACTIVE over the 8 XCDs,
+            MI355X_MICROARCH.md "SQ PMC units" / "DVFS give-back")
+  ldsconf% = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   FETCH_SIZE / WRITE_SIZE are KB per dispatch (rocprofv3 unit) -> MB shown.
 """
 import csv
@@ -26,6 +30,21 @@ def load(d):
         for (disp, k, c), v in per.items():
             acc[k][c].append(v)
     return acc
+
+
+def derived(mean):
+    """MFMA utilisation and LDS bank-conflict rate from per-dispatch means (None if absent)."""
+    out = {}
+    if mean.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and mean.get("GRBM_GUI_ACTIVE"):
+        out["mfma_util"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * mean["GRBM_GUI_ACTIVE"] / 8.0)
+    if mean.get("SQ_LDS_BANK_CONFLICT") is not None and mean.get("SQ_LDS_IDX_ACTIVE"):
+        out["lds_conflict_rate"] = mean["SQ_LDS_BANK_CONFLICT"] / mean["SQ_LDS_IDX_ACTIVE"]
+    wc = mean.get("SQ_WAVE_CYCLES")
+    if wc:
+        for c, lab in (("SQ_WAIT_ANY", "wait"), ("SQ_WAIT_INST_ANY", "stall"), ("SQ_ACTIVE_INST_ANY", "active")):
+            if c in mean:
+                out[lab] = mean[c] / wc
+    return out
 
 
 def short(k):
@@ -50,14 +69,9 @@ def main():
             else:
                 line.append(f"{c}={v:.4g}")
         print("   " + "  ".join(line))
-        wc = mean.get("SQ_WAVE_CYCLES")
-        if wc:
-            parts = []
-            for c, lab in (("SQ_WAIT_ANY", "wait"), ("SQ_WAIT_INST_ANY", "stall"), ("SQ_ACTIVE_INST_ANY", "active")):
-                if c in mean:
-                    parts.append(f"{lab}={100 * mean[c] / wc:.1f}%")
-            if parts:
-                print("   " + "  ".join(parts))
+        dv = derived(mean)
+        if dv:
+            print("   " + "  ".join(f"{k}={100 * v:.1f}%" for k, v in dv.items()))
 
 
 if __name__ == "__main__":

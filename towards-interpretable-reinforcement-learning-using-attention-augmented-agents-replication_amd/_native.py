@@ -22,7 +22,7 @@ BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 EXPORTS = (
     "aaa_abi_version", "aaa_last_error", "aaa_grid", "aaa_param_layout", "aaa_packed_bytes",
     "aaa_workspace_bytes", "aaa_pack_weights", "aaa_forward", "aaa_backward", "aaa_conv2d_nhwc",
-    "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read",
+    "aaa_conv2d_nhwc_dgrad", "aaa_conv2d_nhwc_wgrad", "aaa_linear", "aaa_timing_enable", "aaa_timing_read", "aaa_timing_stats",
     "aaa_adam_step", "aaa_reinforce", "aaa_sample_actions", "aaa_fastdiv_check", "aaa_divisor_log",
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
@@ -41,6 +41,11 @@ IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action"
              "grads", "dh0", "dc0", "workspace",
              "core_h0", "core_c0", "core_hT", "core_cT", "dcore_hT", "dcore_cT", "dcore_h0", "dcore_c0")
 FLAG_STATEFUL_CORE = 1
+
+
+class TimerStats(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("launches", ctypes.c_long), ("work", ctypes.c_double),
+                ("variant", ctypes.c_char * 96)]
 
 
 class IO(ctypes.Structure):
@@ -98,6 +103,7 @@ def load(path: str = LIB_PATH):
             "aaa_linear": (I, [I, I, I, P, P, P, P, P]),
             "aaa_timing_enable": (I, [I]),
             "aaa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
+            "aaa_timing_stats": (I, [I, ctypes.POINTER(TimerStats)]),
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
             "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
@@ -190,6 +196,15 @@ def timing_read(kind: int):
     ms, n = ctypes.c_double(), ctypes.c_long()
     check(load().aaa_timing_read(kind, ctypes.byref(ms), ctypes.byref(n)), "timing_read")
     return ms.value, n.value
+
+
+def timing_stats(kind: int) -> dict:
+    """Kernel class ``kind`` since the last read: device ms, launches, the
+    launches' algorithmic work (FLOP for classes 0-2, bytes for 3-4) as the
+    runtime accounts it, and the variant it dispatched."""
+    s = TimerStats()
+    check(load().aaa_timing_stats(kind, ctypes.byref(s)), "timing_stats")
+    return {"ms": s.total_ms, "launches": s.launches, "work": s.work, "variant": s.variant.decode()}
 
 
 def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None) -> None:

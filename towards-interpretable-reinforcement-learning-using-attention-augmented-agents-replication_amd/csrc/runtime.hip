@@ -306,10 +306,16 @@ static hipError_t stream_order(hipStream_t from, hipStream_t to) {
 }
 
 // ------------------------------------------------- optional kernel timing --
+// Per timer class: the HIP event pairs of each launch, the launches'
+// algorithmic work (FLOP for the MFMA classes, bytes for the HBM ones) and
+// the kernel variant dispatched -- so a benchmark reads the roofline inputs
+// from the library instead of re-deriving its dispatch rules.
 struct Timers {
   std::mutex mu;
   bool on = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[AAA_TIMER_N];
+  double work[AAA_TIMER_N] = {};
+  std::string variant[AAA_TIMER_N];
   std::vector<hipEvent_t> pool;
   hipEvent_t get() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
@@ -324,7 +330,9 @@ struct TimerScope {
   int kind;
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  TimerScope(int k, hipStream_t s) : kind(k), st(s) {
+  double work;
+  std::string variant;
+  TimerScope(int k, hipStream_t s, double w, std::string v) : kind(k), st(s), work(w), variant(std::move(v)) {
     std::lock_guard<std::mutex> lk(g_timers.mu);
     if (!g_timers.on) return;
     a = g_timers.get();
@@ -336,8 +344,25 @@ struct TimerScope {
     (void)hipEventRecord(b, st);
     std::lock_guard<std::mutex> lk(g_timers.mu);
     g_timers.pending[kind].emplace_back(a, b);
+    g_timers.work[kind] += work;
+    g_timers.variant[kind] = variant;
   }
 };
+
+static std::string strf(const char* fmt, ...) {
+  char buf[160];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  return buf;
+}
+
+// Algorithmic bytes per frame of the fused attention readout kernels (fp32):
+// forward reads the frame's O rows (128 ch) and writes its map and answer row;
+// backward reads O, the map and the answer grad, writes dO and dQ.
+static double attn_fwd_bytes(int P, int nq, int ans_ld) { return 4.0 * (128.0 * P + nq * P + ans_ld); }
+static double attn_bwd_bytes(int P, int nq) { return 4.0 * (2.0 * 128 * P + nq * P + 184.0 * nq + 72.0 * nq); }
 
 // --------------------------------------------------------- tile configs ---
 // fp32 uses the exact v_mfma_f32_32x32x2_f32; bf16 v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
@@ -565,7 +590,9 @@ static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const Ep
   const ConvGeo g = ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
   const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
-  TimerScope tim(AAA_TIMER_FWD_STEP, st);
+  TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728,
+                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d", std::is_same<T, float>::value ? "fp32" : "bf16",
+                      ftile));
   if (ftile == 7)
     HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
   else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring
@@ -767,7 +794,7 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                          Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
                          Wf(L.Gt) + (size_t)t * M * 512, M};
     const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
-    TimerScope tim(AAA_TIMER_FWD_STEP, st);
+    TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1152, strf("%s h-part step (x-part batched), K=1152, tile %d", std::is_same<T, float>::value ? "fp32" : "bf16", fwd_tile));
     const T* WpH = (const T*)(pk + L.k_WpH);
     const T* xh = Wt(L.XH) + (size_t)t * M * 192;
     hipError_t e;
@@ -858,7 +885,7 @@ static int forward_tail_stateful(const Layout& L, const aaa_io* io, hipStream_t 
     }
     // attention readout with this step's per-frame queries (basis logits in-kernel)
     {
-      TimerScope tim(AAA_TIMER_ATTN_FWD, st);
+      TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)B * attn_fwd_bytes(P, L.nq, L.ans_ld), "k_attn_fwd, per-frame query (stateful core)");
       HIPCHK(attn_fwd(Wf(L.Hs) + f0 * P * 128, io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
                       io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
                       Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
@@ -906,7 +933,7 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
   const float* Qc = (const float*)(pk + L.k_Q);
   HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
   {
-    TimerScope tim(AAA_TIMER_ATTN_FWD, st);
+    TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld), "k_attn_fwd, 1 WG per frame");
     HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
                     Wf(L.ans), L.ans_ld, st));
   }
@@ -1048,7 +1075,7 @@ static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* g
                            1728, xh_bytes};
     EpiStore<true> ep{gW, 1728, 512, 1728};
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics", CW::BI, CW::BJ, CW::BK, wgrad_splits(tiles, rows, CW::BK)));
     HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
     return AAA_OK;
   };
@@ -1064,7 +1091,7 @@ static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* g
                            1728, xh_bytes};
     EpiAtomicD ep{{gW, 1728, 512, 1728}};
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s);
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("LDS-DMA ring %dx%d BK%d, %d-deep", CW::BI, CW::BJ, CW::BK, NB));
     // split-K over pixels: about one resident wave of workgroups (fewer
     // passes of the output's atomics than the register path's ~1024)
     const int wgs = env_int("AAA_WGRAD_WGS", 256);
@@ -1181,7 +1208,7 @@ static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t
     // readout / softmax / logits backward with this step's queries; dQ gets
     // the logits path plus the answer row's copy of Q
     {
-      TimerScope tim(AAA_TIMER_ATTN_BWD, st);
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)B * attn_bwd_bytes(P, L.nq), "k_attn_bwd, per-frame query (stateful core)");
       HIPCHK(attn_bwd(Wf(L.Hs) + f0 * P * 128, io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
                       Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1));
     }
@@ -1319,7 +1346,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     // attention readout / softmax / logits backward, then the query MLP
     {
-      TimerScope tim(AAA_TIMER_ATTN_BWD, st);
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)F * attn_bwd_bytes(P, L.nq), "k_attn_bwd, 1 WG per frame");
       HIPCHK(attn_bwd(Wf(L.Hs), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
                       Wf(L.dO), Wf(L.dQp), st));
     }
@@ -1461,7 +1488,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
-      TimerScope tim(AAA_TIMER_BPTT_STEP, st);
+      TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608, strf("%s dh dgrad + fused gate bwd, K=4608, AAA_BPTT_TILE %d%s", std::is_same<T, float>::value ? "fp32" : "bf16", bwd_tile, g16 ? ", fp16 gates" : ""));
       auto step = [&](auto gtag) -> hipError_t {
         using GT = decltype(gtag);
         using EB = EpiConvLstmBwd<T, GT>;
@@ -1907,6 +1934,7 @@ const char* aaa_last_error(void) { return g_err.c_str(); }
 int aaa_timing_enable(int on) {
   std::lock_guard<std::mutex> lk(g_timers.mu);
   g_timers.on = on != 0;
+  for (double& w : g_timers.work) w = 0.0;
   for (auto& v : g_timers.pending) {
     for (auto& pr : v) { g_timers.pool.push_back(pr.first); g_timers.pool.push_back(pr.second); }
     v.clear();
@@ -1915,11 +1943,24 @@ int aaa_timing_enable(int on) {
 }
 
 int aaa_timing_read(int kind, double* total_ms, long* launches) {
-  if (kind < 0 || kind >= AAA_TIMER_N || !total_ms || !launches) return fail(AAA_E_ARG, "bad timer query");
+  if (!total_ms || !launches) return fail(AAA_E_ARG, "bad timer query");
+  aaa_timer_stats s;
+  const int rc = aaa_timing_stats(kind, &s);
+  *total_ms = s.total_ms;
+  *launches = s.launches;
+  return rc;
+}
+
+int aaa_timing_stats(int kind, aaa_timer_stats* out) {
+  if (kind < 0 || kind >= AAA_TIMER_N || !out) return fail(AAA_E_ARG, "bad timer query");
   std::vector<std::pair<hipEvent_t, hipEvent_t>> v;
+  memset(out, 0, sizeof *out);
   {
     std::lock_guard<std::mutex> lk(g_timers.mu);
     v.swap(g_timers.pending[kind]);
+    out->work = g_timers.work[kind];
+    snprintf(out->variant, sizeof out->variant, "%s", g_timers.variant[kind].c_str());
+    g_timers.work[kind] = 0.0;
   }
   double tot = 0.0;
   int rc = AAA_OK;
@@ -1933,8 +1974,8 @@ int aaa_timing_read(int kind, double* total_ms, long* launches) {
     std::lock_guard<std::mutex> lk(g_timers.mu);
     for (auto& pr : v) { g_timers.pool.push_back(pr.first); g_timers.pool.push_back(pr.second); }
   }
-  *total_ms = tot;
-  *launches = (long)v.size();
+  out->total_ms = tot;
+  out->launches = (long)v.size();
   return rc;
 }
 
@@ -2242,7 +2283,7 @@ int aaa_attn_fwd(int F, int h, int w, int nq, const float* O, const float* S, co
   if (r) return r;
   if (!O || !S || !Q || !attn || !answer) return fail(AAA_E_ARG, "attn_fwd: O/S/Q/attn/answer must be set");
   if (!aligned16(O) || !aligned16(S)) return fail(AAA_E_ALIGN, "O and S must be 16-byte aligned");
-  TimerScope tim(AAA_TIMER_ATTN_FWD, stream);
+  TimerScope tim(AAA_TIMER_ATTN_FWD, stream, (double)F * attn_fwd_bytes(h * w, nq, 256 * nq + 2), "k_attn_fwd (aaa_attn_fwd)");
   HIPCHK(attn_fwd(O, S, Q, nullptr, prev_reward, prev_action, F, h * w, nq, attn, answer, 256 * nq + 2, stream,
                   q_stride));
   return AAA_OK;
@@ -2255,7 +2296,7 @@ int aaa_attn_bwd(int F, int h, int w, int nq, const float* O, const float* S, co
   if (!O || !S || !Q || !attn || !danswer || !dO || !dQ)
     return fail(AAA_E_ARG, "attn_bwd: O/S/Q/attn/danswer/dO/dQ must be set");
   if (!aligned16(O) || !aligned16(S) || !aligned16(dO)) return fail(AAA_E_ALIGN, "O, S, dO must be 16-byte aligned");
-  TimerScope tim(AAA_TIMER_ATTN_BWD, stream);
+  TimerScope tim(AAA_TIMER_ATTN_BWD, stream, (double)F * attn_bwd_bytes(h * w, nq), "k_attn_bwd (aaa_attn_bwd)");
   HIPCHK(attn_bwd(O, S, Q, attn, danswer, 256 * nq + 2, F, h * w, nq, dO, dQ, stream, q_stride, 1));
   return AAA_OK;
 }

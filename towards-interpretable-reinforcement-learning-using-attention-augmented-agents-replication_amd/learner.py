@@ -42,25 +42,60 @@ class Learner:
         self.bounds = bucket_bounds(r.offsets, r.n_params)
         if self.world > 1:   # identical weights on every rank (they are seeded, but be explicit)
             dist.broadcast(self.flat, src=0, group=group)
+            self.comm = torch.cuda.Stream(self.device)   # the gradient all-reduces (RCCL) run here
 
-    def step(self, frames, dlogits, dvalues, overlap: bool = True):
+    def step(self, frames, dlogits, dvalues, overlap: bool = True, comm_timing: bool = False):
+        """One learner iteration; returns (logits, values).  With N > 1 ranks the
+        gradient buckets are SUM-all-reduced over RCCL on a side stream, each
+        issued as soon as its backward phase is enqueued (the side stream waits
+        on an event recorded after that phase), so HEAD's all-reduce overlaps
+        the ConvLSTM BPTT and CORE's the vision backward.  ``comm_timing``
+        records per-bucket events; read them with comm_stats() after a sync."""
         r = self.runner
         r.pack(self.flat, self.packed)
         logits, values, _, _, _ = r.forward(self.flat, self.packed, self.basis, frames, self.ws, want_attn=False)
         if self.world == 1:
             r.backward(self.flat, self.packed, self.basis, frames, self.ws, dlogits, dvalues, grads=self.grads)
             return logits, values
-        works = []
-        for phase, bnd in zip((N.BWD_HEAD, N.BWD_CORE, N.BWD_VISION), self.bounds):
+        main = torch.cuda.current_stream(self.device)
+        self._events = [] if comm_timing else None
+        phases = list(zip((N.BWD_HEAD, N.BWD_CORE, N.BWD_VISION), self.bounds))
+        for i, (phase, bnd) in enumerate(phases):
             r.backward(self.flat, self.packed, self.basis, frames, self.ws, dlogits, dvalues, grads=self.grads,
                        phases=phase)
-            if overlap:
-                works += allreduce_buckets(self.grads, [bnd], self.group)
-        if not overlap:
-            works = allreduce_buckets(self.grads, self.bounds, self.group)
-        for w in works:
-            w.wait()
+            if overlap or i == len(phases) - 1:
+                self._allreduce(main, [bnd] if overlap else self.bounds, comm_timing)
+        if comm_timing:
+            self._compute_done = torch.cuda.Event(enable_timing=True)
+            self._compute_done.record(main)
+        main.wait_stream(self.comm)
         return logits, values
+
+    def _allreduce(self, main, bounds, timing):
+        ready = torch.cuda.Event(enable_timing=timing)
+        ready.record(main)                          # everything the phase enqueued
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ready)
+            for lo, hi in bounds:
+                t0 = torch.cuda.Event(enable_timing=True) if timing else None
+                if timing:
+                    t0.record(self.comm)
+                allreduce_buckets(self.grads, [(lo, hi)], self.group, async_op=False)
+                if timing:
+                    t1 = torch.cuda.Event(enable_timing=True)
+                    t1.record(self.comm)
+                    self._events.append((lo, hi, ready, t0, t1))
+
+    def comm_stats(self):
+        """Per-bucket all-reduce time (ms) and the communication left exposed
+        after the last backward phase (ms) of the last timed step()."""
+        buckets = []
+        for (lo, hi, ready, t0, t1), name in zip(self._events, ("HEAD", "CORE", "VISION")):
+            buckets.append({"bucket": name, "bytes": 4 * (hi - lo), "allreduce_ms": round(t0.elapsed_time(t1), 4),
+                            "queued_after_phase_ms": round(ready.elapsed_time(t0), 4)})
+        last = self._events[-1][4]
+        exposed = max(0.0, self._compute_done.elapsed_time(last))
+        return {"buckets": buckets, "exposed_ms": round(exposed, 4)}
 
     def optimizer_step(self):
         """Adam (lr=1e-3, torch defaults; main_mp.py:92) on the flat params, one launch."""

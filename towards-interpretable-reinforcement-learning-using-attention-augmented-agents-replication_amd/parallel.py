@@ -38,13 +38,16 @@ def allreduce_buckets(grads: torch.Tensor, bounds, group=None, async_op: bool = 
     return works
 
 
-def init_from_env(backend: str = "nccl"):
-    """torch.distributed init from torchrun's env (RANK/WORLD_SIZE/MASTER_*)."""
+def init_from_env(backend: str = "nccl", device=None):
+    """torch.distributed init from torchrun's env (RANK/WORLD_SIZE/MASTER_*).
+    Call torch.cuda.set_device(LOCAL_RANK) first and pass that ``device``: RCCL
+    then binds the communicator to this rank's GPU eagerly."""
     import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend=backend)
+        kw = {"device_id": device} if device is not None and backend == "nccl" else {}
+        dist.init_process_group(backend=backend, **kw)
     return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
