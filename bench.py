@@ -164,6 +164,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--frames", default="u8", choices=["u8", "fp32"],
+                    help="frame dtype in HBM: u8 (the environment's observation, cast in-kernel) or fp32 "
+                         "(cast on the host as main_mp.py:53 does)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B check only: time the steps without the library's per-kernel HIP events")
     args = ap.parse_args()
@@ -185,8 +188,10 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     B, T, H, W, nq, dtype = cfg["B"], cfg["T"], cfg["H"], cfg["W"], cfg["nq"], cfg["dtype"]
     A = 18
-    learner = Learner(B, T, H, W, nq, A, dtype, dev)
-    frames = torch.from_numpy(detinit.frames_u8(1234 + rank, (T, B, H, W, 3)).astype(np.float32)).to(dev)
+    learner = Learner(B, T, H, W, nq, A, dtype, dev, frames_u8=args.frames == "u8")
+    frames = torch.from_numpy(detinit.frames_u8(1234 + rank, (T, B, H, W, 3))).to(dev)
+    if args.frames == "fp32":
+        frames = frames.float()
     dl = torch.from_numpy(detinit.cotangent(2 + 7 * rank, (T, B, A))).to(dev)
     dv = torch.from_numpy(detinit.cotangent(3 + 7 * rank, (T, B, A))).to(dev)
     log(f"rank {rank}/{world} {cfg['desc']} workspace {learner.runner.ws_bytes / 2**20:.0f} MiB")
@@ -253,8 +258,10 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": dtype,
-        "data": "synthetic: seeded uint8 frames cast to fp32 (raw 0..255), seeded uniform weights of the reference "
-                "architecture, uniform[-1,1) logits/values cotangents",
+        "data": ("synthetic: seeded uint8 frames resident in HBM, cast to fp32 (raw 0..255) inside the first "
+                 "kernel" if args.frames == "u8" else "synthetic: seeded uint8 frames cast to fp32 (raw 0..255) on "
+                 "the host") + ", seeded uniform weights of the reference architecture, uniform[-1,1) logits/values "
+                 "cotangents",
         "config": {"workload": cfg["desc"], "global_batch": B * world, "seq_len": T, "frame": f"{H}x{W}",
                    "heads": nq, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": names[dom], "variant": d["variant"], "achieved": round(achieved, 2),

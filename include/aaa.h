@@ -27,8 +27,9 @@
  *    each tensor in its PyTorch (contiguous) layout.  aaa_param_layout()
  *    returns the offsets.  nq != 4 uses the generalised query / answer widths
  *    (query 256->128->72nq->72nq, answer 256nq+2).
- *  - frames: (T, B, H, W, 3) fp32 NHWC raw pixels (main_mp.py:53 casts the
- *    uint8 observation to float without normalisation).
+ *  - frames: (T, B, H, W, 3) NHWC raw pixels, fp32 (main_mp.py:53 casts the
+ *    uint8 observation to float without normalisation) or the uint8
+ *    observation itself (AAA_FLAG_FRAMES_U8).
  *  - basis: (h, w, 64) fp32 spatial basis (SpatialBasis.S, attention.py:226).
  *  - logits, values: (T, B, A) fp32; attn: (T, B, h, w, nq) fp32 softmax maps.
  *  - prev_reward / prev_action: (T, B) fp32 or NULL (zeros, :303-312).
@@ -77,13 +78,17 @@ typedef struct aaa_cfg {
  * carried across steps (and across calls through io->core_*).  Off, the
  * reference's reachable path: zero query input, zero-state LSTMCell (Q1). */
 #define AAA_FLAG_STATEFUL_CORE 1
+/* io->frames holds uint8 pixels (T, B, H, W, 3) -- the environment's
+ * observation (main_mp.py:49-53 casts it to float on the host); the cast is
+ * fused into the kernel that lays the frames out for conv1. */
+#define AAA_FLAG_FRAMES_U8 2
 
 typedef struct aaa_io {
   /* inputs */
   const float* params;       /* flat fp32 params (state_dict order)            */
   const void* packed;        /* aaa_pack_weights output                        */
   const float* basis;        /* (h, w, 64)                                     */
-  const float* frames;       /* (T, B, H, W, 3)                                */
+  const void* frames;        /* (T, B, H, W, 3) fp32, or uint8 with AAA_FLAG_FRAMES_U8 */
   const float* prev_reward;  /* (T, B) or NULL                                 */
   const float* prev_action;  /* (T, B) or NULL                                 */
   const float* h0;           /* (B, h, w, 128) or NULL                         */

@@ -329,3 +329,22 @@ def test_repeat_is_deterministic_enough(cuda):
     assert torch.equal(a[0], b[0])
     for n in a[3]:
         assert rel_err(a[3][n].numpy(), b[3][n].numpy()) < 1e-5, n
+
+
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_uint8_frames_match_fp32_frames(cuda, conv_dtype):
+    """The environment's uint8 observation fed as is (AAA_FLAG_FRAMES_U8, cast
+    in the frame-layout kernel) gives the fp32-frame results (the cast is exact)."""
+    T, B = 3, 2
+    X8 = torch.from_numpy(detinit.frames_u8(1234, (T, B, 84, 84, 3))).to(cuda)
+    Gl, Gv = (g.to(cuda) for g in _cot(T, B))
+    outs = []
+    for X in (X8, X8.float()):
+        ag = _agent(cuda, conv_dtype=conv_dtype)
+        ag.reset()
+        lg, vl, at = ag.unroll(X)
+        ((lg * Gl).sum() + (vl * Gv).sum()).backward()
+        outs.append((lg.detach(), at.detach(), _grads(ag)))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for n in outs[0][2]:
+        assert rel_err(outs[0][2][n].numpy(), outs[1][2][n].numpy()) < 1e-5, n

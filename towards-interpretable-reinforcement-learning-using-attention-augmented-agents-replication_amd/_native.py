@@ -41,6 +41,7 @@ IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action"
              "grads", "dh0", "dc0", "workspace",
              "core_h0", "core_c0", "core_hT", "core_cT", "dcore_hT", "dcore_cT", "dcore_h0", "dcore_c0")
 FLAG_STATEFUL_CORE = 1
+FLAG_FRAMES_U8 = 2
 
 
 class TimerStats(ctypes.Structure):

@@ -413,7 +413,8 @@ class Agent(nn.Module):
                 raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
                                    f"call agent.to({X.device})")
         stateful = self.stateful_core or self.prev_hidden is not None
-        runner = self._runner(B, T, H, W, X.device, stateful)
+        u8 = X.dtype == torch.uint8      # the environment's observation: cast in-kernel (AAA_FLAG_FRAMES_U8)
+        runner = self._runner(B, T, H, W, X.device, stateful, u8)
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
         cell = self.vision.vision_lstm
         # prev_hidden holds the reference's (B, 128, w, h) tensors (attention.py:125); the
@@ -433,7 +434,7 @@ class Agent(nn.Module):
             for name, v in (("prev_output", ch0), ("prev_hidden", cc0)):
                 if v is not None and tuple(v.shape) != (B, self.hidden_size):
                     raise RuntimeError(f"{name} has shape {tuple(v.shape)}, expected {(B, self.hidden_size)}")
-        Xf = X.float().contiguous()
+        Xf = X.contiguous() if u8 else X.float().contiguous()
         flat, packed = self._packed_params(runner, params)
         logits, values, attn, hT, cT, chT, ccT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0,
                                                                  ch0, cc0, *params)
@@ -462,12 +463,12 @@ class Agent(nn.Module):
         runner._pack_cache = (key, flat, packed)
         return flat, packed
 
-    def _runner(self, B, T, H, W, device, stateful=False):
-        key = (B, T, H, W, str(device), self.conv_dtype, bool(stateful))
+    def _runner(self, B, T, H, W, device, stateful=False, frames_u8=False):
+        key = (B, T, H, W, str(device), self.conv_dtype, bool(stateful), bool(frames_u8))
         r = self._runners.get(key)
         if r is None:
             r = UnrollRunner(B, T, H, W, self.num_queries, self.num_actions, self.conv_dtype, device,
-                             stateful_core=stateful)
+                             stateful_core=stateful, frames_u8=frames_u8)
             self._runners[key] = r
         return r
 

@@ -391,8 +391,18 @@ __device__ __forceinline__ void epilogue_prefetch(const EP& ep, int i0, int j0, 
 // lanes on consecutive row groups of ONE column, so the epilogue's global
 // loads/stores (gate activations, cell state, outputs: all [pixel][channel])
 // are contiguous per column instead of one 16-B access per lane at a 2 KB
-// stride, and all waves share it.  ``smem`` must hold WK*BJ*(BI+4) floats.
-// Tile columns >= jn are skipped (the halo conv's tiles end at a frame edge).
+// stride, and all waves share it.  Tiles too wide for LDS (the fp32 image of a
+// 256x256 tile is 266 KB) go through in EC column chunks of BJ/EC columns: the
+// waves owning a chunk's columns store them, all threads process the chunk's
+// items (item order is column-major, so a chunk is a contiguous run of q).
+// ``smem`` must hold WK*(BJ/EC)*(BI+4) floats.  Tile columns >= jn are skipped
+// (the halo conv's tiles end at a frame edge).
+template <class C>
+constexpr int epi_chunks() {
+  constexpr long full = (long)C::WK * C::BJ * (C::BI + 4) * 4;
+  return full <= 160L * 1024 ? 1 : (full / 2 <= 160L * 1024 ? 2 : 4);
+}
+
 template <class C, class EP, class PL, typename T, int MI, int MJ>
 __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32x16 (&acc)[MI][MJ], int i0, int j0,
                                                 int jn, int tj, typename PL::PreT (&pre)[PL::PD]) {
@@ -400,43 +410,52 @@ __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32
   constexpr int WTI = BI / WI, WTJ = BJ / WJ;
   constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
   constexpr int G4 = PL::G4, NG = PL::NG, NPT = PL::NPT, PD = PL::PD;
+  constexpr int EC = epi_chunks<C>(), BJC = BJ / EC, QC = NPT / EC;
+  static_assert(EC == 1 || (BJC % 32 == 0 && (G4 * BJC) % C::NT == 0), "column chunks: whole items per thread");
   constexpr bool PRE = PL::PRE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wk = wave / (WI * WJ), wr = wave - wk * (WI * WJ);
   const int wi = wr / WJ, wj = wr - (wr / WJ) * WJ;
   const int r32 = lane & 31, h = lane >> 5;
   float* E = reinterpret_cast<float*>(smem);
-  barrier_lds();                              // every wave is done reading the last stage
-#pragma unroll
-  for (int a = 0; a < MI; ++a)
-#pragma unroll
-    for (int b = 0; b < MJ; ++b)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i = wi * WTI + a * 32 + 8 * g + 4 * h;
-        const int j = wj * WTJ + b * 32 + r32;
-        *reinterpret_cast<f32x4*>(E + (wk * BJ + j) * ELD + i) =
-            f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
-      }
-  __syncthreads();
   constexpr bool ACC = has_acc<EP>::value && PRE && C::NT % G4 == 0;
   typename acc_of<EP, ACC>::type eacc{};
 #pragma unroll
-  for (int q = 0; q < NPT; ++q) {
-    const int c = q * C::NT + (int)threadIdx.x;
-    if ((NG % C::NT == 0 || c < NG) && c / G4 < jn) {
-      const int r4 = c % G4, j = c / G4;
-      f32x4 v = *reinterpret_cast<const f32x4*>(E + j * ELD + 4 * r4);
+  for (int ec = 0; ec < EC; ++ec) {
+    if (ec == 0) barrier_lds();                 // every wave is done reading the last stage
+    else __syncthreads();                       // every thread is done reading the last chunk
 #pragma unroll
-      for (int w = 1; w < WK; ++w) {
-        const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJ + j) * ELD + 4 * r4);
-        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+      for (int b = 0; b < MJ; ++b) {
+        const int jb = wj * WTJ + b * 32;       // the fragment's first column (chunk-uniform)
+        if (EC > 1 && jb / BJC != ec) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i = wi * WTI + a * 32 + 8 * g + 4 * h;
+          const int j = jb - ec * BJC + r32;
+          *reinterpret_cast<f32x4*>(E + (wk * BJC + j) * ELD + i) =
+              f32x4{acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]};
+        }
       }
-      if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD], &eacc);
-      else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD]);
-      else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
+    __syncthreads();
+#pragma unroll
+    for (int q = ec * QC; q < (ec + 1) * QC; ++q) {
+      const int c = q * C::NT + (int)threadIdx.x;
+      if ((NG % C::NT == 0 || c < NG) && c / G4 < jn) {
+        const int r4 = c % G4, j = c / G4, jl = j - ec * BJC;
+        f32x4 v = *reinterpret_cast<const f32x4*>(E + jl * ELD + 4 * r4);
+#pragma unroll
+        for (int w = 1; w < WK; ++w) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(E + (w * BJC + jl) * ELD + 4 * r4);
+          v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+        }
+        if constexpr (ACC) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD], &eacc);
+        else if constexpr (PRE) ep.finish(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3], pre[q % PD]);
+        else ep(i0 + 4 * r4, j0 + j, v[0], v[1], v[2], v[3]);
+      }
+      if (q + PD < NPT) epilogue_load<C, EP, PL>(ep, i0, j0, jn, q + PD, pre);
     }
-    if (q + PD < NPT) epilogue_load<C, EP, PL>(ep, i0, j0, jn, q + PD, pre);
   }
   if constexpr (ACC) {
     __syncthreads();                          // every thread is done reading E
@@ -465,7 +484,8 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   constexpr int ELD = BI + 4;                 // epilogue tile pitch (pad: conflict-free b128 writes)
   constexpr bool DIRECT = is_direct<EP>::value;
   static_assert(!DIRECT || WK == 1, "direct epilogue: no in-WG split-K");
-  constexpr int EPI_T = DIRECT ? 0 : (int)((WK * BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
+  constexpr int EPI_T =
+      DIRECT ? 0 : (int)((WK * (BJ / epi_chunks<C>()) * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
   __shared__ __attribute__((aligned(16))) T smem[NBUF * STG > EPI_T ? NBUF * STG : EPI_T];
   static_assert(!has_acc<EP>::value || C::NT * 16 * sizeof(float) <= sizeof(smem),
                 "accumulator reduction does not fit in LDS");

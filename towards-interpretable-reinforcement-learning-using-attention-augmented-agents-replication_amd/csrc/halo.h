@@ -18,7 +18,7 @@
 //
 // LDS images are lane-linear (LDS-DMA writes base + lane*16); the XOR swizzle
 // that keeps the fragment reads conflict-free is applied on the source side:
-// physical 16-B slot pc of halo row R holds logical chunk pc ^ (R & (RS-1)),
+// physical 16-B slot pc of halo row R holds logical chunk pc ^ halo_swz(R),
 // and the weight tile uses lds_swz as in glds.h.  Halo rows outside the frame
 // (the zero border) and beyond the tile's frames read through the buffer
 // descriptor's range check and land as zeros.
@@ -47,8 +47,13 @@ struct HaloParams {
   int transposed;       // dgrad gather
 };
 
+// The halo rows a ds_read_b128 lane group (16 lanes, one 256-B bank row) reads
+// are 16 mostly-consecutive pixels; with 128-B bf16 rows two of them share a
+// bank row, so the XOR must rotate per PAIR of rows ((R/2) & 7, i.e. lds_swz)
+// for the 16 reads to land on 16 distinct 16-B slots.  (R & 7 leaves every
+// group at least 2-way conflicted: 50.7 % SQ_LDS_BANK_CONFLICT at C3.)
 template <int RS>
-__device__ __forceinline__ int halo_swz(int row) { return row & (RS - 1); }
+__device__ __forceinline__ int halo_swz(int row) { return lds_swz<RS>(row); }
 
 template <class C, class EP, int NBUF = 3>
 __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, TileMap tm) {
@@ -64,7 +69,7 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
   static_assert(MI >= 1 && MJ >= 1 && CK % 16 == 0, "tile shape");
   static_assert((BI * RS) % NT == 0 && (C::HMAX * RS) % NT == 0, "every wave must issue the same number of DMA pieces");
   constexpr int ELD = BI + 4;
-  constexpr int EPI_T = (int)((BJ * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
+  constexpr int EPI_T = (int)((BJ / epi_chunks<C>() * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
   constexpr int RING = NBUF * AEL + 2 * HEL;
   __shared__ __attribute__((aligned(16))) T smem[RING > EPI_T ? RING : EPI_T];
   static_assert(!has_acc<EP>::value || NT * 16 * sizeof(float) <= sizeof(smem), "accumulator reduction");

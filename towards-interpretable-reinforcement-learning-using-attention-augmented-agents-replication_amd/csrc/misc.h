@@ -58,7 +58,7 @@ hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T
 template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);
-template <typename T> hipError_t frames_rgbx(int F, int H, int W, const float* x, T* y, hipStream_t st);
+template <typename T, typename TI> hipError_t frames_rgbx(int F, int H, int W, const TI* x, T* y, hipStream_t st);
 template <typename T> hipError_t pack_conv2_classes(const float* w2, T* dst, hipStream_t st);
 template <typename T> hipError_t pack_conv1_rgbx(const float* w, T* dst, hipStream_t st);
 hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st);

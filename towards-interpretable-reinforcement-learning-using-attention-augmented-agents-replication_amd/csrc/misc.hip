@@ -510,14 +510,15 @@ __global__ void k_pack_conv(const float* __restrict__ w, int Cout, int Cin, int 
   }
 }
 
-// Frames (F,H,W,3) -> (F,H+2,W+2,4): a zero 4th channel (conv1's gather is
+// Frames (F,H,W,3) fp32 or uint8 (the environment's observation, cast here
+// instead of on the host as main_mp.py:53 does) -> (F,H+2,W+2,4): a zero 4th channel (conv1's gather is
 // 16-byte vectors instead of scalar loads) and conv1's one-pixel zero padding
 // stored in the image, so every tap of the conv reads in-bounds memory -- a
 // bf16 16-byte chunk (two adjacent taps x 4 channels) never straddles the
 // image border.  Raw pixels 0..255 are exact in bf16; other values are
 // rounded exactly where the bf16 oracle rounds conv1's input.
-template <typename T>
-__global__ void k_frames_rgbx(int F, int H, int W, const float* __restrict__ x, T* __restrict__ y) {
+template <typename T, typename TI>
+__global__ void k_frames_rgbx(int F, int H, int W, const TI* __restrict__ x, T* __restrict__ y) {
   const int Hp = H + 2, Wp = W + 2;
   const long n = (long)F * Hp * Wp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -526,8 +527,8 @@ __global__ void k_frames_rgbx(int F, int H, int W, const float* __restrict__ x, 
     const int iy = py - 1, ix = px - 1;
     float v0 = 0.f, v1 = 0.f, v2 = 0.f;
     if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      const float* s = x + (((long)f * H + iy) * W + ix) * 3;
-      v0 = s[0]; v1 = s[1]; v2 = s[2];
+      const TI* s = x + (((long)f * H + iy) * W + ix) * 3;
+      v0 = (float)s[0]; v1 = (float)s[1]; v2 = (float)s[2];
     }
     store4(y + i * 4, v0, v1, v2, 0.f);
   }
@@ -938,9 +939,9 @@ hipError_t unpack_f32(const F32Unpack& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename T>
-hipError_t frames_rgbx(int F, int H, int W, const float* x, T* y, hipStream_t st) {
-  hipLaunchKernelGGL(k_frames_rgbx<T>, dim3(nblk((long)F * (H + 2) * (W + 2))), dim3(256), 0, st, F, H, W, x, y);
+template <typename T, typename TI>
+hipError_t frames_rgbx(int F, int H, int W, const TI* x, T* y, hipStream_t st) {
+  hipLaunchKernelGGL((k_frames_rgbx<T, TI>), dim3(nblk((long)F * (H + 2) * (W + 2))), dim3(256), 0, st, F, H, W, x, y);
   return hipGetLastError();
 }
 template <typename T>
@@ -967,8 +968,10 @@ template hipError_t gate_bwd_last<float, _Float16>(int, int, const float*, const
                                                    const float*, const float*, float*, float*, float*, hipStream_t);
 template hipError_t gate_bwd_last<__bf16, _Float16>(int, int, const float*, const float*, const _Float16*,
                                                     const float*, const float*, float*, __bf16*, float*, hipStream_t);
-template hipError_t frames_rgbx<float>(int, int, int, const float*, float*, hipStream_t);
-template hipError_t frames_rgbx<__bf16>(int, int, int, const float*, __bf16*, hipStream_t);
+template hipError_t frames_rgbx<float, float>(int, int, int, const float*, float*, hipStream_t);
+template hipError_t frames_rgbx<__bf16, float>(int, int, int, const float*, __bf16*, hipStream_t);
+template hipError_t frames_rgbx<float, uint8_t>(int, int, int, const uint8_t*, float*, hipStream_t);
+template hipError_t frames_rgbx<__bf16, uint8_t>(int, int, int, const uint8_t*, __bf16*, hipStream_t);
 template hipError_t pack_conv2_classes<float>(const float*, float*, hipStream_t);
 template hipError_t pack_conv2_classes<__bf16>(const float*, __bf16*, hipStream_t);
 template hipError_t pack_conv1_rgbx<float>(const float*, float*, hipStream_t);

@@ -67,6 +67,7 @@ enum PIdx {
 struct Layout {
   int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
   int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
+  int fu8;  // frames are uint8 (AAA_FLAG_FRAMES_U8)
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
@@ -88,8 +89,9 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   if (c->nq != 4 && c->nq != 8) return fail(AAA_E_ARG, "nq must be 4 or 8 (got %d)", c->nq);
   if (c->A < 1 || c->A > 256) return fail(AAA_E_ARG, "A out of range (%d)", c->A);
   if (c->dtype != AAA_F32 && c->dtype != AAA_BF16) return fail(AAA_E_ARG, "bad dtype %d", c->dtype);
-  if (c->flags & ~AAA_FLAG_STATEFUL_CORE) return fail(AAA_E_ARG, "unknown flags 0x%x", c->flags);
+  if (c->flags & ~(AAA_FLAG_STATEFUL_CORE | AAA_FLAG_FRAMES_U8)) return fail(AAA_E_ARG, "unknown flags 0x%x", c->flags);
   L.sc = (c->flags & AAA_FLAG_STATEFUL_CORE) != 0;
+  L.fu8 = (c->flags & AAA_FLAG_FRAMES_U8) != 0;
   L.B = c->B; L.T = c->T; L.F = c->B * c->T; L.H = c->H; L.W = c->W;
   L.H1 = conv_out(c->H, 8, 4, 1); L.W1 = conv_out(c->W, 8, 4, 1);
   L.h = conv_out(L.H1, 4, 2, 2); L.w = conv_out(L.W1, 4, 2, 2);
@@ -647,13 +649,14 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
 // activation in between.  Packed conv weights at L.k_Wp1 / L.k_Wp2, biases
 // from the flat params (state_dict order: the vision tensors come first).
 template <typename T, typename OT>
-static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float* prm, const float* frames, T* Xp, T* Y1,
+static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1,
                       OT* out, int out_ld, hipStream_t st) {
   using C = CfgFor<T>;
   constexpr int NT = C::NT;
   const int P = L.P;
   {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
-    HIPCHK(frames_rgbx<T>(F, L.H, L.W, frames, Xp, st));
+    if (L.fu8) HIPCHK((frames_rgbx<T, uint8_t>(F, L.H, L.W, (const uint8_t*)frames, Xp, st)));
+    else HIPCHK((frames_rgbx<T, float>(F, L.H, L.W, (const float*)frames, Xp, st)));
     // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
     constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
     using CP = GemmCfg<T, 32, 128, BKc, 1, 4>;
@@ -686,11 +689,12 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
 }
 
 template <typename T, typename OT>
-static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const float* frames, T* Xp, T* Y1,
+static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1,
                       OT* out, int out_ld, hipStream_t st) {
   for (int f0 = 0; f0 < F; f0 += L.fchunk) {   // descriptor-sized frame chunks (check_ranges)
     const int n = std::min(L.fchunk, F - f0);
-    const int rc = vision_fwd_chunk<T, OT>(L, n, pk, prm, frames + (size_t)f0 * L.H * L.W * 3,
+    const int rc = vision_fwd_chunk<T, OT>(L, n, pk, prm,
+                                           (const char*)frames + (size_t)f0 * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
                                            Xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, Y1 + (size_t)f0 * L.P1 * 32,
                                            out + (size_t)f0 * L.P * out_ld, out_ld, st);
     if (rc) return rc;

@@ -23,8 +23,9 @@ from .runtime import UnrollRunner
 
 class Learner:
     def __init__(self, B: int, T: int, H: int = 84, W: int = 84, nq: int = 4, A: int = 18,
-                 dtype: str = "fp32", device=None, seed: int = 0, group=None, lr: float = 1e-3):
-        self.runner = r = UnrollRunner(B, T, H, W, nq, A, dtype, device)
+                 dtype: str = "fp32", device=None, seed: int = 0, group=None, lr: float = 1e-3,
+                 frames_u8: bool = False):
+        self.runner = r = UnrollRunner(B, T, H, W, nq, A, dtype, device, frames_u8=frames_u8)
         self.device = r.device
         params = detinit.deterministic_params(seed, A, nq)
         self.flat = torch.from_numpy(np.concatenate([v.reshape(-1) for v in params.values()])).to(self.device)

@@ -6,7 +6,8 @@
 test_model.py:42-73 run unchanged with it.  What changes underneath:
 
 * the observation goes to the GPU as uint8 (1/4 of the float bytes the
-  reference copies at main_mp.py:53) and is cast there;
+  reference copies at main_mp.py:53) and is cast inside the kernel that lays
+  the frames out for conv1 (AAA_FLAG_FRAMES_U8);
 * the agent step is the HIP forward (``Agent.forward``, T=1), whose packed
   weights are cached between parameter updates (``Agent._packed_params``);
 * softmax, the Categorical draw and its log-prob are one kernel
@@ -118,9 +119,9 @@ class Policy(nn.Module):
                 buf.copy_(src)
                 x = buf.to(dev, non_blocking=True)
                 done.record(torch.cuda.current_stream(dev))
-                return x.float().unsqueeze(0)
+                return x.unsqueeze(0)           # uint8: cast inside the frame-layout kernel
             x = src.to(dev)
-        return x.float().unsqueeze(0)
+        return (x if x.dtype == torch.uint8 else x.float()).unsqueeze(0)
 
     def act(self, observation, ts: int = 0):
         """One step without a host sync: returns (action int32 (1,), log_prob (1,)) on the device."""
@@ -160,7 +161,8 @@ class GraphActor:
         if dev.type != "cuda":
             raise RuntimeError("GraphActor needs the agent on the gfx950 device (there is no CPU fallback)")
         self.device, self.B, self.H, self.W = dev, B, H, W
-        self.runner = r = UnrollRunner(B, 1, H, W, agent.num_queries, agent.num_actions, agent.conv_dtype, dev)
+        self.runner = r = UnrollRunner(B, 1, H, W, agent.num_queries, agent.num_actions, agent.conv_dtype, dev,
+                                       frames_u8=True)
         self.S = agent._basis_for(r.h, r.w, H, W, dev)
         self.params = list(agent.parameters())
         self.flat = torch.empty(r.n_params, device=dev)
@@ -188,7 +190,7 @@ class GraphActor:
 
     def _body(self):
         r = self.runner
-        X = self.frame_u8.float()
+        X = self.frame_u8                  # uint8, cast in-kernel (AAA_FLAG_FRAMES_U8)
         ws = r.new_workspace()
         logits, values, attn, hT, cT = r.forward(self.flat, self.packed, self.S, X, ws, h0=self.h, c0=self.c,
                                                  want_attn=True, want_state=True)

@@ -15,7 +15,7 @@ from . import _native as N
 
 class UnrollRunner:
     def __init__(self, B: int, T: int, H: int, W: int, nq: int = 4, A: int = 18,
-                 dtype: str = "fp32", device=None, stateful_core: bool = False):
+                 dtype: str = "fp32", device=None, stateful_core: bool = False, frames_u8: bool = False):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
         self.lib = N.load()
@@ -23,8 +23,9 @@ class UnrollRunner:
         if self.device.type != "cuda":
             raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
         self.stateful_core = bool(stateful_core)
+        self.frames_u8 = bool(frames_u8)
         self.cfg = N.Cfg(B, T, H, W, nq, A, N.BF16 if dtype == "bf16" else N.F32,
-                         N.FLAG_STATEFUL_CORE if stateful_core else 0)
+                         (N.FLAG_STATEFUL_CORE if stateful_core else 0) | (N.FLAG_FRAMES_U8 if frames_u8 else 0))
         self.B, self.T, self.H, self.W, self.nq, self.A, self.dtype = B, T, H, W, nq, A, dtype
         self.h, self.w = N.grid(H, W)
         self.P = self.h * self.w
@@ -114,8 +115,9 @@ class UnrollRunner:
 
     def _check_frames(self, frames):
         exp = (self.T, self.B, self.H, self.W, 3)
-        if tuple(frames.shape) != exp or frames.dtype != torch.float32 or not frames.is_contiguous():
-            raise ValueError(f"frames must be contiguous fp32 {exp}, got {tuple(frames.shape)} {frames.dtype}")
+        dt = torch.uint8 if self.frames_u8 else torch.float32
+        if tuple(frames.shape) != exp or frames.dtype != dt or not frames.is_contiguous():
+            raise ValueError(f"frames must be contiguous {dt} {exp}, got {tuple(frames.shape)} {frames.dtype}")
         if frames.device != self.device and frames.device.type != "cuda":
             raise RuntimeError("frames must be on the GPU")
 
