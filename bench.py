@@ -139,6 +139,40 @@ def cpu_baseline(cfg):
     return out
 
 
+def dropin_api(cfg, dev, frames, dl, dv, steps, flat):
+    """The same iteration through the public drop-in API (what a reference user
+    runs): ``attention.Agent.unroll`` -> loss -> ``loss.backward()`` into the
+    parameters' ``.grad`` (autograd Function, per-call workspace, weight
+    re-pack only when a parameter changed), timed like the main line."""
+    import torch
+    import attention
+    B, T, H, W, nq = cfg["B"], cfg["T"], cfg["H"], cfg["W"], cfg["nq"]
+    h, w = (((H + 2 - 8) // 4 + 1) + 4 - 4) // 2 + 1, (((W + 2 - 8) // 4 + 1) + 4 - 4) // 2 + 1
+    agent = attention.Agent(18, num_queries=nq, grid=(h, w), conv_dtype=cfg["dtype"]).to(dev)
+    with torch.no_grad():
+        off = 0
+        for p in agent.parameters():
+            p.copy_(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+
+    def it():
+        agent.reset()
+        agent.zero_grad(set_to_none=True)
+        lg, vl, _ = agent.unroll(frames)
+        ((lg * dl).sum() + (vl * dv).sum()).backward()
+
+    for _ in range(2):
+        it()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        it()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": round(B * T * steps / dt, 2), "unit": "frames/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "path": "attention.Agent.unroll + loss.backward() (autograd .grad), same frames and weights"}
+
+
 def pmc_traffic(config, dtype, world, kernel):
     """HBM bytes per launch of ``kernel`` from the committed PMC passes
     (tools/pmc.sh -> tools/pmc_traffic.py -> profiles/rNN/pmc_traffic_<config>.json).
@@ -163,6 +197,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in Agent API measurement")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--frames", default="u8", choices=["u8", "fp32"],
                     help="frame dtype in HBM: u8 (the environment's observation, cast in-kernel) or fp32 "
@@ -294,6 +329,8 @@ def main():
                         "params": learner.flat.numel(), "bytes_per_launch": opt_bytes,
                         "achieved_GBps": round(opt_bytes / (opt_us * 1e-6) / 1e9, 1), "peak_GBps": 8000.0,
                         "note": "working set (63.6 MB) is Infinity-Cache resident when stepped back to back"}
+    if world == 1 and not args.no_dropin:
+        out["dropin"] = dropin_api(cfg, dev, frames, dl, dv, args.steps, learner.flat)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline (oracle on host cores)...")
         out["cpu_baseline"] = cpu_baseline(cfg)
