@@ -96,6 +96,7 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
                                      (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24), (25, 16), (26, 16)])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")   # the per-step launches (the frame-resident kernel: below)
     monkeypatch.setenv("AAA_STEP_TILE", str(fwd))
     monkeypatch.setenv("AAA_BPTT_TILE", str(bwd))
     monkeypatch.setenv("AAA_PIPE_BATCHED", "0" if fwd == 0 else "1")   # batched conv GEMMs: register vs LDS-DMA
@@ -112,6 +113,7 @@ def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
 def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
     """The x-part of the ConvLSTM either batched over all frames or inside each
     forward step (AAA_FUSED_X; bf16 default fused, fp32 default batched)."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
     monkeypatch.setenv("AAA_FUSED_X", fused)
     T, B = 4, 3
     if conv_dtype == "fp32":
@@ -126,6 +128,7 @@ def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
 @pytest.mark.parametrize("tile", ["4", "7", "8", "9", "10", "11", "12"])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
     monkeypatch.setenv("AAA_FUSED_X", "1")
     monkeypatch.setenv("AAA_FUSED_TILE", tile)
     T, B = 3, 5
@@ -134,6 +137,40 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
     else:
         _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
                  f"bf16 fused tile {tile}: ")
+
+
+# The frame-resident bf16 recurrence (csrc/recur.h: one workgroup per frame for
+# all T steps, images in LDS) against the bf16-emulated oracle and against the
+# per-step launches it replaces: single step, ragged B, a full T=20 unroll,
+# frames padded to 128 pixel columns (P = 121), carried state across calls.
+@pytest.mark.parametrize("T,B", [(1, 1), (3, 5), (20, 3)])
+def test_frame_resident_forward(cuda, monkeypatch, T, B):
+    monkeypatch.setenv("AAA_FRAMES_FWD", "1")
+    out = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
+    _compare(out, _oracle(T, B, conv_mode="bf16"), 2e-2, f"frames T={T} B={B}: ")
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
+    step = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
+    # same bf16 operands, same fp32 accumulation per k step: only the summation
+    # order and the gate approximations (~1e-7) differ
+    for a, b, n in zip(out[:3], step[:3], ("logits", "values", "attn")):
+        assert_close(a.numpy(), b.numpy(), 2e-3, f"frames vs per-step {n}")
+
+
+def test_frame_resident_carried_state(cuda, monkeypatch):
+    """Two calls of T=3 (the state carried in ConvLSTMCell.prev_hidden, i.e. a
+    non-zero h_0 / c_0 image) equal one call of T=6."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", "1")
+    T, B = 6, 3
+    ag = _agent(cuda, conv_dtype="bf16")
+    X = _frames(T, B).to(cuda)
+    ag.reset()
+    with torch.no_grad():
+        full = ag.unroll(X)
+        ag.reset()
+        a = ag.unroll(X[:3])
+        b = ag.unroll(X[3:])
+    for f, x, y, n in zip(full, a, b, ("logits", "values", "attn")):
+        assert_close(torch.cat([x, y]).cpu().numpy(), f.cpu().numpy(), 1e-5, f"carried state {n}")
 
 
 @pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "6", "7"])

@@ -29,6 +29,7 @@
 #include "loaders_b.h"
 #include "glds.h"
 #include "halo.h"
+#include "recur.h"
 #include "misc.h"
 #include "optim.h"
 
@@ -71,7 +72,7 @@ struct Layout {
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
@@ -123,6 +124,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.k_WpX = take(512 * 576 * e);
   L.k_WpH = take(512 * 1152 * e);
   L.k_WpXH = take(512 * 1728 * e);     // [x | h] step operand (fused x-part, bf16 default)
+  L.k_Wfr = take(e == 2 ? (size_t)16 * kRecKSP * 64 * 16 : 0);   // its fragment-order copy (frame-resident recurrence, recur.h)
   L.k_WdTl = take(192 * 4608 * e);
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
@@ -440,6 +442,10 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
 // The x-part rides in the step GEMM for bf16 and for small steps (M = B*P
 // pixels; the actor's B = 1: one launch instead of two latency-bound ones);
 // fp32 at C2 (M = 3872) keeps the batched x-part (measured 5.02 vs 5.09 ms).
+// bf16 ConvLSTM forward on the frame-resident kernel (recur.h): one workgroup
+// per frame for the whole unroll, on grids whose images fit its LDS (84x84
+// frames).  AAA_FRAMES_FWD=0 keeps the per-step launches.
+static bool frames_fwd(const struct Layout& L);
 static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
 static bool gates_f16(int dt, int M) {
   if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
@@ -626,6 +632,7 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
   }
   HIPCHK(pack_lstm_all<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl),
                           (T*)(pk + L.k_WpXH), st));
+  if constexpr (!std::is_same<T, float>::value) HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
@@ -703,6 +710,10 @@ static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, 
 }
 
 // ------------------------------------------------------------- forward ----
+static bool frames_fwd(const Layout& L) {
+  return L.dt == AAA_BF16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_FWD", 1) != 0;
+}
+
 template <typename T>
 static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
 
@@ -736,6 +747,16 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     // small M, e.g. the B=1 actor, fuses the x-part): 128x64 8 waves.
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
+      if constexpr (!std::is_same<T, float>::value) {
+        if (frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
+          RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
+                              Wf(L.Hs), (GT*)(ws + L.Gt), L.T, L.B, L.h, L.w, L.P};
+          TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
+                         strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, 1 WG per frame", L.T));
+          HIPCHK(convlstm_fwd_frames<GT>(rp, st));
+          return AAA_OK;
+        }
+      }
       for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
         EpiConvLstmFwd<T, GT> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
                                  Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
