@@ -3,23 +3,25 @@
 // The recurrence of one frame depends only on that frame (attention.py:110-126:
 // the gate convs are 3x3 over the frame's own grid, no batch coupling), so one
 // workgroup owns a frame for ALL T steps of the unroll: the zero-bordered
-// images of x_t and h_{t-1} live in LDS, the cell state c in registers, and a
-// step is one 512 x P x 1728 GEMM whose B operand (the im2col of [x_t | h_{t-1}])
-// is read straight out of the LDS images by all nine taps -- no per-step launch,
+// images of x_t and h_{t-1} live in LDS, the cell state c in LDS, and a step is
+// one 512 x P x 1728 GEMM whose B operand (the im2col of [x_t | h_{t-1}]) is
+// read straight out of the LDS images by all nine taps -- no per-step launch,
 // no prologue, no re-gathering of the pixel operand from L2, and the epilogue's
 // HBM stores of step t drain under the MFMAs of step t+1.
 //
-// Geometry: 8 waves; wave w owns gate rows [64w, 64w+64) (row = 4*channel +
-// gate, i.e. channels 16w..16w+15) for all P <= 128 pixel columns (4 column
-// blocks of 32), acc 2x4 v_mfma_f32_32x32x16_bf16 tiles.  Lane (r32, hh) of
-// block (rr, cb) holds rows 8g + 4hh + e: the four gates of channel
-// 16w + 8rr + 2g + hh at pixel 32cb + r32 -- the whole cell update is lane-local.
+// Geometry: 4 waves, one per SIMD (512 registers each); wave w owns gate rows
+// [128w, 128w+128) (row = 4*channel + gate: channels 32w..32w+31) for all
+// P <= 128 pixel columns, acc 4x4 v_mfma_f32_32x32x16_bf16 tiles (row block
+// rb, column block cb).  Lane (r32, hh) of tile (rb, cb) holds rows 8g + 4hh + e:
+// the four gates of channel 32w + 8rb + 2g + hh at pixel 32cb + r32 -- the whole
+// cell update is lane-local.
 //
 // A operand (weights): fragment-order copy of the packed [512][1728] matrix
-// (k_pack_wfrag), one contiguous 1 KB wave load per (row block, k step),
-// streamed from L2 continuously across steps (the prefetch wraps into the next
-// step's first k steps).  K order k = tap*192 + c, c < 64 from the x image,
-// c >= 64 from the h image, exactly as the implicit GEMM of fused_step.
+// (k_pack_wfrag), one contiguous 1 KB wave load per (row block, k step) from a
+// buffer descriptor, kRecPD-1 k steps in flight, streamed from L2 continuously
+// across steps (the packed copy repeats its first k steps at the end).  K runs
+// x-part first (9 taps x 64 channels), then the h-part (9 taps x 128 channels),
+// so the single x image can be refilled (LDS-DMA) while the h-part runs.
 #pragma once
 #include <cstdlib>
 #include "common.h"
@@ -28,20 +30,27 @@
 
 namespace aaa {
 
-constexpr int kRecKS = 1728 / 16;   // k steps of one [x|h] step GEMM
-constexpr int kRecPD = 3;           // A k steps in flight (registers); 12 % kRecPD == 0
+constexpr int kRecKS = 1728 / 16;   // k steps of one [x|h] step GEMM: 36 x-part, then 72 h-part
+constexpr int kRecKX = 36;
+constexpr int kRecPD = 4;           // A k steps in flight + 1 (register slots); divides 4 and 8
 constexpr int kRecKSP = kRecKS + kRecPD - 1;   // packed k steps per row block: the first PD-1 repeated at
                                                // the end, so the prefetch runs into the next step unwrapped
 constexpr int kRecNPH = 169;        // LDS image pixels: (h+2)*(w+2) <= 169 (11x11 grids: 84x84 frames)
-constexpr int kRecXB = 22 * 1024;   // x image bytes per buffer: 169 pixels x 128 B, whole 1-KB DMA pieces
+constexpr int kRecXB = 22 * 1024;   // x image bytes: 169 pixels x 128 B, whole 1-KB DMA pieces
 constexpr int kRecHS = 136;         // h image pixel pitch (bf16): 128 + 8 pad (272 B = 17 x 16 B)
+constexpr int kRecStg = 4608;       // per-wave epilogue staging bytes (16 px x 272 B gates; c + h 2 x 16 x 144 B)
 
-// Wf[((rb*kRecKSP + ks)*64 + lane)*8 + e] = W[rb*32 + lane%32][(ks % kRecKS)*16 + (lane/32)*8 + e]
+// k step ks of the x-first order -> element offset k of the [x|h] GEMM (k = tap*192 + c)
+__host__ __device__ constexpr int rec_k(int ks) {
+  return ks < kRecKX ? (ks >> 2) * 192 + (ks & 3) * 16 : ((ks - kRecKX) >> 3) * 192 + 64 + ((ks - kRecKX) & 7) * 16;
+}
+
+// Wf[((rb*kRecKSP + ks)*64 + lane)*8 + e] = W[rb*32 + lane%32][rec_k(ks % kRecKS) + (lane/32)*8 + e]
 __global__ void __launch_bounds__(256) k_pack_wfrag(const __bf16* __restrict__ W, __bf16* __restrict__ Wf) {
   const int c = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
   if (c >= 16 * kRecKSP * 64) return;
   const int lane = c & 63, rk = c >> 6, ks = rk % kRecKSP, rb = rk / kRecKSP;
-  const int row = rb * 32 + (lane & 31), k = (ks % kRecKS) * 16 + (lane >> 5) * 8;
+  const int row = rb * 32 + (lane & 31), k = rec_k(ks % kRecKS) + (lane >> 5) * 8;
   *reinterpret_cast<bf16x8*>(Wf + (size_t)c * 8) = *reinterpret_cast<const bf16x8*>(W + (size_t)row * 1728 + k);
 }
 
@@ -75,41 +84,57 @@ struct RecFwdParams {
 // ABL (diagnostic A/B only, AAA_REC_ABL): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
 template <typename GT, int ABL = 0>
-__global__ void __launch_bounds__(512) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
-  __shared__ __attribute__((aligned(16))) unsigned char xim[2 * kRecXB];
-  __shared__ __attribute__((aligned(16))) __bf16 him[2 * kRecNPH * kRecHS];
+__global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
+  __shared__ __attribute__((aligned(16))) unsigned char xim[kRecXB];
+  __shared__ __attribute__((aligned(16))) __bf16 him[kRecNPH * kRecHS];
+  __shared__ __attribute__((aligned(16))) float cstl[4 * 64 * 64];   // c, lane-native: [wave][rb][cb][g][lane]
   __shared__ __attribute__((aligned(16))) float sbias[512];
-  const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) unsigned char stg[4 * kRecStg];
+  const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR) for the buffer soffsets
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
+  float* cw = cstl + wave * 64 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
 
-  {  // zero the h images (their borders stay zero), bias into LDS
+  {  // zero the h image (its border stays zero), bias into LDS
     u32x4* z = reinterpret_cast<u32x4*>(him);
-    for (int i = tid; i < 2 * kRecNPH * kRecHS / 8; i += 512) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < kRecNPH * kRecHS / 8; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
     sbias[tid] = p.bias[tid];
+    sbias[tid + 256] = p.bias[tid + 256];
   }
   // x image of step t (XH slot t, channels 0..63) by LDS-DMA, border included:
   // image pixel ip holds its 8 16-B channel chunks at slots q ^ xswz(ip) (the
   // fragment reads of 16 consecutive pixels then hit 16 distinct bank groups);
   // border pixels read outside the descriptor and land as zeros.  Wave w issues
-  // the 1-KB pieces w, w+8, ... of the 22 (8 pixels each).
-  auto dma_x = [&](int t, int buf) {
+  // the 1-KB pieces w, w+4, ... of the 22 (8 pixels each).
+  auto dma_x = [&](int t) {
     const __amdgpu_buffer_rsrc_t rs =
         make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
-    for (int i = wave; i < kRecXB / 1024; i += 8) {
+    for (int i = wave; i < kRecXB / 1024; i += 4) {
       const int sl = i * 64 + lane, ip = sl >> 3, q = (sl & 7) ^ ((ip >> 1) & 7);
       const int py = ip / W2 - 1, px = ip % W2 - 1;
       const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
-      dma16(rs, xim + buf * kRecXB + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB);
+      dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB);
     }
   };
-  dma_x(0, 0);
-  __syncthreads();   // h images zeroed
-  {  // h_0 (slot 0, channels 64..191) into image 0
+  dma_x(0);
+  // cell state c_0 (Cst slot 0) into the lane-native LDS copy
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int pp = cb * 32 + r32;
+        cw[(rb * 16 + cb * 4 + g) * 64] =
+            pp < P ? p.Cst[((size_t)b * P + pp) * 128 + 32 * wave + 8 * rb + 2 * g + hh] : 0.f;
+      }
+  __syncthreads();   // h image zeroed
+  {  // h_0 (slot 0, channels 64..191) into the image
     const __bf16* src = p.XH + (size_t)b * P * 192 + 64;
-    for (int i = tid; i < P * 16; i += 512)
+    for (int i = tid; i < P * 16; i += 256)
       *reinterpret_cast<u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8) =
           *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 4) * 192 + (i & 15) * 8);
   }
@@ -122,131 +147,194 @@ __global__ void __launch_bounds__(512) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     const int pp = min(cb * 32 + r32, P - 1);
     hb[cb] = (pp / p.w) * W2 + pp % p.w;
   }
-  const __bf16* A0 = p.Wf + ((size_t)(2 * wave) * kRecKSP * 64 + lane) * 8;
-  const __bf16* A1 = A0 + (size_t)kRecKSP * 64 * 8;
-  constexpr int PD = kRecPD;
-  bf16x8 af[PD][2];
-#pragma unroll
-  for (int s = 0; s < PD - 1; ++s) {
-    af[s][0] = *reinterpret_cast<const bf16x8*>(A0 + s * 512);
-    af[s][1] = *reinterpret_cast<const bf16x8*>(A1 + s * 512);
-  }
-  __syncthreads();   // images of step 0 complete
 
-  for (int t = 0; t < p.T; ++t) {
-    const int cur = t & 1, nxt = cur ^ 1;
-    // x_{t+1} into the other image (last read in step t-1); the wave's later A
-    // loads retire after it (vmcnt is in order), so it has landed by the end of the K loop
-    if (t + 1 < p.T) dma_x(t + 1, nxt);
-    f32x16 acc[2][4];
+  // A stream: one buffer descriptor over the fragment-order weights, the lane's
+  // 16 B at voffset lane*16, the (row block, k step) in the wave-uniform soffset
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wf, (uint32_t)(16 * kRecKSP * 1024));
+  const int wofs = 4 * wave * kRecKSP * 1024;
+  auto lda = [&](int ks, int j) {
+    return __builtin_bit_cast(bf16x8,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, wofs + (j * kRecKSP + ks) * 1024, 0));
+  };
+  constexpr int PD = kRecPD;
+  bf16x8 af[PD][4];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr)
+  for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) af[s][j] = lda(s, j);
+  __syncthreads();   // images of step 0 complete (this wave's x DMA retired before: vmcnt in order)
+
+  unsigned char* sw = stg + wave * kRecStg;   // this wave's epilogue staging
+  for (int t = 0; t < p.T; ++t) {
+    f32x16 acc[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[rr][cb][e] = 0.f;
-    const unsigned char* xb = xim + cur * kRecXB;
+        for (int e = 0; e < 16; ++e) acc[j][cb][e] = 0.f;
+    const __bf16* hbp = him + hh * 8;
     int hbs[4];   // laundered per step: no per-tap address tables hoisted out of the step loop
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       hbs[cb] = hb[cb];
       asm volatile("" : "+v"(hbs[cb]));
     }
-    const __bf16* hbp = him + cur * NPH * kRecHS + hh * 8;
-    // B fragments of k step ks (image, tap offset, channel chunk c16 of 12: 4 from x, 8 from h)
-    auto ldb = [&](int toff, int c16, bf16x8 (&bf)[4]) {
+    // B fragments of a k step: x image (chunk c4 of 4 at tap offset toff) or h image (chunk c8 of 8)
+    auto ldx = [&](int toff, int c4, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-      {
+      for (int cb = 0; cb < 4; ++cb) {
         const int ip = hbs[cb] + toff;
-        bf[cb] = c16 < 4 ? *reinterpret_cast<const bf16x8*>(xb + ip * 128 + (((2 * c16 + hh) ^ ((ip >> 1) & 7)) << 4))
-                         : *reinterpret_cast<const bf16x8*>(hbp + ip * kRecHS + (c16 - 4) * 16);
+        bf[cb] = *reinterpret_cast<const bf16x8*>(xim + ip * 128 + (((2 * c4 + hh) ^ ((ip >> 1) & 7)) << 4));
       }
     };
-    bf16x8 bfr[2][4];
-    ldb(0, 0, bfr[0]);
-    for (int tap = 0; tap < 9; ++tap) {
-      const int toff = (tap / 3) * W2 + tap % 3;
-      const int tnext = tap < 8 ? ((tap + 1) / 3) * W2 + (tap + 1) % 3 : 0;
-      int ko = tap * 12 * 512;   // laundered: one base per tap, immediate offsets inside (no hoisted address table)
-      asm volatile("" : "+s"(ko));
-      const __bf16* a0 = A0 + ko;
-      const __bf16* a1 = A1 + ko;
+    auto ldh = [&](int toff, int c8, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int c16 = 0; c16 < 12; ++c16) {
-        // A fragments of k step ks + PD - 1 (the packed copy runs on into the next step's first ones)
-        if constexpr (!(ABL & 1)) {
-          af[(c16 + PD - 1) % PD][0] = *reinterpret_cast<const bf16x8*>(a0 + (c16 + PD - 1) * 512);
-          af[(c16 + PD - 1) % PD][1] = *reinterpret_cast<const bf16x8*>(a1 + (c16 + PD - 1) * 512);
-        }
-        // B fragments one k step ahead (the last k step's are this step's last use)
-        if constexpr (!(ABL & 8)) {
-          if (c16 < 11) ldb(toff, c16 + 1, bfr[(c16 + 1) & 1]);
-          else if (tap < 8) ldb(tnext, 0, bfr[0]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(hbp + (hbs[cb] + toff) * kRecHS + c8 * 16);
+    };
+    auto tapoff = [&](int tap) { return (tap / 3) * W2 + tap % 3; };
+    // one k step: A prefetch PD-1 ahead, next B fragments, 16 MFMAs
+    auto kstep = [&](int ks, int slot, bf16x8 (&bc)[4], auto&& load_next_b) {
+      if constexpr (!(ABL & 1)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) af[(slot + PD - 1) % PD][j] = lda(ks + PD - 1, j);
+      }
+      if constexpr (!(ABL & 8)) load_next_b();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          if constexpr (ABL & 4) {
-            acc[0][cb][0] += (float)af[c16 % PD][0][0] * (float)bfr[c16 & 1][cb][0];
-          } else {
-            acc[0][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][0], bfr[c16 & 1][cb], acc[0][cb], 0, 0, 0);
-            acc[1][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][1], bfr[c16 & 1][cb], acc[1][cb], 0, 0, 0);
-          }
+          if constexpr (ABL & 4)
+            acc[j][cb][0] += (float)af[slot][j][0] * (float)bc[cb][0];
+          else
+            acc[j][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[slot][j], bc[cb], acc[j][cb], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    bf16x8 bfr[2][4];
+    ldx(0, 0, bfr[0]);
+    // x-part: 9 taps x 4 chunks (k steps 0..35)
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+      int kt = tap * 4;
+      asm volatile("" : "+s"(kt));
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        kstep(kt + c4, c4 % PD, bfr[c4 & 1], [&] {
+          if (c4 < 3) ldx(toff, c4 + 1, bfr[(c4 + 1) & 1]);
+          else if (tap < 8) ldx(tn, 0, bfr[0]);
+          else ldh(0, 0, bfr[0]);
+        });
     }
-    // gate math + cell update (lane-local), h_t into the other h image.  The
-    // lane's pixel is laundered per step so the compiler recomputes the 32
-    // epilogue addresses from one base instead of hoisting them all out of the
-    // step loop into (spilled) registers.
-    int pl = r32;
-    asm volatile("" : "+v"(pl));
-    const size_t rowt = (size_t)t * M + (size_t)b * P;   // this frame's rows of step t (Hs, Gt; Cst slot t)
-    const int c0 = 16 * wave + hh;                       // + 8*rr + 2*g
+    barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
+    if (t + 1 < p.T) dma_x(t + 1);
+    // h-part: 9 taps x 8 chunks (k steps 36..107)
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+      int kt = kRecKX + tap * 8;
+      asm volatile("" : "+s"(kt));
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8)
+        kstep(kt + c8, c8 % PD, bfr[c8 & 1], [&] {
+          if (c8 < 7) ldh(toff, c8 + 1, bfr[(c8 + 1) & 1]);
+          else if (tap < 8) ldh(tn, 0, bfr[0]);
+        });
+    }
+    barrier_lds();   // every wave is done with h_{t-1}: the epilogue overwrites the image with h_t
+
+    // Epilogue, one column block (32 pixels) at a time: gate math + cell update
+    // lane-local, h_t into the h image, c_t into its LDS copy, and the HBM
+    // outputs staged through the wave's LDS scratch in two halves of 16 pixels
+    // so every store instruction writes whole 128-B / 256-B pixel rows (gates, c,
+    // h are [pixel][channel]: a lane's own values are one channel at 32 pixels).
+    // the lane index laundered per step: every epilogue address is recomputed
+    // here instead of hoisted out of the step loop into spilled registers
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int pl = ln & 31, hl_ = ln >> 5;
+    const size_t rowt = (size_t)t * M + (size_t)b * P;   // this frame's rows of step t (Hs, Gt)
+    const int c0 = 32 * wave + hl_;                       // + 8*rb + 2*g
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int pp = cb * 32 + pl;
-      if (pp >= P) continue;
-      const size_t row = rowt + pp;
-      const float* cprev = p.Cst + row * 128 + c0;       // c_{t-1}: the lane's own stores of step t-1 (slot 0: c_0)
-      float* cnext = p.Cst + (row + M) * 128 + c0;
-      float* hout = p.Hs + row * 128 + c0;
-      GT* gout = p.Gt + row * 512 + 4 * c0;
-      __bf16* hl = him + (nxt * NPH + hidx(pp)) * kRecHS + c0;
-      float cp[2][4];
+      __bf16* hl = him + hidx(min(pp, P - 1)) * kRecHS + c0;
+      uint32_t gq[4][4][2];   // fp16 gate quads (i, f, c~, o), packed
+      float hv[4][4], cv[4][4];
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) cp[rr][g] = cprev[8 * rr + 2 * g];
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int co = 8 * rr + 2 * g;
+          const int co = 8 * rb + 2 * g;
           const f32x4 bz = *reinterpret_cast<const f32x4*>(sbias + 4 * (c0 + co));
-          const float gi = sigm_fast(acc[rr][cb][4 * g] + bz[0]);
-          const float gf = sigm_fast(acc[rr][cb][4 * g + 1] + bz[1]);
-          const float gc = tanh_fast(acc[rr][cb][4 * g + 2] + bz[2]);
-          const float go = sigm_fast(acc[rr][cb][4 * g + 3] + bz[3]);
-          const float c = gf * cp[rr][g] + gi * gc;
+          const float gi = sigm_fast(acc[rb][cb][4 * g] + bz[0]);
+          const float gf = sigm_fast(acc[rb][cb][4 * g + 1] + bz[1]);
+          const float gc = tanh_fast(acc[rb][cb][4 * g + 2] + bz[2]);
+          const float go = sigm_fast(acc[rb][cb][4 * g + 3] + bz[3]);
+          float* cl = cstl + wave * 64 * 64 + ln + (rb * 16 + cb * 4 + g) * 64;
+          const float c = gf * *cl + gi * gc;
           const float h = go * tanh_fast(c);
-          if constexpr (!(ABL & 2)) {
-            cnext[co] = c;
-            hout[co] = h;
-            store_gates(gout + 4 * co, f32x4{gi, gf, gc, go});
-          }
-          hl[co] = (__bf16)h;
+          *cl = c;
+          cv[rb][g] = c;
+          hv[rb][g] = h;
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          gq[rb][g][0] = __builtin_bit_cast(uint32_t, h2{(_Float16)gi, (_Float16)gf});
+          gq[rb][g][1] = __builtin_bit_cast(uint32_t, h2{(_Float16)gc, (_Float16)go});
+          if (pp < P) hl[co] = (__bf16)h;
         }
+      if constexpr (!(ABL & 2)) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int pxl = pl & 15;
+          const bool mine = (pl >> 4) == half;
+          const int pbase = cb * 32 + half * 16;   // first pixel of this half
+          if (pbase >= P) break;
+          // gates: staging [16 px][32 ch][4] fp16 at pixel pitch 272 B
+          if (mine) {
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+              for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<uint2*>(sw + pxl * 272 + (8 * rb + 2 * g + hl_) * 8) = uint2{gq[rb][g][0], gq[rb][g][1]};
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {   // 4 x 1 KB: 4 pixel rows of 256 B each
+            const int q = k * 64 + ln, px = q >> 4, pix = pbase + px;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * 272 + (q & 15) * 16);
+            if (pix < P)
+              *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * 32 * wave) +
+                                        (q & 15) * 16) = v;
+          }
+          // c_t and h_t: staging [16 px][32 ch] fp32 at pixel pitch 144 B (c), then (h) 2304 B on
+          if (mine) {
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                *reinterpret_cast<float*>(sw + pxl * 144 + (8 * rb + 2 * g + hl_) * 4) = cv[rb][g];
+                *reinterpret_cast<float*>(sw + 2304 + pxl * 144 + (8 * rb + 2 * g + hl_) * 4) = hv[rb][g];
+              }
+          }
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {   // 2 x 1 KB each: 8 pixel rows of 128 B
+            const int q = k * 64 + ln, px = q >> 3, pix = pbase + px;
+            const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * 144 + (q & 7) * 16);
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 2304 + px * 144 + (q & 7) * 16);
+            if (pix < P) {
+              *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + 32 * wave + (q & 7) * 4) = vc;
+              *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + 32 * wave + (q & 7) * 4) = vh;
+            }
+          }
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);   // one column block at a time (register pressure)
     }
-    barrier_lds();   // step t+1's images complete; every wave is done with step t's (VM stores stay in flight)
+    barrier_lds();   // h_t image and x_{t+1} image complete (this wave's DMA retired under its h-part A loads)
     // h_t (bf16) into XH slot t+1 channels 64..191 (the weight-gradient operand), from the image
-    const size_t rown = rowt + M;                        // slot t+1
-    for (int i = tid; i < ((ABL & 2) ? 0 : P * 16); i += 512)
+    const size_t rown = rowt + M;   // slot t+1
+    for (int i = tid; i < ((ABL & 2) ? 0 : P * 16); i += 256)
       *reinterpret_cast<u32x4*>(p.XH + (rown + (i >> 4)) * 192 + 64 + (i & 15) * 8) =
-          *reinterpret_cast<const u32x4*>(him + (nxt * NPH + hidx(i >> 4)) * kRecHS + (i & 15) * 8);
+          *reinterpret_cast<const u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8);
   }
 }
 
@@ -256,10 +344,10 @@ inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, hipStream_t st)
   const char* e = getenv("AAA_REC_ABL");
   switch (e ? atoi(e) : 0) {
 #define AAA_REC_CASE(a) \
-  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, a>), dim3(p.B), dim3(512), 0, st, p); break;
+  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, a>), dim3(p.B), dim3(256), 0, st, p); break;
     AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12)
 #undef AAA_REC_CASE
-    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 0>), dim3(p.B), dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 0>), dim3(p.B), dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
 }

@@ -444,7 +444,9 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
 // fp32 at C2 (M = 3872) keeps the batched x-part (measured 5.02 vs 5.09 ms).
 // bf16 ConvLSTM forward on the frame-resident kernel (recur.h): one workgroup
 // per frame for the whole unroll, on grids whose images fit its LDS (84x84
-// frames).  AAA_FRAMES_FWD=0 keeps the per-step launches.
+// frames), once the batch fills most of the chip's 256 CUs (C3, B=256: 55 vs
+// 79 us per step; C4's B=128 leaves half the CUs idle: 49 vs 43 us,
+// profiles/r02/frames).  AAA_FRAMES_FWD=1/0 forces it on/off.
 static bool frames_fwd(const struct Layout& L);
 static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
 static bool gates_f16(int dt, int M) {
@@ -711,7 +713,7 @@ static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, 
 
 // ------------------------------------------------------------- forward ----
 static bool frames_fwd(const Layout& L) {
-  return L.dt == AAA_BF16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_FWD", 1) != 0;
+  return L.dt == AAA_BF16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_FWD", L.B >= 160 ? 1 : 0) != 0;
 }
 
 template <typename T>
