@@ -143,17 +143,48 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
 # all T steps, images in LDS) against the bf16-emulated oracle and against the
 # per-step launches it replaces: single step, ragged B, a full T=20 unroll,
 # frames padded to 128 pixel columns (P = 121), carried state across calls.
-@pytest.mark.parametrize("T,B", [(1, 1), (3, 5), (20, 3)])
-def test_frame_resident_forward(cuda, monkeypatch, T, B):
+@pytest.mark.parametrize("T,B", [(1, 1), (2, 2), (3, 5), (20, 3)])
+@pytest.mark.parametrize("bwd", ["0", "1"])
+def test_frame_resident_forward(cuda, monkeypatch, T, B, bwd):
+    """... and the frame-resident BPTT (csrc/recur_bwd.h, AAA_FRAMES_BWD) on top."""
     monkeypatch.setenv("AAA_FRAMES_FWD", "1")
+    monkeypatch.setenv("AAA_FRAMES_BWD", bwd)
     out = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
-    _compare(out, _oracle(T, B, conv_mode="bf16"), 2e-2, f"frames T={T} B={B}: ")
+    _compare(out, _oracle(T, B, conv_mode="bf16"), 2e-2, f"frames T={T} B={B} bwd={bwd}: ")
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")
+    monkeypatch.setenv("AAA_FRAMES_BWD", "0")
     step = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
     # same bf16 operands, same fp32 accumulation per k step: only the summation
     # order and the gate approximations (~1e-7) differ
     for a, b, n in zip(out[:3], step[:3], ("logits", "values", "attn")):
         assert_close(a.numpy(), b.numpy(), 2e-3, f"frames vs per-step {n}")
+    for n in out[3]:
+        if float(step[3][n].norm()) > 0:
+            assert rel_err(out[3][n].numpy(), step[3][n].numpy()) <= 5e-3, f"frames vs per-step grad {n}"
+
+
+@pytest.mark.parametrize("frames", ["0", "1"])
+def test_frame_resident_state_gradients(cuda, monkeypatch, frames):
+    """T single-step calls then one backward (main_mp.py:54,77) on the bf16 path:
+    every call's backward takes dh_T / dc_T from the next call and hands dh_0 /
+    dc_0 to the previous one -- the state-gradient paths of both BPTT kernels."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", frames)
+    monkeypatch.setenv("AAA_FRAMES_BWD", frames)
+    T, B = 4, 3
+    agent = _agent(cuda, conv_dtype="bf16")
+    X = _frames(T, B).to(cuda)
+    Gl, Gv = _cot(T, B)
+    agent.reset()
+    loss = 0
+    for t in range(T):
+        lg, vl = agent(X[t])
+        loss = loss + (lg * Gl[t].to(cuda)).sum() + (vl * Gv[t].to(cuda)).sum()
+    loss.backward()
+    ref = _oracle(T, B, conv_mode="bf16")
+    g = _grads(agent)
+    for n in ref[3]:
+        if float(ref[3][n].norm()) > 0:
+            assert_close(g[n].numpy(), ref[3][n].float().numpy(), 2e-2, "grad " + n)
 
 
 def test_frame_resident_carried_state(cuda, monkeypatch):

@@ -30,6 +30,7 @@
 #include "glds.h"
 #include "halo.h"
 #include "recur.h"
+#include "recur_bwd.h"
 #include "misc.h"
 #include "optim.h"
 
@@ -72,7 +73,7 @@ struct Layout {
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
@@ -126,6 +127,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.k_WpXH = take(512 * 1728 * e);     // [x | h] step operand (fused x-part, bf16 default)
   L.k_Wfr = take(e == 2 ? (size_t)16 * kRecKSP * 64 * 16 : 0);   // its fragment-order copy (frame-resident recurrence, recur.h)
   L.k_WdTl = take(192 * 4608 * e);
+  L.k_Wbf = take(e == 2 ? (size_t)4 * kBwKSP * 64 * 16 : 0);   // fragment-order W_h^T (frame-resident BPTT)
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
   L.k_Wihp = take(1024 * 256 * 4);
@@ -634,7 +636,10 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
   }
   HIPCHK(pack_lstm_all<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl),
                           (T*)(pk + L.k_WpXH), st));
-  if constexpr (!std::is_same<T, float>::value) HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
+  if constexpr (!std::is_same<T, float>::value) {
+    HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
+    HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl) + (size_t)64 * 4608, (__bf16*)(pk + L.k_Wbf), st));
+  }
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
@@ -714,6 +719,12 @@ static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, 
 // ------------------------------------------------------------- forward ----
 static bool frames_fwd(const Layout& L) {
   return L.dt == AAA_BF16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_FWD", L.B >= 160 ? 1 : 0) != 0;
+}
+// The BPTT chain on the frame-resident kernel (recur_bwd.h; fp16 gate storage),
+// from the same batch on (C3: 55 vs 69 us per step; C4: 52 vs 49 us).
+// AAA_FRAMES_BWD=1/0 forces it on/off.
+static bool frames_bwd(const Layout& L, bool g16) {
+  return L.dt == AAA_BF16 && g16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_BWD", L.B >= 160 ? 1 : 0) != 0;
 }
 
 template <typename T>
@@ -1484,7 +1495,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
-    if (g16)
+    const bool fb = frames_bwd(L, g16);   // the whole chain in one frame-resident launch (after flush below)
+    if (fb) {
+    } else if (g16)
       HIPCHK((gate_bwd_last<T, _Float16>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT,
                                          (const _Float16*)(ws + L.Gt) + (size_t)t1 * M * 512,
                                          Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128,
@@ -1508,7 +1521,16 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       }
       return AAA_OK;
     };
-    for (int t = t1; t >= 0; --t) {
+    if (fb) {
+      if constexpr (!std::is_same<T, float>::value) {
+        RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
+                        Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, L.T, L.B, L.h, L.w, L.P};
+        TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
+                       strf("bf16 frame-resident BPTT, %d steps per launch, 1 WG per frame, fp16 gates", L.T));
+        HIPCHK(convlstm_bwd_frames(rp, st));
+      }
+    }
+    for (int t = fb ? -1 : t1; t >= 0; --t) {
       const int rc0 = flush(t);   // dz_t .. dz_{T-1} are final here
       if (rc0) return rc0;
       const bool prev = t > 0;
@@ -1608,7 +1630,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
     // gate-bias gradient: column sum of the per-(step, tile) partials, or of dZ itself
-    if (part) HIPCHK(colsum<float>(part, 512, L.T * ntj, 512, Wf(L.gbl), st));
+    if (fb) HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B, 512, Wf(L.gbl), st));   // per (step, frame) partials
+    else if (part) HIPCHK(colsum<float>(part, 512, L.T * ntj, 512, Wf(L.gbl), st));
     else HIPCHK(colsum<T>(Wt(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     if (ax) HIPCHK(stream_order(ax, st));   // join
