@@ -31,7 +31,7 @@
 namespace aaa {
 
 constexpr int kBwKS = 4608 / 16;   // k steps: 4 chunks x 9 taps x 8 groups of 16 rows
-constexpr int kBwPD = 8;           // A register slots (PD-1 k steps in flight); divides 8
+constexpr int kBwPD = 4;           // A register slots (PD-1 k steps in flight); divides 8
 constexpr int kBwKSP = kBwKS + kBwPD - 1;
 constexpr int kBwIP = 136;         // chunk image pixel pitch (bf16): 128 rows + 8 pad (272 B)
 constexpr int kBwIB = 46080;       // chunk image bytes: 169 px x 272 B rounded up to whole 1-KB DMA pieces
@@ -39,19 +39,33 @@ constexpr int kBwIB = 46080;       // chunk image bytes: 169 px x 272 B rounded 
 // k step ks -> k of the dgrad GEMM (k = tap*512 + gate row)
 __host__ __device__ constexpr int bw_k(int ks) { return ((ks % 72) >> 3) * 512 + (ks / 72) * 128 + (ks & 7) * 16; }
 
-// Wb[((rb*kBwKSP + ks)*64 + lane)*8 + e] = W[rb*32 + lane%32][bw_k(ks % kBwKS) + (lane/32)*8 + e], W = the h
-// rows of the packed dgrad weights ([128][4608], rows 64..191 of k_WdTl)
+// Wb[((rb*kBwKSP + ks)*64 + lane)*8 + e] = W[row(rb, lane%32)][bw_k(ks % kBwKS) + (lane/32)*8 + e], W = the
+// packed dgrad weights [192][4608] (k_WdTl: rows 0..63 x channels, 64..191 h channels); row blocks 0..3 =
+// the h rows (the BPTT GEMM proper), 4..5 = the x rows (dx: conv2's output gradient, fused in the same pass)
 __global__ void __launch_bounds__(256) k_pack_wbfrag(const __bf16* __restrict__ W, __bf16* __restrict__ Wb) {
   const int c = blockIdx.x * 256 + (int)threadIdx.x;
-  if (c >= 4 * kBwKSP * 64) return;
+  if (c >= 6 * kBwKSP * 64) return;
   const int lane = c & 63, rk = c >> 6, ks = rk % kBwKSP, rb = rk / kBwKSP;
-  const int row = rb * 32 + (lane & 31), k = bw_k(ks % kBwKS) + (lane >> 5) * 8;
+  const int row = (rb < 4 ? 64 + rb * 32 : (rb - 4) * 32) + (lane & 31), k = bw_k(ks % kBwKS) + (lane >> 5) * 8;
   *reinterpret_cast<bf16x8*>(Wb + (size_t)c * 8) = *reinterpret_cast<const bf16x8*>(W + (size_t)row * 4608 + k);
 }
 
 inline hipError_t pack_wbfrag(const __bf16* W, __bf16* Wb, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_wbfrag, dim3((4 * kBwKSP * 64 + 255) / 256), dim3(256), 0, st, W, Wb);
+  hipLaunchKernelGGL(k_pack_wbfrag, dim3((6 * kBwKSP * 64 + 255) / 256), dim3(256), 0, st, W, Wb);
   return hipGetLastError();
+}
+
+// gate_bwd (epilogues.h) with the branch-free tanh of the bf16 recurrence (recur.h)
+__device__ __forceinline__ void gate_bwd_fast(float dh, const f32x4& g, float cprev, float ccur, float& dc, float& di,
+                                              float& df, float& dcg, float& dout) {
+  const float gi = g[0], gf = g[1], gc = g[2], go = g[3];
+  const float tc = tanh_fast(ccur);
+  const float dcc = dc + dh * go * (1.f - tc * tc);
+  dout = dh * tc * (1.f - go) * go;
+  di = dcc * gc * (1.f - gi) * gi;
+  df = dcc * cprev * (1.f - gf) * gf;
+  dcg = dcc * gi * (1.f - gc * gc);
+  dc = dcc * gf;
 }
 
 struct RecBwdParams {
@@ -64,13 +78,15 @@ struct RecBwdParams {
   __bf16* dZ;             // (T, B, P, 512) <- gate pre-activation grads
   float* part;            // (T, B, 512) <- gate-bias partials per (step, frame)
   float* dh0;             // (B, P, 128) <- grad of h_{-1}, or null
+  __bf16* dY2;            // (T, B, P, 64) <- dx_t, the conv2 output gradient (bf16: its readers' operand type)
+  float* dxb;             // (B, 64) <- conv2 bias-gradient partials per frame (fp32 sums of dx)
   int T, B, h, w, P;
 };
 
 // ABL (diagnostic A/B only, AAA_RECB_ABL): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA.
 template <int ABL = 0>
-__global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (0: chunks 0, 2; 1: 1, 3)
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];         // dc carry, lane-native [wave][g*4+cb][lane]
   const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
@@ -116,39 +132,46 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
                  : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(4 * kBwKSP * 1024));
-  const int wofs = wave * kBwKSP * 1024;
-  auto lda = [&](int ks) {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, wofs + ks * 1024, 0));
+  // A stream: per k step the wave's h row block (wave) and its dx row block (4 + wave % 2)
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(6 * kBwKSP * 1024));
+  const int wofs = wave * kBwKSP * 1024, xofs = (4 + (wave & 1)) * kBwKSP * 1024;
+  auto lda = [&](int ks, int x) {
+    return __builtin_bit_cast(bf16x8,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, (x ? xofs : wofs) + ks * 1024, 0));
   };
   constexpr int PD = kBwPD;
-  bf16x8 af[PD];
+  bf16x8 af[PD][2];
 #pragma unroll
-  for (int s = 0; s < PD - 1; ++s) af[s] = lda(s);
+  for (int s = 0; s < PD - 1; ++s) {
+    af[s][0] = lda(s, 0);
+    af[s][1] = lda(s, 1);
+  }
+  const int xcb = 2 * (wave >> 1);   // the wave's dx tiles: x row block wave % 2, column blocks xcb, xcb + 1
+  float xbs[16];                     // conv2 bias partials of the lane's 16 x channels, all steps
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xbs[i] = 0.f;
 
-  // The epilogue's HBM inputs for one column block (4 channel groups g of the lane)
-  struct EpIn { f32x4 dO[4], cc[4], cp[4]; u32x4 gt[4][2]; };
-  auto load_in = [&](int s, int cb, int ln) {
+  // The epilogue's HBM inputs of one unit u = (g, cb) (g-major): dO, c_s, c_{s-1}
+  // (16 B each) and the 16 fp16 gates (32 B) of the lane's 4 channels at one pixel.
+  // A ring of kRing units is in flight: the first kRing-1 are requested under the
+  // GEMM's last chunk, each later one as the unit kRing-1 before it is processed.
+  struct EpIn { f32x4 dO, cc, cp; u32x4 gt[2]; };
+  constexpr int kRing = 4;
+  auto load_in = [&](int s, int u, int ln) {
     EpIn in;
-    const int pp = cb * 32 + (ln & 31);
+    const int g = u >> 2, cb = u & 3, pp = cb * 32 + (ln & 31);
     if (pp < P && !(ABL & 2)) {
       const size_t row = (size_t)s * M + (size_t)b * P + pp;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
-        in.dO[g] = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
-        in.cc[g] = *reinterpret_cast<const f32x4*>(p.Cst + (row + M) * 128 + ch);   // c_s
-        in.cp[g] = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
-        const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
-        in.gt[g][0] = gp[0];
-        in.gt[g][1] = gp[1];
-      }
+      const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
+      in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
+      in.cc = *reinterpret_cast<const f32x4*>(p.Cst + (row + M) * 128 + ch);   // c_s
+      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
+      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
+      in.gt[0] = gp[0];
+      in.gt[1] = gp[1];
     } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        in.dO[g] = in.cc[g] = in.cp[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        in.gt[g][0] = in.gt[g][1] = u32x4{0u, 0u, 0u, 0u};
-      }
+      in.dO = in.cc = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
+      in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
     }
     return in;
   };
@@ -156,32 +179,28 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
   // Gate backward of step s on the GEMM result (acc = dh_s from step s+1, zero
   // for s = T-1): dZ_s to HBM (bf16) and, for chunks 0 and 1, into image w; the
   // lane's dc carry advances to step s-1; gate-bias partials of step s.
-  // ``in0``: the inputs of column block 0, already requested.
-  auto epilogue = [&](int s, const f32x16 (&acc)[4], bool gemm, EpIn in0) {
+  // ``ring``: units 0 .. kRing-2 already requested.
+  auto epilogue = [&](int s, const f32x16 (&acc)[4], bool gemm, EpIn (&ring)[kRing]) {
     int ln = lane;   // laundered: the epilogue's addresses are recomputed per step, not hoisted
     asm volatile("" : "+v"(ln));
     const int pl = ln & 31, hq = ln >> 5;
     const int c0 = 32 * wave + 4 * hq;   // + 8g + e
     const size_t rows = (size_t)s * M + (size_t)b * P;
-    float bs[4][4][4];   // [g][e][gate] sums over the lane's pixels
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 4; ++g) {
+      float bs[16];   // [e][gate] sums over the lane's pixels (this channel group)
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int i = 0; i < 16; ++i) bs[i] = 0.f;
+      const int ch = c0 + 8 * g;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bs[g][e][q] = 0.f;
-    EpIn cur = in0;
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      EpIn nxt;
-      if (cb < 3) nxt = load_in(s, cb + 1, ln);   // one column block ahead
-      const int pp = cb * 32 + pl;
-      if (pp < P) {
-        const size_t row = rows + pp;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int ch = c0 + 8 * g;
-          f32x4 dh = cur.dO[g];
+      for (int cb = 0; cb < 4; ++cb) {
+        const int u = g * 4 + cb;
+        if (u + kRing - 1 < 16) ring[(u + kRing - 1) % kRing] = load_in(s, u + kRing - 1, ln);
+        const EpIn& in = ring[u % kRing];
+        const int pp = cb * 32 + pl;
+        if (pp < P) {
+          const size_t row = rows + pp;
+          f32x4 dh = in.dO;
           if (gemm) {
             dh[0] += acc[cb][4 * g]; dh[1] += acc[cb][4 * g + 1]; dh[2] += acc[cb][4 * g + 2]; dh[3] += acc[cb][4 * g + 3];
           } else if (p.dhT) {
@@ -193,15 +212,15 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
           float dz[16];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const uint32_t w01 = cur.gt[g][e >> 1][2 * (e & 1)], w23 = cur.gt[g][e >> 1][2 * (e & 1) + 1];
+            const uint32_t w01 = in.gt[e >> 1][2 * (e & 1)], w23 = in.gt[e >> 1][2 * (e & 1) + 1];
             typedef _Float16 h2 __attribute__((ext_vector_type(2)));
             const h2 a = __builtin_bit_cast(h2, w01), c2 = __builtin_bit_cast(h2, w23);
             const f32x4 gv{(float)a[0], (float)a[1], (float)c2[0], (float)c2[1]};
             float d = dc[e], di, df, dcg, dout;
-            gate_bwd(dh[e], gv, cur.cp[g][e], cur.cc[g][e], d, di, df, dcg, dout);
+            gate_bwd_fast(dh[e], gv, in.cp[e], in.cc[e], d, di, df, dcg, dout);
             dc[e] = d;
             dz[4 * e] = di; dz[4 * e + 1] = df; dz[4 * e + 2] = dcg; dz[4 * e + 3] = dout;
-            bs[g][e][0] += di; bs[g][e][1] += df; bs[g][e][2] += dcg; bs[g][e][3] += dout;
+            bs[4 * e] += di; bs[4 * e + 1] += df; bs[4 * e + 2] += dcg; bs[4 * e + 3] += dout;
           }
           *dcp = dc;
           bf16x8 z0, z1;
@@ -218,57 +237,51 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
             *reinterpret_cast<bf16x8*>(zi + 16) = z1;
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (cb < 3) cur = nxt;
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // gate-bias partials: butterfly transpose-reduce of the 64 row sums over the
-    // 32 pixel lanes of each half: after 5 exchange steps lane r32 holds the
-    // totals of rows 2*r32 and 2*r32+1 of its half's 64 (g, e, gate) rows
-    float v[64];
+      // gate-bias partials of channel group g: butterfly transpose-reduce of the 16
+      // row sums over the 32 pixel lanes of each half; after 4 exchange steps and a
+      // final pair add, lanes pl and pl^1 hold row ridx's total
+      int n = 16;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
+      for (int m = 16; m >= 2; m >>= 1) {
+        const bool up = (pl & m) != 0;
+        n >>= 1;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[16 * g + 4 * e + q] = bs[g][e][q];
-    int n = 64;
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) {
-      const bool up = (pl & m) != 0;
-      n >>= 1;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        if (i < n) {
-          const float send = up ? v[i] : v[i + n];
-          const float keep = up ? v[i + n] : v[i];
-          v[i] = keep + __shfl_xor(send, m, 64);
+        for (int i = 0; i < 8; ++i) {
+          if (i < n) {
+            const float send = up ? bs[i] : bs[i + n];
+            const float keep = up ? bs[i + n] : bs[i];
+            bs[i] = keep + __shfl_xor(send, m, 64);
+          }
         }
       }
-    }
-    // lane pl now owns rows ridx, ridx+1 of its half: the exchange at distance m
-    // kept the upper half of the remaining rows where pl has bit m set
-    const int ridx = ((pl & 16) ? 32 : 0) + ((pl & 8) ? 16 : 0) + ((pl & 4) ? 8 : 0) + ((pl & 2) ? 4 : 0) + ((pl & 1) ? 2 : 0);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int r = ridx + j, g = r >> 4, e = (r >> 2) & 3, q = r & 3;
-      p.part[((size_t)s * p.B + b) * 512 + 4 * (c0 + 8 * g + e) + q] = v[j];
+      bs[0] += __shfl_xor(bs[0], 1, 64);
+      const int ridx = ((pl & 16) ? 8 : 0) + ((pl & 8) ? 4 : 0) + ((pl & 4) ? 2 : 0) + ((pl & 2) ? 1 : 0);
+      if ((pl & 1) == 0)   // row ridx = 4e + gate of channel ch + e
+        p.part[((size_t)s * p.B + b) * 512 + 4 * (ch + (ridx >> 2)) + (ridx & 3)] = bs[0];
     }
   };
 
   {  // step T-1: no GEMM (dh = dO_{T-1} + dhT)
     f32x16 zero[4];
-    epilogue(p.T - 1, zero, false, load_in(p.T - 1, 0, lane));
+    EpIn ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(p.T - 1, u, lane);
+    epilogue(p.T - 1, zero, false, ring);
   }
   barrier_lds();   // chunk images 0, 1 of dZ_{T-1}
 
   for (int t = p.T - 1; t >= 0; --t) {
-    if (t == 0 && !p.dh0) break;
-    f32x16 acc[4];
+    f32x16 acc[4], accx[2];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accx[j][e] = 0.f;
     int hbs[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -284,43 +297,81 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
     };
     constexpr int BD = 4;   // B fragment ring: BD-1 k steps of lookahead (LDS latency vs 4 MFMAs per k step)
     bf16x8 bfr[BD][4];
-    EpIn in0;
-#pragma unroll 1
-    for (int ck = 0; ck < 4; ++ck) {
-      const unsigned char* img = zim + (ck & 1) * kBwIB;
-      if (ck == 1 || ck == 2) {   // every wave is done with image ck-1 and every wave's dZ_t stores have
-                                  // retired (its later A loads did): refill it with chunk ck+1 from HBM
-        if constexpr (!(ABL & 8)) dma_chunk(t, ck + 1);
+    EpIn ring[kRing];
+    // the K loop, with the wave's dx column blocks XC, XC+1 a compile-time constant
+    // (a uniform select between fragment registers would be a per-k-step copy)
+    auto kloop = [&](auto xc) {
+      constexpr int XC = decltype(xc)::value;
+  #pragma unroll 1
+      for (int ck = 0; ck < 4; ++ck) {
+        const unsigned char* img = zim + (ck & 1) * kBwIB;
+        if (ck == 1 || ck == 2) {   // every wave is done with image ck-1 and every wave's dZ_t stores have
+                                    // retired (its later A loads did): refill it with chunk ck+1 from HBM
+          if constexpr (!(ABL & 8)) dma_chunk(t, ck + 1);
+        }
+        if (ck == 3 && t > 0) {   // the epilogue's first inputs, under chunk 3
+          int ln = lane;
+          asm volatile("" : "+v"(ln));
+  #pragma unroll
+          for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(t - 1, u, ln);
+        }
+  #pragma unroll
+        for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
+        for (int tap = 0; tap < 9; ++tap) {
+          const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+          int kt = ck * 72 + tap * 8;
+          asm volatile("" : "+s"(kt));
+  #pragma unroll
+          for (int c16 = 0; c16 < 8; ++c16) {
+            if constexpr (!(ABL & 1)) {
+              af[(c16 + PD - 1) % PD][0] = lda(kt + c16 + PD - 1, 0);
+              af[(c16 + PD - 1) % PD][1] = lda(kt + c16 + PD - 1, 1);
+            }
+            {  // B of k step + BD - 1 (same chunk)
+              const int cn = c16 + BD - 1;
+              if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
+              else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+  #pragma unroll
+            for (int cb = 0; cb < 4; ++cb) {
+              if constexpr (ABL & 4) acc[cb][0] += (float)af[c16 % PD][0][0] * (float)bfr[c16 % BD][cb][0];
+              else acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][0], bfr[c16 % BD][cb], acc[cb], 0, 0, 0);
+            }
+  #pragma unroll
+            for (int j = 0; j < 2; ++j) {   // dx rows: the B fragments of column blocks xcb, xcb + 1
+              const bf16x8 bx = bfr[c16 % BD][XC + j];
+              if constexpr (!(ABL & 4))
+                accx[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][1], bx, accx[j], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        barrier_lds();   // image ck & 1 free; (ck >= 1) the DMA'd chunk ck+1 has landed in every wave
       }
-      if (ck == 3 && t > 0) in0 = load_in(t - 1, 0, lane);   // the epilogue's first inputs, under chunk 3
+    };
+    if (wave >> 1) kloop(std::integral_constant<int, 2>{});
+    else kloop(std::integral_constant<int, 0>{});
+    {  // dx_t (conv2 output grad) to HBM in bf16; its fp32 sums into the conv2 bias partials
+      const size_t rows = (size_t)t * M + (size_t)b * P;
 #pragma unroll
-      for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
-      for (int tap = 0; tap < 9; ++tap) {
-        const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
-        int kt = ck * 72 + tap * 8;
-        asm volatile("" : "+s"(kt));
+      for (int j = 0; j < 2; ++j) {
+        const int pp = (xcb + j) * 32 + r32;
 #pragma unroll
-        for (int c16 = 0; c16 < 8; ++c16) {
-          if constexpr (!(ABL & 1)) af[(c16 + PD - 1) % PD] = lda(kt + c16 + PD - 1);
-          {  // B of k step + BD - 1 (same chunk)
-            const int cn = c16 + BD - 1;
-            if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
-            else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
+        for (int g = 0; g < 4; ++g) {
+          const float v[4] = {accx[j][4 * g], accx[j][4 * g + 1], accx[j][4 * g + 2], accx[j][4 * g + 3]};
+          if (pp < P) {
+            *reinterpret_cast<bf16x4*>(p.dY2 + (rows + pp) * 64 + 32 * (wave & 1) + 8 * g + 4 * hh) =
+                bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) xbs[4 * g + e] += v[e];
           }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            if constexpr (ABL & 4) acc[cb][0] += (float)af[c16 % PD][0] * (float)bfr[c16 % BD][cb][0];
-            else acc[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD], bfr[c16 % BD][cb], acc[cb], 0, 0, 0);
-          }
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
-      barrier_lds();   // image ck & 1 free; (ck >= 1) the DMA'd chunk ck+1 has landed in every wave
     }
     if (t > 0) {
-      epilogue(t - 1, acc, true, in0);
-    } else {   // dh_{-1}: the gradient of the initial state h0
+      epilogue(t - 1, acc, true, ring);
+    } else if (p.dh0) {   // dh_{-1}: the gradient of the initial state h0
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int pp = cb * 32 + r32;
@@ -332,6 +383,31 @@ __global__ void __launch_bounds__(256) k_convlstm_bwd_frames(RecBwdParams p) {
       }
     }
     barrier_lds();   // chunk images 0, 1 of dZ_{t-1} complete
+  }
+  {  // conv2 bias partials: reduce the 16 x-channel sums over the 32 pixel lanes of each half
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xbs[i];
+    int n = 16;
+#pragma unroll
+    for (int m = 16; m >= 2; m >>= 1) {
+      const bool up = (r32 & m) != 0;
+      n >>= 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i < n) {
+          const float send = up ? v[i] : v[i + n];
+          const float keep = up ? v[i + n] : v[i];
+          v[i] = keep + __shfl_xor(send, m, 64);
+        }
+      }
+    }
+    v[0] += __shfl_xor(v[0], 1, 64);   // lanes r32 and r32 ^ 1 now both hold row ridx's total
+    const int ridx = ((r32 & 16) ? 8 : 0) + ((r32 & 8) ? 4 : 0) + ((r32 & 4) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
+    if ((r32 & 1) == 0) {   // row ridx = 4g + e: x channel 32(w%2) + 8g + 4hh + e; two waves share each channel set
+      const int g = ridx >> 2, e = ridx & 3;
+      atomicAdd(p.dxb + (size_t)b * 64 + 32 * (wave & 1) + 8 * g + 4 * hh + e, v[0]);
+    }
   }
   // dc carry out (dc_0)
 #pragma unroll

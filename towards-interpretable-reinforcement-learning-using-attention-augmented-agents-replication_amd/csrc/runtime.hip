@@ -75,7 +75,7 @@ struct Layout {
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
-  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
   // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
@@ -127,7 +127,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.k_WpXH = take(512 * 1728 * e);     // [x | h] step operand (fused x-part, bf16 default)
   L.k_Wfr = take(e == 2 ? (size_t)16 * kRecKSP * 64 * 16 : 0);   // its fragment-order copy (frame-resident recurrence, recur.h)
   L.k_WdTl = take(192 * 4608 * e);
-  L.k_Wbf = take(e == 2 ? (size_t)4 * kBwKSP * 64 * 16 : 0);   // fragment-order W_h^T (frame-resident BPTT)
+  L.k_Wbf = take(e == 2 ? (size_t)6 * kBwKSP * 64 * 16 : 0);   // fragment-order [W_h^T | W_x^T] (frame-resident BPTT)
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
   L.k_Wihp = take(1024 * 256 * 4);
@@ -168,6 +168,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dZp = take((size_t)L.T * ((M + 31) / 32) * 512 * 4);  // gate-bias partials per (step, column tile)
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
+  L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -638,7 +639,7 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
                           (T*)(pk + L.k_WpXH), st));
   if constexpr (!std::is_same<T, float>::value) {
     HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
-    HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl) + (size_t)64 * 4608, (__bf16*)(pk + L.k_Wbf), st));
+    HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
   }
   F32Pack fp;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
@@ -1408,6 +1409,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   // -- the conv2/conv1 backward of those frames.  Every gradient accumulates
   // atomically into zeroed buffers, so chunks may run in any order.
   const bool vision_here = (phases & AAA_BWD_VISION) && (phases & AAA_BWD_CORE);
+  bool dx_fused = false;   // the frame-resident BPTT computed dx (dY2) and conv2's bias gradient itself
   auto core_chunk = [&](int lo, int hi, hipStream_t s) -> int {
     const int rows = (hi - lo) * M;                       // pixels of these frames
     const int F1 = (hi - lo) * L.B;                       // frames
@@ -1416,7 +1418,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       const int rc = lstm_wgrad<T>(dz, Wt(L.XH) + (size_t)lo * M * 192, rows, L.h, L.w, Wf(L.gWpl), s, s != st);
       if (rc) return rc;
     }
-    {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
+    if (!dx_fused) {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       const T* WdT = (const T*)(pk + L.k_WdTl);
       const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
@@ -1524,10 +1526,16 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     if (fb) {
       if constexpr (!std::is_same<T, float>::value) {
         RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
-                        Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, L.T, L.B, L.h, L.w, L.P};
-        TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
-                       strf("bf16 frame-resident BPTT, %d steps per launch, 1 WG per frame, fp16 gates", L.T));
-        HIPCHK(convlstm_bwd_frames(rp, st));
+                        Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), L.T, L.B, L.h, L.w, L.P};
+        HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
+        {
+          // work: the h rows over T-1 steps (+ dh0) and the dx rows over all T (the batched dx it replaces)
+          TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 4608 * (128.0 * (L.T - 1 + (io->dh0 ? 1 : 0)) + 64.0 * L.T),
+                         strf("bf16 frame-resident BPTT + dx, %d steps per launch, 1 WG per frame, fp16 gates", L.T));
+          HIPCHK(convlstm_bwd_frames(rp, st));
+        }
+        HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
+        dx_fused = true;
       }
     }
     for (int t = fb ? -1 : t1; t >= 0; --t) {
