@@ -144,13 +144,14 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
 # per-step launches it replaces: single step, ragged B, a full T=20 unroll,
 # frames padded to 128 pixel columns (P = 121), carried state across calls.
 @pytest.mark.parametrize("T,B", [(1, 1), (2, 2), (3, 5), (20, 3)])
-@pytest.mark.parametrize("bwd", ["0", "1"])
-def test_frame_resident_forward(cuda, monkeypatch, T, B, bwd):
-    """... and the frame-resident BPTT (csrc/recur_bwd.h, AAA_FRAMES_BWD) on top."""
-    monkeypatch.setenv("AAA_FRAMES_FWD", "1")
+@pytest.mark.parametrize("fwd,bwd", [("1", "0"), ("1", "1"), ("2", "0")])
+def test_frame_resident_forward(cuda, monkeypatch, T, B, fwd, bwd):
+    """... with one (1) or two cooperating (2) workgroups per frame, and the
+    frame-resident BPTT (csrc/recur_bwd.h, AAA_FRAMES_BWD) on top."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", fwd)
     monkeypatch.setenv("AAA_FRAMES_BWD", bwd)
     out = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
-    _compare(out, _oracle(T, B, conv_mode="bf16"), 2e-2, f"frames T={T} B={B} bwd={bwd}: ")
+    _compare(out, _oracle(T, B, conv_mode="bf16"), 2e-2, f"frames T={T} B={B} fwd={fwd} bwd={bwd}: ")
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")
     monkeypatch.setenv("AAA_FRAMES_BWD", "0")
     step = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
@@ -187,10 +188,11 @@ def test_frame_resident_state_gradients(cuda, monkeypatch, frames):
             assert_close(g[n].numpy(), ref[3][n].float().numpy(), 2e-2, "grad " + n)
 
 
-def test_frame_resident_carried_state(cuda, monkeypatch):
+@pytest.mark.parametrize("fwd", ["1", "2"])
+def test_frame_resident_carried_state(cuda, monkeypatch, fwd):
     """Two calls of T=3 (the state carried in ConvLSTMCell.prev_hidden, i.e. a
     non-zero h_0 / c_0 image) equal one call of T=6."""
-    monkeypatch.setenv("AAA_FRAMES_FWD", "1")
+    monkeypatch.setenv("AAA_FRAMES_FWD", fwd)
     T, B = 6, 3
     ag = _agent(cuda, conv_dtype="bf16")
     X = _frames(T, B).to(cuda)

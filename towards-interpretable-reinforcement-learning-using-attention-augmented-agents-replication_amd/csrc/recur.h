@@ -78,25 +78,39 @@ struct RecFwdParams {
   float* Cst;          // (T+1, B, P, 128): slot 0 = c_0 (read), slot t+1 <- c_t
   float* Hs;           // (T, B, P, 128) <- h_t (fp32)
   GT* Gt;              // (T, B, P, 512) <- gate activations (i, f, c~, o)
+  int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed), [2B] = timeout word
   int T, B, h, w, P;
 };
 
 // ABL (diagnostic A/B only, AAA_REC_ABL): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
-template <typename GT, int ABL = 0>
+//
+// G = 2 (batches too small to give every CU a frame): two workgroups per frame,
+// half kh owning gate rows [256kh, 256kh+256) (its 64 channels); each step it
+// publishes its half of h_t through XH slot t+1 (written anyway: the weight-
+// gradient operand) and a release / acquire flag, and reads the partner's half
+// into its h image after its own x-part -- the hand-off's latency hides under
+// the x-part GEMM.  Launched cooperatively (co-residency checked), spins bounded.
+template <typename GT, int G = 1, int ABL = 0>
 __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
+  constexpr int NRB = 4 / G, GCH = 8 * NRB;     // row blocks and channels per wave
+  constexpr int GTP = GCH * 8 + 16, CHP = GCH * 4 + 16;   // staging pixel pitches (gates fp16x4, c / h fp32)
   __shared__ __attribute__((aligned(16))) unsigned char xim[kRecXB];
   __shared__ __attribute__((aligned(16))) __bf16 him[kRecNPH * kRecHS];
-  __shared__ __attribute__((aligned(16))) float cstl[4 * 64 * 64];   // c, lane-native: [wave][rb][cb][g][lane]
+  __shared__ __attribute__((aligned(16))) float cstl[4 * NRB * 16 * 64];   // c, lane-native: [wave][rb][cb][g][lane]
   __shared__ __attribute__((aligned(16))) float sbias[512];
-  __shared__ __attribute__((aligned(16))) unsigned char stg[4 * kRecStg];
-  const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) unsigned char stg[4 * 16 * (GTP > 2 * CHP ? GTP : 2 * CHP)];
+  constexpr int STG = 16 * (GTP > 2 * CHP ? GTP : 2 * CHP);
+  const int b = (int)blockIdx.x % p.B, kh = G == 1 ? 0 : (int)blockIdx.x / p.B;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR) for the buffer soffsets
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
-  float* cw = cstl + wave * 64 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
+  const int rb0 = kh * (16 / G) + wave * NRB;   // the wave's first global row block (32 rows = 8 channels)
+  const int cbase = 8 * rb0;                     // its first channel
+  float* cw = cstl + wave * NRB * 16 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
 
   {  // zero the h image (its border stays zero), bias into LDS
     u32x4* z = reinterpret_cast<u32x4*>(him);
@@ -122,14 +136,14 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   dma_x(0);
   // cell state c_0 (Cst slot 0) into the lane-native LDS copy
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int pp = cb * 32 + r32;
         cw[(rb * 16 + cb * 4 + g) * 64] =
-            pp < P ? p.Cst[((size_t)b * P + pp) * 128 + 32 * wave + 8 * rb + 2 * g + hh] : 0.f;
+            pp < P ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
       }
   __syncthreads();   // h image zeroed
   {  // h_0 (slot 0, channels 64..191) into the image
@@ -151,24 +165,24 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   // A stream: one buffer descriptor over the fragment-order weights, the lane's
   // 16 B at voffset lane*16, the (row block, k step) in the wave-uniform soffset
   const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wf, (uint32_t)(16 * kRecKSP * 1024));
-  const int wofs = 4 * wave * kRecKSP * 1024;
+  const int wofs = rb0 * kRecKSP * 1024;
   auto lda = [&](int ks, int j) {
     return __builtin_bit_cast(bf16x8,
                               __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, wofs + (j * kRecKSP + ks) * 1024, 0));
   };
   constexpr int PD = kRecPD;
-  bf16x8 af[PD][4];
+  bf16x8 af[PD][NRB];
 #pragma unroll
   for (int s = 0; s < PD - 1; ++s)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) af[s][j] = lda(s, j);
+    for (int j = 0; j < NRB; ++j) af[s][j] = lda(s, j);
   __syncthreads();   // images of step 0 complete (this wave's x DMA retired before: vmcnt in order)
 
-  unsigned char* sw = stg + wave * kRecStg;   // this wave's epilogue staging
+  unsigned char* sw = stg + wave * STG;   // this wave's epilogue staging
   for (int t = 0; t < p.T; ++t) {
-    f32x16 acc[4][4];
+    f32x16 acc[NRB][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NRB; ++j)
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -197,12 +211,12 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     auto kstep = [&](int ks, int slot, bf16x8 (&bc)[4], auto&& load_next_b) {
       if constexpr (!(ABL & 1)) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) af[(slot + PD - 1) % PD][j] = lda(ks + PD - 1, j);
+        for (int j = 0; j < NRB; ++j) af[(slot + PD - 1) % PD][j] = lda(ks + PD - 1, j);
       }
       if constexpr (!(ABL & 8)) load_next_b();
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NRB; ++j)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           if constexpr (ABL & 4)
@@ -224,11 +238,34 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         kstep(kt + c4, c4 % PD, bfr[c4 & 1], [&] {
           if (c4 < 3) ldx(toff, c4 + 1, bfr[(c4 + 1) & 1]);
           else if (tap < 8) ldx(tn, 0, bfr[0]);
-          else ldh(0, 0, bfr[0]);
+          else if (G == 1) ldh(0, 0, bfr[0]);
         });
     }
     barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
     if (t + 1 < p.T) dma_x(t + 1);
+    if constexpr (G == 2) {
+      if (t > 0) {   // the partner's half of h_{t-1} (XH slot t) into the image, once it has published it
+        if (tid == 0) {
+          int n = 0;
+          while (__hip_atomic_load(p.flags + 2 * b + (1 - kh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++n > (1 << 24)) {   // bounded: a stranded partner reports, never hangs the GPU
+              __hip_atomic_store(p.flags + 2 * p.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        barrier_lds();
+        const __bf16* src = p.XH + ((size_t)t * M + (size_t)b * P) * 192 + 64 + 64 * (1 - kh);
+        for (int i = tid; i < P * 8; i += 256)
+          *reinterpret_cast<u32x4*>(him + hidx(i >> 3) * kRecHS + 64 * (1 - kh) + (i & 7) * 8) =
+              *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 3) * 192 + (i & 7) * 8);
+        barrier_lds();
+      }
+      ldh(0, 0, bfr[0]);
+    }
     // h-part: 9 taps x 8 chunks (k steps 36..107)
     for (int tap = 0; tap < 9; ++tap) {
       const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
@@ -254,15 +291,15 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     asm volatile("" : "+v"(ln));
     const int pl = ln & 31, hl_ = ln >> 5;
     const size_t rowt = (size_t)t * M + (size_t)b * P;   // this frame's rows of step t (Hs, Gt)
-    const int c0 = 32 * wave + hl_;                       // + 8*rb + 2*g
+    const int c0 = cbase + hl_;                          // + 8*rb + 2*g
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int pp = cb * 32 + pl;
       __bf16* hl = him + hidx(min(pp, P - 1)) * kRecHS + c0;
-      uint32_t gq[4][4][2];   // fp16 gate quads (i, f, c~, o), packed
-      float hv[4][4], cv[4][4];
+      uint32_t gq[NRB][4][2];   // fp16 gate quads (i, f, c~, o), packed
+      float hv[NRB][4], cv[NRB][4];
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int co = 8 * rb + 2 * g;
@@ -271,7 +308,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           const float gf = sigm_fast(acc[rb][cb][4 * g + 1] + bz[1]);
           const float gc = tanh_fast(acc[rb][cb][4 * g + 2] + bz[2]);
           const float go = sigm_fast(acc[rb][cb][4 * g + 3] + bz[3]);
-          float* cl = cstl + wave * 64 * 64 + ln + (rb * 16 + cb * 4 + g) * 64;
+          float* cl = cstl + wave * NRB * 16 * 64 + ln + (rb * 16 + cb * 4 + g) * 64;
           const float c = gf * *cl + gi * gc;
           const float h = go * tanh_fast(c);
           *cl = c;
@@ -289,40 +326,41 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           const bool mine = (pl >> 4) == half;
           const int pbase = cb * 32 + half * 16;   // first pixel of this half
           if (pbase >= P) break;
-          // gates: staging [16 px][32 ch][4] fp16 at pixel pitch 272 B
+          // gates: staging [16 px][GCH ch][4] fp16 at pixel pitch GTP
           if (mine) {
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
+            for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
               for (int g = 0; g < 4; ++g)
-                *reinterpret_cast<uint2*>(sw + pxl * 272 + (8 * rb + 2 * g + hl_) * 8) = uint2{gq[rb][g][0], gq[rb][g][1]};
+                *reinterpret_cast<uint2*>(sw + pxl * GTP + (8 * rb + 2 * g + hl_) * 8) = uint2{gq[rb][g][0], gq[rb][g][1]};
           }
+          constexpr int CG = GCH / 2, CC = GCH / 4;   // 16-B chunks per pixel row: gates, c / h
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {   // 4 x 1 KB: 4 pixel rows of 256 B each
-            const int q = k * 64 + ln, px = q >> 4, pix = pbase + px;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * 272 + (q & 15) * 16);
+          for (int k = 0; k < NRB; ++k) {   // 1 KB each: 64 / CG pixel rows of 8 * GCH B
+            const int q = k * 64 + ln, px = q / CG, pix = pbase + px;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * GTP + (q % CG) * 16);
             if (pix < P)
-              *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * 32 * wave) +
-                                        (q & 15) * 16) = v;
+              *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * cbase) +
+                                        (q % CG) * 16) = v;
           }
-          // c_t and h_t: staging [16 px][32 ch] fp32 at pixel pitch 144 B (c), then (h) 2304 B on
+          // c_t and h_t: staging [16 px][GCH ch] fp32 at pixel pitch CHP (c), then (h) 16 * CHP B on
           if (mine) {
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
+            for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
               for (int g = 0; g < 4; ++g) {
-                *reinterpret_cast<float*>(sw + pxl * 144 + (8 * rb + 2 * g + hl_) * 4) = cv[rb][g];
-                *reinterpret_cast<float*>(sw + 2304 + pxl * 144 + (8 * rb + 2 * g + hl_) * 4) = hv[rb][g];
+                *reinterpret_cast<float*>(sw + pxl * CHP + (8 * rb + 2 * g + hl_) * 4) = cv[rb][g];
+                *reinterpret_cast<float*>(sw + 16 * CHP + pxl * CHP + (8 * rb + 2 * g + hl_) * 4) = hv[rb][g];
               }
           }
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {   // 2 x 1 KB each: 8 pixel rows of 128 B
-            const int q = k * 64 + ln, px = q >> 3, pix = pbase + px;
-            const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * 144 + (q & 7) * 16);
-            const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 2304 + px * 144 + (q & 7) * 16);
+          for (int k = 0; k < NRB / 2; ++k) {   // 1 KB each of c and h: 64 / CC pixel rows of 4 * GCH B
+            const int q = k * 64 + ln, px = q / CC, pix = pbase + px;
+            const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * CHP + (q % CC) * 16);
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 16 * CHP + px * CHP + (q % CC) * 16);
             if (pix < P) {
-              *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + 32 * wave + (q & 7) * 4) = vc;
-              *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + 32 * wave + (q & 7) * 4) = vh;
+              *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + cbase + (q % CC) * 4) = vc;
+              *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + cbase + (q % CC) * 4) = vh;
             }
           }
         }
@@ -330,24 +368,45 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       __builtin_amdgcn_sched_barrier(0);   // one column block at a time (register pressure)
     }
     barrier_lds();   // h_t image and x_{t+1} image complete (this wave's DMA retired under its h-part A loads)
-    // h_t (bf16) into XH slot t+1 channels 64..191 (the weight-gradient operand), from the image
+    // h_t (bf16, this workgroup's channels) into XH slot t+1 (the weight-gradient operand), from the image
     const size_t rown = rowt + M;   // slot t+1
-    for (int i = tid; i < ((ABL & 2) ? 0 : P * 16); i += 256)
-      *reinterpret_cast<u32x4*>(p.XH + (rown + (i >> 4)) * 192 + 64 + (i & 15) * 8) =
-          *reinterpret_cast<const u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8);
+    constexpr int HC = 16 / G;      // 16-B chunks (8 channels) per pixel of this workgroup
+    for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
+      const int px = i / HC, q = i % HC + HC * kh;
+      *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
+          *reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8);
+    }
+    if constexpr (G == 2) {   // publish h_t's half: every wave's stores retired, then release + flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.flags + 2 * b + kh, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
+// G = 1: one workgroup per frame; G = 2: two per frame, launched cooperatively
+// (p.flags zeroed by the caller; the launch fails rather than strand a half).
 template <typename GT>
-inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, hipStream_t st) {
-  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1) return hipErrorInvalidValue;
+inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStream_t st) {
+  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (G != 1 && G != 2)) return hipErrorInvalidValue;
+  if (G == 2) {
+    if (!p.flags) return hipErrorInvalidValue;
+    RecFwdParams<GT> q = p;
+    void* args[] = {&q};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>), dim3(2 * p.B),
+                                      dim3(256), args, 0, st);
+  }
   const char* e = getenv("AAA_REC_ABL");
   switch (e ? atoi(e) : 0) {
 #define AAA_REC_CASE(a) \
-  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, a>), dim3(p.B), dim3(256), 0, st, p); break;
+  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, p); break;
     AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12)
 #undef AAA_REC_CASE
-    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 0>), dim3(p.B), dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, 0>), dim3(p.B), dim3(256), 0, st, p); break;
   }
   return hipGetLastError();
 }

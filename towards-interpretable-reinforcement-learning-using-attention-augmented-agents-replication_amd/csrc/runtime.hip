@@ -75,7 +75,7 @@ struct Layout {
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
-  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
   // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
@@ -169,6 +169,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
+  L.rflags = take(((size_t)2 * L.B + 1) * 4);   // hand-off flags of the paired frame-resident kernels
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -450,7 +451,7 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
 // frames), once the batch fills most of the chip's 256 CUs (C3, B=256: 55 vs
 // 79 us per step; C4's B=128 leaves half the CUs idle: 49 vs 43 us,
 // profiles/r02/frames).  AAA_FRAMES_FWD=1/0 forces it on/off.
-static bool frames_fwd(const struct Layout& L);
+static int frames_fwd(const struct Layout& L);
 static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
 static bool gates_f16(int dt, int M) {
   if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
@@ -718,15 +719,31 @@ static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, 
 }
 
 // ------------------------------------------------------------- forward ----
-static bool frames_fwd(const Layout& L) {
-  return L.dt == AAA_BF16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_FWD", L.B >= 160 ? 1 : 0) != 0;
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
+                                                                                                 : 256;
+  }
+  return cus;
 }
+// Workgroups per frame of the frame-resident kernels (0: per-step launches):
+// 1 once the batch fills most of the CUs, 2 (cooperative pairs) while two per
+// frame still fit the chip, else the per-step kernels.  AAA_FRAMES_FWD /
+// AAA_FRAMES_BWD = 0 / 1 / 2 force it.
+static int frames_g(const Layout& L, const char* env) {
+  if (L.dt != AAA_BF16 || !rec_fits(L.h, L.w)) return 0;
+  const int cus = device_cus();
+  const int v = env_int(env, L.B >= (cus * 5) / 8 ? 1 : (L.B >= 32 && 2 * L.B <= cus ? 2 : 0));
+  return v == 1 ? 1 : (v == 2 && 2 * L.B <= cus ? 2 : 0);
+}
+static int frames_fwd(const Layout& L) { return frames_g(L, "AAA_FRAMES_FWD"); }
 // The BPTT chain on the frame-resident kernel (recur_bwd.h; fp16 gate storage),
 // from the same batch on (C3: 55 vs 69 us per step; C4: 52 vs 49 us).
 // AAA_FRAMES_BWD=1/0 forces it on/off.
-static bool frames_bwd(const Layout& L, bool g16) {
-  return L.dt == AAA_BF16 && g16 && rec_fits(L.h, L.w) && env_int("AAA_FRAMES_BWD", L.B >= 160 ? 1 : 0) != 0;
-}
+static bool frames_bwd(const Layout& L, bool g16) { return g16 && frames_g(L, "AAA_FRAMES_BWD") == 1; }
 
 template <typename T>
 static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
@@ -762,12 +779,13 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
       if constexpr (!std::is_same<T, float>::value) {
-        if (frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
+        if (const int G = frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
+          if (G == 2) HIPCHK(hipMemsetAsync(ws + L.rflags, 0, ((size_t)2 * L.B + 1) * 4, st));
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
-                              Wf(L.Hs), (GT*)(ws + L.Gt), L.T, L.B, L.h, L.w, L.P};
+                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P};
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
-                         strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, 1 WG per frame", L.T));
-          HIPCHK(convlstm_fwd_frames<GT>(rp, st));
+                         strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame", L.T, G));
+          HIPCHK(convlstm_fwd_frames<GT>(rp, G, st));
           return AAA_OK;
         }
       }
