@@ -144,10 +144,11 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
 # per-step launches it replaces: single step, ragged B, a full T=20 unroll,
 # frames padded to 128 pixel columns (P = 121), carried state across calls.
 @pytest.mark.parametrize("T,B", [(1, 1), (2, 2), (3, 5), (20, 3)])
-@pytest.mark.parametrize("fwd,bwd", [("1", "0"), ("1", "1"), ("2", "0")])
+@pytest.mark.parametrize("fwd,bwd", [("1", "0"), ("1", "1"), ("2", "0"), ("2", "2")])
 def test_frame_resident_forward(cuda, monkeypatch, T, B, fwd, bwd):
     """... with one (1) or two cooperating (2) workgroups per frame, and the
-    frame-resident BPTT (csrc/recur_bwd.h, AAA_FRAMES_BWD) on top."""
+    frame-resident BPTT (csrc/recur_bwd.h, AAA_FRAMES_BWD: 1 = one workgroup,
+    2 = the paired kernel) on top."""
     monkeypatch.setenv("AAA_FRAMES_FWD", fwd)
     monkeypatch.setenv("AAA_FRAMES_BWD", bwd)
     out = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
@@ -164,7 +165,7 @@ def test_frame_resident_forward(cuda, monkeypatch, T, B, fwd, bwd):
             assert rel_err(out[3][n].numpy(), step[3][n].numpy()) <= 5e-3, f"frames vs per-step grad {n}"
 
 
-@pytest.mark.parametrize("frames", ["0", "1"])
+@pytest.mark.parametrize("frames", ["0", "1", "2"])
 def test_frame_resident_state_gradients(cuda, monkeypatch, frames):
     """T single-step calls then one backward (main_mp.py:54,77) on the bf16 path:
     every call's backward takes dh_T / dc_T from the next call and hands dh_0 /

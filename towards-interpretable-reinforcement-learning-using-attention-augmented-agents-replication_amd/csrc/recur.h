@@ -39,6 +39,7 @@ constexpr int kRecNPH = 169;        // LDS image pixels: (h+2)*(w+2) <= 169 (11x
 constexpr int kRecXB = 22 * 1024;   // x image bytes: 169 pixels x 128 B, whole 1-KB DMA pieces
 constexpr int kRecHS = 136;         // h image pixel pitch (bf16): 128 + 8 pad (272 B = 17 x 16 B)
 constexpr int kRecStg = 4608;       // per-wave epilogue staging bytes (16 px x 272 B gates; c + h 2 x 16 x 144 B)
+constexpr int kSC1 = 16;            // buffer load / store cache policy: sc1 (cross-workgroup hand-off bytes)
 
 // k step ks of the x-first order -> element offset k of the [x|h] GEMM (k = tap*192 + c)
 __host__ __device__ constexpr int rec_k(int ks) {
@@ -88,9 +89,11 @@ struct RecFwdParams {
 // G = 2 (batches too small to give every CU a frame): two workgroups per frame,
 // half kh owning gate rows [256kh, 256kh+256) (its 64 channels); each step it
 // publishes its half of h_t through XH slot t+1 (written anyway: the weight-
-// gradient operand) and a release / acquire flag, and reads the partner's half
-// into its h image after its own x-part -- the hand-off's latency hides under
-// the x-part GEMM.  Launched cooperatively (co-residency checked), spins bounded.
+// gradient operand) with sc1 stores and an sc1 flag, and reads the partner's half
+// (sc1 loads) into its h image after its own x-part -- the hand-off's latency
+// hides under the x-part GEMM, and no agent release / acquire fence is paid
+// (ABL bit 4 = the fenced hand-off, for A/B).  Launched cooperatively
+// (co-residency checked), spins bounded.
 template <typename GT, int G = 1, int ABL = 0>
 __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
   constexpr int NRB = 4 / G, GCH = 8 * NRB;     // row blocks and channels per wave
@@ -254,14 +257,20 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
               break;
             }
           }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if constexpr (ABL & 16) {   // fenced hand-off (A/B only)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
         }
         barrier_lds();
-        const __bf16* src = p.XH + ((size_t)t * M + (size_t)b * P) * 192 + 64 + 64 * (1 - kh);
+        // the partner's bytes: sc1 loads (L2-served) of sc1-stored data behind an
+        // sc1 flag poll -- no acquire needed (MI355X_MICROARCH: inter-workgroup
+        // visibility, hand-off table row 1)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
         for (int i = tid; i < P * 8; i += 256)
           *reinterpret_cast<u32x4*>(him + hidx(i >> 3) * kRecHS + 64 * (1 - kh) + (i & 7) * 8) =
-              *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 3) * 192 + (i & 7) * 8);
+              __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((i >> 3) * 192 + 64 + 64 * (1 - kh) + (i & 7) * 8) * 2),
+                                                    0, (ABL & 16) ? 0 : kSC1);
         barrier_lds();
       }
       ldh(0, 0, bfr[0]);
@@ -371,17 +380,28 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     // h_t (bf16, this workgroup's channels) into XH slot t+1 (the weight-gradient operand), from the image
     const size_t rown = rowt + M;   // slot t+1
     constexpr int HC = 16 / G;      // 16-B chunks (8 channels) per pixel of this workgroup
-    for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
-      const int px = i / HC, q = i % HC + HC * kh;
-      *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
-          *reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8);
-    }
-    if constexpr (G == 2) {   // publish h_t's half: every wave's stores retired, then release + flag
+    if constexpr (G == 1) {
+      for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
+        const int px = i / HC, q = i % HC;
+        *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
+            *reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8);
+      }
+    } else {   // the partner reads these: sc1 stores (write through to the coherent level)
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
+      for (int i = tid; i < P * HC; i += 256) {
+        const int px = i / HC, q = i % HC + HC * kh;
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
+                                               (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, (ABL & 16) ? 0 : kSC1);
+      }
+      // publish h_t's half: every wave's stores retired, a barrier, then one
+      // lane's flag store (sc1; the fenced variant adds an agent release)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       barrier_lds();
       if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (ABL & 16) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __hip_atomic_store(p.flags + 2 * b + kh, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -397,8 +417,10 @@ inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStrea
     if (!p.flags) return hipErrorInvalidValue;
     RecFwdParams<GT> q = p;
     void* args[] = {&q};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>), dim3(2 * p.B),
-                                      dim3(256), args, 0, st);
+    const char* e = getenv("AAA_REC_ABL");
+    const void* k = (e && atoi(e) == 16) ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 16>)
+                                         : reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>);
+    return hipLaunchCooperativeKernel(k, dim3(2 * p.B), dim3(256), args, 0, st);
   }
   const char* e = getenv("AAA_REC_ABL");
   switch (e ? atoi(e) : 0) {

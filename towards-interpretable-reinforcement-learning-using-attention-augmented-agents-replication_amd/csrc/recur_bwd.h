@@ -32,7 +32,8 @@ namespace aaa {
 
 constexpr int kBwKS = 4608 / 16;   // k steps: 4 chunks x 9 taps x 8 groups of 16 rows
 constexpr int kBwPD = 4;           // A register slots (PD-1 k steps in flight); divides 8
-constexpr int kBwKSP = kBwKS + kBwPD - 1;
+constexpr int kBwPD2 = 8;          // the paired kernel's (3 MFMAs per k step: twice the k steps in flight)
+constexpr int kBwKSP = kBwKS + kBwPD2 - 1;   // packed k steps per row block: the first PD2-1 repeated at the end
 constexpr int kBwIP = 136;         // chunk image pixel pitch (bf16): 128 rows + 8 pad (272 B)
 constexpr int kBwIB = 46080;       // chunk image bytes: 169 px x 272 B rounded up to whole 1-KB DMA pieces
 
@@ -76,10 +77,11 @@ struct RecBwdParams {
   const float* dhT;       // (B, P, 128) extra grad of h_{T-1}, or null
   float* dC;              // (B, P, 128) dc carry: in = dc_T, out = dc_0
   __bf16* dZ;             // (T, B, P, 512) <- gate pre-activation grads
-  float* part;            // (T, B, 512) <- gate-bias partials per (step, frame)
+  float* part;            // (T, B, 512) <- gate-bias partials per (step, frame); paired: (T, B, 2, 512)
   float* dh0;             // (B, P, 128) <- grad of h_{-1}, or null
   __bf16* dY2;            // (T, B, P, 64) <- dx_t, the conv2 output gradient (bf16: its readers' operand type)
   float* dxb;             // (B, 64) <- conv2 bias-gradient partials per frame (fp32 sums of dx)
+  int* flags;             // paired kernel: per (frame, half) count of published dZ steps ([2B], zeroed), [2B] = timeout
   int T, B, h, w, P;
 };
 
@@ -418,6 +420,354 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       if (pp < P)
         *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pp) * 128 + 32 * wave + 8 * g + 4 * hh) = dcw[(g * 4 + cb) * 64];
     }
+}
+
+// Paired variant, for batches below the CU count: two workgroups per frame.
+// Half kh owns the h channels [64kh, 64kh+64) -- dZ chunks 2kh and 2kh+1, the
+// dh rows of those channels, their dc carry -- and the x channels [32kh,
+// 32kh+32) of dx.  Per step it runs its own two chunks first (LDS images its
+// epilogue wrote), then the partner's two, read from HBM once the partner has
+// published dZ_t: the partner's dZ stores are sc1, its flag an sc1 store behind
+// every wave's vmcnt(0) and a barrier, and the chunks come back with sc1 loads
+// to registers (then ds_write), so neither side pays an agent fence
+// (MI355X_MICROARCH: inter-workgroup visibility, hand-off table row 1).  Wave w:
+// h row block 2kh + w%2 over column blocks 2(w/2), 2(w/2)+1 and the dx row block
+// 4 + kh over column block w -- 3 MFMAs per k step, so the A stream runs
+// kBwPD2-1 = 7 k steps ahead.  K order: own chunks, then the partner's (the
+// packed stream read from k step 144kh on, wrapping through the repeated tail).
+// Launched cooperatively (co-residency checked); the spins are bounded.
+template <int ABL = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_pairs(RecBwdParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (c & 1)
+  __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 8 * 64];          // dc carry, lane-native [wave][g*2+j][lane]
+  const int b = (int)blockIdx.x % p.B, kh = (int)blockIdx.x / p.B;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int P = p.P, W2 = p.w + 2;
+  const size_t M = (size_t)p.B * P;
+  const int hrb = 2 * kh + (wave & 1);   // the wave's h row block (channels 32 hrb ..) = the dZ chunk it produces
+  const int cbA = 2 * (wave >> 1);       // its column blocks cbA, cbA + 1
+  auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
+
+  {  // zero the images (borders and pads stay zero)
+    u32x4* z = reinterpret_cast<u32x4*>(zim);
+    for (int i = tid; i < 2 * kBwIB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  // the partner's chunk c of dZ_t: sc1 loads of the P x 256 B into registers
+  // (issued at the start of a chunk), then into image c & 1 (three taps later)
+  constexpr int NPR = 8;   // 16-B pieces per thread: P * 16 <= 2048
+  auto pld = [&](int t, int c, u32x4 (&v)[NPR]) {
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
+#pragma unroll
+    for (int r = 0; r < NPR; ++r) {
+      const int i = tid + 256 * r, px = i >> 4, q = i & 15;
+      v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, px < P ? (uint32_t)((px * 512 + 128 * c + q * 8) * 2) : kOOB, 0,
+                                                   kSC1);
+    }
+  };
+  auto pst = [&](int c, const u32x4 (&v)[NPR]) {
+#pragma unroll
+    for (int r = 0; r < NPR; ++r) {
+      const int i = tid + 256 * r, px = i >> 4, q = i & 15;
+      if (px < P) *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIB + hidx(px) * (kBwIP * 2) + q * 16) = v[r];
+    }
+  };
+
+  int hb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pp = min((cbA + j) * 32 + r32, P - 1);
+    hb[j] = (pp / p.w) * W2 + pp % p.w;
+  }
+  // dc carry of the lane's 32 (channel, pixel) pairs: channels 32hrb + 8g + 4hh + e at pixel 32(cbA+j) + r32
+  f32x4* dcw = dcl + wave * 8 * 64 + lane;   // + (g*2 + j) * 64
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pp = (cbA + j) * 32 + r32;
+      dcw[(g * 2 + j) * 64] =
+          pp < P ? *reinterpret_cast<const f32x4*>(p.dC + ((size_t)b * P + pp) * 128 + 32 * hrb + 8 * g + 4 * hh)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(6 * kBwKSP * 1024));
+  const int wofs = hrb * kBwKSP * 1024, xofs = (4 + kh) * kBwKSP * 1024;
+  auto lda = [&](int ks, int x) {
+    return __builtin_bit_cast(bf16x8,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, (x ? xofs : wofs) + ks * 1024, 0));
+  };
+  constexpr int PD = kBwPD2;
+  bf16x8 af[PD][2];
+#pragma unroll
+  for (int s = 0; s < PD - 1; ++s) {
+    af[s][0] = lda(144 * kh + s, 0);
+    af[s][1] = lda(144 * kh + s, 1);
+  }
+  float xbs[16];   // conv2 bias partials of the lane's 16 x channels, all steps
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xbs[i] = 0.f;
+
+  struct EpIn { f32x4 dO, cc, cp; u32x4 gt[2]; };
+  constexpr int kRing = 4, kU = 8;   // units u = (g, j), g-major
+  auto load_in = [&](int s, int u, int ln) {
+    EpIn in;
+    const int g = u >> 1, j = u & 1, pp = (cbA + j) * 32 + (ln & 31);
+    if (pp < P) {
+      const size_t row = (size_t)s * M + (size_t)b * P + pp;
+      const int ch = 32 * hrb + 4 * (ln >> 5) + 8 * g;
+      in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
+      in.cc = *reinterpret_cast<const f32x4*>(p.Cst + (row + M) * 128 + ch);
+      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);
+      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
+      in.gt[0] = gp[0];
+      in.gt[1] = gp[1];
+    } else {
+      in.dO = in.cc = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
+      in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
+    }
+    return in;
+  };
+
+  // gate backward of step s (as the single-workgroup kernel's), then publish
+  // dZ_s: every wave's sc1 stores retired, a barrier, one lane's sc1 flag store
+  auto epilogue = [&](int s, const f32x16 (&acc)[2], bool gemm, EpIn (&ring)[kRing]) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int pl = ln & 31, hq = ln >> 5;
+    const int c0 = 32 * hrb + 4 * hq;   // + 8g + e
+    const size_t rows = (size_t)s * M + (size_t)b * P;
+    const __amdgpu_buffer_rsrc_t rz = make_rsrc(p.dZ + rows * 512, (uint32_t)(P * 512 * 2));
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float bs[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bs[i] = 0.f;
+      const int ch = c0 + 8 * g;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int u = g * 2 + j;
+        if (u + kRing - 1 < kU) ring[(u + kRing - 1) % kRing] = load_in(s, u + kRing - 1, ln);
+        const EpIn& in = ring[u % kRing];
+        const int pp = (cbA + j) * 32 + pl;
+        if (pp < P) {
+          f32x4 dh = in.dO;
+          if (gemm) {
+            dh[0] += acc[j][4 * g]; dh[1] += acc[j][4 * g + 1]; dh[2] += acc[j][4 * g + 2]; dh[3] += acc[j][4 * g + 3];
+          } else if (p.dhT) {
+            const f32x4 x = *reinterpret_cast<const f32x4*>(p.dhT + ((size_t)b * P + pp) * 128 + ch);
+            dh[0] += x[0]; dh[1] += x[1]; dh[2] += x[2]; dh[3] += x[3];
+          }
+          f32x4* dcp = dcl + wave * 8 * 64 + ln + u * 64;
+          f32x4 dc = *dcp;
+          float dz[16];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t w01 = in.gt[e >> 1][2 * (e & 1)], w23 = in.gt[e >> 1][2 * (e & 1) + 1];
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            const h2 a = __builtin_bit_cast(h2, w01), c2 = __builtin_bit_cast(h2, w23);
+            const f32x4 gv{(float)a[0], (float)a[1], (float)c2[0], (float)c2[1]};
+            float d = dc[e], di, df, dcg, dout;
+            gate_bwd_fast(dh[e], gv, in.cp[e], in.cc[e], d, di, df, dcg, dout);
+            dc[e] = d;
+            dz[4 * e] = di; dz[4 * e + 1] = df; dz[4 * e + 2] = dcg; dz[4 * e + 3] = dout;
+            bs[4 * e] += di; bs[4 * e + 1] += df; bs[4 * e + 2] += dcg; bs[4 * e + 3] += dout;
+          }
+          *dcp = dc;
+          bf16x8 z0, z1;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { z0[i] = (__bf16)dz[i]; z1[i] = (__bf16)dz[8 + i]; }
+          const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, kSC1);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, kSC1);
+          unsigned char* zi = zim + (wave & 1) * kBwIB + hidx(pp) * (kBwIP * 2) + (4 * (ch - 32 * hrb)) * 2;
+          *reinterpret_cast<bf16x8*>(zi) = z0;
+          *reinterpret_cast<bf16x8*>(zi + 16) = z1;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      int n = 16;
+#pragma unroll
+      for (int m = 16; m >= 2; m >>= 1) {
+        const bool up = (pl & m) != 0;
+        n >>= 1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (i < n) {
+            const float send = up ? bs[i] : bs[i + n];
+            const float keep = up ? bs[i + n] : bs[i];
+            bs[i] = keep + __shfl_xor(send, m, 64);
+          }
+        }
+      }
+      bs[0] += __shfl_xor(bs[0], 1, 64);
+      const int ridx = ((pl & 16) ? 8 : 0) + ((pl & 8) ? 4 : 0) + ((pl & 4) ? 2 : 0) + ((pl & 2) ? 1 : 0);
+      if ((pl & 1) == 0)   // row 4(ch + e) + gate; the two pixel halves (w / 2) in rows of their own
+        p.part[(((size_t)s * p.B + b) * 2 + (wave >> 1)) * 512 + 4 * (ch + (ridx >> 2)) + (ridx & 3)] = bs[0];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();   // own chunk images of dZ_s complete; every wave's dZ_s stores retired
+    if (tid == 0) __hip_atomic_store(p.flags + 2 * b + kh, p.T - s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  {  // step T-1: no GEMM
+    f32x16 zero[2];
+    EpIn ring[kRing];
+#pragma unroll
+    for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(p.T - 1, u, lane);
+    epilogue(p.T - 1, zero, false, ring);
+  }
+
+  for (int t = p.T - 1; t >= 0; --t) {
+    f32x16 acc[2], accx;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) accx[e] = 0.f;
+    int hbs[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      hbs[j] = hb[j];
+      asm volatile("" : "+v"(hbs[j]));
+    }
+    auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + (2 - tap % 3); };
+    auto ldb = [&](const unsigned char* img, int toff, int c16, bf16x8 (&bf)[2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bf[j] = *reinterpret_cast<const bf16x8*>(img + (hbs[j] + toff) * (kBwIP * 2) + c16 * 32 + hh * 16);
+    };
+    constexpr int BD = 4;
+    bf16x8 bfr[BD][2];
+    EpIn ring[kRing];
+    auto kloop = [&](auto xj) {
+      constexpr int XJ = decltype(xj)::value;   // the dx column block's fragment (w % 2)
+#pragma unroll 1
+      for (int ck = 0; ck < 4; ++ck) {
+        const int c = (ck + 2 * kh) & 3;   // own chunks first, then the partner's
+        const unsigned char* img = zim + (c & 1) * kBwIB;
+        u32x4 pv[NPR];
+        const bool refill = ck == 1 || ck == 2;   // the partner's chunk c+1 into the image chunk ck-1 freed
+        if (refill) pld(t, (c + 1) & 3, pv);
+        if (ck == 3 && t > 0) {
+          int ln = lane;
+          asm volatile("" : "+v"(ln));
+#pragma unroll
+          for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(t - 1, u, ln);
+        }
+#pragma unroll
+        for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
+        for (int tap = 0; tap < 9; ++tap) {
+          const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+          int kt = c * 72 + tap * 8;
+          asm volatile("" : "+s"(kt));
+          if (refill && tap == 3) pst((c + 1) & 3, pv);
+#pragma unroll
+          for (int c16 = 0; c16 < 8; ++c16) {
+            if constexpr (!(ABL & 1)) {
+              af[(c16 + PD - 1) % PD][0] = lda(kt + c16 + PD - 1, 0);
+              af[(c16 + PD - 1) % PD][1] = lda(kt + c16 + PD - 1, 1);
+            }
+            {
+              const int cn = c16 + BD - 1;
+              if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
+              else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][0], bfr[c16 % BD][j], acc[j], 0, 0, 0);
+            accx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][1], bfr[c16 % BD][XJ], accx, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if (ck == 0 && tid == 0) {   // the partner's dZ_t published? (the other waves load after the barrier)
+          int n = 0;
+          while (__hip_atomic_load(p.flags + 2 * b + (1 - kh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.T - t) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++n > (1 << 24)) {
+              __hip_atomic_store(p.flags + 2 * p.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        barrier_lds();   // image c & 1 free for the partner's chunk; (ck = 1, 2) its refill complete
+      }
+    };
+    if (wave & 1) kloop(std::integral_constant<int, 1>{});
+    else kloop(std::integral_constant<int, 0>{});
+    {  // dx_t: x channels 32kh + 8g + 4hh + e at pixel 32w + r32
+      const size_t rows = (size_t)t * M + (size_t)b * P;
+      const int pp = wave * 32 + r32;
+      if (pp < P) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float v[4] = {accx[4 * g], accx[4 * g + 1], accx[4 * g + 2], accx[4 * g + 3]};
+          *reinterpret_cast<bf16x4*>(p.dY2 + (rows + pp) * 64 + 32 * kh + 8 * g + 4 * hh) =
+              bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xbs[4 * g + e] += v[e];
+        }
+      }
+    }
+    if (t > 0) {
+      epilogue(t - 1, acc, true, ring);
+    } else if (p.dh0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int pp = (cbA + j) * 32 + r32;
+        if (pp < P)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + pp) * 128 + 32 * hrb + 8 * g + 4 * hh) =
+                f32x4{acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]};
+      }
+    }
+  }
+  {  // conv2 bias partials (4 waves = 4 column blocks share each channel set)
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xbs[i];
+    int n = 16;
+#pragma unroll
+    for (int m = 16; m >= 2; m >>= 1) {
+      const bool up = (r32 & m) != 0;
+      n >>= 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i < n) {
+          const float send = up ? v[i] : v[i + n];
+          const float keep = up ? v[i + n] : v[i];
+          v[i] = keep + __shfl_xor(send, m, 64);
+        }
+      }
+    }
+    v[0] += __shfl_xor(v[0], 1, 64);
+    const int ridx = ((r32 & 16) ? 8 : 0) + ((r32 & 8) ? 4 : 0) + ((r32 & 4) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
+    if ((r32 & 1) == 0) {
+      const int g = ridx >> 2, e = ridx & 3;
+      atomicAdd(p.dxb + (size_t)b * 64 + 32 * kh + 8 * g + 4 * hh + e, v[0]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pp = (cbA + j) * 32 + r32;
+      if (pp < P)
+        *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pp) * 128 + 32 * hrb + 8 * g + 4 * hh) = dcw[(g * 2 + j) * 64];
+    }
+}
+
+inline hipError_t convlstm_bwd_pairs(const RecBwdParams& p, hipStream_t st) {
+  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags) return hipErrorInvalidValue;
+  RecBwdParams q = p;
+  void* args[] = {&q};
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_convlstm_bwd_pairs<0>), dim3(2 * p.B), dim3(256),
+                                    args, 0, st);
 }
 
 inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {

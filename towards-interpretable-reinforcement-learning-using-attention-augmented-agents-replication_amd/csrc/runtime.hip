@@ -165,7 +165,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dQp = take(F * L.qd * 4);
   L.dC = take(M * 128 * 4);
   L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
-  L.dZp = take((size_t)L.T * ((M + 31) / 32) * 512 * 4);  // gate-bias partials per (step, column tile)
+  L.dZp = take((size_t)L.T * std::max((M + 31) / 32, 2 * (size_t)L.B) * 512 * 4);  // gate-bias partials per (step, column tile | frame half)
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
@@ -740,10 +740,9 @@ static int frames_g(const Layout& L, const char* env) {
   return v == 1 ? 1 : (v == 2 && 2 * L.B <= cus ? 2 : 0);
 }
 static int frames_fwd(const Layout& L) { return frames_g(L, "AAA_FRAMES_FWD"); }
-// The BPTT chain on the frame-resident kernel (recur_bwd.h; fp16 gate storage),
-// from the same batch on (C3: 55 vs 69 us per step; C4: 52 vs 49 us).
-// AAA_FRAMES_BWD=1/0 forces it on/off.
-static bool frames_bwd(const Layout& L, bool g16) { return g16 && frames_g(L, "AAA_FRAMES_BWD") == 1; }
+// The BPTT chain on the frame-resident kernels (recur_bwd.h; fp16 gate storage):
+// workgroups per frame as the forward's (AAA_FRAMES_BWD = 0 / 1 / 2 forces it).
+static int frames_bwd(const Layout& L, bool g16) { return g16 ? frames_g(L, "AAA_FRAMES_BWD") : 0; }
 
 template <typename T>
 static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
@@ -1515,7 +1514,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
-    const bool fb = frames_bwd(L, g16);   // the whole chain in one frame-resident launch (after flush below)
+    const int fb = frames_bwd(L, g16);   // the whole chain in one frame-resident launch (workgroups per frame)
     if (fb) {
     } else if (g16)
       HIPCHK((gate_bwd_last<T, _Float16>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT,
@@ -1544,13 +1543,15 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     if (fb) {
       if constexpr (!std::is_same<T, float>::value) {
         RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
-                        Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), L.T, L.B, L.h, L.w, L.P};
+                        Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), (int*)(ws + L.rflags),
+                        L.T, L.B, L.h, L.w, L.P};
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
+        if (fb == 2) HIPCHK(hipMemsetAsync(ws + L.rflags, 0, ((size_t)2 * L.B + 1) * 4, st));
         {
           // work: the h rows over T-1 steps (+ dh0) and the dx rows over all T (the batched dx it replaces)
           TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 4608 * (128.0 * (L.T - 1 + (io->dh0 ? 1 : 0)) + 64.0 * L.T),
-                         strf("bf16 frame-resident BPTT + dx, %d steps per launch, 1 WG per frame, fp16 gates", L.T));
-          HIPCHK(convlstm_bwd_frames(rp, st));
+                         strf("bf16 frame-resident BPTT + dx, %d steps per launch, %d WG per frame, fp16 gates", L.T, fb));
+          HIPCHK(fb == 2 ? convlstm_bwd_pairs(rp, st) : convlstm_bwd_frames(rp, st));
         }
         HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
         dx_fused = true;
@@ -1656,7 +1657,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
     // gate-bias gradient: column sum of the per-(step, tile) partials, or of dZ itself
-    if (fb) HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B, 512, Wf(L.gbl), st));   // per (step, frame) partials
+    if (fb)   // per (step, frame[, pixel half]) partials
+      HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B * fb, 512, Wf(L.gbl), st));
     else if (part) HIPCHK(colsum<float>(part, 512, L.T * ntj, 512, Wf(L.gbl), st));
     else HIPCHK(colsum<T>(Wt(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
