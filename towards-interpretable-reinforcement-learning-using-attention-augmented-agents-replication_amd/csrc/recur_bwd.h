@@ -153,11 +153,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
   for (int i = 0; i < 16; ++i) xbs[i] = 0.f;
 
-  // The epilogue's HBM inputs of one unit u = (g, cb) (g-major): dO, c_s, c_{s-1}
-  // (16 B each) and the 16 fp16 gates (32 B) of the lane's 4 channels at one pixel.
+  // The epilogue's HBM inputs of one unit u = (g, cb) (g-major): dO and c_{s-1}
+  // (16 B each) and the 16 fp16 gates (32 B) of the lane's 4 channels at one pixel;
+  // c_s = f c_{s-1} + i c~ is recomputed from them (not read: 16 B less per unit).
   // A ring of kRing units is in flight: the first kRing-1 are requested under the
   // GEMM's last chunk, each later one as the unit kRing-1 before it is processed.
-  struct EpIn { f32x4 dO, cc, cp; u32x4 gt[2]; };
+  struct EpIn { f32x4 dO, cp; u32x4 gt[2]; };
   constexpr int kRing = 4;
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
@@ -166,13 +167,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const size_t row = (size_t)s * M + (size_t)b * P + pp;
       const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
       in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
-      in.cc = *reinterpret_cast<const f32x4*>(p.Cst + (row + M) * 128 + ch);   // c_s
       in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
       const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
       in.gt[0] = gp[0];
       in.gt[1] = gp[1];
     } else {
-      in.dO = in.cc = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
+      in.dO = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
       in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
     }
     return in;
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             const h2 a = __builtin_bit_cast(h2, w01), c2 = __builtin_bit_cast(h2, w23);
             const f32x4 gv{(float)a[0], (float)a[1], (float)c2[0], (float)c2[1]};
             float d = dc[e], di, df, dcg, dout;
-            gate_bwd_fast(dh[e], gv, in.cp[e], in.cc[e], d, di, df, dcg, dout);
+            gate_bwd_fast(dh[e], gv, in.cp[e], gv[1] * in.cp[e] + gv[0] * gv[2], d, di, df, dcg, dout);
             dc[e] = d;
             dz[4 * e] = di; dz[4 * e + 1] = df; dz[4 * e + 2] = dcg; dz[4 * e + 3] = dout;
             bs[4 * e] += di; bs[4 * e + 1] += df; bs[4 * e + 2] += dcg; bs[4 * e + 3] += dout;
@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
   for (int i = 0; i < 16; ++i) xbs[i] = 0.f;
 
-  struct EpIn { f32x4 dO, cc, cp; u32x4 gt[2]; };
+  struct EpIn { f32x4 dO, cp; u32x4 gt[2]; };
   constexpr int kRing = 4, kU = 8;   // units u = (g, j), g-major
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
@@ -519,13 +519,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const size_t row = (size_t)s * M + (size_t)b * P + pp;
       const int ch = 32 * hrb + 4 * (ln >> 5) + 8 * g;
       in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
-      in.cc = *reinterpret_cast<const f32x4*>(p.Cst + (row + M) * 128 + ch);
       in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);
       const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
       in.gt[0] = gp[0];
       in.gt[1] = gp[1];
     } else {
-      in.dO = in.cc = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
+      in.dO = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
       in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
     }
     return in;
@@ -570,7 +569,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             const h2 a = __builtin_bit_cast(h2, w01), c2 = __builtin_bit_cast(h2, w23);
             const f32x4 gv{(float)a[0], (float)a[1], (float)c2[0], (float)c2[1]};
             float d = dc[e], di, df, dcg, dout;
-            gate_bwd_fast(dh[e], gv, in.cp[e], in.cc[e], d, di, df, dcg, dout);
+            gate_bwd_fast(dh[e], gv, in.cp[e], gv[1] * in.cp[e] + gv[0] * gv[2], d, di, df, dcg, dout);
             dc[e] = d;
             dz[4 * e] = di; dz[4 * e + 1] = df; dz[4 * e + 2] = dcg; dz[4 * e + 3] = dout;
             bs[4 * e] += di; bs[4 * e + 1] += df; bs[4 * e + 2] += dcg; bs[4 * e + 3] += dout;
