@@ -165,6 +165,38 @@ def test_frame_resident_forward(cuda, monkeypatch, T, B, fwd, bwd):
             assert rel_err(out[3][n].numpy(), step[3][n].numpy()) <= 5e-3, f"frames vs per-step grad {n}"
 
 
+@pytest.mark.parametrize("T,B,src", [(1, 1, "u8"), (3, 5, "u8"), (2, 3, "f32"), (2, 3, "f32x0.37")])
+def test_frame_resident_vision(cuda, monkeypatch, T, B, src):
+    """The frame-resident encoder (csrc/vision.h: frame -> RGBx image -> conv1 ->
+    conv2 in one workgroup) on uint8 and fp32 observations (integer-valued and
+    not: the bf16 rounding of conv1's input), against the bf16 oracle and the
+    layered kernels it replaces (AAA_VIS_FRAMES=0); the gradients check the Xp /
+    Y1 images it leaves for the weight gradients."""
+    scale = 0.37 if src == "f32x0.37" else 1.0
+
+    def run(v):
+        monkeypatch.setenv("AAA_VIS_FRAMES", v)
+        ag = _agent(cuda, conv_dtype="bf16")
+        X = _frames(T, B, scale=scale).to(cuda)
+        if src == "u8":
+            X = X.to(torch.uint8)
+        ag.reset()
+        lg, vl, at = ag.unroll(X)
+        Gl, Gv = _cot(T, B)
+        ((lg * Gl.to(cuda)).sum() + (vl * Gv.to(cuda)).sum()).backward()
+        torch.cuda.synchronize()
+        return lg.detach().cpu(), vl.detach().cpu(), at.detach().cpu(), _grads(ag)
+
+    out = run("1")
+    _compare(out, _oracle(T, B, scale=scale, conv_mode="bf16"), 2e-2, f"vision frames T={T} B={B} {src}: ")
+    lay = run("0")
+    for a, b, n in zip(out[:3], lay[:3], ("logits", "values", "attn")):
+        assert_close(a.numpy(), b.numpy(), 2e-3, f"vision frames vs layered {n}")
+    for n in out[3]:
+        if float(lay[3][n].norm()) > 0:
+            assert rel_err(out[3][n].numpy(), lay[3][n].numpy()) <= 5e-3, f"vision frames vs layered grad {n}"
+
+
 @pytest.mark.parametrize("frames", ["0", "1", "2"])
 def test_frame_resident_state_gradients(cuda, monkeypatch, frames):
     """T single-step calls then one backward (main_mp.py:54,77) on the bf16 path:

@@ -31,6 +31,7 @@
 #include "halo.h"
 #include "recur.h"
 #include "recur_bwd.h"
+#include "vision.h"
 #include "misc.h"
 #include "optim.h"
 
@@ -704,9 +705,20 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
   return AAA_OK;
 }
 
+static int device_cus();
+
 template <typename T, typename OT>
 static int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1,
                       OT* out, int out_ld, hipStream_t st) {
+  if constexpr (std::is_same<T, __bf16>::value && std::is_same<OT, __bf16>::value) {
+    // bf16: the frame-resident encoder (vision.h), one launch; AAA_VIS_FRAMES=0 -> the layered kernels
+    if (vis_fits(L.H, L.W, L.H1, L.W1, L.h, L.w) && env_int("AAA_VIS_FRAMES", 1)) {
+      VisFwdParams vp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], (const __bf16*)(pk + L.k_Wp2),
+                      prm + L.poff[C1B], Xp, Y1, out, out_ld, F, L.H, L.W, L.H1, L.W1, L.h, L.w};
+      HIPCHK(L.fu8 ? vision_fwd_frames<uint8_t>(vp, device_cus(), st) : vision_fwd_frames<float>(vp, device_cus(), st));
+      return AAA_OK;
+    }
+  }
   for (int f0 = 0; f0 < F; f0 += L.fchunk) {   // descriptor-sized frame chunks (check_ranges)
     const int n = std::min(L.fchunk, F - f0);
     const int rc = vision_fwd_chunk<T, OT>(L, n, pk, prm,
