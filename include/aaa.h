@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 3
+#define AAA_ABI_VERSION 4
 
 enum aaa_status {
   AAA_OK = 0,
@@ -229,6 +229,41 @@ int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, 
  * draws are not torch's multinomial stream; the distribution is the same. */
 int aaa_sample_actions(int B, int A, const float* logits, unsigned long long seed, unsigned long long* counter,
                        int* actions, float* logp, float* dlogp_dlogits, hipStream_t stream);
+
+/* ---- actor: one environment step ----
+ * The acting half of the reference's loop -- Policy.forward (main_mp.py:49-59)
+ * = Agent.forward (attention.py:298-368) on one observation per row, with the
+ * ConvLSTM state carried (attention.py:125, 142-149), then the draw of
+ * aaa_sample_actions -- for B <= 16 rows, as a chain of six launches sized for
+ * small B (vision, ConvLSTM step, attention + answer layer 0, answer layer 2,
+ * LSTMCell, heads + draw) instead of aaa_forward's whole-batch kernels.
+ * Results equal aaa_forward with T = 1, h0 = *h, c0 = *c up to fp32
+ * summation order; the draw is bit-identical to aaa_sample_actions on those
+ * logits.  cfg: T = 1, dtype AAA_F32, no AAA_FLAG_STATEFUL_CORE (those use
+ * aaa_forward); ``packed`` from aaa_pack_weights with the same cfg.  h, c
+ * (B, h, w, 128) are read and overwritten with the step's state (zero them for
+ * reset()).  actions == NULL skips the draw (seed/counter/logp/dlogp ignored). */
+typedef struct aaa_actor_io {
+  const float* params;       /* flat fp32 params                               */
+  const void* packed;        /* aaa_pack_weights output (same cfg)             */
+  const float* basis;        /* (h, w, 64)                                     */
+  const void* frames;        /* (B, H, W, 3) fp32, or uint8 with AAA_FLAG_FRAMES_U8 */
+  const float* prev_reward;  /* (B) or NULL                                    */
+  const float* prev_action;  /* (B) or NULL                                    */
+  float* h;                  /* (B, h, w, 128) ConvLSTM state, in/out          */
+  float* c;                  /* (B, h, w, 128) cell state, in/out              */
+  float* logits;             /* (B, A)                                         */
+  float* values;             /* (B, A)                                         */
+  float* attn;               /* (B, h, w, nq) or NULL                          */
+  void* workspace;           /* aaa_actor_workspace_bytes()                    */
+  unsigned long long seed;   /* action draw: as aaa_sample_actions             */
+  unsigned long long* counter;
+  int* actions;              /* (B) or NULL (no draw)                          */
+  float* logp;               /* (B) or NULL                                    */
+  float* dlogp_dlogits;      /* (B, A) or NULL                                 */
+} aaa_actor_io;
+size_t aaa_actor_workspace_bytes(const aaa_cfg* cfg);
+int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t stream);
 
 /* ---- single-kernel entry points (unit tests against PyTorch fp32) ---- */
 

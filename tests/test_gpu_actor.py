@@ -150,8 +150,10 @@ def test_packed_weights_follow_parameter_updates(cuda, optim):
     assert_close(l2.detach().cpu().numpy(), rl[0].detach().numpy(), 1e-4, "logits after update")
 
 
-def test_graph_actor_matches_eager_steps(cuda):
-    """The captured one-step graph reproduces the eager per-step agent (same
+@pytest.mark.parametrize("chain", [True, False])
+def test_graph_actor_matches_eager_steps(cuda, chain):
+    """The captured one-step graph -- on the actor chain (aaa_actor_step) or the
+    learner's T=1 forward -- reproduces the oracle's per-step agent (same
     logits, carried ConvLSTM state, the same draws for the same counter), and
     picks up a parameter update."""
     from aaa_amd.policy import GraphActor
@@ -161,7 +163,8 @@ def test_graph_actor_matches_eager_steps(cuda):
     agent.to(cuda)
     T = 5
     frames = detinit.frames_u8(31, (T, 84, 84, 3))
-    ga = GraphActor(agent, 84, 84, B=1, seed=9)
+    ga = GraphActor(agent, 84, 84, B=1, seed=9, chain=chain)
+    assert ga.chain == chain
     ga.reset()
     got_a, got_l = [], []
     for t in range(T):
@@ -182,3 +185,75 @@ def test_graph_actor_matches_eager_steps(cuda):
     ga.reset()
     ga.step(frames[0])
     assert_close(ga.logits.cpu().numpy(), rl[0].numpy() + 1.0, 1e-4, "logits after bias update")
+
+
+@pytest.mark.parametrize("H,W,B,nq,u8", [(84, 84, 1, 4, True), (84, 84, 3, 8, False), (210, 160, 2, 4, True),
+                                         (84, 84, 16, 4, True)])
+def test_actor_chain_matches_learner_forward(cuda, H, W, B, nq, u8):
+    """aaa_actor_step (six small-B launches) against aaa_forward with T=1 on the
+    same carried state, prev_reward/prev_action, frames and packed weights:
+    logits, values, attention, h_t, c_t at 1e-4 (only the fp32 summation order
+    differs), over three chained steps; and its fused draw is bit-identical to
+    aaa_sample_actions on its own logits with the same seed and counter."""
+    from aaa_amd.runtime import ActorRunner, UnrollRunner
+    A = 18
+    params = detinit.deterministic_params(3, A, nq)
+    ar = ActorRunner(B, H, W, nq, A, cuda, frames_u8=u8)
+    ur = UnrollRunner(B, 1, H, W, nq, A, "fp32", cuda, frames_u8=u8)
+    agent = attention.Agent(A, num_queries=nq, grid=(ar.h, ar.w))
+    detinit.load_into(agent, params)
+    flat = torch.cat([p.detach().reshape(-1) for p in agent.parameters()]).to(cuda)
+    assert flat.numel() == ar.n_params
+    packed = ar.new_packed()
+    ar.pack(flat, packed)
+    S = agent.spatial.S.to(cuda).contiguous()
+    g = torch.Generator().manual_seed(H + B + nq)
+    h = (torch.rand(ar.state_shape(), generator=g) * 2 - 1).to(cuda) * 0.5
+    c = (torch.rand(ar.state_shape(), generator=g) * 2 - 1).to(cuda)
+    ws, uws = ar.new_workspace(), ur.new_workspace()
+    counter = torch.tensor([5], dtype=torch.int64, device=cuda)
+    for step in range(3):
+        fr = torch.from_numpy(detinit.frames_u8(40 + step, (B, H, W, 3))).to(cuda)
+        if not u8:
+            fr = fr.float() * 0.5
+        pr = torch.rand(B, generator=g).to(cuda)
+        pa = torch.randint(0, A, (B,), generator=g).float().to(cuda)
+        rl, rv, ra, rh, rc = ur.forward(flat, packed, S, fr.unsqueeze(0), uws, prev_reward=pr, prev_action=pa,
+                                        h0=h, c0=c, want_attn=True, want_state=True)
+        logits = torch.empty(B, A, device=cuda)
+        values = torch.empty(B, A, device=cuda)
+        attn = torch.empty(B, ar.h, ar.w, nq, device=cuda)
+        acts = torch.empty(B, dtype=torch.int32, device=cuda)
+        logp = torch.empty(B, device=cuda)
+        jac = torch.empty(B, A, device=cuda)
+        c_before = counter.clone()
+        ar.step(flat, packed, S, fr, ws, h, c, logits, values, attn=attn, prev_reward=pr, prev_action=pa,
+                seed=77, counter=counter, actions=acts, logp=logp, dlogp=jac)
+        torch.cuda.synchronize()
+        assert_close(logits.cpu().numpy(), rl[0].cpu().numpy(), 1e-4, f"logits step {step}")
+        assert_close(values.cpu().numpy(), rv[0].cpu().numpy(), 1e-4, f"values step {step}")
+        assert_close(attn.cpu().numpy(), ra[0].cpu().numpy(), 1e-4, f"attention step {step}")
+        assert_close(h.cpu().numpy(), rh.cpu().numpy(), 1e-4, f"h step {step}")
+        assert_close(c.cpu().numpy(), rc.cpu().numpy(), 1e-4, f"c step {step}")
+        assert int(counter.item()) == int(c_before.item()) + 1
+        sa, slp = sample_actions(logits, seed=77, counter=c_before)
+        assert torch.equal(sa, acts) and torch.equal(slp, logp)
+        pj = torch.softmax(logits, -1)
+        ref_jac = torch.nn.functional.one_hot(acts.long(), A).float() - pj
+        assert float((jac - ref_jac).abs().max()) <= 1e-6
+        # continue from the learner's state so both paths see the same inputs next step
+        h.copy_(rh)
+        c.copy_(rc)
+
+
+def test_actor_chain_refuses_unsupported(cuda):
+    """bf16, stateful-core, T > 1 and B > 16 configurations are refused with AAA_E_ARG
+    (they run on aaa_forward), never silently computed."""
+    import ctypes
+    from aaa_amd import _native as N
+    lib = N.load()
+    for cfg in (N.Cfg(1, 1, 84, 84, 4, 18, N.BF16, 0), N.Cfg(1, 1, 84, 84, 4, 18, N.F32, N.FLAG_STATEFUL_CORE),
+                N.Cfg(1, 2, 84, 84, 4, 18, N.F32, 0), N.Cfg(17, 1, 84, 84, 4, 18, N.F32, 0)):
+        assert lib.aaa_actor_workspace_bytes(ctypes.byref(cfg)) == 0
+        io = N.ActorIO()
+        assert lib.aaa_actor_step(ctypes.byref(cfg), ctypes.byref(io), None) == -1

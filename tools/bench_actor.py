@@ -8,8 +8,11 @@ state carries, as in main_mp.py:100), on seeded synthetic uint8 frames:
                contract: an int action for env.step)
   policy_async Policy.act: the same without the per-step host sync (one sync at the end)
   graph_item   GraphActor.step: the step captured once as a HIP graph, replayed per
-               step, .item() per step (inference / actor-learner split)
+               step, .item() per step (inference / actor-learner split); _chain = the
+               actor chain (aaa_actor_step, six small-B launches), _forward = the
+               learner's T=1 forward + aaa_sample_actions
   graph_async  GraphActor.step without the per-step sync
+  device       graph replays back to back (device time per step, no host copy)
   cpu_ref      the oracle's restatement of the same step (reference op sequence,
                torch CPU fp32, host threads as stated) + softmax/Categorical draw
 Prints one JSON line per frame size.  Frames: 210x160 (Seaquest's raw
@@ -58,21 +61,33 @@ def gpu_legs(H, W, steps, warmup, dev):
                 torch.cuda.synchronize()
             out[leg] = (time.perf_counter() - t0) / steps * 1e6
             pol.saved_log_probs.clear()
-    ga = GraphActor(agent, H, W, B=1, seed=1)
-    for leg in ("graph_item", "graph_async"):
-        ga.reset()
-        for t in range(warmup):
-            int(ga.step(frames[t]).item())
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        if leg == "graph_item":
-            for t in range(steps):
-                int(ga.step(frames[warmup + t]).item())
-        else:
-            for t in range(steps):
-                ga.step(frames[warmup + t])
+    for chain in (False, True):
+        ga = GraphActor(agent, H, W, B=1, seed=1, chain=chain)
+        tag = "chain" if chain else "forward"
+        for leg in ("graph_item", "graph_async"):
+            ga.reset()
+            for t in range(warmup):
+                int(ga.step(frames[t]).item())
             torch.cuda.synchronize()
-        out[leg] = (time.perf_counter() - t0) / steps * 1e6
+            t0 = time.perf_counter()
+            if leg == "graph_item":
+                for t in range(steps):
+                    int(ga.step(frames[warmup + t]).item())
+            else:
+                for t in range(steps):
+                    ga.step(frames[warmup + t])
+                torch.cuda.synchronize()
+            out[f"{leg}_{tag}"] = (time.perf_counter() - t0) / steps * 1e6
+        # device time per step: graph replays back to back on a device-resident frame
+        dframe = torch.from_numpy(frames[0]).to(dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ga.step(dframe)
+        ev0.record()
+        for t in range(steps):
+            ga.graph.replay()
+        ev1.record()
+        torch.cuda.synchronize()
+        out[f"device_{tag}"] = ev0.elapsed_time(ev1) / steps * 1e3
     return out
 
 
@@ -112,16 +127,12 @@ def main():
         H, W = (int(v) for v in sz.split("x"))
         g = gpu_legs(H, W, args.steps, args.warmup, dev)
         c = cpu_leg(H, W, args.cpu_steps, threads)
-        print(json.dumps({"metric": "actor step latency (B=1, Policy.forward)", "unit": "us/step",
-                          "frame": sz, "steps": args.steps,
-                          "policy_item_us": round(g["policy_item"], 1),
-                          "policy_async_us": round(g["policy_async"], 1),
-                          "graph_item_us": round(g["graph_item"], 1),
-                          "graph_async_us": round(g["graph_async"], 1),
-                          "cpu_ref_us": round(c, 1), "cpu_threads": threads,
-                          "speedup_vs_cpu": round(c / g["policy_item"], 2),
-                          "graph_speedup_vs_cpu": round(c / g["graph_item"], 2)}), flush=True)
-
+        rec = {"metric": "actor step latency (B=1, Policy.forward)", "unit": "us/step", "frame": sz,
+               "steps": args.steps, "cpu_ref_us": round(c, 1), "cpu_threads": threads}
+        rec.update({f"{k}_us": round(v, 1) for k, v in g.items()})
+        rec["chain_graph_speedup_vs_cpu"] = round(c / g["graph_item_chain"], 2)
+        rec["chain_vs_forward_device"] = round(g["device_forward"] / g["device_chain"], 2)
+        print(json.dumps(rec), flush=True)
 
 if __name__ == "__main__":
     main()

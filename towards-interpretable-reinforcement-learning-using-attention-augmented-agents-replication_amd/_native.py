@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 3   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 4   # include/aaa.h AAA_ABI_VERSION
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 
 # Every symbol include/aaa.h declares (checked by tests/test_native_abi.py).
@@ -27,6 +27,7 @@ EXPORTS = (
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
+    "aaa_actor_workspace_bytes", "aaa_actor_step",
 )
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
 
@@ -51,6 +52,16 @@ class TimerStats(ctypes.Structure):
 
 class IO(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in IO_FIELDS]
+
+
+ACTOR_IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action", "h", "c",
+                   "logits", "values", "attn", "workspace")
+
+
+class ActorIO(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ACTOR_IO_FIELDS] + [
+        ("seed", ctypes.c_ulonglong), ("counter", ctypes.c_void_p), ("actions", ctypes.c_void_p),
+        ("logp", ctypes.c_void_p), ("dlogp_dlogits", ctypes.c_void_p)]
 
 
 class AdamHP(ctypes.Structure):
@@ -122,6 +133,8 @@ def load(path: str = LIB_PATH):
             "aaa_attn_bwd": (I, [I, I, I, I, P, P, P, I, P, P, P, P, P]),
             "aaa_fastdiv_check": (I, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(ctypes.c_ulonglong)]),
             "aaa_divisor_log": (I, [I, ctypes.POINTER(ctypes.c_uint), I]),
+            "aaa_actor_workspace_bytes": (S, [CP]),
+            "aaa_actor_step": (I, [CP, ctypes.POINTER(ActorIO), P]),
         }
         ab_override = "AAA_LIB" in os.environ
         missing = [name for name in sig if not hasattr(lib, name)]

@@ -34,6 +34,7 @@
 #include "vision.h"
 #include "misc.h"
 #include "optim.h"
+#include "actor.h"
 
 namespace aaa {
 
@@ -2236,6 +2237,64 @@ int aaa_sample_actions(int B, int A, const float* logits, unsigned long long see
   int r = check_device();
   if (r) return r;
   HIPCHK(sample_launch(B, A, logits, seed, counter, actions, logp, dlogp_dlogits, stream));
+  return AAA_OK;
+}
+
+// ---- actor step (include/aaa.h; csrc/actor.hip) ----
+// Workspace: conv2 output X (B,P,64), h_t Hs (B,P,128), hid1 (B,512), AO (B,256), LH (B,256).
+static int actor_layout(const aaa_cfg* cfg, Layout& L, size_t off[5], size_t* total) {
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if (cfg->T != 1) return fail(AAA_E_ARG, "actor_step: T must be 1 (got %d)", cfg->T);
+  if (cfg->dtype != AAA_F32) return fail(AAA_E_ARG, "actor_step: fp32 weights only (bf16 agents use aaa_forward)");
+  if (L.sc) return fail(AAA_E_ARG, "actor_step: the stateful policy core uses aaa_forward");
+  if (cfg->B > 16) return fail(AAA_E_ARG, "actor_step: B <= 16 (got %d); larger batches use aaa_forward", cfg->B);
+  const size_t B = cfg->B, P = L.P;
+  const size_t sz[5] = {B * P * 64 * 4, B * P * 128 * 4, B * 512 * 4, B * 256 * 4, B * 256 * 4};
+  size_t o = 0;
+  for (int i = 0; i < 5; ++i) { off[i] = o; o = al256(o + sz[i]); }
+  *total = o;
+  return AAA_OK;
+}
+
+size_t aaa_actor_workspace_bytes(const aaa_cfg* cfg) {
+  Layout L;
+  size_t off[5], tot = 0;
+  return actor_layout(cfg, L, off, &tot) ? 0 : tot;
+}
+
+int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t stream) {
+  Layout L;
+  size_t off[5], tot = 0;
+  int r = actor_layout(cfg, L, off, &tot);
+  if (r) return r;
+  if (!io || !io->params || !io->packed || !io->basis || !io->frames || !io->h || !io->c || !io->logits ||
+      !io->values || !io->workspace)
+    return fail(AAA_E_ARG, "actor_step: NULL argument");
+  if (!aligned16(io->packed) || !aligned16(io->basis) || !aligned16(io->h) || !aligned16(io->c) ||
+      !aligned16(io->workspace) || !aligned16(io->params))
+    return fail(AAA_E_ALIGN, "actor_step: params, packed, basis, h, c and workspace must be 16-byte aligned");
+  if ((r = check_device())) return r;
+  const char* pk = (const char*)io->packed;
+  const float* prm = io->params;
+  char* ws = (char*)io->workspace;
+  ActorParams p;
+  p.B = L.B; p.H = L.H; p.W = L.W; p.H1 = L.H1; p.W1 = L.W1; p.h = L.h; p.w = L.w; p.P = L.P;
+  p.nq = L.nq; p.A = L.A; p.ldy = L.ldy; p.ans_in = L.ans_in; p.ans_ld = L.ans_ld; p.u8 = L.fu8;
+  p.frames = io->frames; p.basis = io->basis; p.prev_reward = io->prev_reward; p.prev_action = io->prev_action;
+  p.Wp1 = (const float*)(pk + L.k_Wp1); p.b1 = prm + L.poff[C0B];
+  p.Wp2 = (const float*)(pk + L.k_Wp2); p.b2 = prm + L.poff[C1B];
+  p.WpXH = (const float*)(pk + L.k_WpXH); p.bl = (const float*)(pk + L.k_bl);
+  p.Q = (const float*)(pk + L.k_Q);
+  p.W1p = (const float*)(pk + L.k_W1p); p.a0b = prm + L.poff[A0B];
+  p.A2W = prm + L.poff[A2W]; p.a2b = prm + L.poff[A2B];
+  p.Wihp = (const float*)(pk + L.k_Wihp); p.blc = (const float*)(pk + L.k_blc);
+  p.Whd = (const float*)(pk + L.k_Whd); p.bhd = (const float*)(pk + L.k_bhd);
+  p.hst = io->h; p.cst = io->c; p.logits = io->logits; p.values = io->values; p.attn = io->attn;
+  p.X = (float*)(ws + off[0]); p.Hs = (float*)(ws + off[1]); p.hid1 = (float*)(ws + off[2]);
+  p.AO = (float*)(ws + off[3]); p.LH = (float*)(ws + off[4]);
+  p.seed = io->seed; p.counter = io->counter; p.actions = io->actions; p.logp = io->logp; p.jac = io->dlogp_dlogits;
+  HIPCHK(actor_launch(p, stream));
   return AAA_OK;
 }
 

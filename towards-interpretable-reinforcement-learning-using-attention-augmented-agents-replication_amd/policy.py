@@ -152,17 +152,37 @@ class GraphActor:
     it, attention.py:293-296).  Weights are re-packed into the graph's own
     buffers whenever a parameter of ``agent`` changed (storage or in-place
     version), so optimizer steps between episodes are picked up.
+
+    ``chain`` selects the step: the actor chain (``aaa_actor_step``: six
+    launches sized for small B; fp32 agents with the reference's zero-state
+    policy core, B <= 16) or the learner's T=1 forward (``aaa_forward`` +
+    ``aaa_sample_actions``); None picks the chain whenever it applies.
     """
 
-    def __init__(self, agent, H: int, W: int, B: int = 1, seed: int = 0):
-        from .runtime import UnrollRunner
+    def __init__(self, agent, H: int, W: int, B: int = 1, seed: int = 0, chain: bool | None = None):
+        from .runtime import ActorRunner, UnrollRunner
         self.agent = agent
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("GraphActor needs the agent on the gfx950 device (there is no CPU fallback)")
         self.device, self.B, self.H, self.W = dev, B, H, W
-        self.runner = r = UnrollRunner(B, 1, H, W, agent.num_queries, agent.num_actions, agent.conv_dtype, dev,
-                                       frames_u8=True)
+        eligible = agent.conv_dtype == "fp32" and not getattr(agent, "stateful_core", False) and B <= 16
+        if chain and not eligible:
+            raise ValueError("the actor chain needs an fp32 agent with the zero-state policy core and B <= 16")
+        self.chain = eligible if chain is None else bool(chain)
+        if self.chain:
+            self.runner = r = ActorRunner(B, H, W, agent.num_queries, agent.num_actions, dev, frames_u8=True)
+            self._ws = r.new_workspace()
+            A = agent.num_actions
+            self._logits = torch.empty(B, A, device=dev)
+            self._values = torch.empty(B, A, device=dev)
+            self._attn = torch.empty(B, r.h, r.w, agent.num_queries, device=dev)
+            self._actions = torch.empty(B, dtype=torch.int32, device=dev)
+            self._logp = torch.empty(B, device=dev)
+        else:
+            r = UnrollRunner(B, 1, H, W, agent.num_queries, agent.num_actions, agent.conv_dtype, dev,
+                             frames_u8=True)
+            self.runner = r
         self.S = agent._basis_for(r.h, r.w, H, W, dev)
         self.params = list(agent.parameters())
         self.flat = torch.empty(r.n_params, device=dev)
@@ -190,6 +210,12 @@ class GraphActor:
 
     def _body(self):
         r = self.runner
+        if self.chain:
+            s = self.sampler
+            r.step(self.flat, self.packed, self.S, self.frame_u8, self._ws, self.h, self.c, self._logits,
+                   self._values, attn=self._attn, seed=s.seed, counter=s.counter, actions=self._actions,
+                   logp=self._logp)
+            return self._actions, self._logp, self._logits, self._values, self._attn
         X = self.frame_u8                  # uint8, cast in-kernel (AAA_FLAG_FRAMES_U8)
         ws = r.new_workspace()
         logits, values, attn, hT, cT = r.forward(self.flat, self.packed, self.S, X, ws, h0=self.h, c0=self.c,

@@ -225,3 +225,68 @@ class CnnRunner:
         N.check(self.lib.aaa_vision_cnn_bwd(ctypes.byref(self.desc), N.ptr(packed), N.ptr(dy2), N.ptr(dy1),
                                             N.ptr(grads), N.ptr(ws), N.stream_ptr(self.device)), "vision_cnn_bwd")
         return grads, dy1
+
+
+class ActorRunner:
+    """One environment step of B <= 16 rows on the actor chain (aaa_actor_step:
+    six launches sized for small B; fp32, zero-state policy core): the acting
+    half of main_mp.py:49-59 / test_model.py:42-73.  The ConvLSTM state
+    tensors ``h``/``c`` (B, h, w, 128) are read and overwritten in place, and
+    every output goes to caller-preallocated tensors, so a step can be
+    captured in a HIP graph and replayed."""
+
+    def __init__(self, B: int, H: int, W: int, nq: int = 4, A: int = 18, device=None, frames_u8: bool = True):
+        self.lib = N.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("aaa: the HIP path needs a ROCm GPU tensor device (no CPU fallback)")
+        self.B, self.H, self.W, self.nq, self.A = B, H, W, nq, A
+        self.frames_u8 = bool(frames_u8)
+        self.cfg = N.Cfg(B, 1, H, W, nq, A, N.F32, N.FLAG_FRAMES_U8 if frames_u8 else 0)
+        self.h, self.w = N.grid(H, W)
+        self.P = self.h * self.w
+        self.n_params, self.offsets, self.sizes = N.param_layout(self.cfg)
+        self.ws_bytes = self.lib.aaa_actor_workspace_bytes(ctypes.byref(self.cfg))
+        self.pk_bytes = self.lib.aaa_packed_bytes(ctypes.byref(self.cfg))
+        if not self.ws_bytes or not self.pk_bytes:
+            N.check(-1, "actor layout")
+
+    def new_workspace(self):
+        return torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+
+    def new_packed(self):
+        return torch.empty(self.pk_bytes, dtype=torch.uint8, device=self.device)
+
+    def state_shape(self):
+        return (self.B, self.h, self.w, 128)
+
+    def pack(self, flat_params, packed):
+        assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
+        assert flat_params.numel() == self.n_params, (flat_params.numel(), self.n_params)
+        N.check(self.lib.aaa_pack_weights(ctypes.byref(self.cfg), N.ptr(flat_params), N.ptr(packed),
+                                          N.stream_ptr(self.device)), "pack_weights")
+
+    def step(self, flat_params, packed, basis, frames, workspace, h, c, logits, values, attn=None,
+             prev_reward=None, prev_action=None, seed: int = 0, counter=None, actions=None, logp=None,
+             dlogp=None):
+        """frames (B, H, W, 3) uint8 (or fp32 without frames_u8); h, c updated in
+        place; logits/values (B, A), attn (B, h, w, nq) or None; actions (B,)
+        int32 (None: no draw) with logp (B,) / dlogp (B, A) and the device draw
+        ``counter`` (one-element int64, advanced per step) as aaa_sample_actions."""
+        exp = (self.B, self.H, self.W, 3)
+        dt = torch.uint8 if self.frames_u8 else torch.float32
+        if tuple(frames.shape[-4:]) != exp or frames.numel() != self.B * self.H * self.W * 3 or \
+                frames.dtype != dt or not frames.is_contiguous():
+            raise ValueError(f"frames must be contiguous {dt} {exp}, got {tuple(frames.shape)} {frames.dtype}")
+        for name, t in (("h", h), ("c", c)):
+            if tuple(t.shape) != self.state_shape() or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"{name} must be contiguous fp32 {self.state_shape()}")
+        io = N.ActorIO()
+        for k, v in dict(params=flat_params, packed=packed, basis=basis, frames=frames, prev_reward=prev_reward,
+                         prev_action=prev_action, h=h, c=c, logits=logits, values=values, attn=attn,
+                         workspace=workspace, counter=counter, actions=actions, logp=logp,
+                         dlogp_dlogits=dlogp).items():
+            setattr(io, k, None if v is None else v.data_ptr())
+        io.seed = int(seed) & (2**64 - 1)
+        N.check(self.lib.aaa_actor_step(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(self.device)),
+                "actor_step")
