@@ -19,7 +19,7 @@ from pmcsum import derived, load  # noqa: E402
 # kernel class (bench.py names) -> alternatives, each a list of substrings that
 # must all appear in the kernel name (fp32 register-staged / bf16 LDS-DMA ring)
 CLASSES = {
-    "ConvLSTM BPTT step": [["EpiConvLstmBwd"], ["k_convlstm_bwd_frames"]],
+    "ConvLSTM BPTT step": [["EpiConvLstmBwd"], ["k_convlstm_bwd_frames"], ["k_convlstm_bwd_pairs"]],
     "ConvLSTM forward step": [["EpiConvLstmFwd"], ["k_convlstm_fwd_frames"]],
     "ConvLSTM weight-gradient GEMM": [["128, 128, 32", "LdIm2colTB", "EpiStore<true>"], ["GIm2colT", "EpiAtomicD"],
                                       ["GIm2colT", "EpiWgrad"]],
