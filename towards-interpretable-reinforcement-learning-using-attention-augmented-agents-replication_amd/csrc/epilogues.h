@@ -135,6 +135,48 @@ struct EpiStoreParityBias : BiasAcc {
   }
 };
 
+// All four stride-2 dgrad parity classes of one tile (the KS = 2 halo conv,
+// halo.h): row i = 32*cls + ci, class cls = (py, px) = (cls>>1, cls&1); column
+// j = (frame, a, b) of the shared Ha x Wa class grid (Ha = ceil(H1/2)) lands at
+// (2a+py, 2b+px) when that is inside H1 x W1 (odd H1: the py = 1 class is one
+// row short).  The bias partials fold the four classes: bg[ci] += sum of the
+// fp32 values of every valid output of channel ci.
+template <typename OT>
+struct EpiStoreParity4 : BiasAcc {
+  OT* out;             // [F][H1][W1][32]
+  int Nj, Wa, H1, W1;
+  FastDiv dHW, dW;
+  float* bg;
+  EpiStoreParity4(OT* o, int nj, int ha, int wa, int h1, int w1, float* b)
+      : out(o), Nj(nj), Wa(wa), H1(h1), W1(w1), dHW((uint32_t)(ha * wa)), dW((uint32_t)wa), bg(b) {}
+  __device__ __forceinline__ void finish(int i, int j, float v0, float v1, float v2, float v3, const Pre&,
+                                         Acc* acc = nullptr) const {
+    if (j >= Nj || i >= 128) return;
+    const int cls = i >> 5, ci = i & 31;
+    const int f = (int)dHW.div((uint32_t)j), r = j - f * (int)dHW.d;
+    const int a = (int)dW.div((uint32_t)r), b = r - a * Wa;
+    const int oy = 2 * a + (cls >> 1), ox = 2 * b + (cls & 1);
+    if (oy >= H1 || ox >= W1) return;
+    store4(out + ((size_t)(f * H1 + oy) * W1 + ox) * 32 + ci, v0, v1, v2, v3);
+    if (acc) { acc->s[0] += v0; acc->s[1] += v1; acc->s[2] += v2; acc->s[3] += v3; }
+  }
+  template <int G4, int NT>
+  __device__ __forceinline__ void flush(const Acc& acc, float* red, int, int) const {
+    static_assert(G4 == 32 && NT % G4 == 0, "one 128-row tile: 32 four-row groups");
+    constexpr int NS = NT / G4;
+    const int r4 = threadIdx.x % G4, sl = threadIdx.x / G4;
+    *reinterpret_cast<f32x4*>(red + (sl * G4 + r4) * 4) = f32x4{acc.s[0], acc.s[1], acc.s[2], acc.s[3]};
+    __syncthreads();
+    for (int c = threadIdx.x; c < 32; c += NT) {   // channel c: rows c, 32+c, 64+c, 96+c
+      float t = 0.f;
+      for (int k = 0; k < NS; ++k)
+#pragma unroll
+        for (int cls = 0; cls < 4; ++cls) t += red[k * G4 * 4 + 32 * cls + c];
+      atomicAdd(bg + c, t);
+    }
+  }
+};
+
 // dx[j*ld + i] = v * (mask[j*ldm + i] > 0)   (ReLU backward through a saved output)
 struct EpiReluBwdT {
   float* out;

@@ -45,6 +45,7 @@ struct HaloParams {
   uint32_t x_bytes;     // buffer range of x
   int h, w, nframes;
   int transposed;       // dgrad gather
+  int oh, ow;           // output grid per frame (0: the input grid); KS = 2 convs only
 };
 
 // The halo rows a ds_read_b128 lane group (16 lanes, one 256-B bank row) reads
@@ -55,7 +56,11 @@ struct HaloParams {
 template <int RS>
 __device__ __forceinline__ int halo_swz(int row) { return lds_swz<RS>(row); }
 
-template <class C, class EP, int NBUF = 3>
+// KS = 3: the 3x3 / pad-1 conv above.  KS = 2: a 2x2 stride-1 conv whose
+// output (a, b) on an oh x ow grid reads input pixels (a + ky, b + kx), rows
+// past the input grid reading the zero border -- conv2's dgrad classes
+// (runtime.hip conv2_dgrad: all four parity classes share this gather).
+template <class C, class EP, int NBUF = 3, int KS = 3>
 __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, TileMap tm) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, CK = C::CK, WI = C::WI, WJ = C::WJ, NT = C::NT;
@@ -78,8 +83,10 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
 
   int ti, tj, tz;
   tile_of(tm, ti, tj, tz);
+  constexpr int NTAP = KS * KS;
   const int P = p.h * p.w, Hp = p.h + 2, Wp = p.w + 2, HP = Hp * Wp;
-  const int i0 = ti * BI, f0 = tj * C::FR, j0 = f0 * P;
+  const int ow = KS == 2 && p.ow ? p.ow : p.w, PO = KS == 2 && p.oh ? p.oh * ow : P;   // output grid
+  const int i0 = ti * BI, f0 = tj * C::FR, j0 = f0 * PO;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wi = wave / WJ, wj = wave - wi * WJ;
   const int r32 = lane & 31, hh = lane >> 5;
@@ -93,8 +100,8 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
     avoff[c] = row < p.Mi ? (uint32_t)((row * p.ldw + lc * VG) * (int)sizeof(T)) : kOOB;
   }
   const int wofs = __builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u) * VG);
-  auto issue_a = [&](int step, int cc) {         // step = chunk*9 + tap
-    const int tap = step - 9 * cc;
+  auto issue_a = [&](int step, int cc) {         // step = chunk*NTAP + tap
+    const int tap = step - NTAP * cc;
     const int ko = __builtin_amdgcn_readfirstlane((tap * p.Cin + cc * CK) * (int)sizeof(T));
     T* dst = As + (step % NBUF) * AEL;
 #pragma unroll
@@ -121,9 +128,9 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
   int hrow[MJ];
 #pragma unroll
   for (int b = 0; b < MJ; ++b) {
-    const int j = wj * WTJ + b * 32 + r32;          // tile-local pixel
-    const int fl = j / P, q = j - fl * P, y = q / p.w, xx = q - y * p.w;
-    hrow[b] = j < C::FR * P ? fl * HP + (y + 1) * Wp + (xx + 1) : C::HMAX - 1;
+    const int j = wj * WTJ + b * 32 + r32;          // tile-local output pixel
+    const int fl = j / PO, q = j - fl * PO, y = q / ow, xx = q - y * ow;
+    hrow[b] = j < C::FR * PO ? fl * HP + (y + 1) * Wp + (xx + 1) : C::HMAX - 1;
   }
   const int sg = p.transposed ? -1 : 1;
 
@@ -137,17 +144,17 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
 
   using PL = EpiPlan<C, EP, has_pre<EP>::value>;
   typename PL::PreT pre[PL::PD];
-  const int jn = min(C::FR, p.nframes - f0) * P;    // valid tile columns (whole frames)
+  const int jn = min(C::FR, p.nframes - f0) * PO;   // valid tile columns (whole frames)
   epilogue_prefetch<C, EP, PL>(ep, i0, j0, jn, pre);
 
-  const int nc = p.Cin / CK, ns = 9 * nc;
+  const int nc = p.Cin / CK, ns = NTAP * nc;
   issue_h(0);
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
-    if (s < ns) issue_a(s, s / 9);
+    if (s < ns) issue_a(s, s / NTAP);
 
   for (int s = 0; s < ns; ++s) {
-    const int cc = s / 9, tap = s - 9 * cc;
+    const int cc = s / NTAP, tap = s - NTAP * cc;
     // A(s) is the oldest weight stage in flight; the next chunk's halo, issued
     // at this chunk's first step right after A(9cc+NBUF-1), is younger than
     // A(s) for the steps 9cc+1 .. 9cc+NBUF-1 (it must not be waited for there).
@@ -159,12 +166,12 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
       wait_vmcnt<0>();
     }
     barrier_lds();
-    if (s + NBUF - 1 < ns) issue_a(s + NBUF - 1, (s + NBUF - 1) / 9);
+    if (s + NBUF - 1 < ns) issue_a(s + NBUF - 1, (s + NBUF - 1) / NTAP);
     if (tap == 0 && cc + 1 < nc) issue_h(cc + 1);
     const T* Ac = As + (s % NBUF) * AEL;
     const T* Hc = Hs + (cc & 1) * HEL;
-    const int ky = tap / 3, kx = tap - 3 * ky;
-    const int toff = sg * ((ky - 1) * Wp + (kx - 1));
+    const int ky = tap / KS, kx = tap - KS * ky;
+    const int toff = KS == 3 ? sg * ((ky - 1) * Wp + (kx - 1)) : ky * Wp + kx;
 #pragma unroll
     for (int s2 = 0; s2 < CK / 16; ++s2) {
       const int kofs = 16 * s2 + 8 * hh;
@@ -215,15 +222,17 @@ inline bool halo_fits(int h, int w, int Cin) {
 
 // Host launcher: Mi output rows, nframes frames of h x w pixels.  Returns
 // hipErrorInvalidValue when the geometry does not fit the compile-time tile.
-template <class C, class EP>
+template <class C, class EP, int KS = 3>
 inline hipError_t launch_halo(const HaloParams& p, const EP& ep, hipStream_t st) {
   const int Hp = p.h + 2, Wp = p.w + 2;
+  const int PO = KS == 2 && p.oh ? p.oh * p.ow : p.h * p.w;
   if (p.Mi <= 0 || p.nframes <= 0) return hipSuccess;
-  if (C::FR * p.h * p.w > C::BJ || C::FR * Hp * Wp + 1 > C::HMAX || p.Cin % C::CK || p.Cin < C::CK)
+  if (C::FR * PO > C::BJ || C::FR * Hp * Wp + 1 > C::HMAX || p.Cin % C::CK || p.Cin < C::CK)
     return hipErrorInvalidValue;
+  if (KS == 2 && p.oh && (p.oh > p.h || p.ow > p.w)) return hipErrorInvalidValue;
   if ((size_t)p.nframes * p.h * p.w * p.cs * sizeof(typename C::type) > 0x7fffffffu) return hipErrorInvalidValue;
   dim3 grid((p.nframes + C::FR - 1) / C::FR, (p.Mi + C::BI - 1) / C::BI, 1);
-  hipLaunchKernelGGL((conv3_halo_kernel<C, EP>), grid, dim3(C::NT), 0, st, p, ep, tile_map(grid));
+  hipLaunchKernelGGL((conv3_halo_kernel<C, EP, 3, KS>), grid, dim3(C::NT), 0, st, p, ep, tile_map(grid));
   return hipGetLastError();
 }
 

@@ -1055,6 +1055,23 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
 template <typename T>
 static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, int frames, float* gbias,
                        hipStream_t s) {
+  {
+    // small grids: the four classes share one gather (output (a, b) reads dY2
+    // (a + ty, b + tx)), so one 128-row tile (class-major rows, [cls][32][256]
+    // = k_WdT2) per frame reads the frame's dY2 once as a zero-bordered LDS
+    // image (halo.h, KS = 2) -- one launch instead of four 32-row GEMMs whose
+    // K = 256 loops were pure latency (4 x 65 us at C3, 0.06 of bf16 peak)
+    using HC = HaloCfg<T, 128, 128, std::is_same<T, float>::value ? 32 : 64, 2, 2, 1, 192>;
+    const int Ha = (L.H1 + 1) / 2, Wa = (L.W1 + 1) / 2;
+    if (Ha * Wa <= HC::BJ && (L.h + 2) * (L.w + 2) + 1 <= HC::HMAX && Ha <= L.h && Wa <= L.w &&
+        env_int("AAA_DGRAD2_HALO", 1)) {
+      EpiStoreParity4<T> ep(dy1, frames * Ha * Wa, Ha, Wa, L.H1, L.W1, gbias);
+      const HaloParams hp{pk + L.k_WdT2, 256, 128, dy2, 64, 0, 64, (uint32_t)((size_t)frames * L.P * 64 * L.esz),
+                          L.h, L.w, frames, 0, Ha, Wa};
+      HIPCHK((launch_halo<HC, EpiStoreParity4<T>, 2>(hp, ep, s)));
+      return AAA_OK;
+    }
+  }
   if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
     // the LDS-DMA ring (dY2 is already in T), dY1 stored in T, conv1's bias
     // gradient summed from the fp32 values in the epilogue (no column-sum pass)
