@@ -29,6 +29,18 @@ struct F32Unpack {
   float* whh = nullptr;
 };
 
+// aaa_pack_weights' param-only layouts in one launch (misc.hip k_pack_all)
+template <typename T>
+struct PackAll {
+  const float *c1w, *c2w;
+  T *Wp1, *Wp2, *WdT2;
+  LstmPtrs lstm;
+  T *WpX, *WpH, *WdT, *WpXH;
+  float* bl;
+  F32Pack f32;
+};
+template <typename T> hipError_t pack_all(const PackAll<T>& a, hipStream_t st);
+
 hipError_t query_pack(const float* b0, const float* W2, const float* b2, const float* W4, const float* b4, int nq,
                       float* q1, float* q2, float* Q, hipStream_t st);
 hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hipStream_t st);
@@ -44,6 +56,18 @@ hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st);
+struct ColSumSeg {
+  const float* X;
+  int ld, N;
+  float* out;   // out[n] += sum over the M rows of X[m*ld + n]
+};
+struct ColSums {
+  ColSumSeg s[6];
+  int n = 0;
+  int cb[7];    // column-block prefix (filled by colsum_multi)
+  void add(const float* X, int ld, int N, float* out) { s[n++] = ColSumSeg{X, ld, N, out}; }
+};
+hipError_t colsum_multi(ColSums c, int M, hipStream_t st);
 template <typename TI> hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st);
 template <typename TZ, typename GT>
 hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const GT* gates, const float* cprev,
@@ -65,5 +89,8 @@ hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st);
 hipError_t unpack_conv(const float* g, int Cout, int Cin, int K, float* dst, hipStream_t st);
 hipError_t unpack_lstm(const float* gW, const float* gb, const LstmGrads& L, hipStream_t st);
 hipError_t unpack_f32(const F32Unpack& p, hipStream_t st);
+// ConvLSTM grads (gW == null: none) + conv2 + conv1 weight grads, one launch
+hipError_t unpack_cv(const float* gW, const float* gb, const LstmGrads& L, const float* g2, float* d2, const float* g1,
+                     float* d1, hipStream_t st);
 
 }  // namespace aaa

@@ -501,13 +501,16 @@ __global__ void k_cast(long n, const TI* __restrict__ src, TO* __restrict__ dst)
 // Conv weight in the reference's (Cout, Cin, kx, ky) orientation (Q3) ->
 // [Cout][(ky*K + kx)*Cin + ci].
 template <typename T>
+__device__ __forceinline__ void pack_conv_el(int idx, const float* __restrict__ w, int Cin, int K, T* dst) {
+  const int o = idx / (K * K * Cin), r = idx - o * (K * K * Cin);
+  const int tap = r / Cin, ci = r - tap * Cin, ky = tap / K, kx = tap - ky * K;
+  dst[idx] = (T)w[((size_t)(o * Cin + ci) * K + kx) * K + ky];
+}
+template <typename T>
 __global__ void k_pack_conv(const float* __restrict__ w, int Cout, int Cin, int K, T* dst) {
   const int n = Cout * K * K * Cin;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int o = idx / (K * K * Cin), r = idx - o * (K * K * Cin);
-    const int tap = r / Cin, ci = r - tap * Cin, ky = tap / K, kx = tap - ky * K;
-    dst[idx] = (T)w[((size_t)(o * Cin + ci) * K + kx) * K + ky];
-  }
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    pack_conv_el(idx, w, Cin, K, dst);
 }
 
 // Frames (F,H,W,3) fp32 or uint8 (the environment's observation, cast here
@@ -538,36 +541,44 @@ __global__ void k_frames_rgbx(int F, int H, int W, const TI* __restrict__ x, T* 
 // pad-0 conv over dY2 with W_c[ci][(ty*2+tx)*64 + co] = W2[co][ci][kx][ky],
 // ky = py + 2(1-ty), kx = px + 2(1-tx) (reference (Cout,Cin,kx,ky) layout, Q3).
 template <typename T>
+__device__ __forceinline__ void pack_conv2_classes_el(int idx, const float* __restrict__ w2, T* dst) {
+  const int cls = idx >> 13, r = idx & 8191, ci = r >> 8, k = r & 255;
+  const int t = k >> 6, co = k & 63, ty = t >> 1, tx = t & 1;
+  const int py = cls >> 1, px = cls & 1;
+  const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
+  dst[idx] = (T)w2[((size_t)(co * 32 + ci) * 4 + kx) * 4 + ky];
+}
+template <typename T>
 __global__ void k_pack_conv2_classes(const float* __restrict__ w2, T* dst) {
   const int n = 4 * 32 * 256;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int cls = idx >> 13, r = idx & 8191, ci = r >> 8, k = r & 255;
-    const int t = k >> 6, co = k & 63, ty = t >> 1, tx = t & 1;
-    const int py = cls >> 1, px = cls & 1;
-    const int ky = py + 2 * (1 - ty), kx = px + 2 * (1 - tx);
-    dst[idx] = (T)w2[((size_t)(co * 32 + ci) * 4 + kx) * 4 + ky];
-  }
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    pack_conv2_classes_el(idx, w2, dst);
 }
 
 // conv1 weights with a zero 4th input channel: [32][(ky*8 + kx)*4 + ci]
 template <typename T>
+__device__ __forceinline__ void pack_conv1_rgbx_el(int idx, const float* __restrict__ w, T* dst) {
+  const int o = idx >> 8, r = idx & 255, tap = r >> 2, ci = r & 3, ky = tap >> 3, kx = tap & 7;
+  dst[idx] = ci < 3 ? (T)w[((size_t)(o * 3 + ci) * 8 + kx) * 8 + ky] : (T)0.f;
+}
+template <typename T>
 __global__ void k_pack_conv1_rgbx(const float* __restrict__ w, T* dst) {
   const int n = 32 * 256;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    const int o = idx >> 8, r = idx & 255, tap = r >> 2, ci = r & 3, ky = tap >> 3, kx = tap & 7;
-    dst[idx] = ci < 3 ? (T)w[((size_t)(o * 3 + ci) * 8 + kx) * 8 + ky] : (T)0.f;
-  }
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    pack_conv1_rgbx_el(idx, w, dst);
 }
 
+__device__ __forceinline__ void unpack_conv1_rgbx_el(int idx, const float* __restrict__ g, float* dst) {
+  int r = idx;
+  const int ky = r % 8; r /= 8;
+  const int kx = r % 8; r /= 8;
+  const int ci = r % 3, o = r / 3;
+  dst[idx] = g[o * 256 + (ky * 8 + kx) * 4 + ci];
+}
 __global__ void k_unpack_conv1_rgbx(const float* __restrict__ g, float* dst) {
   const int n = 32 * 3 * 64;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    int r = idx;
-    const int ky = r % 8; r /= 8;
-    const int kx = r % 8; r /= 8;
-    const int ci = r % 3, o = r / 3;
-    dst[idx] = g[o * 256 + (ky * 8 + kx) * 4 + ci];
-  }
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    unpack_conv1_rgbx_el(idx, g, dst);
 }
 
 
@@ -586,10 +597,11 @@ __device__ __forceinline__ float lstm_w(const LstmPtrs& L, int row, int ky, int 
 //   h-part  WpH[n][tap*128 + ci]     (the recurrent step)
 //   dgrad   WdT[c'][tap*512 + n]     (c' over [x | h]: dx and dh of the BPTT)
 //   fused   WpXH[n][tap*192 + c']    (the step GEMM whose K covers the whole XH slot)
+constexpr int kPackLstmN = 512 * 576 + 512 * 1152 + 192 * 4608 + 512 * 1728;
 template <typename T>
-__global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T* WpXH) {
-  const int nx = 512 * 576, nh = 512 * 1152, nd = 192 * 4608, nf = 512 * 1728;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < nx + nh + nd + nf; idx += gridDim.x * blockDim.x) {
+__device__ __forceinline__ void pack_lstm_el(int idx, const LstmPtrs& L, T* WpX, T* WpH, float* bl, T* WdT, T* WpXH) {
+  const int nx = 512 * 576, nh = 512 * 1152, nd = 192 * 4608;
+  {
     int i = idx;
     if (i < nx) {
       const int row = i / 576, k = i - row * 576;
@@ -612,6 +624,11 @@ __global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T
     }
   }
 }
+template <typename T>
+__global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T* WpXH) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kPackLstmN; idx += gridDim.x * blockDim.x)
+    pack_lstm_el(idx, L, WpX, WpH, bl, WdT, WpXH);
+}
 
 // Step 0 from a zero state: the gates come from the batched x-part alone.
 template <typename T>
@@ -630,70 +647,92 @@ __global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gat
   }
 }
 
-__global__ void k_pack_f32(F32Pack p) {
+__host__ __device__ inline int pack_f32_n(const F32Pack& p) {
+  return 512 * p.ans_ld + 1024 * 256 + 1024 + p.ldy * 256 + p.ldy + (p.Wihhp ? 1024 * 512 : 0);
+}
+__device__ __forceinline__ void pack_f32_el(int idx, const F32Pack& p) {
   const int n1 = 512 * p.ans_ld, n2 = 1024 * 256, n3 = 1024, n4 = p.ldy * 256, n5 = p.ldy;
-  const int n6 = p.Wihhp ? 1024 * 512 : 0;
-  const int tot = n1 + n2 + n3 + n4 + n5 + n6;
+  int i = idx;
+  if (i >= n1 + n2 + n3 + n4 + n5) {   // [W_ih | W_hh] rows 4u+g (stateful core)
+    i -= n1 + n2 + n3 + n4 + n5;
+    const int row = i >> 9, k = i & 511, u = row >> 2, g = row & 3;
+    p.Wihhp[i] = k < 256 ? p.wih[(size_t)(g * 256 + u) * 256 + k] : p.whh[(size_t)(g * 256 + u) * 256 + k - 256];
+    return;
+  }
+  if (i < n1) {
+    const int o = i / p.ans_ld, k = i - o * p.ans_ld;
+    p.W1p[i] = k < p.ans_in ? p.a0w[(size_t)o * p.ans_in + k] : 0.f;
+    return;
+  }
+  i -= n1;
+  if (i < n2) {
+    const int row = i >> 8, k = i & 255, u = row >> 2, g = row & 3;
+    p.Wihp[i] = p.wih[(size_t)(g * 256 + u) * 256 + k];
+    return;
+  }
+  i -= n2;
+  if (i < n3) {
+    const int u = i >> 2, g = i & 3;
+    p.blc[i] = p.bih[g * 256 + u] + p.bhh[g * 256 + u];
+    return;
+  }
+  i -= n3;
+  if (i < n4) {
+    const int o = i >> 8, k = i & 255;
+    float v = 0.f;
+    if (o < p.A) v = p.pw[o * 256 + k];
+    else if (o < 2 * p.A) v = p.vw[(o - p.A) * 256 + k];
+    p.Whd[i] = v;
+    return;
+  }
+  i -= n4;
+  float v = 0.f;
+  if (i < p.A) v = p.pb[i];
+  else if (i < 2 * p.A) v = p.vb[i - p.A];
+  p.bhd[i] = v;
+}
+__global__ void k_pack_f32(F32Pack p) {
+  const int tot = pack_f32_n(p);
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) pack_f32_el(idx, p);
+}
+
+// Every weight layout of aaa_pack_weights that depends on the params alone, in
+// one launch (each was its own ~5 us launch): conv1 RGBx, conv2, conv2's dgrad
+// classes, the four ConvLSTM layouts and the fp32 tail layouts, one grid-stride
+// pass over their concatenated index ranges.
+template <typename T>
+__global__ void k_pack_all(PackAll<T> a) {
+  const int n1 = 32 * 256, n2 = n1 + 64 * 512, n3 = n2 + 4 * 32 * 256, n4 = n3 + kPackLstmN;
+  const int tot = n4 + pack_f32_n(a.f32);
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
-    int i = idx;
-    if (i >= n1 + n2 + n3 + n4 + n5) {   // [W_ih | W_hh] rows 4u+g (stateful core)
-      i -= n1 + n2 + n3 + n4 + n5;
-      const int row = i >> 9, k = i & 511, u = row >> 2, g = row & 3;
-      p.Wihhp[i] = k < 256 ? p.wih[(size_t)(g * 256 + u) * 256 + k] : p.whh[(size_t)(g * 256 + u) * 256 + k - 256];
-      continue;
-    }
-    if (i < n1) {
-      const int o = i / p.ans_ld, k = i - o * p.ans_ld;
-      p.W1p[i] = k < p.ans_in ? p.a0w[(size_t)o * p.ans_in + k] : 0.f;
-      continue;
-    }
-    i -= n1;
-    if (i < n2) {
-      const int row = i >> 8, k = i & 255, u = row >> 2, g = row & 3;
-      p.Wihp[i] = p.wih[(size_t)(g * 256 + u) * 256 + k];
-      continue;
-    }
-    i -= n2;
-    if (i < n3) {
-      const int u = i >> 2, g = i & 3;
-      p.blc[i] = p.bih[g * 256 + u] + p.bhh[g * 256 + u];
-      continue;
-    }
-    i -= n3;
-    if (i < n4) {
-      const int o = i >> 8, k = i & 255;
-      float v = 0.f;
-      if (o < p.A) v = p.pw[o * 256 + k];
-      else if (o < 2 * p.A) v = p.vw[(o - p.A) * 256 + k];
-      p.Whd[i] = v;
-      continue;
-    }
-    i -= n4;
-    {
-      float v = 0.f;
-      if (i < p.A) v = p.pb[i];
-      else if (i < 2 * p.A) v = p.vb[i - p.A];
-      p.bhd[i] = v;
-    }
+    if (idx < n1) pack_conv1_rgbx_el(idx, a.c1w, a.Wp1);
+    else if (idx < n2) pack_conv_el(idx - n1, a.c2w, 32, 4, a.Wp2);
+    else if (idx < n3) pack_conv2_classes_el(idx - n2, a.c2w, a.WdT2);
+    else if (idx < n4) pack_lstm_el(idx - n3, a.lstm, a.WpX, a.WpH, a.bl, a.WdT, a.WpXH);
+    else pack_f32_el(idx - n4, a.f32);
   }
 }
+
 
 // ------------------------------------------------------------ unpacking ---
+__device__ __forceinline__ void unpack_conv_el(int idx, const float* __restrict__ g, int Cin, int K, float* dst) {
+  int r = idx;
+  const int ky = r % K; r /= K;
+  const int kx = r % K; r /= K;
+  const int ci = r % Cin, o = r / Cin;
+  dst[idx] = g[(size_t)o * K * K * Cin + (ky * K + kx) * Cin + ci];
+}
 __global__ void k_unpack_conv(const float* __restrict__ g, int Cout, int Cin, int K, float* dst) {
   const int n = Cout * Cin * K * K;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
-    int r = idx;
-    const int ky = r % K; r /= K;
-    const int kx = r % K; r /= K;
-    const int ci = r % Cin, o = r / Cin;
-    dst[idx] = g[(size_t)o * K * K * Cin + (ky * K + kx) * Cin + ci];
-  }
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    unpack_conv_el(idx, g, Cin, K, dst);
 }
 
-__global__ void k_unpack_lstm(const float* __restrict__ gW, const float* __restrict__ gb, LstmGrads L) {
+constexpr int kUnpackLstmN = 4 * (128 * 64 * 9 + 128 * 128 * 9 + 128);
+__device__ __forceinline__ void unpack_lstm_el(int idx, const float* __restrict__ gW, const float* __restrict__ gb,
+                                               const LstmGrads& L) {
   const int nx = 128 * 64 * 9, nh = 128 * 128 * 9;
-  const int tot = 4 * (nx + nh + 128);
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+  {
     const int per = nx + nh + 128;
     const int g = idx / per;
     int i = idx - g * per;
@@ -713,6 +752,21 @@ __global__ void k_unpack_lstm(const float* __restrict__ gW, const float* __restr
       i -= nh;
       L.bx[g][i] = gb[4 * i + g];
     }
+  }
+}
+__global__ void k_unpack_lstm(const float* __restrict__ gW, const float* __restrict__ gb, LstmGrads L) {
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < kUnpackLstmN; idx += gridDim.x * blockDim.x)
+    unpack_lstm_el(idx, gW, gb, L);
+}
+// The ConvLSTM (optional: gW == null skips it) and both conv weight grads back
+// into the reference layouts in one launch (the end of a CORE + VISION backward).
+__global__ void k_unpack_cv(const float* __restrict__ gW, const float* __restrict__ gb, LstmGrads L,
+                            const float* __restrict__ g2, float* d2, const float* __restrict__ g1, float* d1) {
+  const int n0 = gW ? kUnpackLstmN : 0, n1 = n0 + 64 * 32 * 16, n2 = n1 + 32 * 3 * 64;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n2; idx += gridDim.x * blockDim.x) {
+    if (idx < n0) unpack_lstm_el(idx, gW, gb, L);
+    else if (idx < n1) unpack_conv_el(idx - n0, g2, 32, 4, d2);
+    else unpack_conv1_rgbx_el(idx - n1, g1, d1);
   }
 }
 
@@ -989,5 +1043,55 @@ template hipError_t pack_lstm_all<float>(const LstmPtrs&, float*, float*, float*
 template hipError_t pack_lstm_all<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, __bf16*, hipStream_t);
 template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);
 template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t);
+
+template <typename T>
+hipError_t pack_all(const PackAll<T>& a, hipStream_t st) {
+  const long n = 32L * 256 + 64 * 512 + 4 * 32 * 256 + kPackLstmN + pack_f32_n(a.f32);
+  hipLaunchKernelGGL(k_pack_all<T>, dim3(nblk(n)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+template hipError_t pack_all<float>(const PackAll<float>&, hipStream_t);
+template hipError_t pack_all<__bf16>(const PackAll<__bf16>&, hipStream_t);
+
+hipError_t unpack_cv(const float* gW, const float* gb, const LstmGrads& L, const float* g2, float* d2, const float* g1,
+                     float* d1, hipStream_t st) {
+  const long n = (gW ? kUnpackLstmN : 0) + 64L * 32 * 16 + 32 * 3 * 64;
+  hipLaunchKernelGGL(k_unpack_cv, dim3(nblk(n)), dim3(256), 0, st, gW, gb, L, g2, d2, g1, d1);
+  return hipGetLastError();
+}
+
+// Several column sums over the same M rows in one launch (the heads / LSTMCell /
+// answer-MLP bias grads and the query's dQ, each ~5 us as its own launch):
+// block x runs column block (x - cb[k]) of segment k.
+__global__ void k_colsum_multi(ColSums c, int M, int rows_per) {
+  __shared__ float red[256];
+  int k = 0;
+  while (k + 1 < c.n && (int)blockIdx.x >= c.cb[k + 1]) ++k;
+  const ColSumSeg s = c.s[k];
+  const int col = ((int)blockIdx.x - c.cb[k]) * 64 + (threadIdx.x & 63);
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float acc = 0.f;
+  if (col < s.N) {
+#pragma unroll 8
+    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) acc += s.X[(size_t)r * s.ld + col];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64 && col < s.N)
+    atomicAdd(s.out + col, red[threadIdx.x] + red[threadIdx.x + 64] + red[threadIdx.x + 128] + red[threadIdx.x + 192]);
+}
+
+hipError_t colsum_multi(ColSums c, int M, hipStream_t st) {
+  if (M <= 0 || c.n <= 0) return hipSuccess;
+  c.cb[0] = 0;
+  for (int k = 0; k < c.n; ++k) c.cb[k + 1] = c.cb[k] + (c.s[k].N + 63) / 64;
+  const int cols = c.cb[c.n];
+  int split = (1024 + cols - 1) / cols;
+  int rows_per = (M + split - 1) / split;
+  if (rows_per < 64) rows_per = 64;
+  split = (M + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(k_colsum_multi, dim3(cols, split), dim3(256), 0, st, c, M, rows_per);
+  return hipGetLastError();
+}
 
 }  // namespace aaa

@@ -629,22 +629,18 @@ static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const Ep
 // ------------------------------------------------------------- packing ----
 template <typename T>
 static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
-  HIPCHK(pack_conv1_rgbx<T>(prm + L.poff[C0W], (T*)(pk + L.k_Wp1), st));
-  HIPCHK(pack_conv<T>(prm + L.poff[C1W], 64, 32, 4, (T*)(pk + L.k_Wp2), st));
-  HIPCHK(pack_conv2_classes<T>(prm + L.poff[C1W], (T*)(pk + L.k_WdT2), st));
-  LstmPtrs lp;
+  PackAll<T> a;
+  a.c1w = prm + L.poff[C0W];
+  a.c2w = prm + L.poff[C1W];
+  a.Wp1 = (T*)(pk + L.k_Wp1); a.Wp2 = (T*)(pk + L.k_Wp2); a.WdT2 = (T*)(pk + L.k_WdT2);
   for (int g = 0; g < 4; ++g) {
-    lp.wx[g] = prm + L.poff[XI_W + 3 * g];
-    lp.bx[g] = prm + L.poff[XI_B + 3 * g];
-    lp.wh[g] = prm + L.poff[HI_W + 3 * g];
+    a.lstm.wx[g] = prm + L.poff[XI_W + 3 * g];
+    a.lstm.bx[g] = prm + L.poff[XI_B + 3 * g];
+    a.lstm.wh[g] = prm + L.poff[HI_W + 3 * g];
   }
-  HIPCHK(pack_lstm_all<T>(lp, (T*)(pk + L.k_WpX), (T*)(pk + L.k_WpH), (T*)(pk + L.k_WdTl), (float*)(pk + L.k_bl),
-                          (T*)(pk + L.k_WpXH), st));
-  if constexpr (!std::is_same<T, float>::value) {
-    HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
-    HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
-  }
-  F32Pack fp;
+  a.WpX = (T*)(pk + L.k_WpX); a.WpH = (T*)(pk + L.k_WpH); a.WdT = (T*)(pk + L.k_WdTl);
+  a.WpXH = (T*)(pk + L.k_WpXH); a.bl = (float*)(pk + L.k_bl);
+  F32Pack& fp = a.f32;
   fp.a0w = prm + L.poff[A0W]; fp.wih = prm + L.poff[WIH]; fp.bih = prm + L.poff[BIH]; fp.bhh = prm + L.poff[BHH];
   fp.pw = prm + L.poff[PW]; fp.vw = prm + L.poff[VW]; fp.pb = prm + L.poff[PB]; fp.vb = prm + L.poff[VB];
   fp.W1p = (float*)(pk + L.k_W1p); fp.Wihp = (float*)(pk + L.k_Wihp); fp.blc = (float*)(pk + L.k_blc);
@@ -654,7 +650,11 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     fp.whh = prm + L.poff[WHH];
     fp.Wihhp = (float*)(pk + L.k_Wihhp);
   }
-  HIPCHK(pack_f32(fp, st));
+  HIPCHK(pack_all<T>(a, st));   // conv1, conv2, conv2 dgrad classes, ConvLSTM layouts, fp32 tail: one launch
+  if constexpr (!std::is_same<T, float>::value) {   // fragment orders of the frame-resident kernels (read WpXH / WdT)
+    HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
+    HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
+  }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
   return AAA_OK;
@@ -1368,6 +1368,7 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
   using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
   using LTf = LdRowsT<float, float, CF::BI, CF::BK, NTF>;
   using LTfj = LdRowsT<float, float, CF::BJ, CF::BK, NTF>;
+  LstmGrads core_unpack{};   // the ConvLSTM grads' reference tensors, unpacked with the vision grads when both run here
 
   if (phases & AAA_BWD_HEAD) {
     HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
@@ -1388,7 +1389,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       LTfj::Params pb{Wf(L.LH), 256, 256};
       EpiStore<true> ep{Wf(L.gWhd), 256, L.ldy, 256};
       HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), st)));
-      HIPCHK(colsum(Wf(L.dY), L.ldy, F, L.ldy, Wf(L.gbhd), st));
     }
     {  // LSTMCell input dgrad
       LTf::Params pa{(const float*)(pk + L.k_Wihp), 256, 256};
@@ -1401,7 +1401,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       LTfj::Params pb{Wf(L.AO), 256, 256};
       EpiStore<true> ep{Wf(L.gWihp), 256, 1024, 256};
       HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), st)));
-      HIPCHK(colsum(Wf(L.dLG), 1024, F, 1024, Wf(L.gblc), st));
     }
     {  // answer_processor.2 dgrad fused with ReLU backward
       LTf::Params pa{prm + L.poff[A2W], 512, 512};
@@ -1414,7 +1413,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       LTfj::Params pb{Wf(L.hid1), 512, 512};
       EpiStore<true> ep{grads + L.poff[A2W], 512, 256, 512};
       HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), st)));
-      HIPCHK(colsum(Wf(L.dAO), 256, F, 256, grads + L.poff[A2B], st));
     }
     {  // answer_processor.0 dgrad (readout columns only)
       LTf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, L.da};
@@ -1428,7 +1426,6 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       EpiStore<true> ep{Wf(L.gW1p), L.ans_ld, 512, L.ans_ld};
       HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 512, L.ans_ld, F,
                                         wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), st)));
-      HIPCHK(colsum(Wf(L.dH1), 512, F, 512, grads + L.poff[A0B], st));
     }
     // attention readout / softmax / logits backward, then the query MLP
     {
@@ -1436,7 +1433,15 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       HIPCHK(attn_bwd(Wf(L.Hs), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
                       Wf(L.dO), Wf(L.dQp), st));
     }
-    HIPCHK(colsum(Wf(L.dQp), L.qd, F, L.qd, Wf(L.dQs), st));
+    {  // the bias grads of the heads, the LSTMCell and both answer layers, and dQ summed over frames: one launch
+      ColSums cs;
+      cs.add(Wf(L.dY), L.ldy, L.ldy, Wf(L.gbhd));
+      cs.add(Wf(L.dLG), 1024, 1024, Wf(L.gblc));
+      cs.add(Wf(L.dAO), 256, 256, grads + L.poff[A2B]);
+      cs.add(Wf(L.dH1), 512, 512, grads + L.poff[A0B]);
+      cs.add(Wf(L.dQp), L.qd, L.qd, Wf(L.dQs));
+      HIPCHK(colsum_multi(cs, F, st));
+    }
     HIPCHK(query_bwd(Wf(L.dQs), grads + L.poff[A0B], prm + L.poff[A0W], L.ans_in, L.nq, prm + L.poff[Q2W],
                      prm + L.poff[Q4W], (const float*)(pk + L.k_q1), (const float*)(pk + L.k_q2), grads + L.poff[Q4W],
                      grads + L.poff[Q4B],
@@ -1699,7 +1704,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       lg.bx[g] = grads + L.poff[XI_B + 3 * g];
       lg.wh[g] = grads + L.poff[HI_W + 3 * g];
     }
-    HIPCHK(unpack_lstm(Wf(L.gWpl), Wf(L.gbl), lg, st));
+    // with VISION in this call the ConvLSTM grads unpack in the vision phase's launch
+    if (!(phases & AAA_BWD_VISION)) HIPCHK(unpack_lstm(Wf(L.gWpl), Wf(L.gbl), lg, st));
+    else core_unpack = lg;
   }
 
   if (phases & AAA_BWD_VISION) {
@@ -1713,8 +1720,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
     }
-    HIPCHK(unpack_conv(Wf(L.gWp2), 64, 32, 4, grads + L.poff[C1W], st));
-    HIPCHK(unpack_conv1_rgbx(Wf(L.gWp1), grads + L.poff[C0W], st));
+    HIPCHK(unpack_cv((phases & AAA_BWD_CORE) ? Wf(L.gWpl) : nullptr, Wf(L.gbl), core_unpack, Wf(L.gWp2),
+                     grads + L.poff[C1W], Wf(L.gWp1), grads + L.poff[C0W], st));
   }
   return AAA_OK;
 }
