@@ -81,7 +81,66 @@ struct RecFwdParams {
   GT* Gt;              // (T, B, P, 512) <- gate activations (i, f, c~, o)
   int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed), [2B] = timeout word
   int T, B, h, w, P;
+  // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
+  // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
+  short colpp[128], colhb[128];
 };
+
+// Column order of the frame-resident GEMMs.  A B-fragment ds_read_b128 serves
+// 16 lanes (16 consecutive columns) per 256-B LDS row, and both images put
+// image pixel ip at 16-B slot ip (mod 16) (+ a per-read constant), so a lane
+// group is conflict-free iff its 16 pixels' image indices differ mod 16.  In
+// raster order every 16-column group of an 11-wide grid crosses a row end,
+// where the index jumps by 3 (the border): two slots collide, the read takes
+// two passes (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.50 at C3).  Here
+// the columns are the pixels bucketed by image index mod 16 and dealt out one
+// per residue to each 16-column group (padding columns read a spare interior
+// index of the missing residue).  Measured (profiles/r02/ab/rec_perm.txt): the
+// conflict cycles drop 61 % but the forward gets slower (C3 1136 -> 1177 us,
+// C4 618 -> 652 us): the epilogue's pixel rows of a 16-column half are then
+// scattered over the frame instead of one contiguous run, and the kernel is
+// not bound by these reads.  So the raster order is the default and the
+// dealt order an A/B option (AAA_REC_PERM=1; also kept when a residue holds
+// more than 8 pixels).
+inline void rec_columns(int h, int w, short* colpp, short* colhb) {
+  const int W2 = w + 2, P = h * w, NPH = (h + 2) * W2;
+  auto raster = [&] {
+    for (int c = 0; c < 128; ++c) {
+      const int pp = c < P ? c : P - 1;
+      colpp[c] = (short)(c < P ? c : -1);
+      colhb[c] = (short)((pp / w) * W2 + pp % w);
+    }
+  };
+  raster();
+  const char* e = getenv("AAA_REC_PERM");
+  if (!(e && atoi(e) == 1) || P > 128) return;
+  int bucket[16][9], nb[16] = {0};
+  for (int pp = 0; pp < P; ++pp) {
+    const int r = ((pp / w + 1) * W2 + pp % w + 1) & 15;
+    if (nb[r] == 8) return;   // a residue with more pixels than groups: keep the raster order
+    bucket[r][nb[r]++] = pp;
+  }
+  int spare[16];
+  for (int r = 0; r < 16; ++r) {   // a padding column's window must stay inside the image for all 9 taps
+    spare[r] = -1;
+    for (int ip = W2 + 1; ip <= NPH - W2 - 2 && spare[r] < 0; ++ip)
+      if ((ip & 15) == r) spare[r] = ip;
+    if (spare[r] < 0 && nb[r] < 8) return;
+  }
+  int used[16] = {0};
+  for (int g = 0; g < 8; ++g)
+    for (int r = 0; r < 16; ++r) {
+      const int c = 16 * g + r;
+      if (used[r] < nb[r]) {
+        const int pp = bucket[r][used[r]++];
+        colpp[c] = (short)pp;
+        colhb[c] = (short)((pp / w) * W2 + pp % w);
+      } else {
+        colpp[c] = -1;
+        colhb[c] = (short)(spare[r] - W2 - 1);
+      }
+    }
+}
 
 // ABL (diagnostic A/B only, AAA_REC_ABL): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
@@ -103,6 +162,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   __shared__ __attribute__((aligned(16))) float cstl[4 * NRB * 16 * 64];   // c, lane-native: [wave][rb][cb][g][lane]
   __shared__ __attribute__((aligned(16))) float sbias[512];
   __shared__ __attribute__((aligned(16))) unsigned char stg[4 * 16 * (GTP > 2 * CHP ? GTP : 2 * CHP)];
+  __shared__ short scol[128];   // column -> pixel (LDS: the epilogue's lookups stay off the vmcnt queue of the A stream)
   constexpr int STG = 16 * (GTP > 2 * CHP ? GTP : 2 * CHP);
   const int b = (int)blockIdx.x % p.B, kh = G == 1 ? 0 : (int)blockIdx.x / p.B;
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -120,6 +180,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     for (int i = tid; i < kRecNPH * kRecHS / 8; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
     sbias[tid] = p.bias[tid];
     sbias[tid + 256] = p.bias[tid + 256];
+    if (tid < 128) scol[tid] = p.colpp[tid];
   }
   // x image of step t (XH slot t, channels 0..63) by LDS-DMA, border included:
   // image pixel ip holds its 8 16-B channel chunks at slots q ^ xswz(ip) (the
@@ -144,9 +205,9 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int pp = cb * 32 + r32;
+        const int pp = p.colpp[cb * 32 + r32];
         cw[(rb * 16 + cb * 4 + g) * 64] =
-            pp < P ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
+            pp >= 0 ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
       }
   __syncthreads();   // h image zeroed
   {  // h_0 (slot 0, channels 64..191) into the image
@@ -160,10 +221,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   // window (columns >= P read pixel P-1: their outputs are never stored)
   int hb[4];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    const int pp = min(cb * 32 + r32, P - 1);
-    hb[cb] = (pp / p.w) * W2 + pp % p.w;
-  }
+  for (int cb = 0; cb < 4; ++cb) hb[cb] = p.colhb[cb * 32 + r32];
 
   // A stream: one buffer descriptor over the fragment-order weights, the lane's
   // 16 B at voffset lane*16, the (row block, k step) in the wave-uniform soffset
@@ -303,8 +361,8 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     const int c0 = cbase + hl_;                          // + 8*rb + 2*g
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-      const int pp = cb * 32 + pl;
-      __bf16* hl = him + hidx(min(pp, P - 1)) * kRecHS + c0;
+      const int pp = scol[cb * 32 + pl];   // -1: padding column
+      __bf16* hl = him + hidx(max(pp, 0)) * kRecHS + c0;
       uint32_t gq[NRB][4][2];   // fp16 gate quads (i, f, c~, o), packed
       float hv[NRB][4], cv[NRB][4];
 #pragma unroll
@@ -326,15 +384,14 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           typedef _Float16 h2 __attribute__((ext_vector_type(2)));
           gq[rb][g][0] = __builtin_bit_cast(uint32_t, h2{(_Float16)gi, (_Float16)gf});
           gq[rb][g][1] = __builtin_bit_cast(uint32_t, h2{(_Float16)gc, (_Float16)go});
-          if (pp < P) hl[co] = (__bf16)h;
+          if (pp >= 0) hl[co] = (__bf16)h;
         }
       if constexpr (!(ABL & 2)) {
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int pxl = pl & 15;
           const bool mine = (pl >> 4) == half;
-          const int pbase = cb * 32 + half * 16;   // first pixel of this half
-          if (pbase >= P) break;
+          const int pbase = cb * 32 + half * 16;   // first column of this half
           // gates: staging [16 px][GCH ch][4] fp16 at pixel pitch GTP
           if (mine) {
 #pragma unroll
@@ -346,9 +403,9 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           constexpr int CG = GCH / 2, CC = GCH / 4;   // 16-B chunks per pixel row: gates, c / h
 #pragma unroll
           for (int k = 0; k < NRB; ++k) {   // 1 KB each: 64 / CG pixel rows of 8 * GCH B
-            const int q = k * 64 + ln, px = q / CG, pix = pbase + px;
+            const int q = k * 64 + ln, px = q / CG, pix = scol[pbase + px];
             const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * GTP + (q % CG) * 16);
-            if (pix < P)
+            if (pix >= 0)
               *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * cbase) +
                                         (q % CG) * 16) = v;
           }
@@ -364,10 +421,10 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           }
 #pragma unroll
           for (int k = 0; k < NRB / 2; ++k) {   // 1 KB each of c and h: 64 / CC pixel rows of 4 * GCH B
-            const int q = k * 64 + ln, px = q / CC, pix = pbase + px;
+            const int q = k * 64 + ln, px = q / CC, pix = scol[pbase + px];
             const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * CHP + (q % CC) * 16);
             const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 16 * CHP + px * CHP + (q % CC) * 16);
-            if (pix < P) {
+            if (pix >= 0) {
               *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + cbase + (q % CC) * 4) = vc;
               *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + cbase + (q % CC) * 4) = vh;
             }
@@ -413,9 +470,10 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 template <typename GT>
 inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStream_t st) {
   if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (G != 1 && G != 2)) return hipErrorInvalidValue;
+  RecFwdParams<GT> q = p;
+  rec_columns(p.h, p.w, q.colpp, q.colhb);
   if (G == 2) {
     if (!p.flags) return hipErrorInvalidValue;
-    RecFwdParams<GT> q = p;
     void* args[] = {&q};
     const char* e = getenv("AAA_REC_ABL");
     const void* k = (e && atoi(e) == 16) ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 16>)
@@ -425,10 +483,10 @@ inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStrea
   const char* e = getenv("AAA_REC_ABL");
   switch (e ? atoi(e) : 0) {
 #define AAA_REC_CASE(a) \
-  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, p); break;
+  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, q); break;
     AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12)
 #undef AAA_REC_CASE
-    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, 0>), dim3(p.B), dim3(256), 0, st, p); break;
+    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, 0>), dim3(p.B), dim3(256), 0, st, q); break;
   }
   return hipGetLastError();
 }
