@@ -1161,8 +1161,12 @@ static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* g
                            1728, xh_bytes};
     EpiStore<true> ep{gW, 1728, 512, 1728};
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics", CW::BI, CW::BJ, CW::BK, wgrad_splits(tiles, rows, CW::BK)));
-    HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, wgrad_splits(tiles, rows, CW::BK), s)));
+    // about two workgroups per CU of splits (both fit a CU; the 1024-WG rule of
+    // the other weight gradients doubled the output atomics for the same time:
+    // profiles/r02/ab/wgrad_split.txt)
+    const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, 512 / tiles)), rows / CW::BK));
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics", CW::BI, CW::BJ, CW::BK, ns));
+    HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
   };
   // LDS-DMA ring with transposed fragment reads for both operands (k = pixel)
@@ -1219,7 +1223,10 @@ static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* g
   } else {
     // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
     const int wide = env_int("AAA_AUX_WIDE", aux ? 0 : 1);
-    const int rc = wide ? wgrad_lstm(CfgWFor<T>{}) : wgrad_lstm(CfgFor<T>{});
+    // AAA_WGRAD_TILE=1 (A/B): 128x192 tiles, 1728 = 9 x 192 columns without the half-empty last tile of 128
+    const int rc = !wide ? wgrad_lstm(CfgFor<T>{})
+                   : env_int("AAA_WGRAD_TILE", 0) == 1 ? wgrad_lstm(GemmCfg<T, 128, 192, 32, 2, 2>{})
+                                                       : wgrad_lstm(CfgWFor<T>{});
     if (rc) return rc;
   }
   return AAA_OK;
