@@ -230,6 +230,17 @@ __global__ void __launch_bounds__(256) k_act_attn(ActorParams p) {
   const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* O = p.Hs + (size_t)f * P * 128;
   const float* S = p.basis;
+  // this wave's row of answer_processor.0 (gridDim.x * 4 = 512 rows), requested first: its
+  // loads run under the attention readout instead of after it
+  constexpr int NIT = (NQ * 256 + 2 + 7) / 8 * 8 / 256 + 1;   // float4 slices per lane over ans_ld
+  const int row = blockIdx.x * 4 + wv;
+  f32x4 w1r[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int k = min(4 * lane + 256 * i, p.ans_ld - 4);
+    w1r[i] = ld4(p.W1p + (size_t)row * p.ans_ld + k);
+  }
+  const float a0 = p.a0b[row];
   for (int i = tid; i < NQ * 72; i += 256) Qs[i] = p.Q[i];
   {   // this workgroup's slice of h_t -> the carried state (read by the next step's ConvLSTM kernel)
     const int n4 = P * 32, per = (n4 + gridDim.x - 1) / gridDim.x;
@@ -315,11 +326,14 @@ __global__ void __launch_bounds__(256) k_act_attn(ActorParams p) {
     ans[i] = v;
   }
   __syncthreads();
-  for (int row = blockIdx.x * 4 + wv; row < 512; row += gridDim.x * 4) {
-    const float* wr = p.W1p + (size_t)row * p.ans_ld;
+  {
     float s = 0.f;
-    for (int k = 4 * lane; k < p.ans_ld; k += 256) s += dot4(ld4(wr + k), *reinterpret_cast<const f32x4*>(ans + k));
-    s = wsum(s) + p.a0b[row];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int k = 4 * lane + 256 * i;
+      if (k < p.ans_ld) s += dot4(w1r[i], *reinterpret_cast<const f32x4*>(ans + k));
+    }
+    s = wsum(s) + a0;
     if (lane == 0) p.hid1[(size_t)f * 512 + row] = fmaxf(s, 0.f);
   }
 }
@@ -369,18 +383,36 @@ __global__ void __launch_bounds__(256) k_act_lstmcell(ActorParams p) {
 // (the device counter is read by every wave before the single increment).
 __global__ void __launch_bounds__(256) k_act_heads(ActorParams p) {
   __shared__ float lg[16 * 256];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, A = p.A;
-  for (int o = wv; o < 2 * A; o += 4) {
-    const f32x4 w = ld4(p.Whd + (size_t)o * 256 + 4 * lane);
-    const float b = p.bhd[o];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, A = p.A, R = 2 * A;
+  // rows in chunks of 8 per wave, each chunk's weight and state loads issued before its math
+  for (int o0 = wv * 8; o0 < R; o0 += 32) {
+    f32x4 w[8];
+    float b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = min(o0 + j, R - 1);
+      w[j] = ld4(p.Whd + (size_t)o * 256 + 4 * lane);
+      b[j] = p.bhd[o];
+    }
     for (int f = 0; f < p.B; ++f) {
-      const float s = wsum(dot4(w, ld4(p.LH + (size_t)f * 256 + 4 * lane))) + b;
-      if (lane == 0) {
+      const f32x4 x = ld4(p.LH + (size_t)f * 256 + 4 * lane);
+      float s[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] = dot4(w[j], x);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], o, 64);
+      if (lane < 8 && o0 + lane < R) {   // lane j stores row o0 + j
+        float v = s[0] + b[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) v = lane == j ? s[j] + b[j] : v;
+        const int o = o0 + lane;
         if (o < A) {
-          p.logits[(size_t)f * A + o] = s;
-          lg[f * A + o] = s;
+          p.logits[(size_t)f * A + o] = v;
+          lg[f * A + o] = v;
         } else {
-          p.values[(size_t)f * A + o - A] = s;
+          p.values[(size_t)f * A + o - A] = v;
         }
       }
     }

@@ -1217,6 +1217,13 @@ static int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* g
         else
           rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 4>{}, I3{}, I2{});
         break;
+      case 8:   // bf16: 4 waves of 128x128 (half the LDS fragment reads per MFMA of the 8-wave tile), 4-deep ring:
+                // measured slower (C3 1367 vs 1079 us, C4 691 vs 561 us: one wave per SIMD hides less)
+        if constexpr (std::is_same<T, float>::value)
+          rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
+        else
+          rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 2>{}, std::integral_constant<int, 4>{}, I2{});
+        break;
       default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
     }
     if (rc) return rc;
