@@ -677,15 +677,22 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
     else HIPCHK((frames_rgbx<T, float>(F, L.H, L.W, (const float*)frames, Xp, st)));
     // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
     constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
-    using CP = GemmCfg<T, 32, 128, BKc, 1, 4>;
-    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
-    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
     EpiStoreT<T> ep{Y1, 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
-        typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
-        typename PB::Params{Xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
-                            (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
-        ep, 32, F * L.P1, 256, 1, st)));
+    auto conv1 = [&](auto cfg) -> int {
+      using CP = decltype(cfg);
+      using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+      using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
+      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
+          typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
+          typename PB::Params{Xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
+                              (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
+          ep, 32, F * L.P1, 256, 1, st)));
+      return AAA_OK;
+    };
+    // K = 256 is four BK steps: a wider column tile does more MFMA work per DMA round trip (A/B: AAA_CONV1_TILE)
+    const int c1t = env_int("AAA_CONV1_TILE", 0);
+    const int rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
+    if (rc) return rc;
   }
   {  // conv2 (attention.py:163-169): Y1 -> out
     using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
@@ -1075,22 +1082,29 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
   if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
     // the LDS-DMA ring (dY2 is already in T), dY1 stored in T, conv1's bias
     // gradient summed from the fp32 values in the epilogue (no column-sum pass)
-    using CP = GemmCfg<T, 32, 128, std::is_same<T, float>::value ? 32 : 64, 1, 4>;
-    using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
-    using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
-    for (int cls = 0; cls < 4; ++cls) {
-      const int py = cls >> 1, px = cls & 1;
-      const int Ha = (L.H1 - py + 1) / 2, Wa = (L.W1 - px + 1) / 2;
-      if (Ha <= 0 || Wa <= 0) continue;
-      const int rows = frames * Ha * Wa;
-      EpiStoreParityBias<T> ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, gbias};
-      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreParityBias<T>, 2>(
-          typename PA::Params{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32},
-          typename PB::Params{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
-                              (uint32_t)((size_t)frames * L.P * 64 * L.esz)},
-          ep, 32, rows, 256, 1, s)));
-    }
-    return AAA_OK;
+    constexpr int BKd = std::is_same<T, float>::value ? 32 : 64;
+    auto classes = [&](auto cfg) -> int {
+      using CP = decltype(cfg);
+      using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+      using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
+      for (int cls = 0; cls < 4; ++cls) {
+        const int py = cls >> 1, px = cls & 1;
+        const int Ha = (L.H1 - py + 1) / 2, Wa = (L.W1 - px + 1) / 2;
+        if (Ha <= 0 || Wa <= 0) continue;
+        const int rows = frames * Ha * Wa;
+        EpiStoreParityBias<T> ep{dy1, 32, rows, Ha, Wa, L.H1, L.W1, py, px, gbias};
+        HIPCHK((launch_pipe<CP, PA, PB, EpiStoreParityBias<T>, 2>(
+            typename PA::Params{(const T*)(pk + L.k_WdT2) + (size_t)cls * 32 * 256, 256, 32},
+            typename PB::Params{dy2, ConvGeo{64, 64, 0, L.h, L.w, Ha, Wa, 2, 1, 0, 0}.prep(), rows,
+                                (uint32_t)((size_t)frames * L.P * 64 * L.esz)},
+            ep, 32, rows, 256, 1, s)));
+      }
+      return AAA_OK;
+    };
+    // K = 256: four BK steps per tile, so 256 columns per workgroup (twice the MFMA work per DMA round
+    // trip of 32x128): C5 14.945 -> 14.74 ms per iteration (profiles/r02/ab/vision_tiles.txt); AAA_DGRAD2_TILE=0 the old tile
+    return env_int("AAA_DGRAD2_TILE", 1) == 1 ? classes(GemmCfg<T, 32, 256, BKd, 1, 4>{})
+                                             : classes(GemmCfg<T, 32, 128, BKd, 1, 4>{});
   }
   // register-staged fallback (fp32 only: dY2's loader converts from fp32)
   if constexpr (!std::is_same<T, float>::value) return fail(AAA_E_ARG, "AAA_CONV2_DGRAD_RING=0 needs fp32");
