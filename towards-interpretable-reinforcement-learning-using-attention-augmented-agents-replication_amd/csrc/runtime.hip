@@ -1068,15 +1068,26 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     // = k_WdT2) per frame reads the frame's dY2 once as a zero-bordered LDS
     // image (halo.h, KS = 2) -- one launch instead of four 32-row GEMMs whose
     // K = 256 loops were pure latency (4 x 65 us at C3, 0.06 of bf16 peak)
-    using HC = HaloCfg<T, 128, 128, std::is_same<T, float>::value ? 32 : 64, 2, 2, 1, 192>;
+    constexpr int CKd = std::is_same<T, float>::value ? 32 : 64;
     const int Ha = (L.H1 + 1) / 2, Wa = (L.W1 + 1) / 2;
-    if (Ha * Wa <= HC::BJ && (L.h + 2) * (L.w + 2) + 1 <= HC::HMAX && Ha <= L.h && Wa <= L.w &&
-        env_int("AAA_DGRAD2_HALO", 1)) {
+    auto halo4 = [&](auto cfg) -> int {
+      using HC = decltype(cfg);
       EpiStoreParity4<T> ep(dy1, frames * Ha * Wa, Ha, Wa, L.H1, L.W1, gbias);
       const HaloParams hp{pk + L.k_WdT2, 256, 128, dy2, 64, 0, 64, (uint32_t)((size_t)frames * L.P * 64 * L.esz),
                           L.h, L.w, frames, 0, Ha, Wa};
       HIPCHK((launch_halo<HC, EpiStoreParity4<T>, 2>(hp, ep, s)));
       return AAA_OK;
+    };
+    auto fits = [&](int fr, int bj, int hmax) {
+      return fr * Ha * Wa <= bj && fr * (L.h + 2) * (L.w + 2) + 1 <= hmax && Ha <= L.h && Wa <= L.w;
+    };
+    // bf16: FR = 2 frames per tile -- the 64 KB weight tile streamed once per two frames and twice the
+    // MFMA work per DMA round trip (C3 4.97 -> 4.94 ms); fp32 keeps FR = 1 (C2 4.306 vs 4.341 ms)
+    // (profiles/r02/ab/dgrad_fr.txt; AAA_DGRAD2_FR overrides)
+    const int fr = env_int("AAA_DGRAD2_FR", std::is_same<T, float>::value ? 1 : 2);
+    if (env_int("AAA_DGRAD2_HALO", 1)) {
+      if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{});
+      if (fits(1, 128, 192)) return halo4(HaloCfg<T, 128, 128, CKd, 2, 2, 1, 192>{});
     }
   }
   if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
