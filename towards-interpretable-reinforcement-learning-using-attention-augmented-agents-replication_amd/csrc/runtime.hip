@@ -1145,6 +1145,22 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
   using LA = LdRowsTB<T, T, C::BI, C::BK, C::NT>;
   using LB = LdIm2colTB<T, T, C::BJ, C::BK, C::NT>;
   const int rows = frames * L.P;
+  if constexpr (!std::is_same<T, float>::value) {
+    // bf16 (AAA_CONV2_WGRAD_PIPE, A/B): the LDS-DMA ring of the ConvLSTM weight gradient, 64x256
+    // tiles of 4 waves, split-K over about one wave of workgroups, atomics from the accumulators
+    if (rows % 32 == 0 && env_int("AAA_CONV2_WGRAD_PIPE", 0)) {
+      using CW = GemmCfg<T, 64, 256, 32, 1, 4>;
+      using PA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
+      using PB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
+      typename PA::Params pa{dy2, 64, 64, rows};
+      typename PB::Params pb{y1, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
+                             (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
+      EpiAtomicD ep{{gW, 512, 64, 512}};
+      const int ns = std::max(1, std::min(env_int("AAA_CONV2_WGRAD_WGS", 256) / 2, rows / (8 * CW::BK)));
+      HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 64, 512, rows, ns, s)));
+      return AAA_OK;
+    }
+  }
   typename LA::Params pa{dy2, 64, 64, rows};
   typename LB::Params pb{y1, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
                          (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
