@@ -118,7 +118,7 @@ def test_convlstm_cell_abi_state_grads(cuda):
 
 # ---------------------------------------------------------------- vision ----
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
-@pytest.mark.parametrize("H,W", [(84, 84), (210, 160), (80, 80), (80, 100)])
+@pytest.mark.parametrize("H,W", [(84, 84), (210, 160), (80, 80), (80, 100), (168, 168)])
 def test_vision_network_vs_oracle(cuda, dt, H, W):
     """VisionNetwork.forward over 3 steps: O = the reference's O.transpose(1,3),
     prev_hidden in the reference's (B,128,w,h) layout, grads of all 16 vision

@@ -1088,6 +1088,10 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     if (env_int("AAA_DGRAD2_HALO", 1)) {
       if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{});
       if (fits(1, 128, 192)) return halo4(HaloCfg<T, 128, 128, CKd, 2, 2, 1, 192>{});
+      // bf16, grids up to 21x21 (168x168 frames, C5): one frame per 512-column tile of 8 waves,
+      // 32-channel chunks (two LDS images of 23x23 pixels), the epilogue in two column chunks
+      if constexpr (!std::is_same<T, float>::value)
+        if (fits(1, 512, 640) && env_int("AAA_DGRAD2_WIDE", 1)) return halo4(HaloCfg<T, 128, 512, 32, 2, 4, 1, 640>{});
     }
   }
   if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
