@@ -672,7 +672,15 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
   using C = CfgFor<T>;
   constexpr int NT = C::NT;
   const int P = L.P;
-  {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
+  bool banded = false;   // bf16 frames too large for the frame-resident encoder: the banded conv1 (vision.h)
+  if constexpr (std::is_same<T, __bf16>::value) {
+    if (band_fits(L.H, L.W, L.H1, L.W1) && env_int("AAA_VIS_BAND", 1)) {
+      const VisBandParams bp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], Xp, Y1, F, L.H, L.W, L.H1, L.W1};
+      HIPCHK(L.fu8 ? vision_conv1_band<uint8_t>(bp, st) : vision_conv1_band<float>(bp, st));
+      banded = true;
+    }
+  }
+  if (!banded) {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
     if (L.fu8) HIPCHK((frames_rgbx<T, uint8_t>(F, L.H, L.W, (const uint8_t*)frames, Xp, st)));
     else HIPCHK((frames_rgbx<T, float>(F, L.H, L.W, (const float*)frames, Xp, st)));
     // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
@@ -1556,9 +1564,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         // small grids: halo-staged conv, one frame per 64x128 tile
         // (tools/ubench/halo_tiles: 658 vs 771 us for the ring at C3)
         using HD = HaloCfg<__bf16, 64, 128, 64, 1, 2, 1, 176>;
+        // 21x21 grids (168x168 frames): one frame per 512-column tile of 4 waves, 32-channel chunks
+        using HW = HaloCfg<__bf16, 64, 512, 32, 1, 4, 1, 576>;
         if (halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HD>(hp, ep, s)));
+        } else if (halo_fits<HW>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+          const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
+          HIPCHK((launch_halo<HW>(hp, ep, s)));
         } else {
           // larger grids (21x21 at 168x168): 64x128 on a 3-stage ring (bf16_tiles at C3: 643 vs 716 us for 64x64)
           HIPCHK((step_gemm<GemmCfg<T, 64, 128, 64, 2, 2>, true, T, T, EpiStoreBiasT<T>, 3>(WdT, 4608, 64, dz, g, rows,

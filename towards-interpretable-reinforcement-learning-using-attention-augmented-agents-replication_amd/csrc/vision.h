@@ -239,4 +239,108 @@ inline hipError_t vision_fwd_frames(const VisFwdParams& p, int cus, hipStream_t 
   return hipGetLastError();
 }
 
+// Banded conv1 for frames too large for the frame-resident encoder (C5's
+// 168x168): one workgroup per (frame, band of kBandRows conv1 output rows).
+// It builds the band's 4*rows+4 padded-image rows as a zero-bordered RGBx bf16
+// image in LDS straight from the observation (uint8 or fp32), writes the
+// bordered rows it owns to Xp (conv1's weight-gradient operand; band b owns
+// padded rows [4*y0, 4*(y0+rows)), the last band also the 4 below), and runs
+// conv1 on the band from LDS exactly as k_vision_fwd does -- replacing the
+// frames_rgbx pass and conv1's im2col GEMM, which re-read every pixel of the
+// 740 MB bordered image four times through L2 (C5: 260 + 550 us).
+constexpr int kBandRows = 8;        // conv1 output rows per band
+constexpr int kBandXB = 50 * 1024;  // band image bytes: (4*kBandRows+4) rows x (W+2) x 8 B (36 x 170 x 8 = 48960)
+
+struct VisBandParams {
+  const void* frames;   // (F, H, W, 3) uint8 or fp32
+  const __bf16* Wc1;    // packed conv1 [32][256]
+  const float* b1;      // [32]
+  __bf16* Xp;           // (F, H+2, W+2, 4) <- bordered RGBx rows 0 .. 4*H1+3
+  __bf16* Y1;           // (F, H1*W1, 32) <- conv1 output
+  int F, H, W, H1, W1;
+};
+
+inline bool band_fits(int H, int W, int H1, int W1) {
+  return (4 * kBandRows + 4) * (W + 2) * 8 <= kBandXB && 4 * H1 + 4 <= H + 2 && H1 >= 1 && W1 >= 1 && W % 2 == 0;
+}
+
+template <typename TI>
+__global__ void __launch_bounds__(256) k_vision_conv1_band(VisBandParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char xim[kBandXB];
+  __shared__ __attribute__((aligned(16))) bf16x8 w1s[16 * 64];   // conv1 weights, fragment order [ks][lane]
+  __shared__ float sb[32];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nb = (p.H1 + kBandRows - 1) / kBandRows;
+  const int f = (int)blockIdx.x / nb, band = (int)blockIdx.x - f * nb;
+  const int y0 = band * kBandRows, ny = min(kBandRows, p.H1 - y0);
+  const int Wp = p.W + 2, r0 = 4 * y0, nr = 4 * ny + 4;   // padded rows r0 .. r0+nr-1
+  if (tid < 32) sb[tid] = p.b1[tid];
+  for (int i = tid; i < 16 * 64; i += 256) {
+    const int ks = i >> 6, l = i & 63;
+    w1s[i] = *reinterpret_cast<const bf16x8*>(p.Wc1 + (l & 31) * 256 + ks * 16 + (l >> 5) * 8);
+  }
+  {  // the band image: padded pixel (r0 + rr, px) = frame pixel (r0 + rr - 1, px - 1), zero outside
+    const TI* fr = reinterpret_cast<const TI*>(p.frames) + (size_t)f * p.H * p.W * 3;
+    for (int i = tid; i < nr * Wp; i += 256) {
+      const int rr = i / Wp, px = i - rr * Wp, iy = r0 + rr - 1, ix = px - 1;
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) {
+        const TI* src = fr + ((size_t)iy * p.W + ix) * 3;
+        v0 = (float)src[0]; v1 = (float)src[1]; v2 = (float)src[2];
+      }
+      *reinterpret_cast<bf16x4*>(xim + (size_t)i * 8) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)0.f};
+    }
+  }
+  __syncthreads();
+  {  // the rows this band owns into Xp (16 B = 2 pixels per store)
+    const int rows = 4 * ny + (y0 + ny == p.H1 ? 4 : 0);
+    u32x4* xo = reinterpret_cast<u32x4*>(p.Xp + ((size_t)f * (p.H + 2) + r0) * Wp * 4);
+    const int n = rows * Wp / 2;
+    for (int i = tid; i < n; i += 256) xo[i] = reinterpret_cast<const u32x4*>(xim)[i];
+  }
+  // conv1 on the band: D[32 ch][ny*W1 px] = W1[32][256 = (ky*8+kx)*4 + c] x im2col(band)
+  const int NP = ny * p.W1, NC = (NP + 31) / 32, P1 = p.H1 * p.W1;
+  for (int cb = wave; cb < NC; cb += 4) {
+    const int pp = min(cb * 32 + r32, NP - 1), oy = pp / p.W1, ox = pp - oy * p.W1;
+    const unsigned char* bb = xim + (4 * oy * Wp + 4 * ox) * 8 + hh * 16;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 8) {
+      bf16x8 a[8], b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ks = k0 + k;
+        a[k] = w1s[ks * 64 + lane];
+        b[k] = *reinterpret_cast<const bf16x8*>(bb + ((ks >> 1) * Wp + (ks & 1) * 4) * 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[k], b[k], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cb * 32 + r32 < NP) {
+      __bf16* yd = p.Y1 + ((size_t)f * P1 + (size_t)(y0 + oy) * p.W1 + ox) * 32;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 8 * g + 4 * hh;
+        *reinterpret_cast<bf16x4*>(yd + c) =
+            bf16x4{(__bf16)(acc[4 * g] + sb[c]), (__bf16)(acc[4 * g + 1] + sb[c + 1]),
+                   (__bf16)(acc[4 * g + 2] + sb[c + 2]), (__bf16)(acc[4 * g + 3] + sb[c + 3])};
+      }
+    }
+  }
+}
+
+template <typename TI>
+inline hipError_t vision_conv1_band(const VisBandParams& p, hipStream_t st) {
+  if (!band_fits(p.H, p.W, p.H1, p.W1) || p.F < 1) return hipErrorInvalidValue;
+  const int nb = (p.H1 + kBandRows - 1) / kBandRows;
+  hipLaunchKernelGGL((k_vision_conv1_band<TI>), dim3(p.F * nb), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
 }  // namespace aaa
