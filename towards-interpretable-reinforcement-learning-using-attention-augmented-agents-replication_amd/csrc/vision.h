@@ -261,7 +261,7 @@ struct VisBandParams {
 };
 
 inline bool band_fits(int H, int W, int H1, int W1) {
-  return (4 * kBandRows + 4) * (W + 2) * 8 <= kBandXB && 4 * H1 + 4 <= H + 2 && H1 >= 1 && W1 >= 1 && W % 2 == 0;
+  return (4 * kBandRows + 4) * (W + 2) * 8 <= kBandXB && 4 * H1 + 4 <= H + 2 && H1 >= 1 && W1 >= 1 && W % 4 == 0;
 }
 
 template <typename TI>
@@ -281,16 +281,49 @@ __global__ void __launch_bounds__(256) k_vision_conv1_band(VisBandParams p) {
     const int ks = i >> 6, l = i & 63;
     w1s[i] = *reinterpret_cast<const bf16x8*>(p.Wc1 + (l & 31) * 256 + ks * 16 + (l >> 5) * 8);
   }
-  {  // the band image: padded pixel (r0 + rr, px) = frame pixel (r0 + rr - 1, px - 1), zero outside
-    const TI* fr = reinterpret_cast<const TI*>(p.frames) + (size_t)f * p.H * p.W * 3;
+  {  // the band image: padded pixel (r0 + rr, px) = frame pixel (r0 + rr - 1, px - 1), zero outside.
+     // Border columns and rows outside the frame are zeroed; the interior goes in groups of 4
+     // pixels (12 channel values: 3 dwords of uint8 or 3 x 16 B of fp32), every group's loads
+     // of a batch issued before its stores (the fill is otherwise one latency per pixel).
     for (int i = tid; i < nr * Wp; i += 256) {
-      const int rr = i / Wp, px = i - rr * Wp, iy = r0 + rr - 1, ix = px - 1;
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f;
-      if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) {
-        const TI* src = fr + ((size_t)iy * p.W + ix) * 3;
-        v0 = (float)src[0]; v1 = (float)src[1]; v2 = (float)src[2];
+      const int rr = i / Wp, px = i - rr * Wp, iy = r0 + rr - 1;
+      if ((unsigned)iy >= (unsigned)p.H || px == 0 || px == Wp - 1)
+        *reinterpret_cast<uint2*>(xim + (size_t)i * 8) = uint2{0u, 0u};
+    }
+    constexpr int RW = sizeof(TI) == 1 ? 1 : 4;   // 4-byte words per 4 channel values
+    constexpr int NG = 8;                          // groups per thread per batch
+    const uint32_t* fr = reinterpret_cast<const uint32_t*>(reinterpret_cast<const TI*>(p.frames) +
+                                                           (size_t)f * p.H * p.W * 3);
+    const int G4 = p.W / 4, ry0 = max(r0 - 1, 0), ry1 = min(r0 + nr - 1, p.H);   // frame rows [ry0, ry1)
+    const int ng = (ry1 - ry0) * G4;
+    for (int g0 = 0; g0 < ng; g0 += 256 * NG) {
+      uint32_t raw[NG][3 * RW];
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int g = min(g0 + tid + 256 * k, ng - 1), iy = ry0 + g / G4, gx = g - (g / G4) * G4;
+        const uint32_t* src = fr + ((size_t)iy * p.W + 4 * gx) * 3 * RW / 4;
+#pragma unroll
+        for (int q = 0; q < 3 * RW; ++q) raw[k][q] = src[q];
       }
-      *reinterpret_cast<bf16x4*>(xim + (size_t)i * 8) = bf16x4{(__bf16)v0, (__bf16)v1, (__bf16)v2, (__bf16)0.f};
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int g = g0 + tid + 256 * k;
+        if (g < ng) {
+          const int iy = ry0 + g / G4, gx = g - (g / G4) * G4;
+          unsigned char* d = xim + ((size_t)(iy + 1 - r0) * Wp + 4 * gx + 1) * 8;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float v[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const int e = 3 * j + c;
+              if constexpr (RW == 4) v[c] = __builtin_bit_cast(float, raw[k][e]);
+              else v[c] = (float)((raw[k][e >> 2] >> (8 * (e & 3))) & 255u);
+            }
+            *reinterpret_cast<bf16x4*>(d + j * 8) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)0.f};
+          }
+        }
+      }
     }
   }
   __syncthreads();
