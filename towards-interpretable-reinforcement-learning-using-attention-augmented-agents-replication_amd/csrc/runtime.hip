@@ -1185,17 +1185,23 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
 // conv1 weight gradient over RGBx frames (Cin 4; the 4th channel's grad is dropped on unpack)
 template <typename T>
 static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, float* gW, hipStream_t s) {
-  using C3 = Cfg32For<T>;
-  using LA = LdRowsTB<T, T, C3::BI, C3::BK, C3::NT>;
-  using LB = LdIm2colTB<T, T, C3::BJ, C3::BK, C3::NT>;   // bf16 chunks = 2 taps x 4 ch, in-bounds (bordered image)
   const int rows1 = frames * L.P1;
-  typename LA::Params pa{dy1, 32, 32, rows1};
-  typename LB::Params pb{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
-                         (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
-  EpiStore<true> ep{gW, 256, 32, 256};
-  const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
-  HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
-  return AAA_OK;
+  auto run = [&](auto cfg) -> int {
+    using C3 = decltype(cfg);
+    using LA = LdRowsTB<T, T, C3::BI, C3::BK, C3::NT>;
+    using LB = LdIm2colTB<T, T, C3::BJ, C3::BK, C3::NT>;   // bf16 chunks = 2 taps x 4 ch, in-bounds (bordered image)
+    typename LA::Params pa{dy1, 32, 32, rows1};
+    typename LB::Params pb{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
+                           (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
+    EpiStore<true> ep{gW, 256, 32, 256};
+    const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
+    HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
+    return AAA_OK;
+  };
+  // AAA_CONV1_WGRAD_TILE=1 (A/B): one 32x256 tile covering every (tap, channel) column, so each
+  // pixel's 8x8 window is gathered once instead of by four 64-column tiles
+  if (env_int("AAA_CONV1_WGRAD_TILE", 0) == 1) return run(GemmCfg<T, 32, 256, Cfg32For<T>::BK, 1, 4>{});
+  return run(Cfg32For<T>{});
 }
 
 // All 8 ConvLSTM weight gradients of ``rows`` pixels at once (attention.py:39-102
