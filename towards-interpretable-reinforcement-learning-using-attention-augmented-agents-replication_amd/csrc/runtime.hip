@@ -702,6 +702,14 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
     const int rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
     if (rc) return rc;
   }
+  if constexpr (std::is_same<T, __bf16>::value && std::is_same<OT, __bf16>::value) {
+    // after the banded conv1: the banded conv2 (vision.h), Y1 rows staged in LDS per band
+    if (banded && band2_fits(L.H1, L.W1, L.h, L.w) && env_int("AAA_VIS_BAND2", 1)) {
+      const VisBand2Params bp{Y1, (const __bf16*)(pk + L.k_Wp2), prm + L.poff[C1B], out, out_ld, F, L.H1, L.W1, L.h, L.w};
+      HIPCHK(vision_conv2_band(bp, st));
+      return AAA_OK;
+    }
+  }
   {  // conv2 (attention.py:163-169): Y1 -> out
     using LA = LdRowsB<T, T, C::BI, C::BK, NT>;
     typename LA::Params pa{(const T*)(pk + L.k_Wp2), 512, 64};

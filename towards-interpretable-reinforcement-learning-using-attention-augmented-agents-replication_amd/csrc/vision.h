@@ -376,4 +376,102 @@ inline hipError_t vision_conv1_band(const VisBandParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Banded conv2 (4x4, stride 2, pad 2) for the same frames: one workgroup per (frame, band of
+// kBand2Rows conv2 output rows); the band's 2*rows+2 conv1 output rows are staged once as a
+// zero-bordered bf16 image in LDS (pixel pitch kVisYP, interior at +2, +2) and all 16 taps read
+// their B fragments from it -- the im2col ring GEMM gathered every Y1 pixel four times through L2.
+// Waves: row block wave % 2 (32 of the 64 channels, weights in registers), column blocks
+// wave / 2, wave / 2 + 2, ...
+constexpr int kBand2Rows = 8;
+constexpr int kBand2YB = 72 * 1024;   // (2*kBand2Rows+2) rows x (W1+4) x kVisYP bytes (18 x 45 x 80 = 64800)
+
+struct VisBand2Params {
+  const __bf16* Y1;     // (F, H1*W1, 32)
+  const __bf16* Wc2;    // packed conv2 [64][512]
+  const float* b2;      // [64]
+  __bf16* out;          // (F, h*w, out_ld), channels 0..63
+  int out_ld, F, H1, W1, h, w;
+};
+
+inline bool band2_fits(int H1, int W1, int h, int w) {
+  return (2 * kBand2Rows + 2) * (W1 + 4) * kVisYP <= kBand2YB && h >= 1 && w >= 1 && 2 * (h - 1) + 1 <= H1 + 1;
+}
+
+__global__ void __launch_bounds__(256) k_vision_conv2_band(VisBand2Params p) {
+  __shared__ __attribute__((aligned(16))) unsigned char yim[kBand2YB];
+  __shared__ float sb[64];
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int nb = (p.h + kBand2Rows - 1) / kBand2Rows;
+  const int f = (int)blockIdx.x / nb, band = (int)blockIdx.x - f * nb;
+  const int o0 = band * kBand2Rows, n2 = min(kBand2Rows, p.h - o0);
+  const int W1p = p.W1 + 4, nr = 2 * n2 + 2, iy0 = 2 * o0 - 2, P1 = p.H1 * p.W1;
+  const int rb = wave & 1;
+  bf16x8 a2[32];   // this wave's 32-row block of the conv2 weights, all 32 k steps
+#pragma unroll
+  for (int ks = 0; ks < 32; ++ks)
+    a2[ks] = *reinterpret_cast<const bf16x8*>(p.Wc2 + (32 * rb + r32) * 512 + ks * 16 + hh * 8);
+  if (tid < 64) sb[tid] = p.b2[tid];
+  {  // the band's Y1 rows iy0 .. iy0+nr-1 (zero outside the map), 16-B pieces, 4 per pixel
+    const u32x4* src = reinterpret_cast<const u32x4*>(p.Y1 + (size_t)f * P1 * 32);
+    const int n = nr * W1p * 4;
+    for (int i0 = 0; i0 < n; i0 += 256 * 4) {
+      u32x4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + tid + 256 * k, px = i >> 2, br = px / W1p, bc = px - br * W1p;
+        const int iy = iy0 + br, ix = bc - 2;
+        const bool ok = i < n && (unsigned)iy < (unsigned)p.H1 && (unsigned)ix < (unsigned)p.W1;
+        v[k] = ok ? src[((size_t)iy * p.W1 + ix) * 4 + (i & 3)] : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + tid + 256 * k;
+        if (i < n) *reinterpret_cast<u32x4*>(yim + (i >> 2) * kVisYP + (i & 3) * 16) = v[k];
+      }
+    }
+  }
+  __syncthreads();
+  const int NP = n2 * p.w, NC = (NP + 31) / 32;
+  for (int cb = wave >> 1; cb < NC; cb += 2) {
+    const int pp = min(cb * 32 + r32, NP - 1), y2 = pp / p.w, x2 = pp - y2 * p.w;
+    // output (o0 + y2, x2) reads Y1 rows 2(o0+y2)-2+ky = iy0 + 2 y2 + ky: band row 2 y2 + ky, column 2 x2 + kx
+    const unsigned char* yb = yim + (2 * y2 * W1p + 2 * x2) * kVisYP + hh * 16;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 8) {
+      bf16x8 b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ks = k0 + k, tap = ks >> 1;
+        b[k] = *reinterpret_cast<const bf16x8*>(yb + ((tap >> 2) * W1p + (tap & 3)) * kVisYP + (ks & 1) * 32);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[k0 + k], b[k], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cb * 32 + r32 < NP) {
+      __bf16* o = p.out + ((size_t)f * p.h * p.w + (size_t)(o0 + y2) * p.w + x2) * p.out_ld + 32 * rb;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 8 * g + 4 * hh;
+        const float* bz = sb + 32 * rb + c;
+        *reinterpret_cast<bf16x4*>(o + c) = bf16x4{(__bf16)(acc[4 * g] + bz[0]), (__bf16)(acc[4 * g + 1] + bz[1]),
+                                                   (__bf16)(acc[4 * g + 2] + bz[2]), (__bf16)(acc[4 * g + 3] + bz[3])};
+      }
+    }
+  }
+}
+
+inline hipError_t vision_conv2_band(const VisBand2Params& p, hipStream_t st) {
+  if (!band2_fits(p.H1, p.W1, p.h, p.w) || p.F < 1) return hipErrorInvalidValue;
+  const int nb = (p.h + kBand2Rows - 1) / kBand2Rows;
+  hipLaunchKernelGGL(k_vision_conv2_band, dim3(p.F * nb), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
 }  // namespace aaa
