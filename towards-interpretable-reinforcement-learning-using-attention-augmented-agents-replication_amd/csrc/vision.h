@@ -416,17 +416,18 @@ __global__ void __launch_bounds__(256) k_vision_conv2_band(VisBand2Params p) {
   {  // the band's Y1 rows iy0 .. iy0+nr-1 (zero outside the map), 16-B pieces, 4 per pixel
     const u32x4* src = reinterpret_cast<const u32x4*>(p.Y1 + (size_t)f * P1 * 32);
     const int n = nr * W1p * 4;
-    for (int i0 = 0; i0 < n; i0 += 256 * 4) {
-      u32x4 v[4];
+    constexpr int NB2 = 16;   // pieces in flight per thread (a C5 band is ~13 per thread: one batch)
+    for (int i0 = 0; i0 < n; i0 += 256 * NB2) {
+      u32x4 v[NB2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < NB2; ++k) {
         const int i = i0 + tid + 256 * k, px = i >> 2, br = px / W1p, bc = px - br * W1p;
         const int iy = iy0 + br, ix = bc - 2;
         const bool ok = i < n && (unsigned)iy < (unsigned)p.H1 && (unsigned)ix < (unsigned)p.W1;
         v[k] = ok ? src[((size_t)iy * p.W1 + ix) * 4 + (i & 3)] : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < NB2; ++k) {
         const int i = i0 + tid + 256 * k;
         if (i < n) *reinterpret_cast<u32x4*>(yim + (i >> 2) * kVisYP + (i & 3) * 16) = v[k];
       }
