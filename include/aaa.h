@@ -47,14 +47,17 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 4
+#define AAA_ABI_VERSION 5
 
 enum aaa_status {
   AAA_OK = 0,
   AAA_E_ARG = -1,      /* bad shape / NULL / unsupported configuration */
   AAA_E_ALIGN = -2,    /* a buffer is not 16-byte aligned */
   AAA_E_LAUNCH = -3,   /* a HIP launch or runtime call failed */
-  AAA_E_DEVICE = -4    /* current device is not gfx950 */
+  AAA_E_DEVICE = -4,   /* current device is not gfx950 */
+  AAA_E_STRANDED = -5  /* a paired frame-resident kernel of an EARLIER call timed out
+                          waiting for its partner workgroup: that call's outputs are
+                          invalid (reported once, by the next call or aaa_pair_status) */
 };
 
 enum aaa_dtype {
@@ -158,6 +161,18 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream);
  * ``phases`` is a mask of aaa_bwd_phase; phases must run in order. grads
  * are overwritten (not accumulated) by the phases that own them. */
 int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
+
+/* Health of the paired frame-resident ConvLSTM kernels (two cooperating
+ * workgroups per frame, launched cooperatively; used when B is below the CU
+ * count).  Their partner waits are bounded; a wait that times out is counted
+ * in a word of pinned, device-mapped host memory and the kernel proceeds on a
+ * stale partner half.  aaa_forward / aaa_backward consume pending counts at
+ * entry and return AAA_E_STRANDED; aaa_pair_status synchronises ``stream``
+ * (NULL: the device) and returns the count (>= 0; clear != 0 resets it).
+ * aaa_debug_pair_spin bounds the wait to ``polls`` polls (0 = the default
+ * 2^24, about 0.5 s) -- a test hook that makes the report path reachable. */
+int aaa_pair_status(hipStream_t stream, int clear);
+int aaa_debug_pair_spin(long polls);
 
 /* ---- optional kernel timing (benchmarks) ----
  * While enabled, the runtime records a hipEvent pair on the launch stream

@@ -15,7 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 4   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 5   # include/aaa.h AAA_ABI_VERSION
+E_STRANDED = -5   # AAA_E_STRANDED
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 
 # Every symbol include/aaa.h declares (checked by tests/test_native_abi.py).
@@ -27,7 +28,7 @@ EXPORTS = (
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
-    "aaa_actor_workspace_bytes", "aaa_actor_step",
+    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_debug_pair_spin",
 )
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
 
@@ -135,6 +136,8 @@ def load(path: str = LIB_PATH):
             "aaa_divisor_log": (I, [I, ctypes.POINTER(ctypes.c_uint), I]),
             "aaa_actor_workspace_bytes": (S, [CP]),
             "aaa_actor_step": (I, [CP, ctypes.POINTER(ActorIO), P]),
+            "aaa_pair_status": (I, [P, I]),
+            "aaa_debug_pair_spin": (I, [ctypes.c_long]),
         }
         ab_override = "AAA_LIB" in os.environ
         missing = [name for name in sig if not hasattr(lib, name)]
@@ -219,6 +222,21 @@ def timing_stats(kind: int) -> dict:
     s = TimerStats()
     check(load().aaa_timing_stats(kind, ctypes.byref(s)), "timing_stats")
     return {"ms": s.total_ms, "launches": s.launches, "work": s.work, "variant": s.variant.decode()}
+
+
+def pair_status(clear: bool = True, stream=None) -> int:
+    """Synchronise ``stream`` (default: torch's current) and return how many
+    partner waits of the paired frame-resident kernels timed out since the
+    last clear (0 = every paired launch ran on a co-resident pair)."""
+    n = load().aaa_pair_status(stream if stream is not None else stream_ptr(), 1 if clear else 0)
+    if n < 0:
+        check(n, "pair_status")
+    return n
+
+
+def debug_pair_spin(polls: int) -> None:
+    """Bound the paired kernels' partner wait to ``polls`` polls (0 = default).  Test hook."""
+    check(load().aaa_debug_pair_spin(int(polls)), "debug_pair_spin")
 
 
 def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None) -> None:

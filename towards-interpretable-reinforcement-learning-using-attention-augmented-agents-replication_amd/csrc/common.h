@@ -81,4 +81,43 @@ struct FastDiv {
 };
 
 
+// Bounded wait of one lane for a partner workgroup's published step count
+// (the paired frame-resident kernels, recur.h / recur_bwd.h).  On timeout the
+// lane adds 1 to ``report`` -- a word of pinned host memory mapped into the
+// device (runtime.hip pair_report), so the host reads it with no copy -- and
+// returns: the kernel never hangs, and the host turns the report into
+// AAA_E_STRANDED at the next API call (or aaa_pair_status) instead of handing
+// back results computed from a stale partner half.
+__device__ __forceinline__ void pair_wait(const int* flag, int target, int* report, int spin) {
+  int n = 0;
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++n > spin) {
+      __hip_atomic_fetch_add(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
+// Launch a paired kernel (two cooperating workgroups per frame) as an ordinary
+// dispatch whose whole grid fits one residency wave of the device: every
+// workgroup is placed at once on an idle chip, and the bounded partner waits
+// (pair_wait) report instead of hanging if a pair is ever not co-resident.
+// Not hipLaunchCooperativeKernel: ANY cooperative launch makes a process that
+// rocprofv3 profiles crash in exit() after the tool's finalisation -- a trivial
+// 256-workgroup kernel with no libaaa.so loaded reproduces it
+// (tools/ubench/coop_exit.hip, profiles/r03/coop/) -- which cost every C4 PMC
+// pass its own call in round 2.
+template <class KP>
+inline hipError_t launch_resident(const void* kernel, int grid, int block, KP& params, hipStream_t st) {
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0);
+  if (e != hipSuccess) return e;
+  if ((long)per_cu * cus < grid) return hipErrorCooperativeLaunchTooLarge;
+  void* args[] = {&params};
+  return hipLaunchKernel(kernel, dim3(grid), dim3(block), args, 0, st);
+}
+
 }  // namespace aaa

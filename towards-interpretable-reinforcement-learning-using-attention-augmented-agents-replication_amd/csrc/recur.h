@@ -79,8 +79,10 @@ struct RecFwdParams {
   float* Cst;          // (T+1, B, P, 128): slot 0 = c_0 (read), slot t+1 <- c_t
   float* Hs;           // (T, B, P, 128) <- h_t (fp32)
   GT* Gt;              // (T, B, P, 512) <- gate activations (i, f, c~, o)
-  int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed), [2B] = timeout word
+  int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed)
   int T, B, h, w, P;
+  int* report;         // G = 2: partner-timeout report word (pinned host, device-mapped; pair_wait)
+  int spin;            // G = 2: partner-wait bound in polls
   // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
   // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
   short colpp[128], colhb[128];
@@ -142,7 +144,7 @@ inline void rec_columns(int h, int w, short* colpp, short* colhb) {
     }
 }
 
-// ABL (diagnostic A/B only, AAA_REC_ABL): bit 0 = no A loads in the K loop,
+// ABL (diagnostic A/B only: AAA_REC_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
 //
 // G = 2 (batches too small to give every CU a frame): two workgroups per frame,
@@ -151,8 +153,8 @@ inline void rec_columns(int h, int w, short* colpp, short* colhb) {
 // gradient operand) with sc1 stores and an sc1 flag, and reads the partner's half
 // (sc1 loads) into its h image after its own x-part -- the hand-off's latency
 // hides under the x-part GEMM, and no agent release / acquire fence is paid
-// (ABL bit 4 = the fenced hand-off, for A/B).  Launched cooperatively
-// (co-residency checked), spins bounded.
+// (ABL bit 4 = the fenced hand-off, for A/B).  Launched as one residency wave
+// (launch_resident, co-residency checked), spins bounded and reported.
 template <typename GT, int G = 1, int ABL = 0>
 __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
   constexpr int NRB = 4 / G, GCH = 8 * NRB;     // row blocks and channels per wave
@@ -307,14 +309,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     if constexpr (G == 2) {
       if (t > 0) {   // the partner's half of h_{t-1} (XH slot t) into the image, once it has published it
         if (tid == 0) {
-          int n = 0;
-          while (__hip_atomic_load(p.flags + 2 * b + (1 - kh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++n > (1 << 24)) {   // bounded: a stranded partner reports, never hangs the GPU
-              __hip_atomic_store(p.flags + 2 * p.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
+          pair_wait(p.flags + 2 * b + (1 - kh), t, p.report, p.spin);   // bounded: a stranded partner reports
           if constexpr (ABL & 16) {   // fenced hand-off (A/B only)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -465,29 +460,34 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   }
 }
 
-// G = 1: one workgroup per frame; G = 2: two per frame, launched cooperatively
-// (p.flags zeroed by the caller; the launch fails rather than strand a half).
+// G = 1: one workgroup per frame; G = 2: two per frame in one residency wave
+// (launch_resident: p.flags zeroed by the caller; the launch fails rather than
+// strand a half; a partner wait that still times out is reported via p.report).
 template <typename GT>
 inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStream_t st) {
   if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (G != 1 && G != 2)) return hipErrorInvalidValue;
   RecFwdParams<GT> q = p;
   rec_columns(p.h, p.w, q.colpp, q.colhb);
   if (G == 2) {
-    if (!p.flags) return hipErrorInvalidValue;
-    void* args[] = {&q};
+    if (!p.flags || !p.report || p.spin < 0) return hipErrorInvalidValue;
+    const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>);
+#ifdef AAA_ABLATION   // diagnostic builds only (tools/ubench): the product library never reads AAA_REC_ABL
     const char* e = getenv("AAA_REC_ABL");
-    const void* k = (e && atoi(e) == 16) ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 16>)
-                                         : reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>);
-    return hipLaunchCooperativeKernel(k, dim3(2 * p.B), dim3(256), args, 0, st);
+    if (e && atoi(e) == 16) k = reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 16>);
+#endif
+    return launch_resident(k, 2 * p.B, 256, q, st);
   }
+#ifdef AAA_ABLATION
   const char* e = getenv("AAA_REC_ABL");
   switch (e ? atoi(e) : 0) {
 #define AAA_REC_CASE(a) \
-  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, q); break;
+  case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, q); return hipGetLastError();
     AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12)
 #undef AAA_REC_CASE
-    default: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, 0>), dim3(p.B), dim3(256), 0, st, q); break;
+    default: break;
   }
+#endif
+  hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, 0>), dim3(p.B), dim3(256), 0, st, q);
   return hipGetLastError();
 }
 

@@ -81,11 +81,13 @@ struct RecBwdParams {
   float* dh0;             // (B, P, 128) <- grad of h_{-1}, or null
   __bf16* dY2;            // (T, B, P, 64) <- dx_t, the conv2 output gradient (bf16: its readers' operand type)
   float* dxb;             // (B, 64) <- conv2 bias-gradient partials per frame (fp32 sums of dx)
-  int* flags;             // paired kernel: per (frame, half) count of published dZ steps ([2B], zeroed), [2B] = timeout
+  int* flags;             // paired kernel: per (frame, half) count of published dZ steps ([2B], zeroed)
   int T, B, h, w, P;
+  int* report;            // paired kernel: partner-timeout report word (pinned host, device-mapped; pair_wait)
+  int spin;               // paired kernel: partner-wait bound in polls
 };
 
-// ABL (diagnostic A/B only, AAA_RECB_ABL): bit 0 = no A loads in the K loop,
+// ABL (diagnostic A/B only: AAA_RECB_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA.
 template <int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
@@ -435,7 +437,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 // 4 + kh over column block w -- 3 MFMAs per k step, so the A stream runs
 // kBwPD2-1 = 7 k steps ahead.  K order: own chunks, then the partner's (the
 // packed stream read from k step 144kh on, wrapping through the repeated tail).
-// Launched cooperatively (co-residency checked); the spins are bounded.
+// Launched as one residency wave (launch_resident); the spins are bounded and reported.
 template <int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_pairs(RecBwdParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (c & 1)
@@ -684,14 +686,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           }
         }
         if (ck == 0 && tid == 0) {   // the partner's dZ_t published? (the other waves load after the barrier)
-          int n = 0;
-          while (__hip_atomic_load(p.flags + 2 * b + (1 - kh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.T - t) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++n > (1 << 24)) {
-              __hip_atomic_store(p.flags + 2 * p.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
+          pair_wait(p.flags + 2 * b + (1 - kh), p.T - t, p.report, p.spin);
         }
         barrier_lds();   // image c & 1 free for the partner's chunk; (ck = 1, 2) its refill complete
       }
@@ -762,23 +757,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 }
 
 inline hipError_t convlstm_bwd_pairs(const RecBwdParams& p, hipStream_t st) {
-  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags) return hipErrorInvalidValue;
+  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
+    return hipErrorInvalidValue;
   RecBwdParams q = p;
-  void* args[] = {&q};
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_convlstm_bwd_pairs<0>), dim3(2 * p.B), dim3(256),
-                                    args, 0, st);
+  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_pairs<0>), 2 * p.B, 256, q, st);
 }
 
 inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {
   if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1) return hipErrorInvalidValue;
+#ifdef AAA_ABLATION   // diagnostic builds only (tools/ubench): the product library never reads AAA_RECB_ABL
   const char* e = getenv("AAA_RECB_ABL");
   switch (e ? atoi(e) : 0) {
 #define AAA_RECB_CASE(a) \
-  case a: hipLaunchKernelGGL((k_convlstm_bwd_frames<a>), dim3(p.B), dim3(256), 0, st, p); break;
+  case a: hipLaunchKernelGGL((k_convlstm_bwd_frames<a>), dim3(p.B), dim3(256), 0, st, p); return hipGetLastError();
     AAA_RECB_CASE(1) AAA_RECB_CASE(2) AAA_RECB_CASE(3) AAA_RECB_CASE(4) AAA_RECB_CASE(8) AAA_RECB_CASE(6)
 #undef AAA_RECB_CASE
-    default: hipLaunchKernelGGL((k_convlstm_bwd_frames<0>), dim3(p.B), dim3(256), 0, st, p); break;
+    default: break;
   }
+#endif
+  hipLaunchKernelGGL((k_convlstm_bwd_frames<0>), dim3(p.B), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 

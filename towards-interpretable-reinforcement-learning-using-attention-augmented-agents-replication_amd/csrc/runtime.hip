@@ -171,7 +171,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
-  L.rflags = take(((size_t)2 * L.B + 1) * 4);   // hand-off flags of the paired frame-resident kernels
+  L.rflags = take((size_t)2 * L.B * 4);   // hand-off flags of the paired frame-resident kernels
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -251,6 +251,52 @@ static int check_device() {
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// ------------------------------------------------- paired-kernel reports --
+// The paired frame-resident kernels (two cooperating workgroups per frame)
+// bound their partner waits (common.h pair_wait).  A timed-out wait adds 1 to
+// this device's report word: pinned host memory mapped into the device, so the
+// host reads it without a copy or a sync.  Every aaa_forward / aaa_backward
+// entry consumes pending reports and fails with AAA_E_STRANDED (the results of
+// the call that stranded are invalid); aaa_pair_status syncs a stream first.
+// Allocated once per process on first use, never freed (no HIP call at exit).
+static std::mutex g_pair_mu;
+static int* g_pair_host = nullptr;    // [64] words, one per device ordinal
+static int* g_pair_dev = nullptr;     // the same words, device-mapped
+static long g_pair_spin = 1L << 24;   // partner-wait bound in polls (aaa_debug_pair_spin)
+
+static int* pair_report(int dev) {
+  std::lock_guard<std::mutex> lk(g_pair_mu);
+  if (!g_pair_host) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+        hipSuccess)
+      return nullptr;
+    memset(h, 0, 64 * sizeof(int));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
+    g_pair_host = (int*)h;
+    g_pair_dev = (int*)d;
+  }
+  return g_pair_dev + dev;
+}
+
+// Pending reports of the current device (consumed).
+static int pair_take() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(g_pair_mu);
+  if (!g_pair_host) return 0;
+  return __atomic_exchange_n(g_pair_host + dev, 0, __ATOMIC_ACQ_REL);
+}
+
+static int pair_check() {
+  const int n = pair_take();
+  return n ? fail(AAA_E_STRANDED,
+                  "%d partner wait(s) of a paired frame-resident ConvLSTM kernel timed out in an earlier call on this "
+                  "device: that call's outputs/gradients are invalid (the pair was not co-resident)", n)
+           : AAA_OK;
+}
 
 // ------------------------------------------------------------ aux stream --
 // Work that is off the sequential ConvLSTM chain (the batched x-part of the
@@ -766,7 +812,7 @@ static int device_cus() {
   return cus;
 }
 // Workgroups per frame of the frame-resident kernels (0: per-step launches):
-// 1 once the batch fills most of the CUs, 2 (cooperative pairs) while two per
+// 1 once the batch fills most of the CUs, 2 (paired workgroups) while two per
 // frame still fit the chip, else the per-step kernels.  AAA_FRAMES_FWD /
 // AAA_FRAMES_BWD = 0 / 1 / 2 force it.
 static int frames_g(const Layout& L, const char* env) {
@@ -815,9 +861,16 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
       using GT = decltype(gtag);
       if constexpr (!std::is_same<T, float>::value) {
         if (const int G = frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
-          if (G == 2) HIPCHK(hipMemsetAsync(ws + L.rflags, 0, ((size_t)2 * L.B + 1) * 4, st));
+          int* rep = nullptr;
+          if (G == 2) {
+            HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)2 * L.B * 4, st));
+            int dev = 0;
+            HIPCHK(hipGetDevice(&dev));
+            if (!(rep = pair_report(dev))) return fail(AAA_E_LAUNCH, "cannot map the paired-kernel report word");
+          }
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
-                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P};
+                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
+                              rep, (int)g_pair_spin};
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
                          strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame", L.T, G));
           HIPCHK(convlstm_fwd_frames<GT>(rp, G, st));
@@ -1665,9 +1718,14 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
       if constexpr (!std::is_same<T, float>::value) {
         RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
                         Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), (int*)(ws + L.rflags),
-                        L.T, L.B, L.h, L.w, L.P};
+                        L.T, L.B, L.h, L.w, L.P, nullptr, (int)g_pair_spin};
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
-        if (fb == 2) HIPCHK(hipMemsetAsync(ws + L.rflags, 0, ((size_t)2 * L.B + 1) * 4, st));
+        if (fb == 2) {
+          HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)2 * L.B * 4, st));
+          int dev = 0;
+          HIPCHK(hipGetDevice(&dev));
+          if (!(rp.report = pair_report(dev))) return fail(AAA_E_LAUNCH, "cannot map the paired-kernel report word");
+        }
         {
           // work: the h rows over T-1 steps (+ dh0) and the dx rows over all T (the batched dx it replaces)
           TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 4608 * (128.0 * (L.T - 1 + (io->dh0 ? 1 : 0)) + 64.0 * L.T),
@@ -2240,6 +2298,7 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream) {
   if (r) return r;
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, false))) return r;
+  if ((r = pair_check())) return r;
   return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream) : forward_impl<float>(L, io, stream);
 }
 
@@ -2250,8 +2309,26 @@ int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t s
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, true))) return r;
   if (phases & ~AAA_BWD_ALL || !phases) return fail(AAA_E_ARG, "bad phase mask %d", phases);
+  if ((r = pair_check())) return r;
   return L.dt == AAA_BF16 ? backward_impl<__bf16>(L, io, phases, stream)
                           : backward_impl<float>(L, io, phases, stream);
+}
+
+int aaa_pair_status(hipStream_t stream, int clear) {
+  if (stream && hipStreamSynchronize(stream) != hipSuccess) return fail(AAA_E_LAUNCH, "stream synchronize failed");
+  if (!stream && hipDeviceSynchronize() != hipSuccess) return fail(AAA_E_LAUNCH, "device synchronize failed");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fail(AAA_E_DEVICE, "no HIP device");
+  std::lock_guard<std::mutex> lk(g_pair_mu);
+  if (!g_pair_host) return 0;
+  return clear ? __atomic_exchange_n(g_pair_host + dev, 0, __ATOMIC_ACQ_REL)
+               : __atomic_load_n(g_pair_host + dev, __ATOMIC_ACQUIRE);
+}
+
+int aaa_debug_pair_spin(long polls) {
+  if (polls < 0 || polls > (1L << 30)) return fail(AAA_E_ARG, "pair spin bound must be in [0, 2^30] (0 = default)");
+  g_pair_spin = polls ? polls : (1L << 24);
+  return AAA_OK;
 }
 
 static int check_conv(const aaa_conv_desc* d) {
