@@ -98,7 +98,9 @@ def cpu_baseline(cfg):
     T, nq = cfg["T"], cfg["nq"]
     B = min(cfg["B"], 32)
     H, W = cfg["H"], cfg["W"]
-    mode = "bf16" if cfg["dtype"] == "bf16" else "fp32"
+    # the reference's CPU path is fp32 whatever the GPU config computes in
+    # (SURVEY.md §8d): never the bf16-emulated oracle
+    mode = "fp32"
     P = ref_cpu.tensor_params(detinit.deterministic_params(0, 18, nq))
 
     def it(Tn, Bn, Hn, Wn, md):
@@ -106,8 +108,8 @@ def cpu_baseline(cfg):
             p.grad = None
         X = torch.from_numpy(detinit.frames_u8(1234, (Tn, Bn, Hn, Wn, 3)).astype(np.float32))
         lg, vl, _ = ref_cpu.unroll(P, X, nq=nq, conv_mode=md)
-        Gl = torch.from_numpy(detinit.cotangent(2, tuple(lg.shape)))
-        Gv = torch.from_numpy(detinit.cotangent(3, tuple(vl.shape)))
+        Gl = torch.from_numpy(detinit.normal(2, tuple(lg.shape)))
+        Gv = torch.from_numpy(detinit.normal(3, tuple(vl.shape)))
         ((lg * Gl).sum() + (vl * Gv).sum()).backward()
 
     def timed(Tn, Bn, Hn, Wn, md, budget):
@@ -128,7 +130,7 @@ def cpu_baseline(cfg):
     except OSError:
         pass
     out = {"value": round(n * B * T / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-           "sample": f"{n} iterations of oracle/ref_cpu.py (reference op sequence, torch CPU {mode}), "
+           "sample": f"{n} iterations of oracle/ref_cpu.py (the reference's fp32 op sequence, torch CPU {mode}), "
                      f"B={B} x T={T}, {H}x{W}, nq={nq}, {dt:.1f} s on {cores} threads ({model}; "
                      f"affinity mask {aff} CPUs, OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})"}
     if nq == 4:   # config 1 (BASELINE.json configs[0]): the reference's CPU-runnable case, fp32
@@ -173,6 +175,95 @@ def dropin_api(cfg, dev, frames, dl, dv, steps, flat):
             "path": "attention.Agent.unroll + loss.backward() (autograd .grad), same frames and weights"}
 
 
+def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
+    """The reference's own call pattern (main_mp.py:49-59, 62-80): one episode of
+    T_ep per-step ``Policy.forward(observation)`` calls -- B = 1, Seaquest's
+    210x160 frames, the default 27x20 spatial basis, the ``.item()`` host sync
+    every step -- then finish_episode's discounted-return loss and ONE
+    ``loss.backward()`` through all T_ep per-step graphs (T_ep separate T=1
+    backward calls of the hand-written BPTT).  Reports the host wall time per
+    step, the device-side backward, the memory the episode's graph keeps alive
+    per step (each step's saved workspace), and the CPU oracle on the same
+    episode.  Bounded: T_ep = 64 (main_mp.py:151 allows 10,000 steps; the memory
+    column says what that would hold)."""
+    import numpy as np
+    import torch
+    import attention
+    from aaa_amd import detinit
+    from aaa_amd.policy import Policy
+    agent = attention.Agent(18).to(dev)          # default SpatialBasis(27, 20): 210x160 frames (Q4)
+    detinit.load_into(agent, detinit.deterministic_params(0, 18))
+    agent.to(dev)
+    policy = Policy(agent, seed=0)
+    obs = detinit.frames_u8(4321, (T_ep, H, W, 3))
+    rewards = (detinit.frames_u8(4322, (T_ep,)) % 3).astype(np.float32).tolist()
+    gamma, eps = 0.99, np.finfo(np.float32).eps.item()
+
+    def finish():   # main_mp.py:62-77, verbatim in torch ops
+        R, returns = 0.0, []
+        for r in rewards[::-1]:
+            R = r + gamma * R
+            returns.insert(0, R)
+        returns = torch.tensor(returns, device=dev)
+        returns = (returns - returns.mean()) / (returns.std() + eps)
+        return torch.cat([-lp * Rt for lp, Rt in zip(policy.saved_log_probs, returns)]).sum()
+
+    def episode(n):
+        agent.reset()
+        agent.zero_grad(set_to_none=True)
+        policy.saved_log_probs = []
+        for t in range(n):
+            policy(obs[t])
+        return finish()
+
+    episode(4).backward()                        # warm-up (allocations, code objects)
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(dev)
+    torch.cuda.reset_peak_memory_stats(dev)
+    t0 = time.perf_counter()
+    loss = episode(T_ep)
+    t1 = time.perf_counter()
+    held = torch.cuda.memory_allocated(dev) - base
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    loss.backward()
+    e1.record()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    peak = torch.cuda.max_memory_allocated(dev) - base
+    out = {"pattern": "main_mp.py: T_ep x Policy.forward(obs) (B=1, 210x160, default basis, .item() per step) "
+                      "-> finish_episode loss -> one loss.backward()",
+           "steps": T_ep, "ms_per_step_host": round((t1 - t0) / T_ep * 1e3, 3),
+           "backward_ms_device": round(e0.elapsed_time(e1), 3), "backward_ms_host": round((t2 - t1) * 1e3, 3),
+           "episode_frames_per_s": round(T_ep / (t2 - t0), 1),
+           "graph_bytes_per_step": int(held // T_ep), "peak_bytes_per_step": int(peak // T_ep),
+           "note": "graph_bytes_per_step x main_mp.py:151's max_steps (10,000) is the device memory one "
+                   "full-length episode's autograd graph would hold"}
+    if cpu:
+        from oracle import ref_cpu
+        cores, _ = _cpu_threads()
+        torch.set_num_threads(cores)
+        P = ref_cpu.tensor_params(detinit.deterministic_params(0, 18))
+        X = torch.from_numpy(obs.astype(np.float32)).unsqueeze(1)    # (T_ep, 1, H, W, 3)
+        c0 = time.perf_counter()
+        lg, _, _ = ref_cpu.unroll(P, X, nq=4)                          # the reference op sequence, step by step
+        R, returns = 0.0, []
+        for r in rewards[::-1]:
+            R = r + gamma * R
+            returns.insert(0, R)
+        returns = torch.tensor(returns)
+        returns = (returns - returns.mean()) / (returns.std() + eps)
+        acts = torch.from_numpy(detinit.frames_u8(4323, (T_ep,)).astype(np.int64) % 18)
+        logp = torch.log_softmax(lg[:, 0], dim=1).gather(1, acts[:, None])[:, 0]
+        (-(logp * returns)).sum().backward()
+        c1 = time.perf_counter()
+        out["cpu_oracle"] = {"ms_per_step": round((c1 - c0) / T_ep * 1e3, 2), "episode_frames_per_s":
+                             round(T_ep / (c1 - c0), 1), "cores": cores,
+                             "sample": f"one {T_ep}-step episode, oracle/ref_cpu.py fp32 (forward step by step "
+                                       "+ finish_episode loss + backward)"}
+    return out
+
+
 def pmc_traffic(config, dtype, world, kernel):
     """HBM bytes per launch of ``kernel`` from the committed PMC passes
     (tools/pmc.sh -> tools/pmc_traffic.py -> profiles/rNN/pmc_traffic_<config>.json).
@@ -199,6 +290,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in Agent API measurement")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--no-episode", action="store_true", help="skip the main_mp.py episode leg (C2 line only)")
     ap.add_argument("--frames", default="u8", choices=["u8", "fp32"],
                     help="frame dtype in HBM: u8 (the environment's observation, cast in-kernel) or fp32 "
                          "(cast on the host as main_mp.py:53 does)")
@@ -227,8 +319,8 @@ def main():
     frames = torch.from_numpy(detinit.frames_u8(1234 + rank, (T, B, H, W, 3))).to(dev)
     if args.frames == "fp32":
         frames = frames.float()
-    dl = torch.from_numpy(detinit.cotangent(2 + 7 * rank, (T, B, A))).to(dev)
-    dv = torch.from_numpy(detinit.cotangent(3 + 7 * rank, (T, B, A))).to(dev)
+    dl = torch.from_numpy(detinit.normal(2 + 7 * rank, (T, B, A))).to(dev)   # N(0,1), SURVEY.md §8d
+    dv = torch.from_numpy(detinit.normal(3 + 7 * rank, (T, B, A))).to(dev)
     log(f"rank {rank}/{world} {cfg['desc']} workspace {learner.runner.ws_bytes / 2**20:.0f} MiB")
 
     for i in range(args.warmup):
@@ -295,8 +387,8 @@ def main():
         "vs_baseline": None, "dtype": dtype,
         "data": ("synthetic: seeded uint8 frames resident in HBM, cast to fp32 (raw 0..255) inside the first "
                  "kernel" if args.frames == "u8" else "synthetic: seeded uint8 frames cast to fp32 (raw 0..255) on "
-                 "the host") + ", seeded uniform weights of the reference architecture, uniform[-1,1) logits/values "
-                 "cotangents",
+                 "the host") + ", seeded uniform weights of the reference architecture, N(0,1) logits/values "
+                 "cotangents (seeds 2, 3)",
         "config": {"workload": cfg["desc"], "global_batch": B * world, "seq_len": T, "frame": f"{H}x{W}",
                    "heads": nq, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": names[dom], "variant": d["variant"], "achieved": round(achieved, 2),
@@ -331,6 +423,9 @@ def main():
                         "note": "working set (63.6 MB) is Infinity-Cache resident when stepped back to back"}
     if world == 1 and not args.no_dropin:
         out["dropin"] = dropin_api(cfg, dev, frames, dl, dv, args.steps, learner.flat)
+    if world == 1 and args.config == "c2" and not args.no_episode:
+        log("episode leg (main_mp.py call pattern)...")
+        out["episode"] = episode_leg(dev, cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline (oracle on host cores)...")
         out["cpu_baseline"] = cpu_baseline(cfg)

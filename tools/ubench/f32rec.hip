@@ -1,0 +1,124 @@
+// Microbenchmark of the fp32 frame-group ConvLSTM recurrence (csrc/recur_f32.h)
+// at config 2's shape (B = 32, T = 20, 11x11 grid, G = 8) on random operands:
+// device time per launch of the production kernel and of its ablations
+// (ABL bits: 1 no epilogue, 2 no epilogue HBM stores, 4 no partner exchange,
+// 8 no MFMAs), and -- built with -DAAA_STAMPS -- per-step phase times.
+// Timing only: the results are not checked (tests/test_gpu_f32_frames.py is).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "recur_f32.h"
+
+using namespace aaa;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+static float* dev_rand(size_t n, float scale, unsigned seed) {
+  std::vector<float> h(n);
+  unsigned s = seed;
+  for (auto& v : h) { s = s * 1664525u + 1013904223u; v = scale * (((s >> 8) & 0xffff) / 32768.f - 1.f); }
+  float* d; CK(hipMalloc(&d, n * 4)); CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+template <int G, int ABL>
+static double run(RecF32Params p, int reps, const char* name) {
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_f32<G, ABL>);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  double best = 1e30, sum = 0;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipMemset(p.flags, 0, (size_t)p.B * G * 4));
+    CK(hipEventRecord(a, 0));
+    CK(launch_resident(k, f32_grid(p.B, G), 256, p, 0));
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    if (r >= 2) { best = std::min(best, (double)ms); sum += ms; }
+  }
+  printf("%-34s G=%d  best %8.1f us  mean %8.1f us\n", name, G, best * 1e3, sum / reps * 1e3);
+  return best;
+}
+
+#ifdef AAA_STAMPS
+static void phases(int G, int B, int T) {
+  const int nwg = f32_grid(B, G);
+  std::vector<uint64_t> st((size_t)512 * 64 * 5);
+  CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(aaa_f32_stamps), st.size() * 8));
+  // per step: median over live workgroups of each phase
+  const char* nm[4] = {"x-part+exch", "h-part", "epilogue", "publish"};
+  std::vector<double> tot(4, 0.0);
+  for (int t = 0; t < T; ++t) {
+    std::vector<double> ph[4], span;
+    for (int w = 0; w < nwg; ++w) {
+      const int xcd = w & 7, loc = w >> 3, b = xcd + 8 * (loc / G);
+      if (b >= B) continue;
+      const uint64_t* s = &st[((size_t)w * 64 + t) * 5];
+      for (int k = 0; k < 4; ++k) ph[k].push_back((s[k + 1] - s[k]) * 0.01);
+      if (t + 1 < T) span.push_back((st[((size_t)w * 64 + t + 1) * 5] - s[0]) * 0.01);
+    }
+    printf("  t=%2d", t);
+    for (int k = 0; k < 4; ++k) {
+      std::sort(ph[k].begin(), ph[k].end());
+      const double med = ph[k][ph[k].size() / 2];
+      tot[k] += med;
+      printf("  %s %6.2f (max %6.2f)", nm[k], med, ph[k].back());
+    }
+    printf("\n");
+  }
+  {  // in-kernel shader clock over the h-parts (stamps 1 -> 2), median over workgroups and steps 1..T-1
+    std::vector<uint64_t> ck((size_t)512 * 64 * 5);
+    CK(hipMemcpyFromSymbol(ck.data(), HIP_SYMBOL(aaa_f32_clocks), ck.size() * 8));
+    std::vector<double> ghz;
+    for (int w = 0; w < nwg; ++w) {
+      const int xcd = w & 7, loc = w >> 3, b = xcd + 8 * (loc / G);
+      if (b >= B) continue;
+      for (int t = 1; t < T; ++t) {
+        const size_t i = ((size_t)w * 64 + t) * 5;
+        ghz.push_back((double)(ck[i + 2] - ck[i + 1]) / ((st[i + 2] - st[i + 1]) * 10.0));
+      }
+    }
+    std::sort(ghz.begin(), ghz.end());
+    printf("  shader clock over h-parts: p10 %.3f  p50 %.3f  p90 %.3f GHz\n", ghz[ghz.size() / 10], ghz[ghz.size() / 2],
+           ghz[ghz.size() * 9 / 10]);
+  }
+  printf("  sum of medians:");
+  for (int k = 0; k < 4; ++k) printf("  %s %.1f", nm[k], tot[k]);
+  printf("\n");
+}
+#endif
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 32, T = argc > 2 ? atoi(argv[2]) : 20, h = 11, w = 11, P = h * w;
+  const size_t M = (size_t)B * P;
+  RecF32Params p{};
+  p.Wf = dev_rand((size_t)16 * kF32QP * 256, 0.02f, 1);
+  p.bias = dev_rand(512, 0.1f, 2);
+  p.XH = dev_rand((size_t)(T + 1) * M * 192, 1.f, 3);
+  p.Cst = dev_rand((size_t)(T + 1) * M * 128, 1.f, 4);
+  p.Hs = dev_rand((size_t)T * M * 128, 1.f, 5);
+  p.Gt = dev_rand((size_t)T * M * 512, 1.f, 6);
+  CK(hipMalloc(&p.flags, (size_t)B * 8 * 4));
+  int* hrep = nullptr;
+  CK(hipHostMalloc(&hrep, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  CK(hipHostGetDevicePointer((void**)&p.report, hrep, 0));
+  p.spin = 1 << 24;
+  p.T = T; p.B = B; p.h = h; p.w = w; p.P = P; p.h0_zero = 1;
+  for (int c = 0; c < 128; ++c) {
+    const int pp = c < P ? c : P - 1;
+    p.colhb[c] = (short)((pp / w) * (w + 2) + pp % w);
+  }
+  const int reps = 10;
+  run<8, 0>(p, reps, "production");
+#ifdef AAA_STAMPS
+  phases(8, B, T);
+#endif
+  run<8, 2>(p, reps, "no epilogue HBM stores");
+  run<8, 4>(p, reps, "no partner exchange");
+  run<8, 1>(p, reps, "no epilogue");
+  run<8, 5>(p, reps, "no epilogue, no exchange");
+  run<8, 13>(p, reps, "no epilogue/exchange/MFMA");
+  run<4, 0>(p, reps, "production");
+  printf("timeout reports: %d\n", *hrep);
+  return 0;
+}

@@ -1,0 +1,410 @@
+// Frame-group-resident ConvLSTM recurrence, fp32 (exact v_mfma_f32_32x32x2_f32).
+//
+// The reference's recurrence (attention.py:117-125) couples a frame's pixels
+// only through the 3x3 gate convs over that frame's own h_{t-1}; frames never
+// interact.  The fp32 learner's batch (config 2: B = 32 frames, 84x84 -> 11x11
+// grid) is far below the CU count, so here G workgroups (G = 8 or 4) own
+// one frame for all T steps, each a slice of 512/G gate-interleaved rows
+// (128/G channels), and exchange only h_t: each publishes its channels
+// of h_t (XH slot t+1, written anyway as the weight-gradient operand) with
+// write-through stores and a flag, and reads the other G-1 slices back into
+// its LDS h image under the next step's x-part.  This
+// replaces the 19 per-step launches of the h-part GEMM AND the batched x-part
+// GEMM (one K = 1728 [x | h] GEMM per step, as the bf16 frame-resident kernel
+// in recur.h does), with no launch boundary, prologue or operand re-gather.
+//
+// Workgroup (b, kh): 4 waves; gate rows [512 kh / G, 512 (kh+1) / G) =
+// NRB = 16 / G row blocks of 32; the frame's P <= 128 pixels are 4 column
+// blocks of 32.  Wave w: row blocks (w & 1) * RPW .. + RPW (RPW = NRB / 2),
+// column blocks 2 (w >> 1), 2 (w >> 1) + 1.  The G workgroups of a frame get
+// block indices of equal residue mod 8 (one XCD under round-robin placement),
+// so the hand-off runs through one L2.
+//
+// K order of a step: 216 "quads" of 4 MFMA k-steps (8 channels of one tap):
+// x-part 9 taps x 8 quads, then h-part 9 taps x 16 quads.  Within a quad,
+// lane half hh covers channels 4hh..4hh+3 and k-step j channel 4hh+j, so one
+// ds_read_b128 of the B image and one 16-B load of the fragment-order weights
+// (k_pack_wf32) feed four MFMAs.
+//
+// LDS images (zero border), 16-B chunk q of image pixel ip at slot q ^ (ip & 15)
+// (16 consecutive pixels of a fragment read hit 16 distinct bank groups):
+//   x image: 169 pixels x 64 fp32 (256 B),  DMA-filled from XH slot t+1 under the epilogue
+//   h image: 169 pixels x 128 fp32 (512 B), own channels from the epilogue, the
+//            partners' from XH slot t.
+#pragma once
+#include "common.h"
+#include "epilogues.h"
+#include "glds.h"
+#include "recur.h"
+
+namespace aaa {
+
+constexpr int kF32QX = 72;                 // x-part quads (9 taps x 8)
+constexpr int kF32Q = 216;                 // quads per step
+constexpr int kF32PD = 8;                  // A quads in flight (register slots); divides 8, 16 and kF32Q
+constexpr int kF32QP = kF32Q + kF32PD - 1;  // packed quads per row block: the first PD-1 repeated at the end
+constexpr int kF32XB = 44 * 1024;          // x image bytes: 169 x 256 B rounded up to whole 1-KB DMA pieces
+constexpr int kF32HB = 169 * 512;          // h image bytes
+constexpr int kF32GP = 144;                // epilogue staging: gate tile pixel pitch (128 B + 16)
+constexpr int kF32SG = 32 * kF32GP;        // ... c / h tiles after it, pixel pitch 48 B (32 B + 16)
+constexpr int kF32STG = kF32SG + 2 * 32 * 48;   // staging bytes per wave (7.5 KB)
+
+// element offset k (= tap * 192 + channel) of quad q's channel 0 for lane half 0
+__host__ __device__ constexpr int f32_k(int q) {
+  return q < kF32QX ? (q >> 3) * 192 + (q & 7) * 8 : ((q - kF32QX) >> 4) * 192 + 64 + ((q - kF32QX) & 15) * 8;
+}
+
+// Wf[((rb * kF32QP + q) * 64 + lane) * 4 + j] = W[32 rb + lane % 32][f32_k(q % kF32Q) + 4 (lane / 32) + j]
+__global__ void __launch_bounds__(256) k_pack_wf32(const float* __restrict__ W, float* __restrict__ Wf) {
+  const int c = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
+  if (c >= 16 * kF32QP * 64) return;
+  const int lane = c & 63, rq = c >> 6, q = rq % kF32QP, rb = rq / kF32QP;
+  const int row = rb * 32 + (lane & 31), k = f32_k(q % kF32Q) + (lane >> 5) * 4;
+  *reinterpret_cast<f32x4*>(Wf + (size_t)c * 4) = *reinterpret_cast<const f32x4*>(W + (size_t)row * 1728 + k);
+}
+
+inline hipError_t pack_wf32(const float* W, float* Wf, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_wf32, dim3((16 * kF32QP * 64 + 255) / 256), dim3(256), 0, st, W, Wf);
+  return hipGetLastError();
+}
+
+struct RecF32Params {
+  const float* Wf;     // fragment-order [x|h] weights (k_pack_wf32)
+  const float* bias;   // [512] gate-interleaved x-conv biases
+  float* XH;           // (T+1, B, P, 192): slot t = [x_t | h_{t-1}]; h_t -> slot t+1
+  float* Cst;          // (T+1, B, P, 128): slot 0 = c_0 (read), slot t+1 <- c_t
+  float* Hs;           // (T, B, P, 128) <- h_t
+  float* Gt;           // (T, B, P, 512) <- gate activations (i, f, c~, o)
+  int* flags;          // [B][G] count of published h steps (zeroed by the caller)
+  int* report;         // partner-timeout report word (pair_wait)
+  int spin;            // partner-wait bound in polls
+  int T, B, h, w, P;
+  int h0_zero;         // slot 0's h part is zero (reset()): the t = 0 h-part is skipped
+  short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
+};
+
+// Blocks of the launch: 8 * G * ceil(B / 8) (XCD-local frame groups).
+inline int f32_grid(int B, int G) { return 8 * G * ((B + 7) / 8); }
+
+#ifdef AAA_STAMPS
+// Diagnostic builds only (tools/ubench/f32rec): per (workgroup, step) phase
+// stamps (s_memrealtime, 100 MHz): step start, x-part done (partners' h in),
+// h-part done, epilogue done, flag published.
+__device__ uint64_t aaa_f32_stamps[512 * 64 * 5];
+__device__ uint64_t aaa_f32_clocks[512 * 64 * 5];   // s_memtime (shader clock) at the same points
+#define AAA_F32_STAMP(t, k)                                                                          \
+  do {                                                                                               \
+    if (tid == 0 && (t) < 64) {                                                                      \
+      aaa_f32_stamps[(blk * 64 + (t)) * 5 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+      aaa_f32_clocks[(blk * 64 + (t)) * 5 + (k)] = __builtin_amdgcn_s_memtime();                      \
+    }                                                                                                \
+  } while (0)
+#else
+#define AAA_F32_STAMP(t, k) do {} while (0)
+#endif
+
+// ABL (diagnostic builds only, tools/ubench/f32rec; production launches use 0):
+// bit 0 = no epilogue (gate math, stores), bit 1 = no epilogue HBM stores,
+// bit 2 = no partner exchange, bit 3 = no MFMAs.
+template <int G, int ABL = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_convlstm_fwd_f32(RecF32Params p) {
+  constexpr int NRB = 16 / G, RPW = NRB / 2;       // row blocks per workgroup / per wave
+  constexpr int CPG = 32 / G;                      // 16-B h chunks (4 channels) per workgroup slice
+  constexpr int NPL = (128 * (G - 1) * CPG + 255) / 256;   // partner chunks per thread (P <= 128)
+  static_assert(G == 4 || G == 8, "G");
+  __shared__ __attribute__((aligned(16))) unsigned char xim[kF32XB];
+  __shared__ __attribute__((aligned(16))) unsigned char him[kF32HB];
+  __shared__ __attribute__((aligned(16))) unsigned char stgall[4 * kF32STG];   // per-wave epilogue staging
+
+  const int blk = (int)blockIdx.x, xcd = blk & 7, loc = blk >> 3;
+  const int b = xcd + 8 * (loc / G), kh = loc % G;
+  if (b >= p.B) return;   // padding group of the last XCD column (never a partner of a live frame)
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
+  const size_t M = (size_t)p.B * P;
+  const int rw = wave & 1, cw = wave >> 1;
+  const int rbg0 = kh * NRB + rw * RPW;            // the wave's first global row block
+  auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
+  auto sw16 = [](int q, int ip) { return (q ^ (ip & 15)) << 4; };
+  unsigned char* stg = stgall + wave * kF32STG;
+
+  {  // zero both images (borders stay zero)
+    u32x4* z = reinterpret_cast<u32x4*>(xim);
+    for (int i = tid; i < kF32XB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    z = reinterpret_cast<u32x4*>(him);
+    for (int i = tid; i < kF32HB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  // x image of step t by LDS-DMA (XH slot t, channels 0..63): piece i of 44
+  // covers image bytes [1024 i, 1024 i + 1024) = pixels 4i + lane / 16, slot
+  // lane % 16, which holds chunk slot ^ (ip & 15); border pixels land as zeros.
+  auto dma_x = [&](int t) {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
+    for (int i = wave; i < kF32XB / 1024; i += 4) {
+      const int ip = i * 4 + (lane >> 4), q = (lane & 15) ^ (ip & 15);
+      const int py = ip / W2 - 1, px = ip % W2 - 1;
+      const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
+      dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 4) * 4) : kOOB);
+    }
+  };
+  dma_x(0);
+  if (!p.h0_zero) {   // h_{-1} (XH slot 0, all 128 channels) into the h image
+    const float* src = p.XH + (size_t)b * P * 192 + 64;
+    for (int i = tid; i < P * 32; i += 256) {
+      const int px = i >> 5, q = i & 31, ip = hidx(px);
+      *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(q, ip)) = *reinterpret_cast<const u32x4*>(src + (size_t)px * 192 + q * 4);
+    }
+  }
+
+  // per-lane state: bias of the lane's rows, c of its (pixel, channel) pairs
+  // tile (r, c) lane (r32, hh): element 4g + e = row 8g + 4hh + e of row block
+  // rbg0 + r = gate e of channel 8 (rbg0 + r) + 2g + hh, at column 32 (2cw + c) + r32
+  f32x4 bz[RPW][4];
+  float cst[RPW][2][4];
+  int pcol[2], hb[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int col = 32 * (2 * cw + c) + r32;
+    pcol[c] = col < P ? col : -1;
+    hb[c] = p.colhb[col];
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 8 * (rbg0 + r) + 2 * g + hh;
+      bz[r][g] = *reinterpret_cast<const f32x4*>(p.bias + 4 * ch);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) cst[r][c][g] = pcol[c] >= 0 ? p.Cst[((size_t)b * P + pcol[c]) * 128 + ch] : 0.f;
+    }
+
+  // A stream: the wave's RPW row blocks, quad q at soffset (rb * kF32QP + q) * 1 KB
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wf, (uint32_t)(16 * kF32QP * 1024));
+  auto lda = [&](int q, int r) {
+    return __builtin_bit_cast(f32x4,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, ((rbg0 + r) * kF32QP + q) * 1024, 0));
+  };
+  constexpr int PD = kF32PD;
+  f32x4 af[PD][RPW];
+#pragma unroll
+  for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) af[s][r] = lda(s, r);
+  __syncthreads();   // h_{-1} image written; this wave's x DMA is waited for below
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's x_0 DMA landed
+
+  for (int t = 0; t < p.T; ++t) {
+    f32x16 acc[RPW][2];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
+    int hbs[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      hbs[c] = hb[c];
+      asm volatile("" : "+v"(hbs[c]));
+    }
+    auto tapoff = [&](int tap) { return (tap / 3) * W2 + tap % 3; };
+    // B fragments of a quad: image pixel hbs[c] + toff, 16-B chunk q (x: 0..15, h: 0..31) + hh
+    auto ldb = [&](const unsigned char* img, int pitch, int toff, int q, f32x4 (&bf)[2]) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ip = hbs[c] + toff;
+        bf[c] = *reinterpret_cast<const f32x4*>(img + ip * pitch + sw16(q + hh, ip));
+      }
+    };
+    // one quad: A prefetch PD-1 ahead, next B fragments, 4 k-steps x RPW x 2 MFMAs
+    auto quad = [&](int qn, int slot, f32x4 (&bc)[2], auto&& load_next_b) {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) af[(slot + PD - 1) % PD][r] = lda(qn + PD - 1, r);
+      load_next_b();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            if constexpr (ABL & 8)
+              acc[r][c][j] += af[slot][r][j] * bc[c][j];
+            else
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[slot][r][j], bc[c][j], acc[r][c], 0, 0, 0);
+          }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x4 bfr[2][2];
+    // partners' slices of h_{t-1} (XH slot t): loaded into registers mid x-part
+    u32x4 pv[NPL];
+    const bool exch = G > 1 && t > 0 && !(ABL & 4);
+    AAA_F32_STAMP(t, 0);
+    auto partner_issue = [&] {
+      if (lane == 0)
+        for (int j = 0; j < G; ++j)
+          if (j != kh) pair_wait(p.flags + b * G + j, t, p.report, p.spin);
+      __builtin_amdgcn_wave_barrier();
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
+#pragma unroll
+      for (int n = 0; n < NPL; ++n) {
+        const int i = tid + 256 * n, px = i / ((G - 1) * CPG), rem = i % ((G - 1) * CPG);
+        const int pj = rem / CPG, kq = (pj < kh ? pj : pj + 1) * CPG + rem % CPG;
+        pv[n] = __builtin_amdgcn_raw_buffer_load_b128(rs, px < P ? (uint32_t)((px * 192 + 64 + kq * 4) * 4) : kOOB, 0,
+                                                      kSC1);
+      }
+    };
+    auto partner_store = [&] {
+#pragma unroll
+      for (int n = 0; n < NPL; ++n) {
+        const int i = tid + 256 * n, px = i / ((G - 1) * CPG), rem = i % ((G - 1) * CPG);
+        const int pj = rem / CPG, kq = (pj < kh ? pj : pj + 1) * CPG + rem % CPG;
+        if (px < P) {
+          const int ip = hidx(px);
+          *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(kq, ip)) = pv[n];
+        }
+      }
+    };
+
+    // ---- x-part: 9 taps x 8 quads over the x image
+    ldb(xim, 256, 0, 0, bfr[0]);
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+      int qt = tap * 8;
+      asm volatile("" : "+s"(qt));
+      if (tap == 2 && exch) partner_issue();
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8)
+        quad(qt + c8, c8 % PD, bfr[c8 & 1], [&] {
+          if (c8 < 7) ldb(xim, 256, toff, 2 * (c8 + 1), bfr[(c8 + 1) & 1]);
+          else if (tap < 8) ldb(xim, 256, tn, 0, bfr[0]);
+        });
+    }
+    const bool hpart = t > 0 || !p.h0_zero;
+    if (exch) partner_store();
+    barrier_lds();   // every wave is done with x_t; the partners' h_{t-1} is in the image
+    AAA_F32_STAMP(t, 1);
+    if (hpart) {
+      // ---- h-part: 9 taps x 16 quads over the h image
+      ldb(him, 512, 0, 0, bfr[0]);
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+        int qt = kF32QX + tap * 16;
+        asm volatile("" : "+s"(qt));
+#pragma unroll
+        for (int c16 = 0; c16 < 16; ++c16)
+          quad(qt + c16, c16 % PD, bfr[c16 & 1], [&] {
+            if (c16 < 15) ldb(him, 512, toff, 2 * (c16 + 1), bfr[(c16 + 1) & 1]);
+            else if (tap < 8) ldb(him, 512, tn, 0, bfr[0]);
+          });
+      }
+    } else {   // the prefetched A quads are the h-part's: restart the stream at quad 0
+#pragma unroll
+      for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) af[s][r] = lda(s, r);
+    }
+    barrier_lds();   // every wave is done with h_{t-1}: the epilogue overwrites its own channels
+    AAA_F32_STAMP(t, 2);
+    // x_{t+1} lands under the epilogue: issued here, not under the h-part, because
+    // vmcnt retires in order -- every later A-stream wait would queue behind the DMA
+    if (t + 1 < p.T) dma_x(t + 1);
+
+    // ---- epilogue: gate math + cell update lane-local; h_t into the image;
+    // the HBM outputs staged through the wave's LDS scratch one 32 x 32 tile
+    // at a time, so every store instruction writes whole pixel rows (Gt:
+    // 128 B of the 32 gate rows, c / h: 32 B of the 8 channels).
+    const size_t rowt = (size_t)t * M + (size_t)b * P;   // this frame's rows of step t
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int pp = pcol[c];
+        if constexpr ((ABL & 1) != 0) {   // keep the accumulators alive, no epilogue work
+          if (pp < 0) *reinterpret_cast<float*>(him) = acc[r][c][0] + acc[r][c][15];
+          continue;
+        }
+        const int ip = hidx(max(pp, 0));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int chl = 2 * g + hh, ch = 8 * (rbg0 + r) + chl;
+          float gi, gf, gc, go, cc, h;
+          GateFwd::run(acc[r][c][4 * g] + bz[r][g][0], acc[r][c][4 * g + 1] + bz[r][g][1],
+                       acc[r][c][4 * g + 2] + bz[r][g][2], acc[r][c][4 * g + 3] + bz[r][g][3], cst[r][c][g], gi, gf,
+                       gc, go, cc, h);
+          cst[r][c][g] = cc;
+          *reinterpret_cast<f32x4*>(stg + r32 * kF32GP + 16 * chl) = f32x4{gi, gf, gc, go};
+          *reinterpret_cast<float*>(stg + kF32SG + r32 * 48 + 4 * chl) = cc;
+          *reinterpret_cast<float*>(stg + kF32SG + 32 * 48 + r32 * 48 + 4 * chl) = h;
+          if (pp >= 0) *reinterpret_cast<float*>(him + ip * 512 + sw16(ch >> 2, ip) + (ch & 3) * 4) = h;
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(ABL & 2)) {
+          const int col0 = 32 * (2 * cw + c);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {   // Gt: 32 pixels x 8 chunks of 16 B (rows 32 rbg .. + 32)
+            const int q = k * 64 + lane, px = q >> 3, ch16 = q & 7, pix = col0 + px;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + px * kF32GP + 16 * ch16);
+            if (pix < P) *reinterpret_cast<u32x4*>(p.Gt + (rowt + pix) * 512 + 32 * (rbg0 + r) + 4 * ch16) = v;
+          }
+          {  // c_t, h_t: 32 pixels x 2 chunks of 16 B (channels 8 rbg .. + 8)
+            const int px = lane >> 1, half = lane & 1, pix = col0 + px;
+            const u32x4 vc = *reinterpret_cast<const u32x4*>(stg + kF32SG + px * 48 + 16 * half);
+            const u32x4 vh = *reinterpret_cast<const u32x4*>(stg + kF32SG + 32 * 48 + px * 48 + 16 * half);
+            if (pix < P) {
+              *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + 8 * (rbg0 + r) + 4 * half) = vc;
+              *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + 8 * (rbg0 + r) + 4 * half) = vh;
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    barrier_lds();   // this workgroup's channels of h_t are in the image
+    {  // ... and from there into XH slot t+1 (the partners' and the weight gradient's operand):
+       // 16-B write-through (sc1) stores, whole chunks
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + (rowt + M) * 192, (uint32_t)(P * 192 * 4));
+      for (int i = tid; i < P * CPG; i += 256) {
+        const int px = i / CPG, q = kh * CPG + i % CPG, ip = hidx(px);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + ip * 512 + sw16(q, ip)), rs,
+                                               (uint32_t)((px * 192 + 64 + q * 4) * 4), 0, kSC1);
+      }
+    }
+    AAA_F32_STAMP(t, 3);
+    // publish h_t: every wave's stores (and its x_{t+1} DMA) retired, a barrier, one flag store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();
+    if (G > 1 && tid == 0) __hip_atomic_store(p.flags + b * G + kh, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    AAA_F32_STAMP(t, 4);
+  }
+}
+
+inline bool f32_rec_fits(int h, int w) { return rec_fits(h, w); }
+
+// Workgroups per frame for B frames on a device of ``cus`` CUs (0: does not fit one residency wave).
+inline int f32_rec_g(int B, int cus) {
+  for (int G : {8, 4})   // (G = 2 spills at 1 wave per SIMD: 8 row blocks x 2 column blocks per wave)
+    if (f32_grid(B, G) <= cus) return G;
+  return 0;
+}
+
+inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st) {
+  if (!f32_rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
+    return hipErrorInvalidValue;
+  for (int c = 0; c < 128; ++c) {
+    const int pp = c < p.P ? c : p.P - 1;
+    p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
+  }
+  const void* k = G == 8   ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>)
+                  : G == 4 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4>)
+                           : nullptr;
+  if (!k) return hipErrorInvalidValue;
+  return launch_resident(k, f32_grid(p.B, G), 256, p, st);
+}
+
+}  // namespace aaa

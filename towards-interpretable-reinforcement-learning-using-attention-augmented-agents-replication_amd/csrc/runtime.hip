@@ -31,6 +31,7 @@
 #include "halo.h"
 #include "recur.h"
 #include "recur_bwd.h"
+#include "recur_f32.h"
 #include "vision.h"
 #include "misc.h"
 #include "optim.h"
@@ -75,7 +76,7 @@ struct Layout {
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
@@ -130,6 +131,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.k_Wfr = take(e == 2 ? (size_t)16 * kRecKSP * 64 * 16 : 0);   // its fragment-order copy (frame-resident recurrence, recur.h)
   L.k_WdTl = take(192 * 4608 * e);
   L.k_Wbf = take(e == 2 ? (size_t)6 * kBwKSP * 64 * 16 : 0);   // fragment-order [W_h^T | W_x^T] (frame-resident BPTT)
+  L.k_Wf32 = take(e == 4 ? (size_t)16 * kF32QP * 64 * 16 : 0);   // fp32 fragment-order [x|h] (frame-group recurrence, recur_f32.h)
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
   L.k_Wihp = take(1024 * 256 * 4);
@@ -171,7 +173,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
-  L.rflags = take((size_t)2 * L.B * 4);   // hand-off flags of the paired frame-resident kernels
+  L.rflags = take((size_t)8 * L.B * 4);   // hand-off flags of the multi-workgroup frame kernels ([B][G], G <= 8)
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -700,6 +702,8 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
   if constexpr (!std::is_same<T, float>::value) {   // fragment orders of the frame-resident kernels (read WpXH / WdT)
     HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
     HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
+  } else {   // the fp32 frame-group recurrence's fragment order (recur_f32.h)
+    HIPCHK(pack_wf32((const float*)(pk + L.k_WpXH), (float*)(pk + L.k_Wf32), st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
@@ -822,6 +826,18 @@ static int frames_g(const Layout& L, const char* env) {
   return v == 1 ? 1 : (v == 2 && 2 * L.B <= cus ? 2 : 0);
 }
 static int frames_fwd(const Layout& L) { return frames_g(L, "AAA_FRAMES_FWD"); }
+// fp32 ConvLSTM forward on the frame-group kernel (recur_f32.h): G workgroups
+// per frame for all T steps, once B * G fills at least half the CUs in one
+// residency wave (C2: B = 32, G = 8 on 256 CUs).  AAA_F32_FRAMES = 0 keeps the
+// per-step launches (A/B and parity of both paths); 8 / 4 force that G.
+static int f32_frames(const Layout& L) {
+  if (L.dt != AAA_F32 || !f32_rec_fits(L.h, L.w)) return 0;
+  const int v = env_int("AAA_F32_FRAMES", 1), cus = device_cus();
+  if (v == 8 || v == 4) return f32_grid(L.B, v) <= cus ? v : 0;   // forced G (tests, A/B)
+  if (v != 1) return 0;
+  const int G = f32_rec_g(L.B, cus);
+  return G && 2 * G * L.B >= cus ? G : 0;
+}
 // The BPTT chain on the frame-resident kernels (recur_bwd.h; fp16 gate storage):
 // workgroups per frame as the forward's (AAA_FRAMES_BWD = 0 / 1 / 2 forces it).
 static int frames_bwd(const Layout& L, bool g16) { return g16 ? frames_g(L, "AAA_FRAMES_BWD") : 0; }
@@ -847,6 +863,24 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
   if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  if constexpr (std::is_same<T, float>::value) {
+    if (const int G = f32_frames(L)) {   // one frame-group launch for all T steps, x-part included (recur_f32.h)
+      HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)G * L.B * 4, st));
+      int dev = 0;
+      HIPCHK(hipGetDevice(&dev));
+      int* rep = pair_report(dev);
+      if (!rep) return fail(AAA_E_LAUNCH, "cannot map the frame-group report word");
+      RecF32Params rp{(const float*)(pk + L.k_Wf32), (const float*)(pk + L.k_bl), Wf(L.XH), Wf(L.Cst), Wf(L.Hs),
+                      Wf(L.Gt), (int*)(ws + L.rflags), rep, (int)g_pair_spin, L.T, L.B, L.h, L.w, L.P,
+                      io->h0 ? 0 : 1, {}};
+      {
+        TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
+                       strf("fp32 frame-group [x|h] recurrence, %d steps per launch, %d WG per frame", L.T, G));
+        HIPCHK(convlstm_fwd_f32(rp, G, st));
+      }
+      return forward_tail<T>(L, io, st);
+    }
+  }
   // bf16: the x-part rides in each step's GEMM (K over the whole XH slot,
   // [x_t | h_{t-1}], bias in the epilogue): no batched x-part GEMM and no
   // fp32 x-part round trip through HBM (tools/ubench/bf16_tiles: the step's

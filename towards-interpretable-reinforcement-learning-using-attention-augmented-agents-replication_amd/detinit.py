@@ -110,6 +110,17 @@ def frames_u8(seed: int, shape) -> np.ndarray:
     return (splitmix64(seed, n) >> np.uint64(56)).astype(np.uint8).reshape(shape)
 
 
+def normal(seed: int, shape) -> np.ndarray:
+    """fp32 N(0, 1) by Box-Muller on two splitmix64 uniform streams (seed, seed
+    + 2^32); computed in float64 and rounded once (bench cotangents, SURVEY.md
+    §8d: G_l, G_v ~ N(0,1), seed 2)."""
+    n = int(np.prod(shape))
+    u1 = (splitmix64(seed, n) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    u2 = (splitmix64(seed + (1 << 32), n) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    r = np.sqrt(-2.0 * np.log1p(-u1))          # u1 in [0, 1): 1 - u1 in (0, 1]
+    return (r * np.cos(2.0 * np.pi * u2)).astype(np.float32).reshape(shape)
+
+
 def cotangent(seed: int, shape) -> np.ndarray:
     """fp32 uniform [-1,1) loss cotangents for logits / values."""
     n = int(np.prod(shape))

@@ -41,6 +41,10 @@ class Learner:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.bounds = bucket_bounds(r.offsets, r.n_params)
+        # Phase -> bucket disjointness (checked by tools/dp_check.py): a backward
+        # phase writes no bucket whose all-reduce an EARLIER phase has already
+        # issued -- CORE may write conv2's bias grad (VISION bucket, reduced after
+        # it), never a HEAD tensor; VISION writes neither HEAD nor CORE.
         if self.world > 1:   # identical weights on every rank (they are seeded, but be explicit)
             dist.broadcast(self.flat, src=0, group=group)
             self.comm = torch.cuda.Stream(self.device)   # the gradient all-reduces (RCCL) run here
@@ -90,6 +94,8 @@ class Learner:
     def comm_stats(self):
         """Per-bucket all-reduce time (ms) and the communication left exposed
         after the last backward phase (ms) of the last timed step()."""
+        if not getattr(self, "_events", None):
+            raise RuntimeError("comm_stats(): the last step() ran without comm_timing=True (or on one rank)")
         buckets = []
         for (lo, hi, ready, t0, t1), name in zip(self._events, ("HEAD", "CORE", "VISION")):
             buckets.append({"bucket": name, "bytes": 4 * (hi - lo), "allreduce_ms": round(t0.elapsed_time(t1), 4),
