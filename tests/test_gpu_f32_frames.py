@@ -1,5 +1,6 @@
 """The fp32 frame-group ConvLSTM recurrence (csrc/recur_f32.h: G = 8 or 4
-workgroups own a frame for all T steps and exchange h_t through L2) against
+workgroups own a frame for all T steps and exchange h_t through L2; with G = 8
+also the frame-group BPTT, csrc/recur_bwd_f32.h, which exchanges dZ) against
 the CPU oracle at the fp32 tolerance (1e-4) and against the
 per-step launches it replaces (AAA_F32_FRAMES=0).
 
@@ -29,15 +30,22 @@ def test_f32_frames_vs_oracle(cuda, monkeypatch, T, B, G):
     try:
         out = _run_unroll(_agent(cuda), T, B, cuda)
         var = N.timing_stats(N.TIMER_FWD_STEP)["variant"]
+        bvar = N.timing_stats(N.TIMER_BPTT_STEP)["variant"]
     finally:
         N.timing_enable(False)
     assert f"{G} WG per frame" in var, var
+    if T > 1:
+        assert ("frame-group BPTT" in bvar) == (G == "8"), bvar
     _compare(out, _oracle(T, B), RTOL, f"f32 frames G={G} T={T} B={B}: ")
     assert N.pair_status(clear=True) == 0
     monkeypatch.setenv("AAA_F32_FRAMES", "0")
     step = _run_unroll(_agent(cuda), T, B, cuda)
     for a, b, n in zip(out[:3], step[:3], ("logits", "values", "attn")):
         assert_close(a.numpy(), b.numpy(), 1e-5, f"f32 frames vs per-step {n}")
+    # the frame-group BPTT (G = 8 only; G = 4 keeps the per-step BPTT) against the per-step launches
+    for n in out[3]:
+        if float(step[3][n].norm()) > 0:
+            assert rel_err(out[3][n].numpy(), step[3][n].numpy()) <= 1e-5, f"f32 frames vs per-step grad {n}"
 
 
 @pytest.mark.parametrize("G", ["8", "4"])

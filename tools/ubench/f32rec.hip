@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include "recur_bwd_f32.h"
 #include "recur_f32.h"
 
 using namespace aaa;
@@ -88,6 +89,55 @@ static void phases(int G, int B, int T) {
 }
 #endif
 
+template <int ABL>
+static double run_bwd(RecBwdF32Params p, int reps, const char* name) {
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_f32<ABL>);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  double best = 1e30, sum = 0;
+  for (int r = 0; r < reps + 2; ++r) {
+    CK(hipMemset(p.flags, 0, (size_t)p.B * 8 * 4));
+    CK(hipEventRecord(a, 0));
+    CK(launch_resident(k, f32_grid(p.B, 8), 256, p, 0));
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    if (r >= 2) { best = std::min(best, (double)ms); sum += ms; }
+  }
+  printf("BPTT %-29s G=8  best %8.1f us  mean %8.1f us\n", name, best * 1e3, sum / reps * 1e3);
+  return best;
+}
+
+#ifdef AAA_STAMPS
+static void phases_bwd(int B, int T) {
+  const int nwg = f32_grid(B, 8);
+  std::vector<uint64_t> st((size_t)512 * 64 * 4);
+  CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(aaa_b32_stamps), st.size() * 8));
+  const char* nm[3] = {"K loop", "publish+wait", "sum+gate bwd"};
+  std::vector<double> tot(3, 0.0);
+  for (int it = 0; it < T - 1; ++it) {
+    std::vector<double> ph[3];
+    for (int w = 0; w < nwg; ++w) {
+      const int xcd = w & 7, loc = w >> 3, b = xcd + 8 * (loc / 8);
+      if (b >= B) continue;
+      const uint64_t* s = &st[((size_t)w * 64 + it) * 4];
+      for (int k = 0; k < 3; ++k) ph[k].push_back((s[k + 1] - s[k]) * 0.01);
+    }
+    if (it % 4 == 1) printf("  it=%2d", it);
+    for (int k = 0; k < 3; ++k) {
+      std::sort(ph[k].begin(), ph[k].end());
+      const double med = ph[k][ph[k].size() / 2];
+      tot[k] += med;
+      if (it % 4 == 1) printf("  %s %6.2f (max %6.2f)", nm[k], med, ph[k].back());
+    }
+    if (it % 4 == 1) printf("\n");
+  }
+  printf("  BPTT sum of medians:");
+  for (int k = 0; k < 3; ++k) printf("  %s %.1f", nm[k], tot[k]);
+  printf("\n");
+}
+#endif
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 32, T = argc > 2 ? atoi(argv[2]) : 20, h = 11, w = 11, P = h * w;
   const size_t M = (size_t)B * P;
@@ -119,6 +169,28 @@ int main(int argc, char** argv) {
   run<8, 5>(p, reps, "no epilogue, no exchange");
   run<8, 13>(p, reps, "no epilogue/exchange/MFMA");
   run<4, 0>(p, reps, "production");
+  {  // the frame-group BPTT at the same shape
+    RecBwdF32Params q{};
+    q.Wb = dev_rand((size_t)8 * kB32QP * 4 * 256, 0.02f, 7);
+    q.dO = dev_rand((size_t)T * M * 128, 0.1f, 8);
+    q.Gt = dev_rand((size_t)T * M * 512, 0.5f, 9);
+    q.Cst = p.Cst;
+    q.dC = dev_rand(M * 128, 0.1f, 10);
+    q.dZ = dev_rand((size_t)T * M * 512, 0.1f, 11);
+    q.part = dev_rand((size_t)T * B * 512, 1.f, 12);
+    q.dh0 = nullptr;
+    CK(hipMalloc(&q.xp, b32_xpart_floats(B) * 4));
+    q.flags = p.flags; q.report = p.report; q.spin = p.spin;
+    q.T = T; q.B = B; q.h = h; q.w = w; q.P = P;
+    for (int c = 0; c < 128; ++c) q.colhb[c] = p.colhb[c];
+    run_bwd<0>(q, reps, "production");
+#ifdef AAA_STAMPS
+    phases_bwd(B, T);
+#endif
+    run_bwd<1>(q, reps, "no partner waits");
+    run_bwd<9>(q, reps, "no exchange");
+    run_bwd<11>(q, reps, "no exchange, no MFMA");
+  }
   printf("timeout reports: %d\n", *hrep);
   return 0;
 }

@@ -1,0 +1,367 @@
+// Frame-group-resident ConvLSTM BPTT, fp32 (exact v_mfma_f32_32x32x2_f32).
+//
+// The backward of the reference's recurrence (attention.py:117-125, autograd
+// at main_mp.py:77): per step s = T-1 .. 1, dh_{s-1} = W_h^T (*) dZ_s (the
+// transposed 3x3 gate convs) and the gate backward of step s-1, which turns
+// dh_{s-1} + dO_{s-1} and the carried dc into dZ_{s-1}.  As in the forward
+// (recur_f32.h), G = 8 workgroups own one frame for all steps (config 2:
+// B = 32 -> 256 workgroups).  Workgroup kh owns the h channels
+// [16 kh, 16 kh + 16): the 64 gate-interleaved dZ rows its gate backward
+// produces, which stay in its LDS as the B operand of its next dgrad.  That
+// dgrad is split over the workgroups by K: workgroup kh contracts only its own
+// 64 dZ rows (9 taps x 64 = K 576) but for ALL 128 output channels, and the
+// eight partial dh slices are exchanged -- each workgroup publishes the
+// 7 x 16 channels that belong to the others (write-through stores, a flag) and
+// sums the seven partials addressed to it with its own.  Per step a workgroup
+// moves 2 x 54 KB through L2.  (The alternative, every workgroup re-reading
+// the frame's whole dZ_s -- 248 KB per step by LDS-DMA -- was LDS-DMA bound:
+// 1030 us at config 2 against 980 us for the per-step launches,
+// profiles/r03/f32rec/bwd_dz_exchange.txt.)
+//
+// Workgroup: 4 waves; D[128 channels][128 pixel columns] as 4 x 4 tiles of
+// 32 x 32; wave w owns row blocks 2 (w & 1) + {0, 1} and column blocks
+// 2 (w >> 1) + {0, 1} (two phases of two column blocks each, the first
+// half's partials travelling under the second half's MFMAs, measured slower:
+// 961 vs 916 us, the 8-MFMA quads cost more than the exposed exchange saved).
+// K order: 72 quads (9 taps x 8 groups of 8 dZ rows);
+// lane (r32, hh) reads the 4 rows 8 q8 + 4 hh .. + 3 of its pixel with one
+// ds_read_b128 (4 k-steps) and the matching 16 B of the fragment-order weights
+// (k_pack_wb32).  The dx rows stay in the batched dgrad GEMM after this kernel
+// (runtime.hip), which runs at the MFMA rate already.
+#pragma once
+#include "common.h"
+#include "epilogues.h"
+#include "glds.h"
+#include "recur.h"
+#include "recur_f32.h"
+
+namespace aaa {
+
+constexpr int kB32Q = 72;                     // quads per step (9 taps x 8)
+constexpr int kB32PD = 8;                     // A quads in flight (register slots): slot = q8
+constexpr int kB32QP = kB32Q + kB32PD - 1;    // packed quads per workgroup slice (first PD-1 repeated)
+constexpr int kB32IB = 44 * 1024;             // own dZ image: 169 pixels x 64 rows fp32 (256 B)
+constexpr int kB32NBUF = 3;                   // partial-dh exchange buffers (step mod 3)
+
+// Wb[(((kh * kB32QP + q) * 4 + rb) * 64 + lane) * 4 + j] =
+//   WdT[64 + 32 rb + lane % 32][tap * 512 + 64 kh + 8 q8 + 4 (lane / 32) + j],  q % kB32Q = tap * 8 + q8
+__global__ void __launch_bounds__(256) k_pack_wb32(const float* __restrict__ WdT, float* __restrict__ Wb) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
+  if (i >= 8 * kB32QP * 4 * 64) return;
+  const int lane = i & 63, rb = (i >> 6) & 3, kq = i >> 8, q = kq % kB32QP, kh = kq / kB32QP;
+  const int qq = q % kB32Q, tap = qq >> 3, q8 = qq & 7;
+  const int row = 64 + 32 * rb + (lane & 31), k = tap * 512 + 64 * kh + 8 * q8 + 4 * (lane >> 5);
+  *reinterpret_cast<f32x4*>(Wb + (size_t)i * 4) = *reinterpret_cast<const f32x4*>(WdT + (size_t)row * 4608 + k);
+}
+
+inline hipError_t pack_wb32(const float* WdT, float* Wb, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_wb32, dim3((8 * kB32QP * 4 * 64 + 255) / 256), dim3(256), 0, st, WdT, Wb);
+  return hipGetLastError();
+}
+
+// Exchange buffer floats: [kB32NBUF][B][8 dst][8 src][128 px][16 ch]
+inline size_t b32_xpart_floats(int B) { return (size_t)kB32NBUF * B * 64 * 128 * 16; }
+
+struct RecBwdF32Params {
+  const float* Wb;     // fragment-order W_h^T (k_pack_wb32)
+  const float* dO;     // (T, B, P, 128) attention-path grad of h_t
+  const float* Gt;     // (T, B, P, 512) gate activations
+  const float* Cst;    // (T+1, B, P, 128): slot s+1 = c_s
+  float* dC;           // (B, P, 128) dc carry: in = the carry after step T-1's gate backward, out = dc_0
+  float* dZ;           // (T, B, P, 512): slot T-1 read, slots T-2 .. 0 written
+  float* part;         // (T, B, 512) <- gate-bias partials per (step, frame)
+  float* dh0;          // (B, P, 128) <- grad of h_{-1}, or null
+  float* xp;           // partial-dh exchange (b32_xpart_floats)
+  int* flags;          // [B][8] count of published partial steps (zeroed by the caller)
+  int* report;         // partner-timeout report word (pair_wait)
+  int spin;
+  int T, B, h, w, P;
+  short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
+};
+
+#ifdef AAA_STAMPS
+__device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
+#define AAA_B32_STAMP(s, k)                                                                               \
+  do {                                                                                                    \
+    if (tid == 0 && (s) < 64) aaa_b32_stamps[(blk * 64 + (s)) * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AAA_B32_STAMP(s, k) do {} while (0)
+#endif
+
+// ABL (diagnostic builds only, tools/ubench/f32rec): bit 0 = no partner waits,
+// bit 1 = no MFMAs, bit 3 = no exchange (partials neither stored nor loaded).
+// Production launches use 0.
+template <int ABL = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_convlstm_bwd_f32(RecBwdF32Params p) {
+  constexpr int G = 8, NG = 2;                   // NG: (pixel, 4-channel) groups per thread (484 <= 512)
+  __shared__ __attribute__((aligned(16))) unsigned char zim[kB32IB];   // own dZ rows of the current step
+  __shared__ __attribute__((aligned(16))) f32x4 own[128][4];           // own partial dh [px][channel quad]
+  __shared__ __attribute__((aligned(16))) float bred[4][64];           // per-wave bias partials
+
+  const int blk = (int)blockIdx.x, xcd = blk & 7, loc = blk >> 3;
+  const int b = xcd + 8 * (loc / G), kh = loc % G;
+  if (b >= p.B) return;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int rw = wave & 1, cw = wave >> 1;
+  const int P = p.P, W2 = p.w + 2;
+  const size_t M = (size_t)p.B * P;
+  auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
+  auto sw16 = [](int q, int ip) { return (q ^ (ip & 15)) << 4; };
+  // exchange slot of (buffer, destination, source): [128 px][16 ch]
+  auto xslot = [&](int buf, int dst, int src) {
+    return p.xp + ((((size_t)buf * p.B + b) * 8 + dst) * 8 + src) * 128 * 16;
+  };
+
+  {  // zero the image (borders stay zero)
+    u32x4* z = reinterpret_cast<u32x4*>(zim);
+    for (int i = tid; i < kB32IB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+
+  // per-thread gate-backward groups: g = tid + 256 n -> pixel g / 4, channels 16 kh + 4 (g % 4) .. + 3
+  const int cq = tid & 3;
+  float dcr[NG][4];
+#pragma unroll
+  for (int n = 0; n < NG; ++n) {
+    const int px = (tid + 256 * n) >> 2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dcr[n][e] = px < P ? p.dC[((size_t)b * P + px) * 128 + 16 * kh + 4 * cq + e] : 0.f;
+  }
+  // gate-bias partials of this workgroup's 64 rows of dZ_s over the frame's pixels -> part[s][b]
+  auto bias_flush = [&](int s, f32x4 (&bs)[4]) {
+    // lanes of one wave with equal cq (lane % 4) hold the same 16 rows: reduce over lane / 4
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v = bs[e][g];
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        bs[e][g] = v;
+      }
+    if (lane < 4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *reinterpret_cast<f32x4*>(&bred[wave][16 * cq + 4 * e]) = bs[e];
+    __syncthreads();
+    if (tid < 64)
+      p.part[((size_t)s * p.B + b) * 512 + 64 * kh + tid] = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+  };
+  {  // dZ_{T-1} (step T-1's gate backward ran before this kernel): own rows into the image, bias partials
+    f32x4 bs[4] = {};
+#pragma unroll
+    for (int n = 0; n < NG; ++n) {
+      const int px = (tid + 256 * n) >> 2;
+      if (px < P) {
+        const int ip = hidx(px);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f32x4 z = *reinterpret_cast<const f32x4*>(p.dZ + ((size_t)(p.T - 1) * M + (size_t)b * P + px) * 512 +
+                                                          64 * kh + 16 * cq + 4 * e);
+          bs[e] += z;
+          *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(4 * cq + e, ip)) = z;
+        }
+      }
+    }
+    bias_flush(p.T - 1, bs);   // (its barrier also completes the image)
+  }
+
+  int hb[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) hb[c] = p.colhb[32 * (2 * cw + c) + r32];
+  const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(8 * kB32QP * 4 * 1024));
+  auto lda = [&](int q, int r) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rsw, lane * 16, ((kh * kB32QP + q) * 4 + 2 * rw + r) * 1024, 0));
+  };
+  constexpr int PD = kB32PD;
+  static_assert(kB32Q % PD == 0 && PD == 8, "slot = q8");
+  f32x4 af[PD][2];
+#pragma unroll
+  for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) af[s][r] = lda(s, r);
+
+  // the dgrad is the transposed conv: tap (ky, kx) of W^T (packed in the forward's
+  // orientation) reads dZ at (y + 1 - ky, x + 1 - kx) (ConvGeo transposed gather)
+  auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + 2 - tap % 3; };
+  const int nsteps = p.T - 1 + (p.dh0 ? 1 : 0);   // dgrads: dZ_{T-1} .. dZ_1 (+ dZ_0 for dh0)
+  for (int it = 0; it < nsteps; ++it) {
+    const int s = p.T - 1 - it;   // this dgrad reads dZ_s and yields dh_{s-1}
+    const int buf = it % kB32NBUF;
+    AAA_B32_STAMP(it, 0);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
+    int hbs[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      hbs[c] = hb[c];
+      asm volatile("" : "+v"(hbs[c]));
+    }
+    // gate-backward inputs of step s-1, loaded at the start (they land under the K loop)
+    f32x4 gpre[NG][7];
+    if (s >= 1) {
+#pragma unroll
+      for (int n = 0; n < NG; ++n) {
+        const int px = min((tid + 256 * n) >> 2, P - 1), ch = 16 * kh + 4 * cq;
+        const size_t r = (size_t)(s - 1) * M + (size_t)b * P + px;
+        gpre[n][0] = *reinterpret_cast<const f32x4*>(p.dO + r * 128 + ch);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gpre[n][1 + e] = *reinterpret_cast<const f32x4*>(p.Gt + r * 512 + 4 * (ch + e));
+        gpre[n][5] = *reinterpret_cast<const f32x4*>(p.Cst + r * 128 + ch);         // c_{s-2}
+        gpre[n][6] = *reinterpret_cast<const f32x4*>(p.Cst + (r + M) * 128 + ch);   // c_{s-1}
+      }
+    }
+    auto ldb = [&](int tap, int q8, f32x4 (&bf)[2]) {
+      const int toff = tapoff(tap);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int ip = hbs[c] + toff;
+        bf[c] = *reinterpret_cast<const f32x4*>(zim + ip * 256 + sw16(2 * q8 + hh, ip));
+      }
+    };
+    f32x4 bfr[2][2];
+    ldb(0, 0, bfr[0]);
+    for (int tap = 0; tap < 9; ++tap) {
+      int qt = tap * 8;
+      asm volatile("" : "+s"(qt));
+#pragma unroll
+      for (int q8 = 0; q8 < 8; ++q8) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) af[(q8 + PD - 1) % PD][r] = lda(qt + q8 + PD - 1, r);
+        if (q8 < 7) ldb(tap, q8 + 1, bfr[(q8 + 1) & 1]);
+        else if (tap < 8) ldb(tap + 1, 0, bfr[0]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              if constexpr (ABL & 2)
+                acc[r][c][j] += af[q8][r][j] * bfr[q8 & 1][c][j];
+              else
+                acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[q8][r][j], bfr[q8 & 1][c][j], acc[r][c], 0, 0, 0);
+            }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    AAA_B32_STAMP(it, 1);
+    // partial dh: lane (r32, hh) of tile (r, c), element 4g + e = channel
+    // 32 (2 rw + r) + 8 g + 4 hh + e at column 32 (2 cw + c) + r32, i.e. the
+    // 16-B quad 8 (g & 1) + 4 hh of destination 2 (2 rw + r) + (g >> 1)
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int px = 32 * (2 * cw + c) + r32;
+        if (px >= P) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dst = 2 * (2 * rw + r) + (g >> 1), cl = 8 * (g & 1) + 4 * hh;
+          const f32x4 v{acc[r][c][4 * g], acc[r][c][4 * g + 1], acc[r][c][4 * g + 2], acc[r][c][4 * g + 3]};
+          if (dst == kh) {
+            own[px][cl >> 2] = v;
+          } else if constexpr (!(ABL & 8)) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v),
+                                                   make_rsrc(xslot(buf, dst, kh), 128 * 16 * 4),
+                                                   (uint32_t)((px * 16 + cl) * 4), 0, kSC1);
+          }
+        }
+      }
+    // publish this step's partials: every wave's stores retired, a barrier, one flag store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();
+    if (tid == 0) __hip_atomic_store(p.flags + b * G + kh, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every wave waits for the seven partners, then sums their partials into its groups
+    if constexpr (!(ABL & 1)) {
+      if (lane == 0)
+        for (int j = 0; j < G; ++j)
+          if (j != kh) pair_wait(p.flags + b * G + j, it + 1, p.report, p.spin);
+    }
+    __builtin_amdgcn_wave_barrier();
+    AAA_B32_STAMP(it, 2);
+    f32x4 dhv[NG];
+#pragma unroll
+    for (int n = 0; n < NG; ++n) {
+      const int px = min((tid + 256 * n) >> 2, 127);
+      dhv[n] = own[px][cq];
+      if constexpr (!(ABL & 8)) {
+        f32x4 pv[G - 1];
+#pragma unroll
+        for (int j = 0; j < G - 1; ++j) {
+          const int src = j < kh ? j : j + 1;
+          pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                make_rsrc(xslot(buf, kh, src), 128 * 16 * 4),
+                                                (uint32_t)((px * 16 + 4 * cq) * 4), 0, kSC1));
+        }
+#pragma unroll
+        for (int j = 0; j < G - 1; ++j) dhv[n] += pv[j];
+      }
+    }
+    if (s == 0) {   // dh0 = dh_{-1}: no gate backward
+#pragma unroll
+      for (int n = 0; n < NG; ++n) {
+        const int px = (tid + 256 * n) >> 2;
+        if (px < P) *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + px) * 128 + 16 * kh + 4 * cq) = dhv[n];
+      }
+      break;
+    }
+    // (every wave is past the K loop -- the barrier behind the flag store -- so
+    // the image and own[] are free to rewrite)
+    // gate backward of step s-1 (EpiConvLstmBwd's math): dZ_{s-1} into the
+    // image (the next dgrad's B operand) and to HBM (the weight gradient's)
+    f32x4 bs[4] = {};
+#pragma unroll
+    for (int n = 0; n < NG; ++n) {
+      const int px = (tid + 256 * n) >> 2;
+      if (px >= P) continue;
+      const int ip = hidx(px);
+      float* zo = p.dZ + ((size_t)(s - 1) * M + (size_t)b * P + px) * 512 + 64 * kh;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float di, df, dcg, dout;
+        gate_bwd(dhv[n][e] + gpre[n][0][e], gpre[n][1 + e], gpre[n][5][e], gpre[n][6][e], dcr[n][e], di, df, dcg,
+                 dout);
+        const f32x4 z{di, df, dcg, dout};
+        bs[e] += z;
+        const int q = 4 * cq + e;   // 16-B chunk (4 rows) of the workgroup's 64 rows
+        *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(q, ip)) = z;
+        *reinterpret_cast<f32x4*>(zo + 4 * q) = z;
+      }
+    }
+    bias_flush(s - 1, bs);   // (its barrier also completes the image before the next dgrad)
+    AAA_B32_STAMP(it, 3);
+  }
+  // the final dc carry (dc_0) back to dC
+#pragma unroll
+  for (int n = 0; n < NG; ++n) {
+    const int px = (tid + 256 * n) >> 2;
+    if (px < P)
+      *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + px) * 128 + 16 * kh + 4 * cq) =
+          f32x4{dcr[n][0], dcr[n][1], dcr[n][2], dcr[n][3]};
+  }
+}
+
+inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st) {
+  if (!f32_rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0 ||
+      !p.part || !p.xp)
+    return hipErrorInvalidValue;
+  for (int c = 0; c < 128; ++c) {
+    const int pp = c < p.P ? c : p.P - 1;
+    p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
+  }
+  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>), f32_grid(p.B, 8), 256, p, st);
+}
+
+}  // namespace aaa

@@ -32,6 +32,7 @@
 #include "recur.h"
 #include "recur_bwd.h"
 #include "recur_f32.h"
+#include "recur_bwd_f32.h"
 #include "vision.h"
 #include "misc.h"
 #include "optim.h"
@@ -76,9 +77,9 @@ struct Layout {
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
-  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags, xpart;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
   // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
@@ -132,6 +133,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.k_WdTl = take(192 * 4608 * e);
   L.k_Wbf = take(e == 2 ? (size_t)6 * kBwKSP * 64 * 16 : 0);   // fragment-order [W_h^T | W_x^T] (frame-resident BPTT)
   L.k_Wf32 = take(e == 4 ? (size_t)16 * kF32QP * 64 * 16 : 0);   // fp32 fragment-order [x|h] (frame-group recurrence, recur_f32.h)
+  L.k_Wb32 = take(e == 4 ? (size_t)8 * kB32QP * 4 * 64 * 16 : 0);   // fp32 fragment-order W_h^T (frame-group BPTT, recur_bwd_f32.h)
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
   L.k_Wihp = take(1024 * 256 * 4);
@@ -174,6 +176,7 @@ static int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0) {
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
   L.rflags = take((size_t)8 * L.B * 4);   // hand-off flags of the multi-workgroup frame kernels ([B][G], G <= 8)
+  L.xpart = take(L.esz == 4 && rec_fits(L.h, L.w) ? b32_xpart_floats(L.B) * 4 : 0);   // fp32 frame-group BPTT exchange
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
@@ -704,6 +707,7 @@ static int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st
     HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
   } else {   // the fp32 frame-group recurrence's fragment order (recur_f32.h)
     HIPCHK(pack_wf32((const float*)(pk + L.k_WpXH), (float*)(pk + L.k_Wf32), st));
+    HIPCHK(pack_wb32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wb32), st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
@@ -1723,6 +1727,9 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
     const int fb = frames_bwd(L, g16);   // the whole chain in one frame-resident launch (workgroups per frame)
+    // fp32: the frame-group BPTT (recur_bwd_f32.h, G = 8) behind the forward's frame-group kernel
+    const bool fb32 = std::is_same<T, float>::value && f32_frames(L) == 8 && env_int("AAA_F32_FRAMES_BWD", 1);
+    if (fb32) part = nullptr;   // the kernel writes per-(step, frame) bias partials, step T-1's included
     if (fb) {
     } else if (g16)
       HIPCHK((gate_bwd_last<T, _Float16>(M, bj, Wf(L.dO) + (size_t)t1 * M * 128, io->dhT,
@@ -1770,7 +1777,22 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
         dx_fused = true;
       }
     }
-    for (int t = fb ? -1 : t1; t >= 0; --t) {
+    if (fb32) {
+      if constexpr (std::is_same<T, float>::value) {
+        HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)8 * L.B * 4, st));
+        int dev = 0;
+        HIPCHK(hipGetDevice(&dev));
+        int* rep = pair_report(dev);
+        if (!rep) return fail(AAA_E_LAUNCH, "cannot map the frame-group report word");
+        RecBwdF32Params rp{(const float*)(pk + L.k_Wb32), Wf(L.dO), Wf(L.Gt), Wf(L.Cst), Wf(L.dC), Wf(L.dZ),
+                           Wf(L.dZp), io->dh0, Wf(L.xpart), (int*)(ws + L.rflags), rep, (int)g_pair_spin,
+                           L.T, L.B, L.h, L.w, L.P, {}};
+        TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
+                       strf("fp32 frame-group BPTT (dh rows), %d steps per launch, 8 WG per frame", L.T));
+        HIPCHK(convlstm_bwd_f32(rp, st));
+      }
+    }
+    for (int t = (fb || fb32) ? -1 : t1; t >= 0; --t) {
       const int rc0 = flush(t);   // dz_t .. dz_{T-1} are final here
       if (rc0) return rc0;
       const bool prev = t > 0;
@@ -1872,6 +1894,8 @@ static int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStrea
     // gate-bias gradient: column sum of the per-(step, tile) partials, or of dZ itself
     if (fb)   // per (step, frame[, pixel half]) partials
       HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B * fb, 512, Wf(L.gbl), st));
+    else if (fb32)   // per (step, frame) partials
+      HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B, 512, Wf(L.gbl), st));
     else if (part) HIPCHK(colsum<float>(part, 512, L.T * ntj, 512, Wf(L.gbl), st));
     else HIPCHK(colsum<T>(Wt(L.dZ), 512, F * P, 512, Wf(L.gbl), st));
     if (io->dc0) HIPCHK(hipMemcpyAsync(io->dc0, Wf(L.dC), (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
