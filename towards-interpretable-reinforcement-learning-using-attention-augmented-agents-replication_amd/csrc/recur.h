@@ -35,8 +35,10 @@ constexpr int kRecKX = 36;
 constexpr int kRecPD = 4;           // A k steps in flight + 1 (register slots); divides 4 and 8
 constexpr int kRecKSP = kRecKS + kRecPD - 1;   // packed k steps per row block: the first PD-1 repeated at
                                                // the end, so the prefetch runs into the next step unwrapped
-constexpr int kRecNPH = 169;        // LDS image pixels: (h+2)*(w+2) <= 169 (11x11 grids: 84x84 frames)
-constexpr int kRecXB = 22 * 1024;   // x image bytes: 169 pixels x 128 B, whole 1-KB DMA pieces
+constexpr int kRecNPH = 169;        // whole-frame LDS images: (h+2)*(w+2) <= 169 (11x11 grids: 84x84 frames)
+constexpr int kRecNPHB = 184;       // image buffer pixels: also one band of <= 6 rows of a 21-wide grid + its halo rows
+constexpr int kRecXB = 23 * 1024;   // x image bytes: 184 pixels x 128 B (whole 1-KB DMA pieces)
+constexpr int kRecBands = 4;        // grid bands per frame in band mode (168x168 frames: 21 rows -> 5,5,5,6)
 constexpr int kRecHS = 136;         // h image pixel pitch (bf16): 128 + 8 pad (272 B = 17 x 16 B)
 constexpr int kRecStg = 4608;       // per-wave epilogue staging bytes (16 px x 272 B gates; c + h 2 x 16 x 144 B)
 constexpr int kSC1 = 16;            // buffer load / store cache policy: sc1 (cross-workgroup hand-off bytes)
@@ -70,6 +72,13 @@ inline hipError_t pack_wfrag(const __bf16* W, __bf16* Wf, hipStream_t st) {
 
 // Whether a grid runs on the frame-resident kernels.
 inline bool rec_fits(int h, int w) { return h * w <= 128 && (h + 2) * (w + 2) <= kRecNPH; }
+// Band mode: the grid split into kRecBands bands of whole rows, each band's
+// pixels (<= 128 columns) plus one halo row above and below in the LDS images.
+inline int rec_band_rows(int h, int k) { return (k + 1) * h / kRecBands - k * h / kRecBands; }
+inline bool rec_band_fits(int h, int w) {
+  const int rmax = (h + kRecBands - 1) / kRecBands;
+  return h >= kRecBands && rmax * w <= 128 && (rmax + 2) * (w + 2) <= kRecNPHB;
+}
 
 template <typename GT>
 struct RecFwdParams {
@@ -79,7 +88,7 @@ struct RecFwdParams {
   float* Cst;          // (T+1, B, P, 128): slot 0 = c_0 (read), slot t+1 <- c_t
   float* Hs;           // (T, B, P, 128) <- h_t (fp32)
   GT* Gt;              // (T, B, P, 512) <- gate activations (i, f, c~, o)
-  int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed)
+  int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed); band mode: [B][bands]
   int T, B, h, w, P;
   int* report;         // G = 2: partner-timeout report word (pinned host, device-mapped; pair_wait)
   int spin;            // G = 2: partner-wait bound in polls
@@ -155,34 +164,55 @@ inline void rec_columns(int h, int w, short* colpp, short* colhb) {
 // hides under the x-part GEMM, and no agent release / acquire fence is paid
 // (ABL bit 4 = the fenced hand-off, for A/B).  Launched as one residency wave
 // (launch_resident, co-residency checked), spins bounded and reported.
-template <typename GT, int G = 1, int ABL = 0>
+//
+// BAND (G = 1): 168x168 frames (21x21 grid) do not fit one workgroup's LDS,
+// so kRecBands workgroups split a frame by whole grid rows (5-6 rows = <= 126
+// pixel columns each) and all 512 gate rows.  A band's images hold its rows
+// plus one halo row above and below; per step each band publishes its h_t rows
+// (XH slot t+1, written anyway) with sc1 stores and a flag, and after its own
+// x-part reads the neighbours' boundary rows into its halo rows (sc1 loads),
+// like the G = 2 hand-off.  The bands of a frame get block indices of equal
+// residue mod 8 (one XCD under round-robin placement).
+template <typename GT, int G = 1, int ABL = 0, bool BAND = false>
 __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p) {
+  static_assert(!BAND || G == 1, "band mode splits pixels, not channels");
   constexpr int NRB = 4 / G, GCH = 8 * NRB;     // row blocks and channels per wave
   constexpr int GTP = GCH * 8 + 16, CHP = GCH * 4 + 16;   // staging pixel pitches (gates fp16x4, c / h fp32)
   __shared__ __attribute__((aligned(16))) unsigned char xim[kRecXB];
-  __shared__ __attribute__((aligned(16))) __bf16 him[kRecNPH * kRecHS];
+  __shared__ __attribute__((aligned(16))) __bf16 him[kRecNPHB * kRecHS];
   __shared__ __attribute__((aligned(16))) float cstl[4 * NRB * 16 * 64];   // c, lane-native: [wave][rb][cb][g][lane]
   __shared__ __attribute__((aligned(16))) float sbias[512];
   __shared__ __attribute__((aligned(16))) unsigned char stg[4 * 16 * (GTP > 2 * CHP ? GTP : 2 * CHP)];
   __shared__ short scol[128];   // column -> pixel (LDS: the epilogue's lookups stay off the vmcnt queue of the A stream)
   constexpr int STG = 16 * (GTP > 2 * CHP ? GTP : 2 * CHP);
-  const int b = (int)blockIdx.x % p.B, kh = G == 1 ? 0 : (int)blockIdx.x / p.B;
+  int b = (int)blockIdx.x % p.B;
+  const int kh = G == 1 ? 0 : (int)blockIdx.x / p.B;
+  int band = 0, r0 = 0, r1 = p.h;   // band mode: this workgroup's grid rows [r0, r1)
+  if constexpr (BAND) {
+    const int blk = (int)blockIdx.x, loc = blk >> 3;
+    b = (blk & 7) + 8 * (loc / kRecBands);
+    band = loc % kRecBands;
+    if (b >= p.B) return;   // padding group of the last XCD column
+    r0 = band * p.h / kRecBands;
+    r1 = (band + 1) * p.h / kRecBands;
+  }
   const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR) for the buffer soffsets
   const int r32 = lane & 31, hh = lane >> 5;
-  const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
+  const int P = p.P, W2 = p.w + 2, NPH = (r1 - r0 + 2) * W2;
+  const int Pb = (r1 - r0) * p.w, pix0 = r0 * p.w;   // the band's pixels (the whole frame without BAND)
   const size_t M = (size_t)p.B * P;
-  auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
+  auto hidx = [&](int pp) { return (pp / p.w - r0 + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
   const int rb0 = kh * (16 / G) + wave * NRB;   // the wave's first global row block (32 rows = 8 channels)
   const int cbase = 8 * rb0;                     // its first channel
   float* cw = cstl + wave * NRB * 16 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
 
   {  // zero the h image (its border stays zero), bias into LDS
     u32x4* z = reinterpret_cast<u32x4*>(him);
-    for (int i = tid; i < kRecNPH * kRecHS / 8; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < kRecNPHB * kRecHS / 8; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
     sbias[tid] = p.bias[tid];
     sbias[tid + 256] = p.bias[tid + 256];
-    if (tid < 128) scol[tid] = p.colpp[tid];
+    if (tid < 128) scol[tid] = BAND ? (short)(tid < Pb ? pix0 + tid : -1) : p.colpp[tid];
   }
   // x image of step t (XH slot t, channels 0..63) by LDS-DMA, border included:
   // image pixel ip holds its 8 16-B channel chunks at slots q ^ xswz(ip) (the
@@ -194,7 +224,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
     for (int i = wave; i < kRecXB / 1024; i += 4) {
       const int sl = i * 64 + lane, ip = sl >> 3, q = (sl & 7) ^ ((ip >> 1) & 7);
-      const int py = ip / W2 - 1, px = ip % W2 - 1;
+      const int py = r0 + ip / W2 - 1, px = ip % W2 - 1;
       const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
       dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB);
     }
@@ -207,14 +237,15 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int pp = p.colpp[cb * 32 + r32];
+        const int pp = BAND ? (cb * 32 + r32 < Pb ? pix0 + cb * 32 + r32 : -1) : p.colpp[cb * 32 + r32];
         cw[(rb * 16 + cb * 4 + g) * 64] =
             pp >= 0 ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
       }
   __syncthreads();   // h image zeroed
-  {  // h_0 (slot 0, channels 64..191) into the image
+  {  // h_0 (slot 0, channels 64..191) into the image (band mode: the band's rows and its halo rows)
     const __bf16* src = p.XH + (size_t)b * P * 192 + 64;
-    for (int i = tid; i < P * 16; i += 256)
+    const int hr0 = BAND ? max(r0 - 1, 0) : 0, hr1 = BAND ? min(r1 + 1, p.h) : p.h;
+    for (int i = hr0 * p.w * 16 + tid; i < hr1 * p.w * 16; i += 256)
       *reinterpret_cast<u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8) =
           *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 4) * 192 + (i & 15) * 8);
   }
@@ -223,7 +254,14 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   // window (columns >= P read pixel P-1: their outputs are never stored)
   int hb[4];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) hb[cb] = p.colhb[cb * 32 + r32];
+  for (int cb = 0; cb < 4; ++cb) {
+    if constexpr (BAND) {
+      const int pp = pix0 + min(cb * 32 + r32, Pb - 1);
+      hb[cb] = (pp / p.w - r0) * W2 + pp % p.w;
+    } else {
+      hb[cb] = p.colhb[cb * 32 + r32];
+    }
+  }
 
   // A stream: one buffer descriptor over the fragment-order weights, the lane's
   // 16 B at voffset lane*16, the (row block, k step) in the wave-uniform soffset
@@ -301,11 +339,32 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         kstep(kt + c4, c4 % PD, bfr[c4 & 1], [&] {
           if (c4 < 3) ldx(toff, c4 + 1, bfr[(c4 + 1) & 1]);
           else if (tap < 8) ldx(tn, 0, bfr[0]);
-          else if (G == 1) ldh(0, 0, bfr[0]);
+          else if (G == 1 && !BAND) ldh(0, 0, bfr[0]);
         });
     }
     barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
     if (t + 1 < p.T) dma_x(t + 1);
+    if constexpr (BAND) {
+      if (t > 0) {   // the neighbour bands' boundary rows of h_{t-1} (XH slot t) into the halo rows
+        if (tid == 0) {
+          if (band > 0) pair_wait(p.flags + b * kRecBands + band - 1, t, p.report, p.spin);
+          if (band < kRecBands - 1) pair_wait(p.flags + b * kRecBands + band + 1, t, p.report, p.spin);
+        }
+        barrier_lds();
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
+        const int nh = p.w * 16;   // 16-B pieces of one grid row
+        for (int i = tid; i < 2 * nh; i += 256) {
+          const int gy = i < nh ? r0 - 1 : r1, j = i < nh ? i : i - nh;
+          if ((unsigned)gy < (unsigned)p.h) {
+            const int pp = gy * p.w + (j >> 4);
+            *reinterpret_cast<u32x4*>(him + hidx(pp) * kRecHS + (j & 15) * 8) =
+                __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((pp * 192 + 64 + (j & 15) * 8) * 2), 0, kSC1);
+          }
+        }
+        barrier_lds();
+      }
+      ldh(0, 0, bfr[0]);
+    }
     if constexpr (G == 2) {
       if (t > 0) {   // the partner's half of h_{t-1} (XH slot t) into the image, once it has published it
         if (tid == 0) {
@@ -432,7 +491,18 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     // h_t (bf16, this workgroup's channels) into XH slot t+1 (the weight-gradient operand), from the image
     const size_t rown = rowt + M;   // slot t+1
     constexpr int HC = 16 / G;      // 16-B chunks (8 channels) per pixel of this workgroup
-    if constexpr (G == 1) {
+    if constexpr (BAND) {   // the neighbours read these rows: sc1 stores, then publish
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
+      for (int i = tid; i < Pb * HC; i += 256) {
+        const int px = pix0 + i / HC, q = i % HC;
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
+                                               (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, kSC1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();
+      if (tid == 0)
+        __hip_atomic_store(p.flags + b * kRecBands + band, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (G == 1) {
       for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
         const int px = i / HC, q = i % HC;
         *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
@@ -463,6 +533,14 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 // G = 1: one workgroup per frame; G = 2: two per frame in one residency wave
 // (launch_resident: p.flags zeroed by the caller; the launch fails rather than
 // strand a half; a partner wait that still times out is reported via p.report).
+template <typename GT>
+inline hipError_t convlstm_fwd_frames_band(RecFwdParams<GT>& p, hipStream_t st) {
+  if (!rec_band_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
+    return hipErrorInvalidValue;
+  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 1, 0, true>),
+                         8 * kRecBands * ((p.B + 7) / 8), 256, p, st);
+}
+
 template <typename GT>
 inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStream_t st) {
   if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (G != 1 && G != 2)) return hipErrorInvalidValue;

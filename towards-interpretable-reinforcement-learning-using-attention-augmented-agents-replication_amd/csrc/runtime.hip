@@ -830,6 +830,15 @@ static int frames_g(const Layout& L, const char* env) {
   return v == 1 ? 1 : (v == 2 && 2 * L.B <= cus ? 2 : 0);
 }
 static int frames_fwd(const Layout& L) { return frames_g(L, "AAA_FRAMES_FWD"); }
+// bf16 forward on the band-mode frame-resident kernel (recur.h BAND): grids too
+// large for one workgroup's images (168x168 frames: 21x21) split into kRecBands
+// row bands, one workgroup each, when B * kRecBands workgroups fit one
+// residency wave (config 5: B = 64 per GPU -> 256).  AAA_FRAMES_BAND = 0 keeps
+// the per-step launches.
+static int frames_band(const Layout& L) {
+  if (L.dt != AAA_BF16 || rec_fits(L.h, L.w) || !rec_band_fits(L.h, L.w) || !env_int("AAA_FRAMES_BAND", 1)) return 0;
+  return 8 * kRecBands * ((L.B + 7) / 8) <= device_cus() ? kRecBands : 0;
+}
 // fp32 ConvLSTM forward on the frame-group kernel (recur_f32.h): G workgroups
 // per frame for all T steps, once B * G fills at least half the CUs in one
 // residency wave (C2: B = 32, G = 8 on 256 CUs).  AAA_F32_FRAMES = 0 keeps the
@@ -898,6 +907,21 @@ static int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     auto steps = [&](auto gtag) -> int {
       using GT = decltype(gtag);
       if constexpr (!std::is_same<T, float>::value) {
+        if (const int NBd = frames_band(L)) {   // one band-mode launch for all T steps (recur.h BAND)
+          HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)NBd * L.B * 4, st));
+          int dev = 0;
+          HIPCHK(hipGetDevice(&dev));
+          int* rep = pair_report(dev);
+          if (!rep) return fail(AAA_E_LAUNCH, "cannot map the band-mode report word");
+          RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
+                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
+                              rep, (int)g_pair_spin};
+          TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
+                         strf("bf16 band-mode frame-resident [x|h] recurrence, %d steps per launch, %d bands per frame",
+                              L.T, NBd));
+          HIPCHK(convlstm_fwd_frames_band<GT>(rp, st));
+          return AAA_OK;
+        }
         if (const int G = frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
           int* rep = nullptr;
           if (G == 2) {
