@@ -1,6 +1,7 @@
-"""Band-mode frame-resident bf16 ConvLSTM forward (csrc/recur.h BAND): 168x168
-frames (21x21 grid, config 5) split into four row bands, one workgroup each,
-exchanging their boundary rows of h_t through L2 every step.
+"""Band-mode frame-resident bf16 ConvLSTM forward (csrc/recur.h BAND) and BPTT
+(csrc/recur_bwd.h BAND): 168x168 frames (21x21 grid, config 5) split into four
+row bands, one workgroup each, exchanging their boundary rows of h_t (forward)
+or dZ_t (BPTT) through L2 every step.
 
 Against the bf16-emulated oracle (2e-2) and against the
 per-step launches it replaces (AAA_FRAMES_BAND=0: same bf16 operands and fp32
@@ -25,9 +26,14 @@ def _run(cuda, monkeypatch, band, T, B, nq=8):
     try:
         out = _run_unroll(_agent(cuda, nq=nq, grid=(21, 21), conv_dtype="bf16"), T, B, cuda, H=168, W=168)
         var = N.timing_stats(N.TIMER_FWD_STEP)["variant"]
+        sb = N.timing_stats(N.TIMER_BPTT_STEP)
     finally:
         N.timing_enable(False)
     assert ("band-mode" in var) == (band == "1"), var
+    if band == "1":   # one band-mode BPTT launch for the whole chain
+        assert sb["launches"] == 1 and "band-mode" in sb["variant"], sb
+    else:             # per-step launches (none at T = 1: no dh of an earlier step)
+        assert "band-mode" not in sb["variant"], sb
     return out
 
 

@@ -115,3 +115,16 @@ def test_reinforce_loss_has_no_cpu_fallback():
     from aaa_amd.reinforce import reinforce_loss
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         reinforce_loss(torch.zeros(3, 1, 18), [0, 1, 2], [1.0, 0.0, 1.0])
+
+
+def test_actor_layout_refuses_readout_lds_overflow():
+    """The actor chain's readout kernel keeps a frame's P x nq logits in LDS
+    (csrc/actor.h actor_attn_lds): a grid whose readout exceeds the LDS is
+    refused by the layout query (GraphActor then takes the learner's T=1
+    forward) instead of failing at launch."""
+    lib = N.load()
+    small = N.Cfg(1, 1, 210, 160, 8, 18, N.F32, N.FLAG_FRAMES_U8)
+    big = N.Cfg(1, 1, 506, 506, 8, 18, N.F32, N.FLAG_FRAMES_U8)   # 64x64 grid: 4096 x 8 logits
+    assert N.grid(506, 506) == (64, 64)
+    assert lib.aaa_actor_workspace_bytes(ctypes.byref(small)) > 0
+    assert lib.aaa_actor_workspace_bytes(ctypes.byref(big)) == 0

@@ -40,4 +40,11 @@ struct ActorParams {
 
 hipError_t actor_launch(const ActorParams& p, hipStream_t st);
 
+// Dynamic LDS of the attention-readout launch (k_act_attn): the logits of all P
+// positions x nq queries, the queries, the readout's partial sums, the answer
+// row.  Above 64 KB the launch raises the kernel's limit; above kActLdsMax the
+// chain does not apply (actor_layout refuses it: such grids use aaa_forward).
+constexpr size_t kActLdsMax = 160 * 1024;
+size_t actor_attn_lds(int P, int nq, int ans_ld);
+
 }  // namespace aaa

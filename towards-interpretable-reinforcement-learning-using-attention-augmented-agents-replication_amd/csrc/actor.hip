@@ -427,15 +427,25 @@ __global__ void __launch_bounds__(256) k_act_heads(ActorParams p) {
 
 }  // namespace
 
+size_t actor_attn_lds(int P, int nq, int ans_ld) {
+  return sizeof(float) * ((size_t)P * nq + (size_t)nq * 72 + (size_t)kActAttnSlices * nq * 184 + ans_ld);
+}
+
 hipError_t actor_launch(const ActorParams& p, hipStream_t st) {
   if (p.B < 1 || p.B > 16 || (p.nq != 4 && p.nq != 8) || p.A < 1 || p.A > 256) return hipErrorInvalidValue;
+  const size_t lds = actor_attn_lds(p.P, p.nq, p.ans_ld);
+  if (lds > kActLdsMax) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: raise it for this launch's kernel
+    const void* k = p.nq == 4 ? reinterpret_cast<const void*>(&k_act_attn<4>) : reinterpret_cast<const void*>(&k_act_attn<8>);
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (p.u8)
     hipLaunchKernelGGL(k_act_vision<uint8_t>, dim3(p.P, p.B), dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(k_act_vision<float>, dim3(p.P, p.B), dim3(256), 0, st, p);
   const int npg = (p.P + 15) / 16;
   hipLaunchKernelGGL(k_act_convlstm, dim3(32 * npg, p.B), dim3(512), 0, st, p, npg);
-  const size_t lds = sizeof(float) * ((size_t)p.P * p.nq + p.nq * 72 + kActAttnSlices * p.nq * 184 + p.ans_ld);
   if (p.nq == 4)
     hipLaunchKernelGGL(k_act_attn<4>, dim3(128, p.B), dim3(256), lds, st, p);
   else

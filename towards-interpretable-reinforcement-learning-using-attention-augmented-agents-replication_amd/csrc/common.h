@@ -99,6 +99,18 @@ __device__ __forceinline__ void pair_wait(const int* flag, int target, int* repo
   }
 }
 
+// Start-time offset of half the frames of a frame-resident kernel: a wave
+// waits ``ticks`` of the 100-MHz real-time counter.  All frames of such a
+// kernel run their steps in lock step, so their epilogues' HBM traffic comes in
+// one chip-wide burst per step while the memory system idles under the GEMMs;
+// offsetting half of them by about half a step interleaves the bursts with
+// the other half's GEMMs.
+__device__ __forceinline__ void stagger_wait(int ticks) {
+  if (ticks <= 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 // Launch a paired kernel (two cooperating workgroups per frame) as an ordinary
 // dispatch whose whole grid fits one residency wave of the device: every
 // workgroup is placed at once on an idle chip, and the bounded partner waits

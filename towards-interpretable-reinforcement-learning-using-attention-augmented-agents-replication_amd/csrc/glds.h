@@ -44,6 +44,10 @@ __device__ __forceinline__ int lds_swz(int row) {
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff, int soff = 0) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, soff, 0, 0);
 }
+// the same with the sc1 cache policy (bytes another workgroup published with sc1 stores)
+__device__ __forceinline__ void dma16_sc1(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, 0, 0, 16);
+}
 
 // Epilogues with a split prefetch()/finish() (EP::Pre) have their global
 // inputs loaded before the K loop, so the loads' latency hides under it.

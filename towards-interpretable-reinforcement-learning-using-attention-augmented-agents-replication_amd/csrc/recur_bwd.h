@@ -34,8 +34,6 @@ constexpr int kBwKS = 4608 / 16;   // k steps: 4 chunks x 9 taps x 8 groups of 1
 constexpr int kBwPD = 4;           // A register slots (PD-1 k steps in flight); divides 8
 constexpr int kBwPD2 = 8;          // the paired kernel's (3 MFMAs per k step: twice the k steps in flight)
 constexpr int kBwKSP = kBwKS + kBwPD2 - 1;   // packed k steps per row block: the first PD2-1 repeated at the end
-constexpr int kBwIP = 136;         // chunk image pixel pitch (bf16): 128 rows + 8 pad (272 B)
-constexpr int kBwIB = 46080;       // chunk image bytes: 169 px x 272 B rounded up to whole 1-KB DMA pieces
 
 // k step ks -> k of the dgrad GEMM (k = tap*512 + gate row)
 __host__ __device__ constexpr int bw_k(int ks) { return ((ks % 72) >> 3) * 512 + (ks / 72) * 128 + (ks & 7) * 16; }
@@ -43,7 +41,7 @@ __host__ __device__ constexpr int bw_k(int ks) { return ((ks % 72) >> 3) * 512 +
 // Wb[((rb*kBwKSP + ks)*64 + lane)*8 + e] = W[row(rb, lane%32)][bw_k(ks % kBwKS) + (lane/32)*8 + e], W = the
 // packed dgrad weights [192][4608] (k_WdTl: rows 0..63 x channels, 64..191 h channels); row blocks 0..3 =
 // the h rows (the BPTT GEMM proper), 4..5 = the x rows (dx: conv2's output gradient, fused in the same pass)
-__global__ void __launch_bounds__(256) k_pack_wbfrag(const __bf16* __restrict__ W, __bf16* __restrict__ Wb) {
+static __global__ void __launch_bounds__(256) k_pack_wbfrag(const __bf16* __restrict__ W, __bf16* __restrict__ Wb) {
   const int c = blockIdx.x * 256 + (int)threadIdx.x;
   if (c >= 6 * kBwKSP * 64) return;
   const int lane = c & 63, rk = c >> 6, ks = rk % kBwKSP, rb = rk / kBwKSP;
@@ -85,44 +83,81 @@ struct RecBwdParams {
   int T, B, h, w, P;
   int* report;            // paired kernel: partner-timeout report word (pinned host, device-mapped; pair_wait)
   int spin;               // paired kernel: partner-wait bound in polls
+  int stagger;            // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
 };
+
+// Chunk images of the single-workgroup and band kernels: image pixel ip (a
+// (rows+2) x (w+2) zero-bordered grid) holds its 16 row groups of 8 bf16 at
+// 16-B slots s ^ bw_fz(ip) of a 256-B row, bw_fz = the pixel's index with the
+// two border columns of every image row skipped (mod 16).  A B-fragment read
+// of 16 consecutive GEMM columns (pixels in raster order, any tap) then covers
+// 16 consecutive bw_fz values across grid-row ends: each ds_read_b128 lane
+// group (MI355X_MICROARCH: 4 x 16 lanes) hits 16 distinct bank groups.  (A
+// 272-B pitch instead puts pixel ip at slot ip mod 16 and collides where a
+// column group crosses a row end: 0.53 conflicts per LDS access at C3.)
+__device__ __forceinline__ int bw_fz(int ip, int W2) { return (ip - 2 * (ip / W2)) & 15; }
+constexpr int kBwIBS = 47104;   // swizzled chunk image bytes: 184 px x 256 B (46 whole 1-KB DMA pieces)
 
 // ABL (diagnostic A/B only: AAA_RECB_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA.
-template <int ABL = 0>
+//
+// BAND: 21x21 grids (168x168 frames) do not fit one workgroup's images, so
+// kRecBands workgroups split a frame by whole grid rows (recur.h band mode:
+// 5-6 rows = <= 126 GEMM columns each, all 128 h rows and the 64 dx rows).
+// A band's images hold its rows plus one halo row above and below.  Each step
+// the band stores dZ_s with sc1 stores and publishes a count; before the GEMM
+// over dZ_t it waits for its neighbours' counts and reads their boundary rows
+// of chunks 0 and 1 (its own are in the images, written by its epilogue) with
+// sc1 loads into the halo rows; chunks 2 and 3 come whole, halo rows included,
+// by LDS-DMA with the sc1 policy.  The bands of a frame get block indices of
+// equal residue mod 8 (one XCD under round-robin placement).
+template <int ABL = 0, bool BAND = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (0: chunks 0, 2; 1: 1, 3)
-  __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];         // dc carry, lane-native [wave][g*4+cb][lane]
-  const int b = blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBS];   // chunk images (0: chunks 0, 2; 1: 1, 3)
+  __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];          // dc carry, lane-native [wave][g*4+cb][lane]
+  int b = (int)blockIdx.x, band = 0, r0 = 0, r1 = p.h;   // band mode: this workgroup's grid rows [r0, r1)
+  if constexpr (BAND) {
+    const int blk = (int)blockIdx.x, loc = blk >> 3;
+    b = (blk & 7) + 8 * (loc / kRecBands);
+    band = loc % kRecBands;
+    if (b >= p.B) return;   // padding group of the last XCD column
+    r0 = band * p.h / kRecBands;
+    r1 = (band + 1) * p.h / kRecBands;
+  }
+  const int tid = (int)threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
-  const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
+  const int P = p.P, W2 = p.w + 2, NPH = (r1 - r0 + 2) * W2;
+  const int Pb = (r1 - r0) * p.w, pix0 = r0 * p.w;   // the band's pixels (the whole frame without BAND)
   const size_t M = (size_t)p.B * P;
-  auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
+  auto hidx = [&](int pp) { return (pp / p.w - r0 + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
 
   {  // zero the images (borders and pads stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < 2 * kBwIB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < 2 * kBwIBS / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
-  // chunk c (rows 128c .. 128c+127) of dZ_t from HBM into image c & 1: 16-B
-  // slot s of the image = pixel s / 17, row group s % 17 (16 = pad); borders,
-  // pads and the tail read outside the descriptor and land as zeros
+  // chunk c (rows 128c .. 128c+127) of dZ_t from HBM into image c & 1, whole
+  // 1-KB pieces of 4 image pixels; borders and the tail read outside the
+  // descriptor and land as zeros
   auto dma_chunk = [&](int t, int c) {
     const __amdgpu_buffer_rsrc_t rs =
         make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
-    for (int i = wave; i < kBwIB / 1024; i += 4) {
-      const int sl = i * 64 + lane, ip = sl / 17, q = sl - ip * 17;
-      const int py = ip / W2 - 1, px = ip % W2 - 1;
-      const bool v = q < 16 && ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
-      dma16(rs, zim + (c & 1) * kBwIB + i * 1024, v ? (uint32_t)(((py * p.w + px) * 512 + 128 * c + q * 8) * 2) : kOOB);
+    for (int i = wave; i < (NPH + 3) >> 2; i += 4) {
+      const int sl = i * 64 + lane, ip = sl >> 4, iy = ip / W2, ix = ip - iy * W2;
+      const int py = r0 + iy - 1, px = ix - 1, lq = (sl & 15) ^ ((ip - 2 * iy) & 15);
+      const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
+      const uint32_t vo = v ? (uint32_t)(((py * p.w + px) * 512 + 128 * c + lq * 8) * 2) : kOOB;
+      if constexpr (BAND) dma16_sc1(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
+      else dma16(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
     }
   };
 
-  int hb[4];
+  int hb[4], fb[4];   // per column block: top-left image pixel of the lane's window, and its bw_fz (= the column)
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
-    const int pp = min(cb * 32 + r32, P - 1);
-    hb[cb] = (pp / p.w) * W2 + pp % p.w;
+    const int col = min(cb * 32 + r32, Pb - 1), pp = pix0 + col;   // columns >= Pb read column Pb-1: never stored
+    hb[cb] = (pp / p.w - r0) * W2 + pp % p.w;
+    fb[cb] = col;
   }
   // dc carry of the lane's 64 (channel, pixel) pairs: channels 32w + 8g + 4hh + e at pixel 32cb + r32
   f32x4* dcw = dcl + wave * 16 * 64 + lane;   // + (g*4 + cb) * 64
@@ -130,10 +165,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-      const int pp = cb * 32 + r32;
+      const int col = cb * 32 + r32;
       dcw[(g * 4 + cb) * 64] =
-          pp < P ? *reinterpret_cast<const f32x4*>(p.dC + ((size_t)b * P + pp) * 128 + 32 * wave + 8 * g + 4 * hh)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
+          col < Pb ? *reinterpret_cast<const f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
   // A stream: per k step the wave's h row block (wave) and its dx row block (4 + wave % 2)
@@ -164,9 +199,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   constexpr int kRing = 4;
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
-    const int g = u >> 2, cb = u & 3, pp = cb * 32 + (ln & 31);
-    if (pp < P && !(ABL & 2)) {
-      const size_t row = (size_t)s * M + (size_t)b * P + pp;
+    const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
+    if (col < Pb && !(ABL & 2)) {
+      const size_t row = (size_t)s * M + (size_t)b * P + pix0 + col;
       const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
       in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
       in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
@@ -183,13 +218,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   // Gate backward of step s on the GEMM result (acc = dh_s from step s+1, zero
   // for s = T-1): dZ_s to HBM (bf16) and, for chunks 0 and 1, into image w; the
   // lane's dc carry advances to step s-1; gate-bias partials of step s.
-  // ``ring``: units 0 .. kRing-2 already requested.
+  // ``ring``: units 0 .. kRing-2 already requested.  BAND: then publishes dZ_s.
   auto epilogue = [&](int s, const f32x16 (&acc)[4], bool gemm, EpIn (&ring)[kRing]) {
     int ln = lane;   // laundered: the epilogue's addresses are recomputed per step, not hoisted
     asm volatile("" : "+v"(ln));
     const int pl = ln & 31, hq = ln >> 5;
     const int c0 = 32 * wave + 4 * hq;   // + 8g + e
     const size_t rows = (size_t)s * M + (size_t)b * P;
+    const __amdgpu_buffer_rsrc_t rz = make_rsrc(p.dZ + rows * 512, (uint32_t)(P * 512 * 2));
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       float bs[16];   // [e][gate] sums over the lane's pixels (this channel group)
@@ -201,9 +237,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int u = g * 4 + cb;
         if (u + kRing - 1 < 16) ring[(u + kRing - 1) % kRing] = load_in(s, u + kRing - 1, ln);
         const EpIn& in = ring[u % kRing];
-        const int pp = cb * 32 + pl;
-        if (pp < P) {
-          const size_t row = rows + pp;
+        const int col = cb * 32 + pl;
+        if (col < Pb) {
+          const int pp = pix0 + col;
           f32x4 dh = in.dO;
           if (gemm) {
             dh[0] += acc[cb][4 * g]; dh[1] += acc[cb][4 * g + 1]; dh[2] += acc[cb][4 * g + 2]; dh[3] += acc[cb][4 * g + 3];
@@ -230,15 +266,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           bf16x8 z0, z1;
 #pragma unroll
           for (int i = 0; i < 8; ++i) { z0[i] = (__bf16)dz[i]; z1[i] = (__bf16)dz[8 + i]; }
-          __bf16* zo = p.dZ + row * 512 + 4 * ch;
           if constexpr (!(ABL & 2)) {
-            *reinterpret_cast<bf16x8*>(zo) = z0;
-            *reinterpret_cast<bf16x8*>(zo + 8) = z1;
+            const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, BAND ? kSC1 : 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, BAND ? kSC1 : 0);
           }
-          if (wave < 2) {   // chunk w of the next step's B operand, rows 4(ch - 32w) + gate
-            unsigned char* zi = zim + wave * kBwIB + hidx(pp) * (kBwIP * 2) + (4 * (ch - 32 * wave)) * 2;
-            *reinterpret_cast<bf16x8*>(zi) = z0;
-            *reinterpret_cast<bf16x8*>(zi + 16) = z1;
+          if (wave < 2) {   // chunk w of the next step's B operand: rows 4(ch - 32w) + gate = slots 4g + 2hq, +1
+            unsigned char* zi = zim + wave * kBwIBS + hidx(pp) * 256;
+            const int fz = (col + p.w + 1) & 15, s0 = 4 * g + 2 * hq;
+            *reinterpret_cast<bf16x8*>(zi + ((s0 ^ fz) << 4)) = z0;
+            *reinterpret_cast<bf16x8*>(zi + (((s0 + 1) ^ fz) << 4)) = z1;
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -262,11 +299,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       bs[0] += __shfl_xor(bs[0], 1, 64);
       const int ridx = ((pl & 16) ? 8 : 0) + ((pl & 8) ? 4 : 0) + ((pl & 4) ? 2 : 0) + ((pl & 2) ? 1 : 0);
-      if ((pl & 1) == 0)   // row ridx = 4e + gate of channel ch + e
-        p.part[((size_t)s * p.B + b) * 512 + 4 * (ch + (ridx >> 2)) + (ridx & 3)] = bs[0];
+      if ((pl & 1) == 0)   // row ridx = 4e + gate of channel ch + e; band mode: a row of partials per band
+        p.part[(((size_t)s * p.B + b) * (BAND ? kRecBands : 1) + band) * 512 + 4 * (ch + (ridx >> 2)) + (ridx & 3)] =
+            bs[0];
+    }
+    if constexpr (BAND) {   // publish dZ_s: every wave's sc1 stores retired, a barrier, one lane's flag store
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      barrier_lds();
+      if (tid == 0) __hip_atomic_store(p.flags + b * kRecBands + band, p.T - s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
 
+  if ((b >> 3) & 1) stagger_wait(p.stagger);
   {  // step T-1: no GEMM (dh = dO_{T-1} + dhT)
     f32x16 zero[4];
     EpIn ring[kRing];
@@ -277,6 +321,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   barrier_lds();   // chunk images 0, 1 of dZ_{T-1}
 
   for (int t = p.T - 1; t >= 0; --t) {
+    if constexpr (BAND) {   // the neighbours' boundary rows of dZ_t, chunks 0 and 1, into the halo rows
+      if (tid == 0) {
+        if (band > 0) pair_wait(p.flags + b * kRecBands + band - 1, p.T - t, p.report, p.spin);
+        if (band < kRecBands - 1) pair_wait(p.flags + b * kRecBands + band + 1, p.T - t, p.report, p.spin);
+      }
+      barrier_lds();
+      const __amdgpu_buffer_rsrc_t rs =
+          make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
+      const int nh = p.w * 16;   // 16-B pieces of one grid row of one chunk
+      constexpr int NHL = 6;     // pieces per thread in flight
+      for (int i0 = 0; i0 < 4 * nh; i0 += 256 * NHL) {
+        u32x4 v[NHL];
+#pragma unroll
+        for (int r = 0; r < NHL; ++r) {   // piece i: (side, chunk) = i / nh, pixel (i % nh) / 16, slot i % 16
+          const int i = i0 + tid + 256 * r, k = i / nh, j = i - k * nh;
+          const int gy = (k >> 1) ? r1 : r0 - 1;
+          const bool ok = i < 4 * nh && (unsigned)gy < (unsigned)p.h;
+          v[r] = __builtin_amdgcn_raw_buffer_load_b128(
+              rs, ok ? (uint32_t)(((gy * p.w + (j >> 4)) * 512 + 128 * (k & 1) + (j & 15) * 8) * 2) : kOOB, 0, kSC1);
+        }
+#pragma unroll
+        for (int r = 0; r < NHL; ++r) {
+          const int i = i0 + tid + 256 * r, k = i / nh, j = i - k * nh;
+          const int gy = (k >> 1) ? r1 : r0 - 1, iy = (k >> 1) ? r1 - r0 + 1 : 0, gx = j >> 4;
+          if (i < 4 * nh && (unsigned)gy < (unsigned)p.h) {
+            const int ip = iy * W2 + gx + 1, fz = (iy * p.w + gx + 1) & 15;
+            *reinterpret_cast<u32x4*>(zim + (k & 1) * kBwIBS + ip * 256 + (((j & 15) ^ fz) << 4)) = v[r];
+          }
+        }
+      }
+      barrier_lds();
+    }
     f32x16 acc[4], accx[2];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
@@ -286,18 +362,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) accx[j][e] = 0.f;
-    int hbs[4];
+    int hbs[4], fbs[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       hbs[cb] = hb[cb];
-      asm volatile("" : "+v"(hbs[cb]));
+      fbs[cb] = fb[cb];
+      asm volatile("" : "+v"(hbs[cb]), "+v"(fbs[cb]));
     }
-    // transposed gather: output pixel q reads dZ at q - d(tap): image offset (2-ky)*W2 + (2-kx)
-    auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + (2 - tap % 3); };
-    auto ldb = [&](const unsigned char* img, int toff, int c16, bf16x8 (&bf)[4]) {
+    // transposed gather: output pixel q reads dZ at q - d(tap): image offset (2-ky)*W2 + (2-kx),
+    // bw_fz offset (2-ky)*w + (2-kx).  Per tap and column block: the byte address of the
+    // lane's pixel row or'ed with its swizzled slot for c16 = 0; row group c16 xors in c16 << 5.
+    auto bases = [&](int tap, int (&tb)[4]) {
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const int toff = (2 - ky) * W2 + (2 - kx), tf = (2 - ky) * p.w + (2 - kx);
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        bf[cb] = *reinterpret_cast<const bf16x8*>(img + (hbs[cb] + toff) * (kBwIP * 2) + c16 * 32 + hh * 16);
+      for (int cb = 0; cb < 4; ++cb) tb[cb] = ((hbs[cb] + toff) << 8) | (((((fbs[cb] + tf) & 15) ^ hh)) << 4);
+    };
+    auto ldb = [&](const unsigned char* img, const int (&tb)[4], int c16, bf16x8 (&bf)[4]) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(img + (tb[cb] ^ (c16 << 5)));
     };
     constexpr int BD = 4;   // B fragment ring: BD-1 k steps of lookahead (LDS latency vs 4 MFMAs per k step)
     bf16x8 bfr[BD][4];
@@ -308,7 +391,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       constexpr int XC = decltype(xc)::value;
   #pragma unroll 1
       for (int ck = 0; ck < 4; ++ck) {
-        const unsigned char* img = zim + (ck & 1) * kBwIB;
+        const unsigned char* img = zim + (ck & 1) * kBwIBS;
         if (ck == 1 || ck == 2) {   // every wave is done with image ck-1 and every wave's dZ_t stores have
                                     // retired (its later A loads did): refill it with chunk ck+1 from HBM
           if constexpr (!(ABL & 8)) dma_chunk(t, ck + 1);
@@ -319,10 +402,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   #pragma unroll
           for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(t - 1, u, ln);
         }
+        int tcur[4], tnxt[4];
+        bases(0, tcur);
   #pragma unroll
-        for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
+        for (int j = 0; j < BD - 1; ++j) ldb(img, tcur, j, bfr[j]);
         for (int tap = 0; tap < 9; ++tap) {
-          const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+          if (tap < 8) bases(tap + 1, tnxt);
           int kt = ck * 72 + tap * 8;
           asm volatile("" : "+s"(kt));
   #pragma unroll
@@ -333,8 +418,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             {  // B of k step + BD - 1 (same chunk)
               const int cn = c16 + BD - 1;
-              if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
-              else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
+              if (cn < 8) ldb(img, tcur, cn, bfr[cn % BD]);
+              else if (tap < 8) ldb(img, tnxt, cn - 8, bfr[cn % BD]);
             }
             __builtin_amdgcn_sched_barrier(0);
   #pragma unroll
@@ -350,6 +435,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             __builtin_amdgcn_sched_barrier(0);
           }
+  #pragma unroll
+          for (int cb = 0; cb < 4; ++cb) tcur[cb] = tnxt[cb];
         }
         barrier_lds();   // image ck & 1 free; (ck >= 1) the DMA'd chunk ck+1 has landed in every wave
       }
@@ -360,12 +447,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const size_t rows = (size_t)t * M + (size_t)b * P;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int pp = (xcb + j) * 32 + r32;
+        const int col = (xcb + j) * 32 + r32;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float v[4] = {accx[j][4 * g], accx[j][4 * g + 1], accx[j][4 * g + 2], accx[j][4 * g + 3]};
-          if (pp < P) {
-            *reinterpret_cast<bf16x4*>(p.dY2 + (rows + pp) * 64 + 32 * (wave & 1) + 8 * g + 4 * hh) =
+          if (col < Pb) {
+            *reinterpret_cast<bf16x4*>(p.dY2 + (rows + pix0 + col) * 64 + 32 * (wave & 1) + 8 * g + 4 * hh) =
                 bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
 #pragma unroll
             for (int e = 0; e < 4; ++e) xbs[4 * g + e] += v[e];
@@ -378,11 +465,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     } else if (p.dh0) {   // dh_{-1}: the gradient of the initial state h0
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const int pp = cb * 32 + r32;
-        if (pp < P)
+        const int col = cb * 32 + r32;
+        if (col < Pb)
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + pp) * 128 + 32 * wave + 8 * g + 4 * hh) =
+            *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh) =
                 f32x4{acc[cb][4 * g], acc[cb][4 * g + 1], acc[cb][4 * g + 2], acc[cb][4 * g + 3]};
       }
     }
@@ -408,7 +495,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     v[0] += __shfl_xor(v[0], 1, 64);   // lanes r32 and r32 ^ 1 now both hold row ridx's total
     const int ridx = ((r32 & 16) ? 8 : 0) + ((r32 & 8) ? 4 : 0) + ((r32 & 4) ? 2 : 0) + ((r32 & 2) ? 1 : 0);
-    if ((r32 & 1) == 0) {   // row ridx = 4g + e: x channel 32(w%2) + 8g + 4hh + e; two waves share each channel set
+    if ((r32 & 1) == 0) {   // row ridx = 4g + e: x channel 32(w%2) + 8g + 4hh + e; two waves (and the bands) share each
       const int g = ridx >> 2, e = ridx & 3;
       atomicAdd(p.dxb + (size_t)b * 64 + 32 * (wave & 1) + 8 * g + 4 * hh + e, v[0]);
     }
@@ -418,9 +505,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   for (int g = 0; g < 4; ++g)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-      const int pp = cb * 32 + r32;
-      if (pp < P)
-        *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pp) * 128 + 32 * wave + 8 * g + 4 * hh) = dcw[(g * 4 + cb) * 64];
+      const int col = cb * 32 + r32;
+      if (col < Pb)
+        *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh) =
+            dcw[(g * 4 + cb) * 64];
     }
 }
 
@@ -440,7 +528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 // Launched as one residency wave (launch_resident); the spins are bounded and reported.
 template <int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_pairs(RecBwdParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (c & 1)
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBS];   // chunk images (c & 1), bw_fz-swizzled
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 8 * 64];          // dc carry, lane-native [wave][g*2+j][lane]
   const int b = (int)blockIdx.x % p.B, kh = (int)blockIdx.x / p.B;
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -454,7 +542,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 
   {  // zero the images (borders and pads stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < 2 * kBwIB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < 2 * kBwIBS / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   // the partner's chunk c of dZ_t: sc1 loads of the P x 256 B into registers
   // (issued at the start of a chunk), then into image c & 1 (three taps later)
@@ -473,15 +561,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
     for (int r = 0; r < NPR; ++r) {
       const int i = tid + 256 * r, px = i >> 4, q = i & 15;
-      if (px < P) *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIB + hidx(px) * (kBwIP * 2) + q * 16) = v[r];
+      if (px < P)
+        *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIBS + hidx(px) * 256 + ((q ^ ((px + p.w + 1) & 15)) << 4)) = v[r];
     }
   };
 
-  int hb[2];
+  int hb[2], fb[2];   // top-left image pixel of the lane's window per column block, and its bw_fz (= the pixel)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int pp = min((cbA + j) * 32 + r32, P - 1);
     hb[j] = (pp / p.w) * W2 + pp % p.w;
+    fb[j] = pp;
   }
   // dc carry of the lane's 32 (channel, pixel) pairs: channels 32hrb + 8g + 4hh + e at pixel 32(cbA+j) + r32
   f32x4* dcw = dcl + wave * 8 * 64 + lane;   // + (g*2 + j) * 64
@@ -583,9 +673,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, kSC1);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, kSC1);
-          unsigned char* zi = zim + (wave & 1) * kBwIB + hidx(pp) * (kBwIP * 2) + (4 * (ch - 32 * hrb)) * 2;
-          *reinterpret_cast<bf16x8*>(zi) = z0;
-          *reinterpret_cast<bf16x8*>(zi + 16) = z1;
+          unsigned char* zi = zim + (wave & 1) * kBwIBS + hidx(pp) * 256;
+          const int fz = (pp + p.w + 1) & 15, s0 = 4 * g + 2 * hq;   // rows 4(ch - 32 hrb) + gate
+          *reinterpret_cast<bf16x8*>(zi + ((s0 ^ fz) << 4)) = z0;
+          *reinterpret_cast<bf16x8*>(zi + (((s0 + 1) ^ fz) << 4)) = z1;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -613,6 +704,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (tid == 0) __hip_atomic_store(p.flags + 2 * b + kh, p.T - s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
 
+  if ((b >> 3) & 1) stagger_wait(p.stagger);
   {  // step T-1: no GEMM
     f32x16 zero[2];
     EpIn ring[kRing];
@@ -629,17 +721,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) accx[e] = 0.f;
-    int hbs[2];
+    int hbs[2], fbs[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       hbs[j] = hb[j];
-      asm volatile("" : "+v"(hbs[j]));
+      fbs[j] = fb[j];
+      asm volatile("" : "+v"(hbs[j]), "+v"(fbs[j]));
     }
-    auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + (2 - tap % 3); };
-    auto ldb = [&](const unsigned char* img, int toff, int c16, bf16x8 (&bf)[2]) {
+    auto bases = [&](int tap, int (&tb)[2]) {   // as the single-workgroup kernel's
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      const int toff = (2 - ky) * W2 + (2 - kx), tf = (2 - ky) * p.w + (2 - kx);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bf[j] = *reinterpret_cast<const bf16x8*>(img + (hbs[j] + toff) * (kBwIP * 2) + c16 * 32 + hh * 16);
+      for (int j = 0; j < 2; ++j) tb[j] = ((hbs[j] + toff) << 8) | (((((fbs[j] + tf) & 15) ^ hh)) << 4);
+    };
+    auto ldb = [&](const unsigned char* img, const int (&tb)[2], int c16, bf16x8 (&bf)[2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(img + (tb[j] ^ (c16 << 5)));
     };
     constexpr int BD = 4;
     bf16x8 bfr[BD][2];
@@ -649,7 +746,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll 1
       for (int ck = 0; ck < 4; ++ck) {
         const int c = (ck + 2 * kh) & 3;   // own chunks first, then the partner's
-        const unsigned char* img = zim + (c & 1) * kBwIB;
+        const unsigned char* img = zim + (c & 1) * kBwIBS;
         u32x4 pv[NPR];
         const bool refill = ck == 1 || ck == 2;   // the partner's chunk c+1 into the image chunk ck-1 freed
         if (refill) pld(t, (c + 1) & 3, pv);
@@ -659,10 +756,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
           for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(t - 1, u, ln);
         }
+        int tcur[2], tnxt[2];
+        bases(0, tcur);
 #pragma unroll
-        for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
+        for (int j = 0; j < BD - 1; ++j) ldb(img, tcur, j, bfr[j]);
         for (int tap = 0; tap < 9; ++tap) {
-          const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+          if (tap < 8) bases(tap + 1, tnxt);
           int kt = c * 72 + tap * 8;
           asm volatile("" : "+s"(kt));
           if (refill && tap == 3) pst((c + 1) & 3, pv);
@@ -674,8 +773,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             {
               const int cn = c16 + BD - 1;
-              if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
-              else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
+              if (cn < 8) ldb(img, tcur, cn, bfr[cn % BD]);
+              else if (tap < 8) ldb(img, tnxt, cn - 8, bfr[cn % BD]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -684,6 +783,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             accx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][1], bfr[c16 % BD][XJ], accx, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
           }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) tcur[j] = tnxt[j];
         }
         if (ck == 0 && tid == 0) {   // the partner's dZ_t published? (the other waves load after the barrier)
           pair_wait(p.flags + 2 * b + (1 - kh), p.T - t, p.report, p.spin);
@@ -777,6 +878,18 @@ inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {
 #endif
   hipLaunchKernelGGL((k_convlstm_bwd_frames<0>), dim3(p.B), dim3(256), 0, st, p);
   return hipGetLastError();
+}
+
+// Band mode (recur.h rec_band_fits; the image holds <= kRecNPHB = 184 pixels, kBwIBS
+// bytes): kRecBands workgroups per frame in one residency wave (launch_resident;
+// p.flags [B][kRecBands] zeroed by the caller, p.part rows per (step, frame, band)).
+inline bool bw_band_fits(int h, int w) { return rec_band_fits(h, w) && kRecNPHB * 256 <= kBwIBS; }
+inline hipError_t convlstm_bwd_band(const RecBwdParams& p, hipStream_t st) {
+  if (!bw_band_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
+    return hipErrorInvalidValue;
+  RecBwdParams q = p;
+  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_frames<0, true>),
+                         8 * kRecBands * ((p.B + 7) / 8), 256, q, st);
 }
 
 }  // namespace aaa

@@ -45,7 +45,7 @@ constexpr int kB32NBUF = 3;                   // partial-dh exchange buffers (st
 
 // Wb[(((kh * kB32QP + q) * 4 + rb) * 64 + lane) * 4 + j] =
 //   WdT[64 + 32 rb + lane % 32][tap * 512 + 64 kh + 8 q8 + 4 (lane / 32) + j],  q % kB32Q = tap * 8 + q8
-__global__ void __launch_bounds__(256) k_pack_wb32(const float* __restrict__ WdT, float* __restrict__ Wb) {
+static __global__ void __launch_bounds__(256) k_pack_wb32(const float* __restrict__ WdT, float* __restrict__ Wb) {
   const int i = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
   if (i >= 8 * kB32QP * 4 * 64) return;
   const int lane = i & 63, rb = (i >> 6) & 3, kq = i >> 8, q = kq % kB32QP, kh = kq / kB32QP;

@@ -55,7 +55,7 @@ __host__ __device__ constexpr int f32_k(int q) {
 }
 
 // Wf[((rb * kF32QP + q) * 64 + lane) * 4 + j] = W[32 rb + lane % 32][f32_k(q % kF32Q) + 4 (lane / 32) + j]
-__global__ void __launch_bounds__(256) k_pack_wf32(const float* __restrict__ W, float* __restrict__ Wf) {
+static __global__ void __launch_bounds__(256) k_pack_wf32(const float* __restrict__ W, float* __restrict__ Wf) {
   const int c = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
   if (c >= 16 * kF32QP * 64) return;
   const int lane = c & 63, rq = c >> 6, q = rq % kF32QP, rb = rq / kF32QP;

@@ -1,0 +1,433 @@
+// Internal header of the host runtime (csrc/runtime.hip and the rt_*.hip
+// translation units): the buffer layout, error/timing/stream state (defined
+// once in rt_core.hip), the tile configurations and the GEMM launch helpers
+// shared by the forward (rt_forward.hip), the backward (rt_backward.hip) and
+// the component entries (rt_components.hip).
+#pragma once
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "aaa.h"
+#include "epilogues.h"
+#include "gemm.h"
+#include "loaders_b.h"
+#include "glds.h"
+#include "halo.h"
+#include "recur.h"
+#include "recur_bwd.h"
+#include "recur_f32.h"
+#include "recur_bwd_f32.h"
+#include "vision.h"
+#include "misc.h"
+#include "optim.h"
+#include "actor.h"
+
+
+namespace aaa {
+
+extern thread_local std::string g_err;   // aaa_last_error()
+
+int fail(int code, const char* fmt, ...);
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(AAA_E_LAUNCH, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline int conv_out(int n, int k, int s, int p) { return (n + 2 * p - k) / s + 1; }
+
+enum PIdx {
+  C0W = 0, C0B, C1W, C1B,
+  XI_W, XI_B, HI_W, XF_W, XF_B, HF_W, XC_W, XC_B, HC_W, XO_W, XO_B, HO_W,
+  Q0W, Q0B, Q2W, Q2B, Q4W, Q4B, A0W, A0B, A2W, A2B, WIH, WHH, BIH, BHH, PW, PB, VW, VB, NPARAM
+};
+
+struct Layout {
+  int B, T, F, H, W, H1, W1, P1, h, w, P, nq, A, dt, esz;
+  int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
+  int fu8;  // frames are uint8 (AAA_FLAG_FRAMES_U8)
+  int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
+  int qd, da, ans_in, ans_ld, ldy;
+  size_t poff[NPARAM], psz[NPARAM], ptotal;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags, xpart;
+  size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
+  // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
+  size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
+};
+
+// min_frames: the frames one launch must be able to address (a step's B for
+// the unroll; 1 for the frame-independent vision encoder entries).
+int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0);
+int check_device();
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// ------------------------------------------------- paired-kernel reports --
+// The paired frame-resident kernels (two cooperating workgroups per frame)
+// bound their partner waits (common.h pair_wait).  A timed-out wait adds 1 to
+// this device's report word: pinned host memory mapped into the device, so the
+// host reads it without a copy or a sync.  Every aaa_forward / aaa_backward
+// entry consumes pending reports and fails with AAA_E_STRANDED (the results of
+// the call that stranded are invalid); aaa_pair_status syncs a stream first.
+// Allocated once per process on first use, never freed (no HIP call at exit).
+extern long g_pair_spin;   // partner-wait bound in polls (aaa_debug_pair_spin)
+int* pair_report(int dev);  // this device's report word, device-mapped (nullptr: cannot map)
+int pair_take();            // pending reports of the current device (consumed)
+int pair_peek();            // ... (left pending)
+int pair_check();           // AAA_E_STRANDED if any are pending
+
+// ------------------------------------------------------------ aux stream --
+// Work that is off the sequential ConvLSTM chain (the batched x-part of the
+// forward, every weight/bias gradient and dx/conv backward) is issued on a
+// per-device low-priority stream, chunked every few steps and ordered against
+// the caller's stream by events; the caller's stream waits for it before the
+// call returns (fork/join inside each call).  Created lazily, once per device.
+hipStream_t aux_stream();   // nullptr unless AAA_OVERLAP=1 (measured slower on C2, round 1)
+// Record a pooled event on ``s`` (everything enqueued on s so far).
+hipError_t record_event(hipStream_t s, hipEvent_t* out);
+// ``to`` waits for everything enqueued on ``from`` so far.
+hipError_t stream_order(hipStream_t from, hipStream_t to);
+
+// ------------------------------------------------- optional kernel timing --
+// Per timer class: the HIP event pairs of each launch, the launches'
+// algorithmic work (FLOP for the MFMA classes, bytes for the HBM ones) and
+// the kernel variant dispatched -- so a benchmark reads the roofline inputs
+// from the library instead of re-deriving its dispatch rules.
+struct Timers {
+  std::mutex mu;
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[AAA_TIMER_N];
+  double work[AAA_TIMER_N] = {};
+  std::string variant[AAA_TIMER_N];
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+};
+extern Timers g_timers;
+
+struct TimerScope {
+  int kind;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  double work;
+  std::string variant;
+  TimerScope(int k, hipStream_t s, double w, std::string v) : kind(k), st(s), work(w), variant(std::move(v)) {
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    if (!g_timers.on) return;
+    a = g_timers.get();
+    b = g_timers.get();
+    if (a && b) (void)hipEventRecord(a, st);
+  }
+  ~TimerScope() {
+    if (!a || !b) return;
+    (void)hipEventRecord(b, st);
+    std::lock_guard<std::mutex> lk(g_timers.mu);
+    g_timers.pending[kind].emplace_back(a, b);
+    g_timers.work[kind] += work;
+    g_timers.variant[kind] = variant;
+  }
+};
+
+std::string strf(const char* fmt, ...);
+
+// Algorithmic bytes per frame of the fused attention readout kernels (fp32):
+// forward reads the frame's O rows (128 ch) and writes its map and answer row;
+// backward reads O, the map and the answer grad, writes dO and dQ.
+inline double attn_fwd_bytes(int P, int nq, int ans_ld) { return 4.0 * (128.0 * P + nq * P + ans_ld); }
+inline double attn_bwd_bytes(int P, int nq) { return 4.0 * (2.0 * 128 * P + nq * P + 184.0 * nq + 72.0 * nq); }
+
+// --------------------------------------------------------- tile configs ---
+// fp32 uses the exact v_mfma_f32_32x32x2_f32; bf16 v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
+using CF = GemmCfg<float, 64, 64, 32, 2, 2>;      // default 64x64 tile, 4 waves
+using CF32 = GemmCfg<float, 32, 64, 32, 1, 2>;    // 32-row tile, 2 waves: small-Mi GEMMs / more WGs
+using CFW = GemmCfg<float, 128, 128, 32, 2, 2>;   // long-K weight gradients: 64x64 per wave
+using CFK = GemmCfg<float, 32, 64, 64, 1, 2, 2>;  // per-step ConvLSTM kernels: 2-way split-K in the WG
+using CFK4 = GemmCfg<float, 32, 64, 64, 1, 2, 4>; // 4-way split-K (8 waves)
+using CFK4B = GemmCfg<float, 32, 64, 128, 1, 2, 4>; // 4-way split-K, 2 k-steps per wave per barrier
+using CF64 = GemmCfg<float, 64, 64, 64, 2, 2>;     // 64x64, BK 64
+using CFJ = GemmCfg<float, 64, 128, 32, 2, 2>;     // 64-row GEMMs with long N (batched dx)
+using CFS = GemmCfg<float, 128, 64, 32, 4, 2>;     // forward step: 8 waves, ~1 WG per CU at C2 (balanced)
+using CB = GemmCfg<__bf16, 64, 64, 64, 2, 2>;
+using CB32 = GemmCfg<__bf16, 32, 64, 64, 1, 2>;
+using CBW = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
+using CBK = GemmCfg<__bf16, 32, 64, 64, 1, 2, 2>;
+using CBK4 = GemmCfg<__bf16, 32, 64, 64, 1, 2, 4>;
+using CBK4B = GemmCfg<__bf16, 32, 64, 128, 1, 2, 4>;
+using CB64 = GemmCfg<__bf16, 64, 64, 128, 2, 2>;
+using CBJ = GemmCfg<__bf16, 64, 128, 64, 2, 2>;
+using CBS = GemmCfg<__bf16, 128, 64, 64, 4, 2>;
+template <typename T> using CfgFor = std::conditional_t<std::is_same<T, float>::value, CF, CB>;
+template <typename T> using Cfg32For = std::conditional_t<std::is_same<T, float>::value, CF32, CB32>;
+template <typename T> using CfgWFor = std::conditional_t<std::is_same<T, float>::value, CFW, CBW>;
+template <typename T> using CfgKFor = std::conditional_t<std::is_same<T, float>::value, CFK, CBK>;
+template <typename T> using CfgK4For = std::conditional_t<std::is_same<T, float>::value, CFK4, CBK4>;
+template <typename T> using CfgK4BFor = std::conditional_t<std::is_same<T, float>::value, CFK4B, CBK4B>;
+template <typename T> using Cfg64For = std::conditional_t<std::is_same<T, float>::value, CF64, CB64>;
+template <typename T> using CfgJFor = std::conditional_t<std::is_same<T, float>::value, CFJ, CBJ>;
+template <typename T> using CfgSFor = std::conditional_t<std::is_same<T, float>::value, CFS, CBS>;
+
+// Step-kernel tile choice (env AAA_STEP_TILE / AAA_BPTT_TILE override):
+//   0 64x64 BK32 | 1 32x64 BK64 2-way in-WG split-K | 2 ... 4-way | 3 32x64 BK128 4-way
+//   (forward: 3 = 64x64 BK64) | 4-6 the same shapes on the LDS-DMA ring of glds.h
+//   (forward 4 = 128x64 8 waves, 5 = 32x64 split-K, 6 = 64x64 BK64; BPTT 4 = 32x64 BK128
+//   4-way, 5 = BK64 4-way, 6 = 64x64, 9 = 64x32 BK128 4-way).  The default picks by how many 32x32
+//   output tiles the step has, i.e. how many waves it can feed; measured on C2.
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+// Steps per off-chain chunk: the whole unroll unless overlapping, and never
+// more than the frames one launch may address (Layout::fchunk).
+static int chunk_steps(const Layout& L) {
+  const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : L.T);
+  return std::max(1, std::min({c, L.T, L.fchunk / L.B}));
+}
+static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
+  const int v = env_int(env, -1);
+  if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
+    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || (v >= 19 && v <= 24);
+    if (v >= 19 && v <= 24 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
+    const bool fwd_only = v == 14 || v == 17 || v == 18 || v == 25 || v == 26;
+    return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
+  }
+  // bf16 BPTT: 128x128 from ~3/4 of a workgroup per CU (C3: 242 WGs), else 128x64
+  // (tools/ubench/bf16_tiles at B=128: 34.6 vs 39.6 us)
+  // below that, 128x64 with a 4-way in-WG split-K (8 waves; C4: 50.0 vs 52.5 us for the 4-wave
+  // 2-way tile 8, tools/ab_bptt_bf16.sh)
+  if (bptt && bf16) return out_tiles32 >= 4L * 4 * 192 ? 7 : 22;
+  // fp32 (C2: 484 BPTT / 1936 forward tiles): 32x32 BK64 4-way BPTT on a 3-stage ring, two WGs
+  // per CU whose barriers are not in step (51.6 vs 54.4 us for 64x32 BK128, 54.6 vs 55.9 for
+  // 32x64); 64x64 BK64 forward 47.4 us (32x64 / 32x32 / 64x32 split-K rings: 52-55 us)
+  // (bench.py kernel table, tools/ab_bptt.sh)
+  if (bptt) return out_tiles32 < 1024 ? 16 : (out_tiles32 < 1536 ? 1 : 0);
+  return out_tiles32 < 1024 ? 5 : 6;
+}
+
+// fp16 gate-activation storage (halves the step epilogues' largest stream):
+// bf16 operands, fused x-part (the gate buffer then holds activations only)
+// and the bf16 BPTT tiles 7/8.  AAA_GATES_F16=0 keeps fp32.  Forward and
+// backward evaluate this identically (same env, same shapes).
+// The x-part rides in the step GEMM for bf16 and for small steps (M = B*P
+// pixels; the actor's B = 1: one launch instead of two latency-bound ones);
+// fp32 at C2 (M = 3872) keeps the batched x-part (measured 5.02 vs 5.09 ms).
+// bf16 ConvLSTM forward on the frame-resident kernel (recur.h): one workgroup
+// per frame for the whole unroll, on grids whose images fit its LDS (84x84
+// frames), once the batch fills most of the chip's 256 CUs (C3, B=256: 55 vs
+// 79 us per step; C4's B=128 leaves half the CUs idle: 49 vs 43 us,
+// profiles/r02/frames).  AAA_FRAMES_FWD=1/0 forces it on/off.
+int frames_fwd(const Layout& L);
+static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
+static bool gates_f16(int dt, int M) {
+  if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
+  const int bt = step_tile((long)(128 / 32) * ((M + 31) / 32), "AAA_BPTT_TILE", true, true);
+  return bt == 7 || bt == 8 || bt >= 19;
+}
+
+// Whether the LDS-DMA ring can run tile config CK (every wave issues the same DMA count).
+template <class CK>
+constexpr bool pipe_even() {
+  constexpr int VG = 16 / (int)sizeof(typename CK::type);
+  return (CK::BI * CK::BK / VG) % CK::NT == 0 && (CK::BJ * CK::BK / VG) % CK::NT == 0;
+}
+
+// One per-step ConvLSTM GEMM: D[Mi][M] = W[Mi][K] x im2col(src)[K][M] with
+// epilogue ep.  PIPE = LDS-DMA ring (glds.h; needs src already in T),
+// otherwise the register-staged kernel (which can convert fp32 -> bf16).
+template <class CK, bool PIPE, typename T, typename G, class EP, int NBUF = 2, bool ILV = false>
+static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const ConvGeo& g, int M, uint32_t src_bytes,
+                            const EP& ep, int Mi, int K, hipStream_t st) {
+  if constexpr (PIPE && pipe_even<CK>() && std::is_same<G, T>::value) {
+    using LA = GRowsB<T, CK::BI, CK::BK, CK::NT>;
+    using LB = GIm2colB<T, CK::BJ, CK::BK, CK::NT>;
+    return launch_pipe<CK, LA, LB, EP, NBUF, ILV>(typename LA::Params{W, ldw, wrows},
+                                                  typename LB::Params{src, g, M, src_bytes}, ep, Mi, M, K, 1, st);
+  } else {
+    using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
+    using LB = LdIm2colB<G, T, CK::BJ, CK::BK, CK::NT>;
+    return launch_gemm<CK, LA, LB>(typename LA::Params{W, ldw, wrows}, typename LB::Params{src, g, M, src_bytes}, ep,
+                                   Mi, M, K, 1, st);
+  }
+}
+
+// Small GEMMs of the head (F = T*B rows; answer MLP, LSTMCell, policy/value
+// heads): 64x64 tiles leave most CUs idle, so below ~192 tiles use the 32x64
+// tile with a 4-way in-WG split-K (8 waves per WG: the serial K loop of these
+// long-K, few-tile GEMMs is what they wait on; C2 4.487 -> 4.414 ms per
+// iteration vs the plain 32x64 tile, tools/ab_head.sh).  AAA_HEAD_TILE=1 forces
+// 64x64, =2 the plain 32x64, =3/4/5 the 2-way / 4-way / 4-way BK128 split-K tiles.
+template <template <typename, typename, int, int, int> class LA_,
+          template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
+static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, int nsplit,
+                            hipStream_t st) {
+  const int mode = env_int("AAA_HEAD_TILE", 0);
+  const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
+  auto splitk = [&](auto cfg) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
+    using C = decltype(cfg);
+    using A = LA_<float, float, C::BI, C::BK, C::NT>;
+    using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+    return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
+                                ep, Mi, Nj, K, nsplit, st);
+  };
+  if (mode == 3) return splitk(CFK{});
+  if (mode == 4) return splitk(CFK4{});
+  if (mode == 5) return splitk(CFK4B{});
+  if (mode == 0 && tiles < 192) return splitk(CFK4{});
+  if (mode == 1 || (mode == 0 && tiles >= 192)) {
+    using C = CF;
+    using A = LA_<float, float, C::BI, C::BK, C::NT>;
+    using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+    return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
+                                ep, Mi, Nj, K, nsplit, st);
+  }
+  using C = CF32;
+  using A = LA_<float, float, C::BI, C::BK, C::NT>;
+  using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+  return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows}, ep,
+                              Mi, Nj, K, nsplit, st);
+}
+
+// Tail GEMMs with very few columns (the actor's B=1, T=1 step: F = 1):
+// D[i][j] = sum_k W[i][k] X[j][k], one wavefront per 4-row group, lanes split
+// K in 16-B pieces (coalesced weight rows), butterfly reduction, then the same
+// epilogue functor.  A 64x64 tile spends ~20 us on its serial K loop there;
+// this reads the weight matrix once at full width.
+constexpr int kSkinnyMaxCols = 8;
+template <class EP, int NJ>
+__global__ void __launch_bounds__(256)
+k_skinny_gemm(const float* __restrict__ W, int ldw, int Mi, const float* __restrict__ X, int ldx, int Nj, int K,
+              EP ep) {
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * 4;
+  if (i >= Mi) return;
+  float acc[4][NJ];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[r][j] = 0.f;
+  for (int k = lane * 4; k < K; k += 256) {
+    f32x4 w[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      w[r] = i + r < Mi ? *reinterpret_cast<const f32x4*>(W + (size_t)(i + r) * ldw + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j < Nj) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(X + (size_t)j * ldx + k);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r][j] += w[r][0] * x[0] + w[r][1] * x[1] + w[r][2] * x[2] + w[r][3] * x[3];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc[r][j] += __shfl_xor(acc[r][j], o, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (j < Nj) ep(i, j, acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+}
+
+// Forward tail GEMM (row-major weights [Mi][K] x activations [Nj][K]): the
+// skinny kernel for <= kSkinnyMaxCols columns (AAA_SKINNY=0 disables), else head_gemm.
+template <class PA, class PB, class EP>
+static hipError_t tail_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, hipStream_t st) {
+  if (Nj <= kSkinnyMaxCols && K % 4 == 0 && pa.ld % 4 == 0 && pb.ld % 4 == 0 && env_int("AAA_SKINNY", 1)) {
+    const int blocks = cdiv(cdiv(Mi, 4), 4);
+    if (Nj == 1)
+      hipLaunchKernelGGL((k_skinny_gemm<EP, 1>), dim3(blocks), dim3(256), 0, st, pa.src, pa.ld, Mi, pb.src, pb.ld, Nj,
+                         K, ep);
+    else
+      hipLaunchKernelGGL((k_skinny_gemm<EP, kSkinnyMaxCols>), dim3(blocks), dim3(256), 0, st, pa.src, pa.ld, Mi,
+                         pb.src, pb.ld, Nj, K, ep);
+    return hipGetLastError();
+  }
+  return head_gemm<LdRows, LdRows>(pa, pb, ep, Mi, Nj, K, 1, st);
+}
+
+// Batched (off-chain) conv GEMMs on the LDS-DMA ring (env AAA_PIPE_BATCHED=0: register-staged).
+static bool pipe_batched() { return env_int("AAA_PIPE_BATCHED", 1) != 0; }
+
+static int wgrad_splits(int tiles, int K, int BK) {
+  int s = std::max(1, 1024 / std::max(tiles, 1));
+  int maxs = std::max(1, K / (8 * BK));
+  return std::min(s, maxs);
+}
+
+// One fused ConvLSTM forward step (attention.py:110-126): D[512][M] = WpXH x
+// im2col([x_t | h_{t-1}]) (K = 9*192), gate math and cell update in the
+// epilogue ``ep``.  Tile: AAA_FUSED_TILE, default bf16 128x128 of 4 waves
+// (64x64 per wave; tools/ab_fused.sh), fp32 (small M only, e.g. the B=1 actor
+// and the standalone cell) 128x64 of 8 waves.
+template <typename T, typename GT>
+static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const EpiConvLstmFwd<T, GT>& ep,
+                      hipStream_t st) {
+  using EF = EpiConvLstmFwd<T, GT>;
+  const ConvGeo g = ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
+  const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
+  const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
+  TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728,
+                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d", std::is_same<T, float>::value ? "fp32" : "bf16",
+                      ftile));
+  if (ftile == 7)
+    HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring
+    HIPCHK((step_gemm<CfgSFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 9)   // 128x128, 4 waves of 64x64
+    HIPCHK((step_gemm<GemmCfg<T, 128, 128, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 10)   // 64x64, 4 waves, 3-stage ring
+    HIPCHK((step_gemm<CfgFor<T>, true, T, T, EF, 3, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 11)   // 64x64, 2-way in-WG split-K (8 waves), BK64 (K = 1728 = 27 x 64)
+    HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else if (ftile == 12)   // 128x64, 2x2 waves of 64x32
+    HIPCHK((step_gemm<GemmCfg<T, 128, 64, 64, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  else
+    HIPCHK((step_gemm<CfgSFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+  return AAA_OK;
+}
+
+// ---------------------------------------------- frame-resident dispatch ----
+int device_cus();   // CUs of the current device
+// Workgroups per frame of the bf16 frame-resident kernels (0: per-step launches).
+int frames_g(const Layout& L, const char* env);
+int frames_band(const Layout& L);   // band mode (recur.h BAND): kRecBands, else 0
+int f32_frames(const Layout& L);    // fp32 frame-group G (recur_f32.h), else 0
+int frames_bwd(const Layout& L, bool g16);
+int rec_stagger(const char* env);   // start offset of half the frames, 100-MHz ticks
+
+// ------------------------------------------------------- cross-unit paths --
+template <typename T> int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st);
+template <typename T, typename OT>
+int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1, OT* out,
+               int out_ld, hipStream_t st);
+template <typename T> int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st);
+template <typename T>
+int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipStream_t s, bool aux);
+template <typename T>
+int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, const T* xp, T* dy1, int F, float* gW2,
+               float* gW1, float* gb1, hipStream_t s);
+template <typename T> int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st);
+
+}  // namespace aaa

@@ -397,7 +397,7 @@ inline bool band2_fits(int H1, int W1, int h, int w) {
   return (2 * kBand2Rows + 2) * (W1 + 4) * kVisYP <= kBand2YB && h >= 1 && w >= 1 && 2 * (h - 1) + 1 <= H1 + 1;
 }
 
-__global__ void __launch_bounds__(256) k_vision_conv2_band(VisBand2Params p) {
+static __global__ void __launch_bounds__(256) k_vision_conv2_band(VisBand2Params p) {
   __shared__ __attribute__((aligned(16))) unsigned char yim[kBand2YB];
   __shared__ float sb[64];
   const int tid = (int)threadIdx.x, lane = tid & 63;

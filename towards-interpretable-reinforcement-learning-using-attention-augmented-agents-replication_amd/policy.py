@@ -171,7 +171,14 @@ class GraphActor:
             raise ValueError("the actor chain needs an fp32 agent with the zero-state policy core and B <= 16")
         self.chain = eligible if chain is None else bool(chain)
         if self.chain:
-            self.runner = r = ActorRunner(B, H, W, agent.num_queries, agent.num_actions, dev, frames_u8=True)
+            try:
+                r = ActorRunner(B, H, W, agent.num_queries, agent.num_actions, dev, frames_u8=True)
+            except RuntimeError:
+                if chain:   # asked for explicitly: the library's reason (e.g. the readout LDS of a large grid)
+                    raise
+                self.chain = False   # not applicable to this geometry: the learner's T=1 forward
+        if self.chain:
+            self.runner = r
             self._ws = r.new_workspace()
             A = agent.num_actions
             self._logits = torch.empty(B, A, device=dev)
