@@ -111,6 +111,25 @@ __device__ __forceinline__ void stagger_wait(int ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// The same for several partners at once, by one wave: lane j polls flags[j]
+// for every bit j of ``mask`` (j < 64), all in one round trip per poll (a loop
+// of pair_wait calls pays one L2 round trip per partner, in sequence).  On
+// timeout one lane adds 1 to ``report`` and the wave returns.
+__device__ __forceinline__ void wave_wait_flags(const int* flags, unsigned long long mask, int target, int* report,
+                                                int spin) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool mine = (mask >> lane) & 1ull;
+  for (int n = 0;; ++n) {
+    const int v = mine ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+    if (__all(v >= target)) return;
+    if (n >= spin) {
+      if (lane == 0) __hip_atomic_fetch_add(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Launch a paired kernel (two cooperating workgroups per frame) as an ordinary
 // dispatch whose whole grid fits one residency wave of the device: every
 // workgroup is placed at once on an idle chip, and the bounded partner waits

@@ -39,7 +39,7 @@ constexpr int kRecNPH = 169;        // whole-frame LDS images: (h+2)*(w+2) <= 16
 constexpr int kRecNPHB = 184;       // image buffer pixels: also one band of <= 6 rows of a 21-wide grid + its halo rows
 constexpr int kRecXB = 23 * 1024;   // x image bytes: 184 pixels x 128 B (whole 1-KB DMA pieces)
 constexpr int kRecBands = 4;        // grid bands per frame in band mode (168x168 frames: 21 rows -> 5,5,5,6)
-constexpr int kRecHS = 128;         // h image pixel pitch (bf16): 256 B, 16-B slots swizzled by rec_fz
+constexpr int kRecHS = 136;         // h image pixel pitch (bf16): 128 + 8 pad (272 B = 17 x 16 B)
 constexpr int kRecStg = 4608;       // per-wave epilogue staging bytes (16 px x 272 B gates; c + h 2 x 16 x 144 B)
 constexpr int kSC1 = 16;            // buffer load / store cache policy: sc1 (cross-workgroup hand-off bytes)
 
@@ -93,23 +93,79 @@ struct RecFwdParams {
   int* report;         // G = 2: partner-timeout report word (pinned host, device-mapped; pair_wait)
   int spin;            // G = 2: partner-wait bound in polls
   int stagger;         // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
+  // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
+  // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
+  short colpp[128], colhb[128];
 };
 
-// Image swizzle of the frame-resident kernels.  GEMM columns are the grid
-// pixels in raster order; a B-fragment ds_read_b128 lane group (4 x 16 lanes,
-// MI355X_MICROARCH) reads 16 consecutive columns at one tap.  Their image
-// indices run consecutively except for a jump by 2 (the border columns) at a
-// grid-row end, so a slot order keyed on the image index collides there
-// (0.50 conflicts per LDS access at C3 in round 2).  Keyed instead on
-// rec_fz(ip) = ip - 2 * (image row of ip) -- the index with the border columns
-// skipped, consecutive across row ends for every tap -- the 16 lanes hit 16
-// distinct bank groups while the columns (and so the epilogue's HBM stores)
-// stay pixel-contiguous.  h image: 16-B slot s of pixel ip at s ^ (rec_fz & 15)
-// of its 256-B row; x image (128-B pixels, two per 256-B row): s ^ ((rec_fz >> 1) & 7)
-// (rec_fz & 1 = ip & 1 picks the row half).  For an interior pixel of band
-// column col (pixel pix0 + col), rec_fz = col + w + 1; for its window's
-// top-left at tap (ky, kx), rec_fz = col + ky * w + kx.
-__host__ __device__ __forceinline__ int rec_fz(int ip, int W2) { return ip - 2 * (ip / W2); }
+// Column order of the frame-resident GEMMs.  A B-fragment ds_read_b128 serves
+// 16 lanes (16 consecutive columns) per 256-B LDS row, and both images put
+// image pixel ip at 16-B slot ip (mod 16) (+ a per-read constant), so a lane
+// group is conflict-free iff its 16 pixels' image indices differ mod 16.  In
+// raster order every 16-column group of an 11-wide grid crosses a row end,
+// where the index jumps by 3 (the border): two slots collide, the read takes
+// two passes (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.50 at C3).  Here
+// the columns are the pixels bucketed by image index mod 16 and dealt out one
+// per residue to each 16-column group (padding columns read a spare interior
+// index of the missing residue).  Measured (profiles/r02/ab/rec_perm.txt): the
+// conflict cycles drop 61 % but the forward gets slower (C3 1136 -> 1177 us,
+// C4 618 -> 652 us): the epilogue's pixel rows of a 16-column half are then
+// scattered over the frame instead of one contiguous run, and the kernel is
+// not bound by these reads.  So the raster order is the default and the
+// dealt order an A/B option (AAA_REC_PERM=1; also kept when a residue holds
+// more than 8 pixels).
+inline void rec_columns(int h, int w, short* colpp, short* colhb) {
+  const int W2 = w + 2, P = h * w, NPH = (h + 2) * W2;
+  auto raster = [&] {
+    for (int c = 0; c < 128; ++c) {
+      const int pp = c < P ? c : P - 1;
+      colpp[c] = (short)(c < P ? c : -1);
+      colhb[c] = (short)((pp / w) * W2 + pp % w);
+    }
+  };
+  raster();
+  const char* e = getenv("AAA_REC_PERM");
+  if (!(e && atoi(e) == 1) || P > 128) return;
+  int bucket[16][9], nb[16] = {0};
+  for (int pp = 0; pp < P; ++pp) {
+    const int r = ((pp / w + 1) * W2 + pp % w + 1) & 15;
+    if (nb[r] == 8) return;   // a residue with more pixels than groups: keep the raster order
+    bucket[r][nb[r]++] = pp;
+  }
+  int spare[16];
+  for (int r = 0; r < 16; ++r) {   // a padding column's window must stay inside the image for all 9 taps
+    spare[r] = -1;
+    for (int ip = W2 + 1; ip <= NPH - W2 - 2 && spare[r] < 0; ++ip)
+      if ((ip & 15) == r) spare[r] = ip;
+    if (spare[r] < 0 && nb[r] < 8) return;
+  }
+  int used[16] = {0};
+  for (int g = 0; g < 8; ++g)
+    for (int r = 0; r < 16; ++r) {
+      const int c = 16 * g + r;
+      if (used[r] < nb[r]) {
+        const int pp = bucket[r][used[r]++];
+        colpp[c] = (short)pp;
+        colhb[c] = (short)((pp / w) * W2 + pp % w);
+      } else {
+        colpp[c] = -1;
+        colhb[c] = (short)(spare[r] - W2 - 1);
+      }
+    }
+}
+
+#ifdef AAA_STAMPS
+// Diagnostic builds only (tools/ubench/bwband): per (workgroup, step) phase stamps
+// (s_memrealtime, 100 MHz): step start, x-part done, neighbour h in, h-part done,
+// epilogue done, h_t stored / published.
+__device__ uint64_t aaa_fw_stamps[1024 * 64 * 8];
+#define AAA_FW_STAMP(t, k)                                                                                    \
+  do {                                                                                                        \
+    if (tid == 0 && (t) < 64) aaa_fw_stamps[((size_t)blockIdx.x * 64 + (t)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AAA_FW_STAMP(t, k) do {} while (0)
+#endif
 
 // ABL (diagnostic A/B only: AAA_REC_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
@@ -161,8 +217,6 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   const int Pb = (r1 - r0) * p.w, pix0 = r0 * p.w;   // the band's pixels (the whole frame without BAND)
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w - r0 + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
-  // h image element offset of 16-B slot q (channels 8q..8q+7) of grid pixel pp (band rows and halo rows)
-  auto hsw = [&](int pp, int q) { return hidx(pp) * kRecHS + ((q ^ ((pp - pix0 + p.w + 1) & 15)) << 3); };
   const int rb0 = kh * (16 / G) + wave * NRB;   // the wave's first global row block (32 rows = 8 channels)
   const int cbase = 8 * rb0;                     // its first channel
   float* cw = cstl + wave * NRB * 16 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
@@ -172,7 +226,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     for (int i = tid; i < kRecNPHB * kRecHS / 8; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
     sbias[tid] = p.bias[tid];
     sbias[tid + 256] = p.bias[tid + 256];
-    if (tid < 128) scol[tid] = (short)(tid < Pb ? pix0 + tid : -1);
+    if (tid < 128) scol[tid] = BAND ? (short)(tid < Pb ? pix0 + tid : -1) : p.colpp[tid];
   }
   // x image of step t (XH slot t, channels 0..63) by LDS-DMA, border included:
   // image pixel ip holds its 8 16-B channel chunks at slots q ^ xswz(ip) (the
@@ -183,8 +237,8 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     const __amdgpu_buffer_rsrc_t rs =
         make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
     for (int i = wave; i < kRecXB / 1024; i += 4) {
-      const int sl = i * 64 + lane, ip = sl >> 3, iy = ip / W2, q = (sl & 7) ^ (((ip - 2 * iy) >> 1) & 7);
-      const int py = r0 + iy - 1, px = ip - iy * W2 - 1;
+      const int sl = i * 64 + lane, ip = sl >> 3, q = (sl & 7) ^ ((ip >> 1) & 7);
+      const int py = r0 + ip / W2 - 1, px = ip % W2 - 1;
       const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
       dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB);
     }
@@ -197,7 +251,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int pp = cb * 32 + r32 < Pb ? pix0 + cb * 32 + r32 : -1;
+        const int pp = BAND ? (cb * 32 + r32 < Pb ? pix0 + cb * 32 + r32 : -1) : p.colpp[cb * 32 + r32];
         cw[(rb * 16 + cb * 4 + g) * 64] =
             pp >= 0 ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
       }
@@ -206,19 +260,21 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     const __bf16* src = p.XH + (size_t)b * P * 192 + 64;
     const int hr0 = BAND ? max(r0 - 1, 0) : 0, hr1 = BAND ? min(r1 + 1, p.h) : p.h;
     for (int i = hr0 * p.w * 16 + tid; i < hr1 * p.w * 16; i += 256)
-      *reinterpret_cast<u32x4*>(him + hsw(i >> 4, i & 15)) =
+      *reinterpret_cast<u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8) =
           *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 4) * 192 + (i & 15) * 8);
   }
 
   // per-lane B fragment bases: top-left image pixel of each column block's 3x3
-  // window and its rec_fz (= the column; columns >= Pb read column Pb-1: their
-  // outputs are never stored)
-  int hb[4], fb[4];
+  // window (columns >= P read pixel P-1: their outputs are never stored)
+  int hb[4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
-    const int col = min(cb * 32 + r32, Pb - 1), pp = pix0 + col;
-    hb[cb] = (pp / p.w - r0) * W2 + pp % p.w;
-    fb[cb] = col;
+    if constexpr (BAND) {
+      const int pp = pix0 + min(cb * 32 + r32, Pb - 1);
+      hb[cb] = (pp / p.w - r0) * W2 + pp % p.w;
+    } else {
+      hb[cb] = p.colhb[cb * 32 + r32];
+    }
   }
 
   // A stream: one buffer descriptor over the fragment-order weights, the lane's
@@ -240,6 +296,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   unsigned char* sw = stg + wave * STG;   // this wave's epilogue staging
   if ((b >> 3) & 1) stagger_wait(p.stagger);
   for (int t = 0; t < p.T; ++t) {
+    AAA_FW_STAMP(t, 0);
     f32x16 acc[NRB][4];
 #pragma unroll
     for (int j = 0; j < NRB; ++j)
@@ -247,35 +304,26 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][cb][e] = 0.f;
-    int hbs[4], fbs[4];   // laundered per step: no per-tap address tables hoisted out of the step loop
+    const __bf16* hbp = him + hh * 8;
+    int hbs[4];   // laundered per step: no per-tap address tables hoisted out of the step loop
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       hbs[cb] = hb[cb];
-      fbs[cb] = fb[cb];
-      asm volatile("" : "+v"(hbs[cb]), "+v"(fbs[cb]));
+      asm volatile("" : "+v"(hbs[cb]));
     }
-    // per tap and column block: byte address of the lane's window pixel or'ed with its
-    // swizzled slot of chunk 0; chunk c4 (x) / c8 (h) xors in c << 5
-    auto xbases = [&](int tap, int (&tb)[4]) {
-      const int ky = tap / 3, kx = tap - 3 * ky, toff = ky * W2 + kx, tf = ky * p.w + kx;
+    // B fragments of a k step: x image (chunk c4 of 4 at tap offset toff) or h image (chunk c8 of 8)
+    auto ldx = [&](int toff, int c4, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) tb[cb] = ((hbs[cb] + toff) << 7) | ((hh ^ (((fbs[cb] + tf) >> 1) & 7)) << 4);
+      for (int cb = 0; cb < 4; ++cb) {
+        const int ip = hbs[cb] + toff;
+        bf[cb] = *reinterpret_cast<const bf16x8*>(xim + ip * 128 + (((2 * c4 + hh) ^ ((ip >> 1) & 7)) << 4));
+      }
     };
-    auto hbases = [&](int tap, int (&tb)[4]) {
-      const int ky = tap / 3, kx = tap - 3 * ky, toff = ky * W2 + kx, tf = ky * p.w + kx;
+    auto ldh = [&](int toff, int c8, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) tb[cb] = ((hbs[cb] + toff) << 8) | ((hh ^ ((fbs[cb] + tf) & 15)) << 4);
+      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(hbp + (hbs[cb] + toff) * kRecHS + c8 * 16);
     };
-    // B fragments of a k step: x image (chunk c4 of 4) or h image (chunk c8 of 8)
-    auto ldx = [&](const int (&tb)[4], int c4, bf16x8 (&bf)[4]) {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(xim + (tb[cb] ^ (c4 << 5)));
-    };
-    auto ldh = [&](const int (&tb)[4], int c8, bf16x8 (&bf)[4]) {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        bf[cb] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const unsigned char*>(him) + (tb[cb] ^ (c8 << 5)));
-    };
+    auto tapoff = [&](int tap) { return (tap / 3) * W2 + tap % 3; };
     // one k step: A prefetch PD-1 ahead, next B fragments, 16 MFMAs
     auto kstep = [&](int ks, int slot, bf16x8 (&bc)[4], auto&& load_next_b) {
       if constexpr (!(ABL & 1)) {
@@ -296,33 +344,29 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       __builtin_amdgcn_sched_barrier(0);
     };
     bf16x8 bfr[2][4];
-    int tcur[4], tnxt[4];
-    xbases(0, tcur);
-    ldx(tcur, 0, bfr[0]);
+    ldx(0, 0, bfr[0]);
     // x-part: 9 taps x 4 chunks (k steps 0..35)
     for (int tap = 0; tap < 9; ++tap) {
-      if (tap < 8) xbases(tap + 1, tnxt);
-      else hbases(0, tnxt);
+      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
       int kt = tap * 4;
       asm volatile("" : "+s"(kt));
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4)
         kstep(kt + c4, c4 % PD, bfr[c4 & 1], [&] {
-          if (c4 < 3) ldx(tcur, c4 + 1, bfr[(c4 + 1) & 1]);
-          else if (tap < 8) ldx(tnxt, 0, bfr[0]);
-          else if (G == 1 && !BAND) ldh(tnxt, 0, bfr[0]);
+          if (c4 < 3) ldx(toff, c4 + 1, bfr[(c4 + 1) & 1]);
+          else if (tap < 8) ldx(tn, 0, bfr[0]);
+          else if (G == 1 && !BAND) ldh(0, 0, bfr[0]);
         });
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) tcur[cb] = tnxt[cb];
     }
     barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
+    AAA_FW_STAMP(t, 1);
     if (t + 1 < p.T) dma_x(t + 1);
     if constexpr (BAND) {
       if (t > 0) {   // the neighbour bands' boundary rows of h_{t-1} (XH slot t) into the halo rows
-        if (tid == 0) {
-          if (band > 0) pair_wait(p.flags + b * kRecBands + band - 1, t, p.report, p.spin);
-          if (band < kRecBands - 1) pair_wait(p.flags + b * kRecBands + band + 1, t, p.report, p.spin);
-        }
+        if (wave == 0)   // the neighbour bands' flags, both in one poll
+          wave_wait_flags(p.flags + b * kRecBands,
+                          (band > 0 ? 1ull << (band - 1) : 0ull) | (band < kRecBands - 1 ? 1ull << (band + 1) : 0ull), t,
+                          p.report, p.spin);
         barrier_lds();
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
         const int nh = p.w * 16;   // 16-B pieces of one grid row
@@ -330,13 +374,13 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           const int gy = i < nh ? r0 - 1 : r1, j = i < nh ? i : i - nh;
           if ((unsigned)gy < (unsigned)p.h) {
             const int pp = gy * p.w + (j >> 4);
-            *reinterpret_cast<u32x4*>(him + hsw(pp, j & 15)) =
+            *reinterpret_cast<u32x4*>(him + hidx(pp) * kRecHS + (j & 15) * 8) =
                 __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((pp * 192 + 64 + (j & 15) * 8) * 2), 0, kSC1);
           }
         }
         barrier_lds();
       }
-      ldh(tcur, 0, bfr[0]);
+      ldh(0, 0, bfr[0]);
     }
     if constexpr (G == 2) {
       if (t > 0) {   // the partner's half of h_{t-1} (XH slot t) into the image, once it has published it
@@ -353,28 +397,28 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         // visibility, hand-off table row 1)
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
         for (int i = tid; i < P * 8; i += 256)
-          *reinterpret_cast<u32x4*>(him + hsw(i >> 3, 8 * (1 - kh) + (i & 7))) =
+          *reinterpret_cast<u32x4*>(him + hidx(i >> 3) * kRecHS + 64 * (1 - kh) + (i & 7) * 8) =
               __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((i >> 3) * 192 + 64 + 64 * (1 - kh) + (i & 7) * 8) * 2),
                                                     0, (ABL & 16) ? 0 : kSC1);
         barrier_lds();
       }
-      ldh(tcur, 0, bfr[0]);
+      ldh(0, 0, bfr[0]);
     }
-    // h-part: 9 taps x 8 chunks (k steps 36..107); tcur = the h bases of tap 0
+    AAA_FW_STAMP(t, 2);
+    // h-part: 9 taps x 8 chunks (k steps 36..107)
     for (int tap = 0; tap < 9; ++tap) {
-      if (tap < 8) hbases(tap + 1, tnxt);
+      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
       int kt = kRecKX + tap * 8;
       asm volatile("" : "+s"(kt));
 #pragma unroll
       for (int c8 = 0; c8 < 8; ++c8)
         kstep(kt + c8, c8 % PD, bfr[c8 & 1], [&] {
-          if (c8 < 7) ldh(tcur, c8 + 1, bfr[(c8 + 1) & 1]);
-          else if (tap < 8) ldh(tnxt, 0, bfr[0]);
+          if (c8 < 7) ldh(toff, c8 + 1, bfr[(c8 + 1) & 1]);
+          else if (tap < 8) ldh(tn, 0, bfr[0]);
         });
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) tcur[cb] = tnxt[cb];
     }
     barrier_lds();   // every wave is done with h_{t-1}: the epilogue overwrites the image with h_t
+    AAA_FW_STAMP(t, 3);
 
     // Epilogue, one column block (32 pixels) at a time: gate math + cell update
     // lane-local, h_t into the h image, c_t into its LDS copy, and the HBM
@@ -391,8 +435,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int pp = scol[cb * 32 + pl];   // -1: padding column
-      __bf16* hl = him + hidx(max(pp, 0)) * kRecHS;   // + the swizzled slot of channel c0 + co
-      const int hfz = (cb * 32 + pl + p.w + 1) & 15;
+      __bf16* hl = him + hidx(max(pp, 0)) * kRecHS + c0;
       uint32_t gq[NRB][4][2];   // fp16 gate quads (i, f, c~, o), packed
       float hv[NRB][4], cv[NRB][4];
 #pragma unroll
@@ -414,7 +457,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           typedef _Float16 h2 __attribute__((ext_vector_type(2)));
           gq[rb][g][0] = __builtin_bit_cast(uint32_t, h2{(_Float16)gi, (_Float16)gf});
           gq[rb][g][1] = __builtin_bit_cast(uint32_t, h2{(_Float16)gc, (_Float16)go});
-          if (pp >= 0) hl[((((c0 + co) >> 3) ^ hfz) << 3) | ((c0 + co) & 7)] = (__bf16)h;
+          if (pp >= 0) hl[co] = (__bf16)h;
         }
       if constexpr (!(ABL & 2)) {
 #pragma unroll
@@ -464,6 +507,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       __builtin_amdgcn_sched_barrier(0);   // one column block at a time (register pressure)
     }
     barrier_lds();   // h_t image and x_{t+1} image complete (this wave's DMA retired under its h-part A loads)
+    AAA_FW_STAMP(t, 4);
     // h_t (bf16, this workgroup's channels) into XH slot t+1 (the weight-gradient operand), from the image
     const size_t rown = rowt + M;   // slot t+1
     constexpr int HC = 16 / G;      // 16-B chunks (8 channels) per pixel of this workgroup
@@ -471,7 +515,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
       for (int i = tid; i < Pb * HC; i += 256) {
         const int px = pix0 + i / HC, q = i % HC;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hsw(px, q)), rs,
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
                                                (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, kSC1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -482,13 +526,13 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
         const int px = i / HC, q = i % HC;
         *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
-            *reinterpret_cast<const u32x4*>(him + hsw(px, q));
+            *reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8);
       }
     } else {   // the partner reads these: sc1 stores (write through to the coherent level)
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
       for (int i = tid; i < P * HC; i += 256) {
         const int px = i / HC, q = i % HC + HC * kh;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hsw(px, q)), rs,
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
                                                (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, (ABL & 16) ? 0 : kSC1);
       }
       // publish h_t's half: every wave's stores retired, a barrier, then one
@@ -503,6 +547,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         __hip_atomic_store(p.flags + 2 * b + kh, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    AAA_FW_STAMP(t, 5);
   }
 }
 
@@ -521,6 +566,7 @@ template <typename GT>
 inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStream_t st) {
   if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (G != 1 && G != 2)) return hipErrorInvalidValue;
   RecFwdParams<GT> q = p;
+  rec_columns(p.h, p.w, q.colpp, q.colhb);
   if (G == 2) {
     if (!p.flags || !p.report || p.spin < 0) return hipErrorInvalidValue;
     const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_frames<GT, 2, 0>);

@@ -34,6 +34,8 @@ constexpr int kBwKS = 4608 / 16;   // k steps: 4 chunks x 9 taps x 8 groups of 1
 constexpr int kBwPD = 4;           // A register slots (PD-1 k steps in flight); divides 8
 constexpr int kBwPD2 = 8;          // the paired kernel's (3 MFMAs per k step: twice the k steps in flight)
 constexpr int kBwKSP = kBwKS + kBwPD2 - 1;   // packed k steps per row block: the first PD2-1 repeated at the end
+constexpr int kBwIP = 136;         // chunk image pixel pitch (bf16) of the unswizzled images: 128 rows + 8 pad (272 B)
+constexpr int kBwIB = 46080;       // unswizzled chunk image bytes: 169 px x 272 B rounded up to whole 1-KB DMA pieces
 
 // k step ks -> k of the dgrad GEMM (k = tap*512 + gate row)
 __host__ __device__ constexpr int bw_k(int ks) { return ((ks % 72) >> 3) * 512 + (ks / 72) * 128 + (ks & 7) * 16; }
@@ -86,20 +88,35 @@ struct RecBwdParams {
   int stagger;            // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
 };
 
-// Chunk images of the single-workgroup and band kernels: image pixel ip (a
-// (rows+2) x (w+2) zero-bordered grid) holds its 16 row groups of 8 bf16 at
-// 16-B slots s ^ bw_fz(ip) of a 256-B row, bw_fz = the pixel's index with the
-// two border columns of every image row skipped (mod 16).  A B-fragment read
-// of 16 consecutive GEMM columns (pixels in raster order, any tap) then covers
-// 16 consecutive bw_fz values across grid-row ends: each ds_read_b128 lane
-// group (MI355X_MICROARCH: 4 x 16 lanes) hits 16 distinct bank groups.  (A
-// 272-B pitch instead puts pixel ip at slot ip mod 16 and collides where a
-// column group crosses a row end: 0.53 conflicts per LDS access at C3.)
+// Chunk images of the band kernel: image pixel ip (a (rows+2) x (w+2)
+// zero-bordered grid) holds its 16 row groups of 8 bf16 at 16-B slots
+// s ^ bw_fz(ip) of a 256-B row, bw_fz = the pixel's index with the two border
+// columns of every image row skipped (mod 16): 184 pixels of a band image fit
+// two images and the dc carry in the LDS only at a 256-B pitch, and a
+// B-fragment read of 16 consecutive GEMM columns then covers 16 consecutive
+// bw_fz values across grid-row ends (each ds_read_b128 lane group hits 16
+// distinct bank groups).  The single-workgroup kernel keeps the 272-B pitch
+// (slot ip mod 16 + s; conflicting where a column group crosses a row end):
+// the swizzle's XOR addressing (no immediate offsets) measured slower there
+// (C3 BPTT 1340 -> 1358 us, C4 paired 756 -> 790; profiles/r03/ab/swizzle.txt).
 __device__ __forceinline__ int bw_fz(int ip, int W2) { return (ip - 2 * (ip / W2)) & 15; }
 constexpr int kBwIBS = 47104;   // swizzled chunk image bytes: 184 px x 256 B (46 whole 1-KB DMA pieces)
 
+#ifdef AAA_STAMPS
+// Diagnostic builds only (tools/ubench/bwband): per (workgroup, step) phase stamps
+// (s_memrealtime, 100 MHz): step start, halo in, chunks 0..3 done, dx stored, epilogue done.
+__device__ uint64_t aaa_bw_stamps[1024 * 64 * 8];
+#define AAA_BW_STAMP(t, k)                                                                                    \
+  do {                                                                                                        \
+    if (tid == 0 && (t) < 64) aaa_bw_stamps[((size_t)blockIdx.x * 64 + (t)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AAA_BW_STAMP(t, k) do {} while (0)
+#endif
+
 // ABL (diagnostic A/B only: AAA_RECB_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
-// bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA.
+// bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA, bit 4 = no halo exchange (band),
+// bit 5 = no dZ stores (epilogue loads kept), bit 6 = no epilogue loads (dZ stores kept).
 //
 // BAND: 21x21 grids (168x168 frames) do not fit one workgroup's images, so
 // kRecBands workgroups split a frame by whole grid rows (recur.h band mode:
@@ -111,8 +128,10 @@ constexpr int kBwIBS = 47104;   // swizzled chunk image bytes: 184 px x 256 B (4
 // sc1 loads into the halo rows; chunks 2 and 3 come whole, halo rows included,
 // by LDS-DMA with the sc1 policy.  The bands of a frame get block indices of
 // equal residue mod 8 (one XCD under round-robin placement).
-template <int ABL = 0, bool BAND = false>
+template <int ABL = 0, bool BAND = false, bool DOACC = !BAND>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
+  constexpr bool SWZ = BAND;             // swizzled 256-B pixel rows (band) or 272-B rows
+  constexpr int PIT = SWZ ? 256 : 272;   // image pixel pitch (bytes)
   __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBS];   // chunk images (0: chunks 0, 2; 1: 1, 3)
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];          // dc carry, lane-native [wave][g*4+cb][lane]
   int b = (int)blockIdx.x, band = 0, r0 = 0, r1 = p.h;   // band mode: this workgroup's grid rows [r0, r1)
@@ -142,10 +161,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto dma_chunk = [&](int t, int c) {
     const __amdgpu_buffer_rsrc_t rs =
         make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
-    for (int i = wave; i < (NPH + 3) >> 2; i += 4) {
-      const int sl = i * 64 + lane, ip = sl >> 4, iy = ip / W2, ix = ip - iy * W2;
-      const int py = r0 + iy - 1, px = ix - 1, lq = (sl & 15) ^ ((ip - 2 * iy) & 15);
-      const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
+    for (int i = wave; i < (SWZ ? (NPH + 3) >> 2 : kBwIB / 1024); i += 4) {
+      const int sl = i * 64 + lane, ip = SWZ ? sl >> 4 : sl / 17, iy = ip / W2, ix = ip - iy * W2;
+      const int q = SWZ ? sl & 15 : sl - 17 * ip;   // 16-B slot of the pixel row (17: the pad)
+      const int py = r0 + iy - 1, px = ix - 1, lq = SWZ ? q ^ ((ip - 2 * iy) & 15) : q;
+      const bool v = (SWZ || q < 16) && ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
       const uint32_t vo = v ? (uint32_t)(((py * p.w + px) * 512 + 128 * c + lq * 8) * 2) : kOOB;
       if constexpr (BAND) dma16_sc1(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
       else dma16(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
@@ -190,20 +210,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
   for (int i = 0; i < 16; ++i) xbs[i] = 0.f;
 
-  // The epilogue's HBM inputs of one unit u = (g, cb) (g-major): dO and c_{s-1}
-  // (16 B each) and the 16 fp16 gates (32 B) of the lane's 4 channels at one pixel;
-  // c_s = f c_{s-1} + i c~ is recomputed from them (not read: 16 B less per unit).
-  // A ring of kRing units is in flight: the first kRing-1 are requested under the
-  // GEMM's last chunk, each later one as the unit kRing-1 before it is processed.
+  // The epilogue's HBM inputs of one unit u = (g, cb) (g-major): c_{s-1} (16 B)
+  // and the 16 fp16 gates (32 B) of the lane's 4 channels at one pixel; c_s =
+  // f c_{s-1} + i c~ is recomputed from them (not read).  A ring of kRing units is
+  // in flight: the first kRing-1 are requested under the GEMM's last chunk, each
+  // later one as the unit kRing-1 before it is processed.  DOACC: the
+  // attention-path grad dO_s is not in the ring but the initial value of the
+  // GEMM's accumulators (acc = dO_{t-1} + W^T dZ_t = dh_{t-1}), requested into
+  // each accumulator slot as soon as the epilogue before has consumed it (the
+  // band kernel keeps dO in the ring: its accumulators carried across steps
+  // spill there).
   struct EpIn { f32x4 dO, cp; u32x4 gt[2]; };
   constexpr int kRing = 4;
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
-    if (col < Pb && !(ABL & 2)) {
+    if (col < Pb && !(ABL & 66)) {
       const size_t row = (size_t)s * M + (size_t)b * P + pix0 + col;
       const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
-      in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
+      if constexpr (!DOACC) in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
       in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
       const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
       in.gt[0] = gp[0];
@@ -214,12 +239,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     return in;
   };
+  // dO_s of unit u into its accumulator slot (zero past the band's columns, or for s < 0: dh_{-1} has no dO)
+  auto load_dO = [&](f32x16 (&acc)[4], int s, int u, int ln) {
+    const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
+    f32x4 v{0.f, 0.f, 0.f, 0.f};
+    if (s >= 0 && col < Pb && !(ABL & 66))
+      v = *reinterpret_cast<const f32x4*>(p.dO + ((size_t)s * M + (size_t)b * P + pix0 + col) * 128 + 32 * wave +
+                                          4 * (ln >> 5) + 8 * g);
+    acc[cb][4 * g] = v[0]; acc[cb][4 * g + 1] = v[1]; acc[cb][4 * g + 2] = v[2]; acc[cb][4 * g + 3] = v[3];
+  };
 
-  // Gate backward of step s on the GEMM result (acc = dh_s from step s+1, zero
-  // for s = T-1): dZ_s to HBM (bf16) and, for chunks 0 and 1, into image w; the
-  // lane's dc carry advances to step s-1; gate-bias partials of step s.
+  // Gate backward of step s on dh_s = acc (dO_s + the GEMM of step s+1, dO_{T-1} +
+  // dhT for s = T-1): dZ_s to HBM (bf16) and, for chunks 0 and 1, into image w;
+  // the lane's dc carry advances to step s-1; gate-bias partials of step s; each
+  // consumed accumulator slot is refilled with dO_{s-1} (the next GEMM's start).
   // ``ring``: units 0 .. kRing-2 already requested.  BAND: then publishes dZ_s.
-  auto epilogue = [&](int s, const f32x16 (&acc)[4], bool gemm, EpIn (&ring)[kRing]) {
+  auto epilogue = [&](int s, f32x16 (&acc)[4], EpIn (&ring)[kRing], bool first) {
     int ln = lane;   // laundered: the epilogue's addresses are recomputed per step, not hoisted
     asm volatile("" : "+v"(ln));
     const int pl = ln & 31, hq = ln >> 5;
@@ -240,12 +275,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int col = cb * 32 + pl;
         if (col < Pb) {
           const int pp = pix0 + col;
-          f32x4 dh = in.dO;
-          if (gemm) {
-            dh[0] += acc[cb][4 * g]; dh[1] += acc[cb][4 * g + 1]; dh[2] += acc[cb][4 * g + 2]; dh[3] += acc[cb][4 * g + 3];
-          } else if (p.dhT) {
-            const f32x4 x = *reinterpret_cast<const f32x4*>(p.dhT + ((size_t)b * P + pp) * 128 + ch);
-            dh[0] += x[0]; dh[1] += x[1]; dh[2] += x[2]; dh[3] += x[3];
+          f32x4 dh{acc[cb][4 * g], acc[cb][4 * g + 1], acc[cb][4 * g + 2], acc[cb][4 * g + 3]};
+          if constexpr (!DOACC) {
+            dh[0] += in.dO[0]; dh[1] += in.dO[1]; dh[2] += in.dO[2]; dh[3] += in.dO[3];
+            if (first && p.dhT) {
+              const f32x4 x = *reinterpret_cast<const f32x4*>(p.dhT + ((size_t)b * P + pp) * 128 + ch);
+              dh[0] += x[0]; dh[1] += x[1]; dh[2] += x[2]; dh[3] += x[3];
+            }
           }
           f32x4* dcp = dcl + wave * 16 * 64 + ln + (g * 4 + cb) * 64;
           f32x4 dc = *dcp;
@@ -266,18 +302,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           bf16x8 z0, z1;
 #pragma unroll
           for (int i = 0; i < 8; ++i) { z0[i] = (__bf16)dz[i]; z1[i] = (__bf16)dz[8 + i]; }
-          if constexpr (!(ABL & 2)) {
+          if constexpr (!(ABL & 34) && BAND) {   // the neighbour bands read these: sc1 stores
             const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, BAND ? kSC1 : 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, BAND ? kSC1 : 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, kSC1);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, kSC1);
+          } else if constexpr (!(ABL & 34)) {
+            __bf16* zo = p.dZ + (rows + pp) * 512 + 4 * ch;
+            *reinterpret_cast<bf16x8*>(zo) = z0;
+            *reinterpret_cast<bf16x8*>(zo + 8) = z1;
           }
           if (wave < 2) {   // chunk w of the next step's B operand: rows 4(ch - 32w) + gate = slots 4g + 2hq, +1
-            unsigned char* zi = zim + wave * kBwIBS + hidx(pp) * 256;
-            const int fz = (col + p.w + 1) & 15, s0 = 4 * g + 2 * hq;
+            unsigned char* zi = zim + wave * kBwIBS + hidx(pp) * PIT;
+            const int fz = SWZ ? (col + p.w + 1) & 15 : 0, s0 = 4 * g + 2 * hq;
             *reinterpret_cast<bf16x8*>(zi + ((s0 ^ fz) << 4)) = z0;
             *reinterpret_cast<bf16x8*>(zi + (((s0 + 1) ^ fz) << 4)) = z1;
           }
         }
+        if constexpr (DOACC) load_dO(acc, s - 1, u, ln);   // the slot's next value: dO_{s-1}
         __builtin_amdgcn_sched_barrier(0);
       }
       // gate-bias partials of channel group g: butterfly transpose-reduce of the 16
@@ -311,26 +352,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   };
 
   if ((b >> 3) & 1) stagger_wait(p.stagger);
+  f32x16 acc_carry[4];   // DOACC: the GEMM accumulators, carried across steps (dO_{t-1} at the start of step t's GEMM)
   {  // step T-1: no GEMM (dh = dO_{T-1} + dhT)
-    f32x16 zero[4];
+    f32x16 (&acc)[4] = acc_carry;
     EpIn ring[kRing];
 #pragma unroll
     for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(p.T - 1, u, lane);
-    epilogue(p.T - 1, zero, false, ring);
+    if constexpr (DOACC) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        load_dO(acc, p.T - 1, u, lane);
+        const int g = u >> 2, cb = u & 3, col = cb * 32 + r32;
+        if (p.dhT && col < Pb) {
+          const f32x4 x =
+              *reinterpret_cast<const f32x4*>(p.dhT + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh);
+          acc[cb][4 * g] += x[0]; acc[cb][4 * g + 1] += x[1]; acc[cb][4 * g + 2] += x[2]; acc[cb][4 * g + 3] += x[3];
+        }
+      }
+    } else {   // dO (ring) and dhT (epilogue) are added in the epilogue
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+    }
+    epilogue(p.T - 1, acc, ring, true);
   }
   barrier_lds();   // chunk images 0, 1 of dZ_{T-1}
 
   for (int t = p.T - 1; t >= 0; --t) {
-    if constexpr (BAND) {   // the neighbours' boundary rows of dZ_t, chunks 0 and 1, into the halo rows
-      if (tid == 0) {
-        if (band > 0) pair_wait(p.flags + b * kRecBands + band - 1, p.T - t, p.report, p.spin);
-        if (band < kRecBands - 1) pair_wait(p.flags + b * kRecBands + band + 1, p.T - t, p.report, p.spin);
-      }
+    AAA_BW_STAMP(t, 0);
+    if constexpr (BAND && !(ABL & 16)) {   // the neighbours' boundary rows of dZ_t, chunks 0 and 1, into the halo rows
+      if (wave == 0)   // the neighbour bands' flags, both in one poll
+        wave_wait_flags(p.flags + b * kRecBands,
+                        ((band > 0 ? 1ull : 0ull) << (band - 1 + (band == 0))) | (band < kRecBands - 1 ? 2ull << band : 0ull),
+                        p.T - t, p.report, p.spin);
       barrier_lds();
       const __amdgpu_buffer_rsrc_t rs =
           make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
       const int nh = p.w * 16;   // 16-B pieces of one grid row of one chunk
-      constexpr int NHL = 6;     // pieces per thread in flight
+      constexpr int NHL = 3;     // pieces per thread in flight
       for (int i0 = 0; i0 < 4 * nh; i0 += 256 * NHL) {
         u32x4 v[NHL];
 #pragma unroll
@@ -353,11 +413,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
       barrier_lds();
     }
-    f32x16 acc[4], accx[2];
+    AAA_BW_STAMP(t, 1);
+    f32x16 acc_local[4];
+    f32x16 (&acc)[4] = *(DOACC ? &acc_carry : &acc_local);
+    if constexpr (!DOACC) {
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
+      for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+        for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+    }
+    f32x16 accx[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -372,17 +437,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     // transposed gather: output pixel q reads dZ at q - d(tap): image offset (2-ky)*W2 + (2-kx),
     // bw_fz offset (2-ky)*w + (2-kx).  Per tap and column block: the byte address of the
     // lane's pixel row or'ed with its swizzled slot for c16 = 0; row group c16 xors in c16 << 5.
+    // (unswizzled: the lane's part hbs * PIT + hh * 16 is per step, the tap's offset wave-uniform, the row
+    // group an immediate; tb then carries the tap offset only)
     auto bases = [&](int tap, int (&tb)[4]) {
       const int ky = tap / 3, kx = tap - 3 * ky;
       const int toff = (2 - ky) * W2 + (2 - kx), tf = (2 - ky) * p.w + (2 - kx);
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) tb[cb] = ((hbs[cb] + toff) << 8) | (((((fbs[cb] + tf) & 15) ^ hh)) << 4);
+      for (int cb = 0; cb < 4; ++cb)
+        tb[cb] = SWZ ? ((hbs[cb] + toff) << 8) | (((((fbs[cb] + tf) & 15) ^ hh)) << 4) : toff * PIT;
     };
     auto ldb = [&](const unsigned char* img, const int (&tb)[4], int c16, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(img + (tb[cb] ^ (c16 << 5)));
+      for (int cb = 0; cb < 4; ++cb)
+        bf[cb] = SWZ ? *reinterpret_cast<const bf16x8*>(img + (tb[cb] ^ (c16 << 5)))
+                     : *reinterpret_cast<const bf16x8*>(img + tb[0] + hbs[cb] * PIT + hh * 16 + c16 * 32);
     };
-    constexpr int BD = 4;   // B fragment ring: BD-1 k steps of lookahead (LDS latency vs 4 MFMAs per k step)
+    constexpr int BD = 4;   // B fragment ring: BD-1 k steps of lookahead (LDS latency vs 4 MFMAs per k step); divides 8
     bf16x8 bfr[BD][4];
     EpIn ring[kRing];
     // the K loop, with the wave's dx column blocks XC, XC+1 a compile-time constant
@@ -439,6 +509,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           for (int cb = 0; cb < 4; ++cb) tcur[cb] = tnxt[cb];
         }
         barrier_lds();   // image ck & 1 free; (ck >= 1) the DMA'd chunk ck+1 has landed in every wave
+        AAA_BW_STAMP(t, 2 + ck);
       }
     };
     if (wave >> 1) kloop(std::integral_constant<int, 2>{});
@@ -460,8 +531,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
       }
     }
+    AAA_BW_STAMP(t, 6);
     if (t > 0) {
-      epilogue(t - 1, acc, true, ring);
+      epilogue(t - 1, acc, ring, false);
     } else if (p.dh0) {   // dh_{-1}: the gradient of the initial state h0
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
@@ -474,6 +546,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       }
     }
     barrier_lds();   // chunk images 0, 1 of dZ_{t-1} complete
+    AAA_BW_STAMP(t, 7);
   }
   {  // conv2 bias partials: reduce the 16 x-channel sums over the 32 pixel lanes of each half
     float v[16];
@@ -528,7 +601,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 // Launched as one residency wave (launch_resident); the spins are bounded and reported.
 template <int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_pairs(RecBwdParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBS];   // chunk images (c & 1), bw_fz-swizzled
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (c & 1)
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 8 * 64];          // dc carry, lane-native [wave][g*2+j][lane]
   const int b = (int)blockIdx.x % p.B, kh = (int)blockIdx.x / p.B;
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -542,7 +615,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 
   {  // zero the images (borders and pads stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < 2 * kBwIBS / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < 2 * kBwIB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   // the partner's chunk c of dZ_t: sc1 loads of the P x 256 B into registers
   // (issued at the start of a chunk), then into image c & 1 (three taps later)
@@ -561,17 +634,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
     for (int r = 0; r < NPR; ++r) {
       const int i = tid + 256 * r, px = i >> 4, q = i & 15;
-      if (px < P)
-        *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIBS + hidx(px) * 256 + ((q ^ ((px + p.w + 1) & 15)) << 4)) = v[r];
+      if (px < P) *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIB + hidx(px) * (kBwIP * 2) + q * 16) = v[r];
     }
   };
 
-  int hb[2], fb[2];   // top-left image pixel of the lane's window per column block, and its bw_fz (= the pixel)
+  int hb[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int pp = min((cbA + j) * 32 + r32, P - 1);
     hb[j] = (pp / p.w) * W2 + pp % p.w;
-    fb[j] = pp;
   }
   // dc carry of the lane's 32 (channel, pixel) pairs: channels 32hrb + 8g + 4hh + e at pixel 32(cbA+j) + r32
   f32x4* dcw = dcl + wave * 8 * 64 + lane;   // + (g*2 + j) * 64
@@ -673,10 +744,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, kSC1);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, kSC1);
-          unsigned char* zi = zim + (wave & 1) * kBwIBS + hidx(pp) * 256;
-          const int fz = (pp + p.w + 1) & 15, s0 = 4 * g + 2 * hq;   // rows 4(ch - 32 hrb) + gate
-          *reinterpret_cast<bf16x8*>(zi + ((s0 ^ fz) << 4)) = z0;
-          *reinterpret_cast<bf16x8*>(zi + (((s0 + 1) ^ fz) << 4)) = z1;
+          unsigned char* zi = zim + (wave & 1) * kBwIB + hidx(pp) * (kBwIP * 2) + (4 * (ch - 32 * hrb)) * 2;
+          *reinterpret_cast<bf16x8*>(zi) = z0;
+          *reinterpret_cast<bf16x8*>(zi + 16) = z1;
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -721,22 +791,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) accx[e] = 0.f;
-    int hbs[2], fbs[2];
+    int hbs[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       hbs[j] = hb[j];
-      fbs[j] = fb[j];
-      asm volatile("" : "+v"(hbs[j]), "+v"(fbs[j]));
+      asm volatile("" : "+v"(hbs[j]));
     }
-    auto bases = [&](int tap, int (&tb)[2]) {   // as the single-workgroup kernel's
-      const int ky = tap / 3, kx = tap - 3 * ky;
-      const int toff = (2 - ky) * W2 + (2 - kx), tf = (2 - ky) * p.w + (2 - kx);
+    auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + (2 - tap % 3); };
+    auto ldb = [&](const unsigned char* img, int toff, int c16, bf16x8 (&bf)[2]) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) tb[j] = ((hbs[j] + toff) << 8) | (((((fbs[j] + tf) & 15) ^ hh)) << 4);
-    };
-    auto ldb = [&](const unsigned char* img, const int (&tb)[2], int c16, bf16x8 (&bf)[2]) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = *reinterpret_cast<const bf16x8*>(img + (tb[j] ^ (c16 << 5)));
+      for (int j = 0; j < 2; ++j)
+        bf[j] = *reinterpret_cast<const bf16x8*>(img + (hbs[j] + toff) * (kBwIP * 2) + c16 * 32 + hh * 16);
     };
     constexpr int BD = 4;
     bf16x8 bfr[BD][2];
@@ -746,7 +811,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll 1
       for (int ck = 0; ck < 4; ++ck) {
         const int c = (ck + 2 * kh) & 3;   // own chunks first, then the partner's
-        const unsigned char* img = zim + (c & 1) * kBwIBS;
+        const unsigned char* img = zim + (c & 1) * kBwIB;
         u32x4 pv[NPR];
         const bool refill = ck == 1 || ck == 2;   // the partner's chunk c+1 into the image chunk ck-1 freed
         if (refill) pld(t, (c + 1) & 3, pv);
@@ -756,12 +821,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
           for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(t - 1, u, ln);
         }
-        int tcur[2], tnxt[2];
-        bases(0, tcur);
 #pragma unroll
-        for (int j = 0; j < BD - 1; ++j) ldb(img, tcur, j, bfr[j]);
+        for (int j = 0; j < BD - 1; ++j) ldb(img, tapoff(0), j, bfr[j]);
         for (int tap = 0; tap < 9; ++tap) {
-          if (tap < 8) bases(tap + 1, tnxt);
+          const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
           int kt = c * 72 + tap * 8;
           asm volatile("" : "+s"(kt));
           if (refill && tap == 3) pst((c + 1) & 3, pv);
@@ -773,8 +836,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             {
               const int cn = c16 + BD - 1;
-              if (cn < 8) ldb(img, tcur, cn, bfr[cn % BD]);
-              else if (tap < 8) ldb(img, tnxt, cn - 8, bfr[cn % BD]);
+              if (cn < 8) ldb(img, toff, cn, bfr[cn % BD]);
+              else if (tap < 8) ldb(img, tn, cn - 8, bfr[cn % BD]);
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -783,8 +846,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             accx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[c16 % PD][1], bfr[c16 % BD][XJ], accx, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
           }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) tcur[j] = tnxt[j];
         }
         if (ck == 0 && tid == 0) {   // the partner's dZ_t published? (the other waves load after the barrier)
           pair_wait(p.flags + 2 * b + (1 - kh), p.T - t, p.report, p.spin);
@@ -872,6 +933,7 @@ inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {
 #define AAA_RECB_CASE(a) \
   case a: hipLaunchKernelGGL((k_convlstm_bwd_frames<a>), dim3(p.B), dim3(256), 0, st, p); return hipGetLastError();
     AAA_RECB_CASE(1) AAA_RECB_CASE(2) AAA_RECB_CASE(3) AAA_RECB_CASE(4) AAA_RECB_CASE(8) AAA_RECB_CASE(6)
+    AAA_RECB_CASE(32) AAA_RECB_CASE(64)
 #undef AAA_RECB_CASE
     default: break;
   }
@@ -888,8 +950,19 @@ inline hipError_t convlstm_bwd_band(const RecBwdParams& p, hipStream_t st) {
   if (!bw_band_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
     return hipErrorInvalidValue;
   RecBwdParams q = p;
-  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_frames<0, true>),
-                         8 * kRecBands * ((p.B + 7) / 8), 256, q, st);
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_frames<0, true>);
+#ifdef AAA_ABLATION   // diagnostic builds only
+  const char* e = getenv("AAA_RECB_ABL");
+  switch (e ? atoi(e) : 0) {
+#define AAA_RECB_BCASE(a) \
+  case a: k = reinterpret_cast<const void*>(&k_convlstm_bwd_frames<a, true>); break;
+    AAA_RECB_BCASE(1) AAA_RECB_BCASE(2) AAA_RECB_BCASE(4) AAA_RECB_BCASE(8) AAA_RECB_BCASE(16) AAA_RECB_BCASE(6)
+    AAA_RECB_BCASE(18) AAA_RECB_BCASE(32) AAA_RECB_BCASE(64)
+#undef AAA_RECB_BCASE
+    default: break;
+  }
+#endif
+  return launch_resident(k, 8 * kRecBands * ((p.B + 7) / 8), 256, q, st);
 }
 
 }  // namespace aaa

@@ -284,12 +284,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     barrier_lds();
     if (tid == 0) __hip_atomic_store(p.flags + b * G + kh, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every wave waits for the seven partners, then sums their partials into its groups
-    if constexpr (!(ABL & 1)) {
-      if (lane == 0)
-        for (int j = 0; j < G; ++j)
-          if (j != kh) pair_wait(p.flags + b * G + j, it + 1, p.report, p.spin);
-    }
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (!(ABL & 1)) wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), it + 1, p.report, p.spin);
     AAA_B32_STAMP(it, 2);
     f32x4 dhv[NG];
 #pragma unroll

@@ -245,10 +245,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
     const bool exch = G > 1 && t > 0 && !(ABL & 4);
     AAA_F32_STAMP(t, 0);
     auto partner_issue = [&] {
-      if (lane == 0)
-        for (int j = 0; j < G; ++j)
-          if (j != kh) pair_wait(p.flags + b * G + j, t, p.report, p.spin);
-      __builtin_amdgcn_wave_barrier();
+      wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), t, p.report, p.spin);
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
 #pragma unroll
       for (int n = 0; n < NPL; ++n) {

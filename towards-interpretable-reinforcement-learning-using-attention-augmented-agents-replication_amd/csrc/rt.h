@@ -24,6 +24,7 @@
 #include "halo.h"
 #include "recur.h"
 #include "recur_bwd.h"
+#include "recur_bwd_split.h"
 #include "recur_f32.h"
 #include "recur_bwd_f32.h"
 #include "vision.h"

@@ -617,8 +617,11 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                                     "fp16 gates", L.T, fb)
                              : strf("bf16 frame-resident BPTT + dx, %d steps per launch, %d WG per frame, fp16 gates",
                                     L.T, fb));
+          // AAA_BWD_SPLIT=1: the split-role kernel (recur_bwd_split.h) for G = 1 and band mode
+          const bool split = fb != 2 && env_int("AAA_BWD_SPLIT", 0);
           HIPCHK(fb == 2 ? convlstm_bwd_pairs(rp, st)
-                         : (fb == 1 ? convlstm_bwd_frames(rp, st) : convlstm_bwd_band(rp, st)));
+                         : split ? convlstm_bwd_split(rp, fb != 1, st)
+                                 : (fb == 1 ? convlstm_bwd_frames(rp, st) : convlstm_bwd_band(rp, st)));
         }
         HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
         dx_fused = true;

@@ -323,15 +323,21 @@ int device_cus() {   // per device ordinal, queried once
   }
   return cus[dev];
 }
-// Workgroups per frame of the frame-resident kernels (0: per-step launches):
-// 1 once the batch fills most of the CUs, 2 (paired workgroups) while two per
-// frame still fit the chip, else the per-step kernels.  AAA_FRAMES_FWD /
-// AAA_FRAMES_BWD = 0 / 1 / 2 force it.
+// Workgroups per frame of the frame-resident kernels (0: per-step launches).
+// Every frame-resident workgroup holds more than half a CU's LDS, so the chip
+// has exactly one slot per CU (launch_resident re-checks the occupancy of the
+// paired kernels).  G = 1 once the frames fill at least 5/8 of the slots (the
+// measured crossover against the per-step launches: C3's B = 256 on 256 CUs
+// 55 vs 79 us per step, B = 128 49 vs 43, profiles/r02/frames); G = 2 (paired)
+// while both workgroups of every frame fit one residency wave and they still
+// occupy at least a quarter of the slots; else the per-step kernels.
+// AAA_FRAMES_FWD / AAA_FRAMES_BWD = 0 / 1 / 2 force it.
+static_assert(2 * kBwIBS + 4 * 16 * 64 * 16 > 160 * 1024 / 2, "one frame-resident workgroup per CU");
 int frames_g(const Layout& L, const char* env) {
   if (L.dt != AAA_BF16 || !rec_fits(L.h, L.w)) return 0;
-  const int cus = device_cus();
-  const int v = env_int(env, L.B >= (cus * 5) / 8 ? 1 : (L.B >= 32 && 2 * L.B <= cus ? 2 : 0));
-  return v == 1 ? 1 : (v == 2 && 2 * L.B <= cus ? 2 : 0);
+  const int slots = device_cus();
+  const int v = env_int(env, 8 * L.B >= 5 * slots ? 1 : (8 * L.B >= slots && 2 * L.B <= slots ? 2 : 0));
+  return v == 1 ? 1 : (v == 2 && 2 * L.B <= slots ? 2 : 0);
 }
 int frames_fwd(const Layout& L) { return frames_g(L, "AAA_FRAMES_FWD"); }
 // bf16 forward on the band-mode frame-resident kernel (recur.h BAND): grids too
