@@ -3,6 +3,7 @@
 // on the LDS-DMA ring with transposed fragment reads (runtime.hip
 // AAA_WGRAD_PIPE), with parts removed (glds.h ABL bits).  Diagnostic only.
 //   tools/ubench/build.sh wgrad_ablate.hip && tools/ubench/wgrad_ablate [B] [T]
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 #include "glds.h"
@@ -52,6 +53,21 @@ static void run(const char* name, const __bf16* dz, const __bf16* xh, float* out
   });
   const double flop = 2.0 * 512 * 1728 * rows;
   printf("%-44s %9.1f us  %7.1f TF/s\n", name, us, flop / (us * 1e-6) / 1e12);
+#ifdef AAA_STAMPS
+  // medians over workgroups of the last launch: prologue, K loop, epilogue (us)
+  const int nwg = grid.x * grid.y * grid.z;
+  std::vector<uint64_t> st((size_t)nwg * 4);
+  CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(aaa_stamps), st.size() * 8));
+  std::vector<double> ph[3];
+  uint64_t t0 = ~0ull, t3 = 0;
+  for (int i = 0; i < nwg; ++i) {
+    for (int k = 0; k < 3; ++k) ph[k].push_back((double)(st[i * 4 + k + 1] - st[i * 4 + k]) * 0.01);
+    t0 = std::min(t0, st[i * 4]); t3 = std::max(t3, st[i * 4 + 3]);
+  }
+  for (auto& v : ph) std::sort(v.begin(), v.end());
+  printf("    phases (median / max us): prologue %.1f/%.1f  K loop %.1f/%.1f  epilogue %.1f/%.1f  | span %.1f\n",
+         ph[0][nwg / 2], ph[0].back(), ph[1][nwg / 2], ph[1].back(), ph[2][nwg / 2], ph[2].back(), (t3 - t0) * 0.01);
+#endif
 }
 
 int main(int argc, char** argv) {
@@ -60,23 +76,16 @@ int main(int argc, char** argv) {
   __bf16* dz = dev_rand((size_t)rows * 512, 1.f, 3);
   __bf16* xh = dev_rand((size_t)rows * 192, 1.f, 10);
   float* out; CK(hipMalloc(&out, (size_t)512 * 1728 * 4));
-  using C8 = GemmCfg<__bf16, 256, 256, 64, 2, 4>;
-  run<C8, 2, 0>("256x256 8w ring2 (production)", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 0>("256x256 8w ring2, 512 WGs", dz, xh, out, rows, h, w, 512);
-  run<C8, 2, 0, 1>("256x256 ring2 ILV1 (A first, B last)", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 0, 2>("256x256 ring2 ILV2 (spread)", dz, xh, out, rows, h, w, 256);
   using C8k = GemmCfg<__bf16, 256, 256, 32, 2, 4>;
+  run<C8k, 4, 0, 2>("256x256 BK32 ring4 ILV2 (production)", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 0, 2>("256x256 BK32 ring4 ILV2 (production, again)", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 4, 2>("  no epilogue", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 1, 2>("  no in-loop DMA", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 2, 2>("  no MFMA (DMA + fragment reads)", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 5, 2>("  MFMA + fragment reads only", dz, xh, out, rows, h, w, 256);
+  run<C8k, 4, 3, 2>("  skeleton (no DMA, no MFMA)", dz, xh, out, rows, h, w, 256);
   run<C8k, 3, 0, 2>("256x256 BK32 ring3 ILV2", dz, xh, out, rows, h, w, 256);
-  run<C8k, 4, 0, 2>("256x256 BK32 ring4 ILV2", dz, xh, out, rows, h, w, 256);
-  run<C8k, 3, 0, 0>("256x256 BK32 ring3", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 4>("256x256 no epilogue", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 1>("256x256 no in-loop DMA", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 2>("256x256 no MFMA (DMA + fragment reads)", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 5>("256x256 MFMA + fragment reads only", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 3>("256x256 skeleton (no DMA, no MFMA)", dz, xh, out, rows, h, w, 256);
-  run<C8, 2, 7>("256x256 skeleton, no epilogue", dz, xh, out, rows, h, w, 256);
-  using C4 = GemmCfg<__bf16, 128, 128, 64, 2, 2>;
-  run<C4, 2, 0>("128x128 4w ring2, 512 WGs", dz, xh, out, rows, h, w, 512);
-  run<C4, 2, 5>("128x128 MFMA + fragment reads only", dz, xh, out, rows, h, w, 512);
+  using C8 = GemmCfg<__bf16, 256, 256, 64, 2, 4>;
+  run<C8, 2, 0, 2>("256x256 BK64 ring2 ILV2", dz, xh, out, rows, h, w, 256);
   return 0;
 }

@@ -49,6 +49,22 @@ __device__ __forceinline__ void dma16_sc1(__amdgpu_buffer_rsrc_t r, const void* 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_vptr)(const_cast<void*>(lds)), 16, (int)voff, 0, 0, 16);
 }
 
+// The same issued from inline asm, for loaders whose consumer waits with its
+// own counted vmcnt (gemm_pipe_kernel): the compiler does not see the LDS
+// write, so it cannot insert the vmcnt(0) it otherwise places before the
+// first LDS read after an LDS-DMA (which drains every tile still in flight
+// and reduces the ring to one stage of latency cover).  M0 carries the
+// wave-uniform LDS destination (an M0 operand, so the compiler sets it);
+// s_nop 0 covers the M0 -> LDS-DMA hazard.
+__device__ __forceinline__ void dma16a(__amdgpu_buffer_rsrc_t r, const void* lds, uint32_t voff, int soff = 0) {
+  __builtin_assume(lds != nullptr);   // no generic-null select on the address-space cast
+  const int m = __builtin_amdgcn_readfirstlane((int)(size_t)(lds_vptr)(const_cast<void*>(lds)));
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               :
+               : "v"(voff), "s"(r), "s"(soff), "{m0}"(m)
+               : "memory");
+}
+
 // Epilogues with a split prefetch()/finish() (EP::Pre) have their global
 // inputs loaded before the K loop, so the loads' latency hides under it.
 template <class EP, class = void> struct has_pre : std::false_type {};
@@ -120,7 +136,7 @@ struct GRowsB {
   __device__ __forceinline__ void issue(T* lds, int k0) {
     const int ko = __builtin_amdgcn_readfirstlane(k0 * (int)sizeof(T));
 #pragma unroll
-    for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, voff[c], ko);
+    for (int c = 0; c < PER; ++c) dma16a(rs, lds + c * NT * VG + wofs, voff[c], ko);
   }
 };
 
@@ -179,14 +195,14 @@ struct GIm2colB {
       }
       const int so = __builtin_amdgcn_readfirstlane(ci0 * (int)sizeof(T));
 #pragma unroll
-      for (int c = 0; c < PER; ++c) dma16(rs, lds + c * NT * VG + wofs, vo[c], so);
+      for (int c = 0; c < PER; ++c) dma16a(rs, lds + c * NT * VG + wofs, vo[c], so);
       return;
     }
     const int toff = tv + ci0;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const bool v = (vmask[c] >> (tap + dt[c])) & 1ull;
-      dma16(rs, lds + c * NT * VG + wofs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(T)) : kOOB);
+      dma16a(rs, lds + c * NT * VG + wofs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(T)) : kOOB);
     }
   }
 };
@@ -256,13 +272,17 @@ struct GRowsT {
     const int ko = __builtin_amdgcn_readfirstlane(k0 * rowbytes);
 #pragma unroll
     for (int c = 0; c < PER; ++c)
-      if (c % nparts == part) dma16(rs, lds + c * NT * VG + wofs, voff[c], ko);
+      if (c % nparts == part) dma16a(rs, lds + c * NT * VG + wofs, voff[c], ko);
   }
 };
 
 // Weight-gradient gather, staged RC: row = (tap, ci) fixed per piece, k =
 // output pixel (forward geometry, as LdIm2colTB).  Cin % VG == 0.  Pixels
 // past the source's frames fall outside src_bytes and land as zeros.
+// Consecutive issues advance k by BK (the pipe kernel's ring order), so each
+// piece carries its pixel's window origin (iy0, ix0) and source offset from
+// tile to tile with two carries (x wraps the row, y wraps the frame) instead
+// of decoding the pixel index with FastDivs every tile; start(k) seeds them.
 template <typename T, int R, int BK, int NT>
 struct GIm2colT {
   static constexpr bool KC = false;
@@ -276,6 +296,10 @@ struct GIm2colT {
   __amdgpu_buffer_rsrc_t rs;
   ConvGeo g;
   int kr[PER], ky[PER], kx[PER], toff[PER];
+  int iy0[PER], ix0[PER], off[PER];   // per piece: window origin and source element offset of its current pixel
+  // per-tile advance: BK = fq*HW + yq*Wout + xq (xq < Wout, yq < Hout), and the
+  // offset / origin steps of one x wrap and one y wrap
+  int dix, diy, doff, xlim, xw, xwoff, ylim, yw, ywoff;
   int wofs;
   __device__ static bool ok_shape(const ConvGeo& g) { return g.Cin % VG == 0 && !g.transposed; }
   __device__ __forceinline__ GIm2colT(const Params& p, int row0) : g(p.g) {
@@ -293,24 +317,51 @@ struct GIm2colT {
       kx[c] = tap - (int)g.dKW.div(tap) * g.KW;
       toff[c] = (ky[c] * g.Win + kx[c]) * g.cs + ci + g.coff;
     }
+    const int hw = g.Hout * g.Wout;
+    const int fq = BK / hw, rem = BK - fq * hw, yq = rem / g.Wout, xq = rem - yq * g.Wout;
+    const int xs = g.stride * g.cs, ys = g.stride * g.Win * g.cs, fs = g.Hin * g.Win * g.cs;
+    dix = xq * g.stride;
+    diy = yq * g.stride;
+    doff = fq * fs + yq * ys + xq * xs;
+    xlim = g.Wout * g.stride - g.pad;   // ix0 >= xlim: x wrapped
+    xw = g.Wout * g.stride;
+    xwoff = ys - g.Wout * xs;
+    ylim = g.Hout * g.stride - g.pad;
+    yw = g.Hout * g.stride;
+    ywoff = fs - g.Hout * ys;
   }
-  __device__ __forceinline__ void issue(T* lds, int k0) { issue_part(lds, k0, 0, 1); }
-  __device__ __forceinline__ void issue_part(T* lds, int k0, int part, int nparts) {
+  __device__ __forceinline__ void start(int k0) {
     const int hw = g.Hout * g.Wout;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
-      if (c % nparts != part) continue;
       const int m = k0 + kr[c];
       const int f = (int)g.dHW.div(m), pix = m - f * hw;
       const int oy = (int)g.dWout.div(pix), ox = pix - oy * g.Wout;
-      const int iy0 = oy * g.stride - g.pad, ix0 = ox * g.stride - g.pad;
-      const int iy = iy0 + ky[c], ix = ix0 + kx[c];
+      iy0[c] = oy * g.stride - g.pad;
+      ix0[c] = ox * g.stride - g.pad;
+      off[c] = ((f * g.Hin + iy0[c]) * g.Win + ix0[c]) * g.cs + toff[c];
+    }
+  }
+  __device__ __forceinline__ void issue(T* lds, int k0) { issue_part(lds, k0, 0, 1); }
+  __device__ __forceinline__ void issue_part(T* lds, int, int part, int nparts) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      if (c % nparts != part) continue;
+      const int iy = iy0[c] + ky[c], ix = ix0[c] + kx[c];
       const bool v = (unsigned)iy < (unsigned)g.Hin && (unsigned)ix < (unsigned)g.Win;
-      const int off = ((f * g.Hin + iy0) * g.Win + ix0) * g.cs + toff[c];
-      dma16(rs, lds + c * NT * VG + wofs, v ? (uint32_t)(off * (int)sizeof(T)) : kOOB);
+      dma16a(rs, lds + c * NT * VG + wofs, v ? (uint32_t)(off[c] * (int)sizeof(T)) : kOOB);
+      // next tile: k += BK
+      int nx = ix0[c] + dix, ny = iy0[c] + diy, no = off[c] + doff;
+      if (nx >= xlim) { nx -= xw; ny += g.stride; no += xwoff; }
+      if (ny >= ylim) { ny -= yw; no += ywoff; }
+      ix0[c] = nx; iy0[c] = ny; off[c] = no;
     }
   }
 };
+
+// Loaders whose per-piece state follows the k order seed it here (GIm2colT).
+template <class LD, class = void> struct has_start : std::false_type {};
+template <class LD> struct has_start<LD, std::void_t<decltype(std::declval<LD&>().start(0))>> : std::true_type {};
 
 // Fragments from an RC stage (same lane -> (row, k) map as frag_sw).
 template <int R>
@@ -339,6 +390,28 @@ __device__ __forceinline__ bf16x8 frag_rc(const __bf16* t, int r, int kofs) {
   const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
+// The same read with the lane's offsets precomputed: for a k offset kl + 16 j
+// (kl = the lane/wave part, j uniform) the XOR key lds_swz_rc depends on kl
+// only, so the two offsets are lane constants and the uniform 16 j R goes in
+// the address base (the reads' immediate offsets), not per-read VALU.
+struct RcOff { int o0, o1; };
+template <int R>
+__device__ __forceinline__ RcOff rc_off(int r, int kl) {
+  constexpr int RS = R / 8;
+  static_assert(RS < 8 || (RS >= 16 ? 1 : 16 / RS) <= 2, "swizzle key must not depend on the 16-k step");
+  const int li = (int)(threadIdx.x & 15), q = li >> 2, p = li & 3;
+  const int lc = (r - li + 4 * p) >> 3, e = 4 * (p & 1);
+  const int k0 = kl + q, k1 = k0 + 4;
+  return {k0 * R + ((lc ^ lds_swz_rc<RS>(k0)) << 3) + e, k1 * R + ((lc ^ lds_swz_rc<RS>(k1)) << 3) + e};
+}
+__device__ __forceinline__ bf16x8 frag_rc_at(const __bf16* t, const RcOff& o) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(t + o.o0)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const_cast<__bf16*>(t + o.o1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // Dispatch on the loader's stage layout.
 template <class LD, int R, int BK>
 __device__ __forceinline__ void frag_any(const float* t, int r, int kofs, float (&a)[8]) {
@@ -525,6 +598,8 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   typename PL::PreT pre[PL::PD];
   epilogue_prefetch<C, EP, PL>(ep, i0, j0, BJ, pre);
 
+  if constexpr (has_start<LA>::value) la.start(kb);
+  if constexpr (has_start<LB>::value) lb.start(kb);
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s)
     if (s < nk) {
@@ -532,6 +607,12 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       lb.issue(smem + s * STG + AEL, kb + s * BK);
     }
 
+  // lane offsets of the RC-stage fragment reads (rc_off; unused for KC stages)
+  RcOff ofa[MI], ofb[MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a) ofa[a] = LA::KC ? RcOff{0, 0} : rc_off<BI>(wi * WTI + a * 32 + r32, 16 * wk + 8 * h);
+#pragma unroll
+  for (int b = 0; b < MJ; ++b) ofb[b] = LB::KC ? RcOff{0, 0} : rc_off<BJ>(wj * WTJ + b * 32 + r32, 16 * wk + 8 * h);
   AAA_STAMP(1);
   for (int kt = 0; kt < nk; ++kt) {
     // tile kt is the oldest of the (up to NBUF-1) tiles in flight
@@ -547,12 +628,14 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     }
     const T* Ac = smem + (kt % NBUF) * STG;
     const T* Bc = Ac + AEL;
-    constexpr int S2 = (ABL & 2) ? 0 : BK / 16 / WK;
+    constexpr int S2 = BK / 16 / WK;
+    constexpr bool MF = (ABL & 2) == 0;   // fragment reads + MFMAs
     if constexpr (is_f32<T>::value) {
 #pragma unroll
       for (int s2 = 0; s2 < S2; ++s2) {
         const int kofs = 16 * (s2 * WK + wk) + 8 * h;
         float af[MI][8], bfr[MJ][8];
+        if constexpr (MF) {
 #pragma unroll
         for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
 #pragma unroll
@@ -564,6 +647,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
 #pragma unroll
             for (int b = 0; b < MJ; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+        }
         if constexpr (ILV == 1) {
           if (pf && s2 == 0) la.issue(st, kn);
           if (pf && s2 == S2 - 1) lb.issue(st + AEL, kn);
@@ -584,22 +668,28 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
       auto ld = [&](int s2, int slot) {
         const int kofs = 16 * (s2 * WK + wk) + 8 * h;
 #pragma unroll
-        for (int a = 0; a < MI; ++a) fa[slot][a] = frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs);
+        for (int a = 0; a < MI; ++a)
+          fa[slot][a] = LA::KC ? frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, kofs)
+                               : frag_rc_at(Ac + 16 * s2 * WK * BI, ofa[a]);
 #pragma unroll
-        for (int b = 0; b < MJ; ++b) fb[slot][b] = frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs);
+        for (int b = 0; b < MJ; ++b)
+          fb[slot][b] = LB::KC ? frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, kofs)
+                               : frag_rc_at(Bc + 16 * s2 * WK * BJ, ofb[b]);
       };
 #pragma unroll
       for (int s2 = 0; s2 < NS - 1; ++s2)
-        if (s2 < S2) ld(s2, s2);
+        if (MF && s2 < S2) ld(s2, s2);
 #pragma unroll
       for (int s2 = 0; s2 < S2; ++s2) {
-        if (s2 + NS - 1 < S2) ld(s2 + NS - 1, (s2 + NS - 1) % NS);
+        if (MF && s2 + NS - 1 < S2) ld(s2 + NS - 1, (s2 + NS - 1) % NS);
         __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of these MFMAs
+        if constexpr (MF) {
 #pragma unroll
-        for (int a = 0; a < MI; ++a)
+          for (int a = 0; a < MI; ++a)
 #pragma unroll
-          for (int b = 0; b < MJ; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s2 % NS][a], fb[s2 % NS][b], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < MJ; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s2 % NS][a], fb[s2 % NS][b], acc[a][b], 0, 0, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (ILV == 1) {
           if (pf && s2 == 0) la.issue(st, kn);
@@ -614,8 +704,17 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
     }
   }
 
-  if constexpr ((ABL & 4) != 0) {   // keep acc alive without the epilogue's memory traffic
-    if (acc[0][0][0] == 1234.5f) ep(i0, j0, acc[0][0][1], 0.f, 0.f, 0.f);
+  if constexpr ((ABL & 4) != 0) {   // keep every accumulator alive without the epilogue's memory traffic
+    float sum = 0.f;
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum += acc[a][b][e];
+    if (sum == 1234.5f) ep(i0, j0, sum, 0.f, 0.f, 0.f);
+    AAA_STAMP(2);
+    AAA_STAMP(3);
     return;
   }
   AAA_STAMP(2);
@@ -628,6 +727,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
         for (int g = 0; g < 4; ++g)
           ep(i0 + wi * WTI + a * 32 + 8 * g + 4 * h, j0 + wj * WTJ + b * 32 + r32, acc[a][b][4 * g],
              acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+    AAA_STAMP(3);
     return;
   }
   staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, BJ, tj, pre);

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
     const int ko = __builtin_amdgcn_readfirstlane((tap * p.Cin + cc * CK) * (int)sizeof(T));
     T* dst = As + (step % NBUF) * AEL;
 #pragma unroll
-    for (int c = 0; c < PA; ++c) dma16(wr, dst + c * NT * VG + wofs, avoff[c], ko);
+    for (int c = 0; c < PA; ++c) dma16a(wr, dst + c * NT * VG + wofs, avoff[c], ko);
   };
   // ---- halo DMA: halo row R = (frame fl, padded y, padded x); border / absent frames -> zeros
   const __amdgpu_buffer_rsrc_t xr = make_rsrc(p.x, p.x_bytes);
@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
     const int co = __builtin_amdgcn_readfirstlane(cc * CK * (int)sizeof(T));
     T* dst = Hs + (cc & 1) * HEL;
 #pragma unroll
-    for (int c = 0; c < PH; ++c) dma16(xr, dst + c * NT * VG + wofs, hvoff[c], co);
+    for (int c = 0; c < PH; ++c) dma16a(xr, dst + c * NT * VG + wofs, hvoff[c], co);
   };
   // ---- per-lane halo row of each B column block (tap (1,1)); padding columns read the zero row
   int hrow[MJ];
