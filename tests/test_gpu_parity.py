@@ -239,11 +239,11 @@ def test_frame_resident_carried_state(cuda, monkeypatch, fwd):
         assert_close(torch.cat([x, y]).cpu().numpy(), f.cpu().numpy(), 1e-5, f"carried state {n}")
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "6", "7"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9"])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_lstm_wgrad_ring_variants(cuda, monkeypatch, mode, conv_dtype):
     """ConvLSTM weight gradient on the LDS-DMA ring with transposed fragment
-    reads (AAA_WGRAD_PIPE 1-7: tile shape / ring depth / DMA issue variants; bf16 default 6) or the
+    reads (AAA_WGRAD_PIPE 1-9: tile shape / ring depth / DMA issue variants, 9 = read-ahead ring, the bf16 default) or the
     register-staged GEMM (0).  T*B*121 = 7744 pixels: a whole number of K tiles,
     which the ring requires (the 1728 im2col columns are 13.5 tiles: ragged)."""
     monkeypatch.setenv("AAA_WGRAD_PIPE", mode)

@@ -34,6 +34,38 @@ static __bf16* dev_rand(size_t n, float scale, unsigned seed) {
   return d;
 }
 
+template <class C, int NB, int ABL>
+static void run_ra(const char* name, const __bf16* dz, const __bf16* xh, float* out, int rows, int h, int w, int wgs) {
+  using LA = GRowsT<__bf16, C::BI, C::BK, C::NT>;
+  using LB = GIm2colT<__bf16, C::BJ, C::BK, C::NT>;
+  typename LA::Params pa{dz, 512, 512, rows};
+  typename LB::Params pb{xh, ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep(), 1728, (uint32_t)((size_t)rows * 192 * 2)};
+  EpiAtomicD ep{{out, 1728, 512, 1728}};
+  const int tiles = ((512 + C::BI - 1) / C::BI) * ((1728 + C::BJ - 1) / C::BJ);
+  int ns = std::max(1, wgs / tiles);
+  int kchunk = (rows + ns - 1) / ns;
+  kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
+  ns = (rows + kchunk - 1) / kchunk;
+  dim3 grid((1728 + C::BJ - 1) / C::BJ, (512 + C::BI - 1) / C::BI, ns);
+  const float us = time_us([&] {
+    hipLaunchKernelGGL((gemm_pipe_ra_kernel<C, LA, LB, EpiAtomicD, NB, ABL>), grid, dim3(C::NT), 0, 0, pa, pb, ep, rows,
+                       kchunk, tile_map(grid));
+  });
+  const double flop = 2.0 * 512 * 1728 * rows;
+  printf("%-44s %9.1f us  %7.1f TF/s\n", name, us, flop / (us * 1e-6) / 1e12);
+#ifdef AAA_STAMPS
+  const int nwg = grid.x * grid.y * grid.z;
+  std::vector<uint64_t> st((size_t)nwg * 4);
+  CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(aaa_stamps), st.size() * 8));
+  std::vector<double> ph[3];
+  for (int i = 0; i < nwg; ++i)
+    for (int k = 0; k < 3; ++k) ph[k].push_back((double)(st[i * 4 + k + 1] - st[i * 4 + k]) * 0.01);
+  for (auto& v : ph) std::sort(v.begin(), v.end());
+  printf("    phases (median / max us): prologue %.1f/%.1f  K loop %.1f/%.1f  epilogue %.1f/%.1f\n", ph[0][nwg / 2],
+         ph[0].back(), ph[1][nwg / 2], ph[1].back(), ph[2][nwg / 2], ph[2].back());
+#endif
+}
+
 template <class C, int NB, int ABL, int ILV = 0>
 static void run(const char* name, const __bf16* dz, const __bf16* xh, float* out, int rows, int h, int w, int wgs) {
   using LA = GRowsT<__bf16, C::BI, C::BK, C::NT>;
@@ -87,5 +119,13 @@ int main(int argc, char** argv) {
   run<C8k, 3, 0, 2>("256x256 BK32 ring3 ILV2", dz, xh, out, rows, h, w, 256);
   using C8 = GemmCfg<__bf16, 256, 256, 64, 2, 4>;
   run<C8, 2, 0, 2>("256x256 BK64 ring2 ILV2", dz, xh, out, rows, h, w, 256);
+  using C16 = GemmCfg<__bf16, 256, 256, 16, 2, 4>;
+  run_ra<C16, 8, 0>("read-ahead 256x256 BK16 ring8", dz, xh, out, rows, h, w, 256);
+  run_ra<C16, 8, 0>("read-ahead 256x256 BK16 ring8 (again)", dz, xh, out, rows, h, w, 256);
+  run_ra<C16, 8, 1>("  no in-loop DMA", dz, xh, out, rows, h, w, 256);
+  run_ra<C16, 8, 5>("  no in-loop DMA, no epilogue", dz, xh, out, rows, h, w, 256);
+  run_ra<C16, 6, 0>("read-ahead 256x256 BK16 ring6", dz, xh, out, rows, h, w, 256);
+  run_ra<C8k, 4, 0>("read-ahead 256x256 BK32 ring4", dz, xh, out, rows, h, w, 256);
+  run_ra<C16, 8, 0>("read-ahead 256x256 BK16 ring8, 512 WGs", dz, xh, out, rows, h, w, 512);
   return 0;
 }

@@ -734,6 +734,186 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   AAA_STAMP(3);
 }
 
+// Read-ahead ring (bf16): the fragments of tile kt+1 are read from LDS into a
+// second register set right after the barrier of iteration kt, while the
+// MFMAs of tile kt run on the set read one iteration earlier, so no LDS read
+// latency is exposed behind the per-tile barrier (in gemm_pipe_kernel every
+// wave reads its fragments right after the barrier and the MFMA pipe idles
+// until they return).  The barrier of iteration kt needs tile kt+1 landed
+// (every wave's own pieces: counted vmcnt), so NBUF-2 tiles stay in flight
+// across it; the DMA of tile kt+NBUF-1 refills the stage of tile kt-1, whose
+// reads completed before the MFMAs of iteration kt-1.  The lgkmcnt(0) before
+// each barrier is a builtin the compiler sees, so it does not add waits for
+// the current set behind the reads of the next one.  ABL (diagnostic builds):
+// bit 0 = no in-loop DMA, bit 2 = no epilogue.
+template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0>
+__global__ void __launch_bounds__(C::NT)
+gemm_pipe_ra_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
+  using T = typename C::type;
+  static_assert(std::is_same<T, __bf16>::value, "bf16 only");
+  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
+  constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32, S2 = BK / 16;
+  static_assert(MI >= 1 && MJ >= 1 && WK == 1 && BK % 16 == 0, "tile shape");
+  static_assert(NBUF >= 3, "ring depth: tile kt+1 landed while kt+2.. stay in flight");
+  constexpr int AEL = LA::ELEMS, STG = LA::ELEMS + LB::ELEMS;
+  constexpr int PIECES = LA::PER + LB::PER;
+  constexpr int ELD = BI + 4;
+  constexpr bool DIRECT = is_direct<EP>::value;
+  constexpr int EPI_T =
+      DIRECT ? 0 : (int)((WK * (BJ / epi_chunks<C>()) * ELD * sizeof(float) + sizeof(T) - 1) / sizeof(T));
+  __shared__ __attribute__((aligned(16))) T smem[NBUF * STG > EPI_T ? NBUF * STG : EPI_T];
+  AAA_STAMP(0);
+
+  int ti, tj, tz;
+  tile_of(tm, ti, tj, tz);
+  const int i0 = ti * BI, j0 = tj * BJ;
+  const int kb = tz * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+
+  LA la(pa, i0);
+  LB lb(pb, j0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wi = wave / WJ, wj = wave - (wave / WJ) * WJ;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[MI][MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nk = (ke - kb) / BK;
+  using PL = EpiPlan<C, EP, has_pre<EP>::value && (ABL & 4) == 0>;
+  typename PL::PreT pre[PL::PD];
+  epilogue_prefetch<C, EP, PL>(ep, i0, j0, BJ, pre);
+
+  if constexpr (has_start<LA>::value) la.start(kb);
+  if constexpr (has_start<LB>::value) lb.start(kb);
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nk) {
+      la.issue(smem + s * STG, kb + s * BK);
+      lb.issue(smem + s * STG + AEL, kb + s * BK);
+    }
+  RcOff ofa[MI], ofb[MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a) ofa[a] = LA::KC ? RcOff{0, 0} : rc_off<BI>(wi * WTI + a * 32 + r32, 8 * h);
+#pragma unroll
+  for (int b = 0; b < MJ; ++b) ofb[b] = LB::KC ? RcOff{0, 0} : rc_off<BJ>(wj * WTJ + b * 32 + r32, 8 * h);
+
+  bf16x8 fa[2][S2][MI], fb[2][S2][MJ];
+  auto rd = [&](int tile, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    const T* Ac = smem + (tile % NBUF) * STG;
+    const T* Bc = Ac + AEL;
+#pragma unroll
+    for (int s2 = 0; s2 < S2; ++s2) {
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+        fb[buf][s2][b] = LB::KC ? frag_sw<BK>(Bc, wj * WTJ + b * 32 + r32, 16 * s2 + 8 * h)
+                                : frag_rc_at(Bc + 16 * s2 * BJ, ofb[b]);
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+        fa[buf][s2][a] = LA::KC ? frag_sw<BK>(Ac, wi * WTI + a * 32 + r32, 16 * s2 + 8 * h)
+                                : frag_rc_at(Ac + 16 * s2 * BI, ofa[a]);
+    }
+  };
+  auto lds_sync = [] {
+    __builtin_amdgcn_s_waitcnt((7 << 4) | (0 << 8) | 15 | (3 << 14));   // lgkmcnt(0) only
+    asm volatile("s_barrier" ::: "memory");                           // (no LDS access moves across it)
+  };
+  // iteration kt: tile kt+1 landed everywhere -> barrier -> read tile kt+1 ->
+  // MFMAs of tile kt (DMA of tile kt+NBUF-1 issued between them)
+  auto step = [&](int kt, auto curc) {
+    constexpr int cur = decltype(curc)::value;
+    const bool nx = kt + 1 < nk;
+    if (nx) {
+      if (kt + NBUF - 2 < nk) wait_vmcnt<PIECES * (NBUF - 3)>();
+      else wait_vmcnt<0>();
+    }
+    lds_sync();
+    if (nx) rd(kt + 1, std::integral_constant<int, cur ^ 1>{});
+    const bool pf = !(ABL & 1) && kt + NBUF - 1 < nk;
+    T* const st = smem + ((kt + NBUF - 1) % NBUF) * STG;
+    const int kn = kb + (kt + NBUF - 1) * BK;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < S2; ++s2) {
+#pragma unroll
+      for (int a = 0; a < MI; ++a) {
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][s2][a], fb[cur][s2][b], acc[a][b], 0, 0, 0);
+        if (s2 == S2 - 1 && a == MI / 2 - 1) {   // DMA issue between the MFMAs
+          __builtin_amdgcn_sched_barrier(0);
+          if (pf) la.issue(st, kn);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (pf) lb.issue(st + AEL, kn);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if (NBUF - 2 < nk) wait_vmcnt<PIECES * (NBUF - 2)>();
+  else wait_vmcnt<0>();
+  lds_sync();
+  rd(0, std::integral_constant<int, 0>{});
+  AAA_STAMP(1);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{});
+  }
+
+  if constexpr ((ABL & 4) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum += acc[a][b][e];
+    if (sum == 1234.5f) ep(i0, j0, sum, 0.f, 0.f, 0.f);
+    AAA_STAMP(2);
+    AAA_STAMP(3);
+    return;
+  }
+  AAA_STAMP(2);
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int a = 0; a < MI; ++a)
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          ep(i0 + wi * WTI + a * 32 + 8 * g + 4 * h, j0 + wj * WTJ + b * 32 + r32, acc[a][b][4 * g],
+             acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+    AAA_STAMP(3);
+    return;
+  }
+  staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, BJ, tj, pre);
+  AAA_STAMP(3);
+}
+
+template <class C, class LA, class LB, class EP, int NBUF>
+inline hipError_t launch_pipe_ra(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep, int Mi,
+                                 int Nj, int K, int nsplit, hipStream_t st) {
+  if (Mi <= 0 || Nj <= 0 || K <= 0) return hipSuccess;
+  if (K % C::BK) return hipErrorInvalidValue;
+  if (nsplit < 1) nsplit = 1;
+  int kchunk = (K + nsplit - 1) / nsplit;
+  kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
+  nsplit = (K + kchunk - 1) / kchunk;
+  dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
+  hipLaunchKernelGGL((gemm_pipe_ra_kernel<C, LA, LB, EP, NBUF>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
+                     tile_map(grid));
+  return hipGetLastError();
+}
+
 template <class C, class LA, class LB, class EP, int NBUF = 2, int ILV = 0>
 inline hipError_t launch_pipe(const typename LA::Params& pa, const typename LB::Params& pb, const EP& ep, int Mi,
                               int Nj, int K, int nsplit, hipStream_t st) {

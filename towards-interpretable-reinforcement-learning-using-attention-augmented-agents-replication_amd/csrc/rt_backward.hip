@@ -189,12 +189,30 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     HIPCHK((launch_pipe<CW, LA, LB, EpiAtomicD, NB, IL>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
   };
-  // bf16 default: 256x256 (8 waves of 128x64), BK=32 in a 4-deep ring with the
-  // DMA pieces spread over the k steps (tools/ubench/wgrad_ablate at C3: 1163 us
-  // vs 1296 for BK=64 in a 2-deep ring and 1400 for the register-staged GEMM)
+  // read-ahead ring (glds.h gemm_pipe_ra_kernel): fragments of tile kt+1 read during the MFMAs of tile kt
+  auto wgrad_lstm_ra = [&](auto cfg, auto nbuf) -> int {
+    using CW = decltype(cfg);
+    constexpr int NB = decltype(nbuf)::value;
+    using LA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
+    using LB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
+    typename LA::Params pa{dz, 512, 512, rows};
+    typename LB::Params pb{xh, ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep(), 1728, xh_bytes};
+    EpiAtomicD ep{{gW, 1728, 512, 1728}};
+    const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
+                   strf("LDS-DMA read-ahead ring %dx%d BK%d, %d-deep", CW::BI, CW::BJ, CW::BK, NB));
+    const int wgs = env_int("AAA_WGRAD_WGS", 256);
+    const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
+    HIPCHK((launch_pipe_ra<CW, LA, LB, EpiAtomicD, NB>(pa, pb, ep, 512, 1728, rows, ns, s)));
+    return AAA_OK;
+  };
+  // bf16 default (9): 256x256 (8 waves of 128x64), BK=32 in a 4-deep read-ahead
+  // ring (C3 941 vs 988 us for the same tile with the reads behind each barrier
+  // (6), C4 516 vs 531, C5 2206 vs 2235: profiles/r03/ab/wgrad_ra_*.json; round 2:
+  // 6 at 1163 us vs 1296 for BK=64 in a 2-deep ring and 1400 register-staged)
   constexpr int WBK = std::is_same<T, float>::value ? 32 : 64;
   // (not on the aux stream: its 128 KB of LDS would keep the chain's step kernels off the CU)
-  const int wpipe = rows % WBK == 0 ? env_int("AAA_WGRAD_PIPE", std::is_same<T, float>::value || aux ? 0 : 6) : 0;
+  const int wpipe = rows % WBK == 0 ? env_int("AAA_WGRAD_PIPE", std::is_same<T, float>::value || aux ? 0 : 9) : 0;
   if (wpipe) {
     using I0 = std::integral_constant<int, 0>;
     using I2 = std::integral_constant<int, 2>;
@@ -223,6 +241,12 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
           rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
         else
           rc = wgrad_lstm_pipe(GemmCfg<T, 256, 256, 32, 2, 2>{}, std::integral_constant<int, 4>{}, I2{});
+        break;
+      case 9:   // bf16: read-ahead ring, 8 waves, BK=32, 4-deep
+        if constexpr (std::is_same<T, float>::value)
+          rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I3{}, I2{});
+        else
+          rc = wgrad_lstm_ra(GemmCfg<T, 256, 256, 32, 2, 4>{}, std::integral_constant<int, 4>{});
         break;
       default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
     }
