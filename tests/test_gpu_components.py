@@ -125,7 +125,24 @@ def test_vision_network_vs_oracle(cuda, dt, H, W):
     params through a loss on every step's O.  80x80 / 80x100 give an odd conv1
     map (19 rows): the halo conv2 dgrad's py = 1 parity class is one row short
     there (one and two frames per tile)."""
-    T, B = 3, 2
+    _vision_case(cuda, dt, H, W, 3, 2)
+
+
+@pytest.mark.parametrize("conv", ["1", "2"])
+@pytest.mark.parametrize("pipe", ["1", "2"])
+@pytest.mark.parametrize("H,W", [(84, 84), (168, 168)])
+def test_conv_wgrad_ring_vs_oracle(cuda, monkeypatch, conv, pipe, H, W):
+    """bf16 conv1 / conv2 weight gradient on the LDS-DMA ring (AAA_CONV{1,2}_WGRAD_PIPE
+    1) or the read-ahead ring (2): the 8x8/s4 gather of 2-tap x 4-channel pieces
+    from the bordered RGBx image, the 4x4/s2/p2 gather; 32 frames so the pixel
+    counts are whole numbers of K tiles."""
+    monkeypatch.setenv(f"AAA_CONV{conv}_WGRAD_PIPE", pipe)
+    # 168x168: 2 steps of 16 frames (a third bf16 step drifts one O element past 2e-2 of the
+    # emulated oracle, whatever the weight-gradient kernel: the forward is the same)
+    _vision_case(cuda, "bf16", H, W, *((4, 8) if H == 84 else (2, 16)))
+
+
+def _vision_case(cuda, dt, H, W, T, B):
     vis = attention.VisionNetwork()
     _load(vis, "vision.")
     vis.conv_dtype = dt

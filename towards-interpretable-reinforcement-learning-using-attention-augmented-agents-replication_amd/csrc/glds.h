@@ -847,7 +847,7 @@ gemm_pipe_ra_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K
 #pragma unroll
         for (int b = 0; b < MJ; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][s2][a], fb[cur][s2][b], acc[a][b], 0, 0, 0);
-        if (s2 == S2 - 1 && a == MI / 2 - 1) {   // DMA issue between the MFMAs
+        if (s2 == S2 - 1 && a == (MI + 1) / 2 - 1) {   // DMA issue between the MFMAs (after the first half)
           __builtin_amdgcn_sched_barrier(0);
           if (pf) la.issue(st, kn);
           __builtin_amdgcn_sched_barrier(0);

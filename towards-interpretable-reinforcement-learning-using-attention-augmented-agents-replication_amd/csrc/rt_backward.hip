@@ -99,9 +99,12 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
   using LB = LdIm2colTB<T, T, C::BJ, C::BK, C::NT>;
   const int rows = frames * L.P;
   if constexpr (!std::is_same<T, float>::value) {
-    // bf16 (AAA_CONV2_WGRAD_PIPE, A/B): the LDS-DMA ring of the ConvLSTM weight gradient, 64x256
+    // bf16 (AAA_CONV2_WGRAD_PIPE): the LDS-DMA ring of the ConvLSTM weight gradient, 64x256
     // tiles of 4 waves, split-K over about one wave of workgroups, atomics from the accumulators
-    if (rows % 32 == 0 && env_int("AAA_CONV2_WGRAD_PIPE", 0)) {
+    // default 1 (C3 1.063M -> 1.075M frames/s, C5 277.4k -> 279.0k vs the register-staged GEMM;
+    // 2 = the read-ahead ring, slower here: profiles/r03/ab/convwgrad/); 0 = register-staged
+    const int pipe = env_int("AAA_CONV2_WGRAD_PIPE", 1);
+    if (rows % 32 == 0 && pipe) {
       using CW = GemmCfg<T, 64, 256, 32, 1, 4>;
       using PA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
       using PB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
@@ -110,7 +113,8 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
                              (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
       EpiAtomicD ep{{gW, 512, 64, 512}};
       const int ns = std::max(1, std::min(env_int("AAA_CONV2_WGRAD_WGS", 256) / 2, rows / (8 * CW::BK)));
-      HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 64, 512, rows, ns, s)));
+      if (pipe == 2) HIPCHK((launch_pipe_ra<CW, PA, PB, EpiAtomicD, 4>(pa, pb, ep, 64, 512, rows, ns, s)));
+      else HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 64, 512, rows, ns, s)));
       return AAA_OK;
     }
   }
@@ -139,6 +143,26 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
     HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
     return AAA_OK;
   };
+  if constexpr (!std::is_same<T, float>::value) {
+    // bf16 on the LDS-DMA rings (AAA_CONV1_WGRAD_PIPE 1: pipe, 2: read-ahead): one 32x256 tile of 4
+    // waves over all (tap, channel) columns, BK = 64 pixels; a 16-B piece = 2 taps x 4 channels,
+    // contiguous in the bordered RGBx image (KW = 8 even, pad 0: every piece in bounds)
+    // default 1 (C3 +0.5 %, C5 +0.8 % vs the register-staged GEMM: profiles/r03/ab/convwgrad/)
+    const int pipe = env_int("AAA_CONV1_WGRAD_PIPE", 1);
+    if (rows1 % 64 == 0 && pipe) {
+      using CW = GemmCfg<T, 32, 256, 64, 1, 4>;
+      using PA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
+      using PB = GIm2colT<T, CW::BJ, CW::BK, CW::NT>;
+      typename PA::Params pa{dy1, 32, 32, rows1};
+      typename PB::Params pb{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
+                             (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
+      EpiAtomicD ep{{gW, 256, 32, 256}};
+      const int ns = std::max(1, std::min(env_int("AAA_CONV1_WGRAD_WGS", 256), rows1 / (8 * CW::BK)));
+      if (pipe == 2) HIPCHK((launch_pipe_ra<CW, PA, PB, EpiAtomicD, 4>(pa, pb, ep, 32, 256, rows1, ns, s)));
+      else HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 32, 256, rows1, ns, s)));
+      return AAA_OK;
+    }
+  }
   // AAA_CONV1_WGRAD_TILE=1 (A/B): one 32x256 tile covering every (tap, channel) column, so each
   // pixel's 8x8 window is gathered once instead of by four 64-column tiles
   if (env_int("AAA_CONV1_WGRAD_TILE", 0) == 1) return run(GemmCfg<T, 32, 256, Cfg32For<T>::BK, 1, 4>{});
