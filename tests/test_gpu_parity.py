@@ -255,6 +255,27 @@ def test_lstm_wgrad_ring_variants(cuda, monkeypatch, mode, conv_dtype):
                  f"bf16 wgrad pipe {mode}: ")
 
 
+@pytest.mark.parametrize("T,B", [(3, 16), (2, 96)])
+def test_bf16_tail_split_operands_match_fp32_tail(cuda, monkeypatch, T, B):
+    """The bf16 path's fp32 tail GEMMs (answer MLP, LSTMCell, heads and their
+    backward) on the bf16 MFMA with each operand split into a bf16 pair
+    (AAA_TAIL_SPLIT3, gemm.h GemmCfgS3) against the same run on the fp32 MFMA:
+    the dropped lo*lo term is ~2^-16 of a product, so logits, values and maps
+    agree to 1e-4; the gradients to 5e-3 (below the tail they pass through the
+    bf16 conv operands, where a 1e-5 change can move a rounding).  B = 96 takes
+    the 64x64 tiles, B = 16 the split-K ones."""
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("AAA_TAIL_SPLIT3", mode)
+        outs[mode] = _run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda)
+    a, b = outs["1"], outs["0"]
+    for x, y, n in zip(a[:3], b[:3], ("logits", "values", "attn")):
+        assert_close(x.numpy(), y.numpy(), 1e-4, f"split tail vs fp32 tail {n}")
+    for n in b[3]:
+        if float(b[3][n].norm()) > 0:
+            assert rel_err(a[3][n].numpy(), b[3][n].numpy()) <= 5e-3, f"split tail vs fp32 tail grad {n}"
+
+
 def test_c1_against_reference_fixture(cuda, golden):
     """Config 1 (B=1, T=20) against the fixture made by the reference itself."""
     g = golden("G3")

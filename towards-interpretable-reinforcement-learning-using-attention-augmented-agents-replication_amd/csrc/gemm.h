@@ -18,6 +18,7 @@
 // that is exactly the four LSTM gates of one (pixel, channel), which is what
 // lets the gate math run in the GEMM epilogue.
 #pragma once
+#include <type_traits>
 #include "common.h"
 
 namespace aaa {
@@ -387,6 +388,25 @@ struct GemmCfg {
   static constexpr int NT = WI * WJ * WK * 64;
 };
 
+// fp32 operands on the bf16 MFMA (configs with SPLIT3): each fp32 fragment
+// value x = hi + lo, hi = bf16(x), lo = bf16(x - hi), and a.b is accumulated as
+// hi.hi + hi.lo + lo.hi (the dropped lo.lo is ~2^-16 of the product) -- three
+// 32x32x16 bf16 MFMAs per 16-k step instead of eight 32x32x2 fp32 ones.  Used for
+// the fp32 tail GEMMs of the bf16 path (rt.h head_gemm).
+template <class C, class = void> struct split3_of : std::false_type {};
+template <class C> struct split3_of<C, std::enable_if_t<C::SPLIT3>> : std::true_type {};
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
+struct GemmCfgS3 : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, WK_> {
+  static constexpr bool SPLIT3 = true;
+};
+__device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hi[e] = (__bf16)x[e];
+    lo[e] = (__bf16)(x[e] - (float)hi[e]);
+  }
+}
+
 template <class C, class LA, class LB, class EP>
 __global__ void __launch_bounds__(C::NT)
 gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
@@ -453,13 +473,31 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
         for (int a = 0; a < MI; ++a) frag_f32<TA>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
 #pragma unroll
         for (int b = 0; b < MJ; ++b) frag_f32<TB>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+        if constexpr (split3_of<C>::value) {
+          // the 8 k of a lane's fp32 fragment are the 8 k of the bf16 operand layout
+          // (lane (r32, h): k 8h .. 8h+7 of the 16-k step)
+          bf16x8 ah[MI], al[MI], bh[MJ], bl[MJ];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
+          for (int a = 0; a < MI; ++a) split_bf16(af[a], ah[a], al[a]);
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) split_bf16(bfr[b], bh[b], bl[b]);
 #pragma unroll
           for (int a = 0; a < MI; ++a)
 #pragma unroll
-            for (int b = 0; b < MJ; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < MJ; ++b) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int a = 0; a < MI; ++a)
+#pragma unroll
+              for (int b = 0; b < MJ; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+        }
       } else {
         bf16x8 af[MI], bfr[MJ];
 #pragma unroll

@@ -419,6 +419,8 @@ static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t
 template <typename T>
 int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st) {
   using C = CfgFor<T>;
+  // bf16 path: the fp32 tail GEMMs on the bf16 MFMA with split operands (AAA_TAIL_SPLIT3=0: fp32 MFMA)
+  TailPrecision tail_prec(std::is_same<T, __bf16>::value && env_int("AAA_TAIL_SPLIT3", 1));
   constexpr int NTF = CF::NT;
   char* ws = (char*)io->workspace;
   const char* pk = (const char*)io->packed;
