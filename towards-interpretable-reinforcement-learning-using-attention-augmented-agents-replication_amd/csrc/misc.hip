@@ -229,6 +229,17 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
 constexpr int kAttnChunk = 32;   // positions per staged V chunk (attention backward)
 constexpr int kVld = 188;        // its row pitch in floats (184 + 4: 16-B aligned rows, spread banks)
 
+#ifdef AAA_STAMPS
+// Diagnostic builds only (tools/ubench/attn_stamps): per-workgroup phase stamps (s_memrealtime, 100 MHz).
+__device__ uint64_t aaa_attn_stamps[16384 * 8];
+#define AAA_AT_STAMP(k)                                                                                      \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) aaa_attn_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define AAA_AT_STAMP(k) do {} while (0)
+#endif
+
 // Backward of the readout / softmax / logits for one frame: from da (the
 // answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
 // this frame's dQ (logits path, plus the answer row's Q columns when addq).
@@ -249,6 +260,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   float* Vc = red + G * NQ * 72; // kAttnChunk * kVld
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float* O = Hs + (size_t)f * P * 128;
+  AAA_AT_STAMP(0);
   // V chunk pieces of this thread (16 B each, consecutive threads along a row),
   // loaded into registers one chunk AHEAD of its LDS staging: chunk c+1's
   // loads are in flight while chunk c's dot products run (the barriers below
@@ -273,6 +285,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
   for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
+  AAA_AT_STAMP(1);
   // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S], in chunks of
   // kAttnChunk positions staged in LDS, then thread (p, q) takes its dot
   // product from LDS (no cross-lane reductions).
@@ -300,6 +313,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
     lds_barrier();
   }
+  AAA_AT_STAMP(2);
   // softmax backward: dlogit = A (dA - sum_p A dA)
   for (int q = wave; q < NQ; q += NW) {
     float s = 0.f;
@@ -313,6 +327,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     dA[i] = A[i] * (dA[i] - ss[q]);
   }
   __syncthreads();
+  AAA_AT_STAMP(3);
   // dO: 16 B per thread, rows written by consecutive threads
   float* dOf = dO + (size_t)f * P * 128;
   for (int i = tid; i < P * 32; i += NT) {
@@ -335,6 +350,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     }
     *reinterpret_cast<f32x4*>(dOf + p * 128 + c4) = acc;
   }
+  AAA_AT_STAMP(4);
   // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] | S]: G position groups,
   // every loaded K element feeds all NQ heads, partials reduced through LDS.
   if (tid < G * 72) {
@@ -356,6 +372,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     for (int q = 0; q < NQ; ++q) red[(g * NQ + q) * 72 + c] = acc[q];
   }
   __syncthreads();
+  AAA_AT_STAMP(5);
   for (int i = tid; i < NQ * 72; i += NT) {
     float acc = 0.f;
 #pragma unroll 4
@@ -363,6 +380,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     if (addq) acc += dAns[(size_t)f * da_ld + NQ * 184 + i];   // the answer row's copy of Q (stateful core)
     dQp[(size_t)f * NQ * 72 + i] = acc;
   }
+  AAA_AT_STAMP(6);
 }
 
 // Backward of the query MLP (one workgroup of 1024 threads).  dQ = sum over
