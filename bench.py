@@ -264,21 +264,34 @@ def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
     return out
 
 
-def pmc_traffic(config, dtype, world, kernel):
-    """HBM bytes per launch of ``kernel`` from the committed PMC passes
-    (tools/pmc.sh -> tools/pmc_traffic.py -> profiles/rNN/pmc_traffic_<config>.json).
-    rocprofv3 counters cannot be read from inside the timed run, so the value is
-    the profile of the same binary and config; null when none is committed."""
+def pmc_traffic(config, world, variant):
+    """HBM bytes per launch of the dispatched kernel from the committed PMC
+    passes (tools/pmc_cfg_r04.sh -> tools/pmc_traffic.py ->
+    profiles/rNN/pmc_traffic_<config>.json, newest round first).  rocprofv3
+    counters cannot be read from inside the timed run, so the value comes from
+    a profile of the same config -- attached only when that profile holds the
+    kernel the library reports it dispatched (the ``[kernel: a+b]`` marker of
+    the variant: every substring must be in the profiled kernel's name);
+    otherwise null with the reason."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{config}.json")))
-    if not files or world != 1:
-        return {"traffic": None}
-    d = json.load(open(files[-1]))
-    c = d.get("classes", {}).get(kernel)
-    if not c:
-        return {"traffic": None}
-    return {"traffic": round(c["hbm_bytes_per_launch"]), "traffic_unit": "bytes/launch",
-            "traffic_source": os.path.relpath(files[-1], ROOT) + " (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc)"}
+    import re
+    if world != 1:
+        return {"traffic": None, "traffic_note": "PMC passes are single-GPU"}
+    m = re.search(r"\[kernel: ([^\]]+)\]", variant or "")
+    if not m:
+        return {"traffic": None, "traffic_note": "the dispatched variant names no kernel"}
+    subs = m.group(1).split("+")
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{config}.json")), reverse=True):
+        d = json.load(open(f))
+        hits = [(k, e) for k, e in d.get("kernels", {}).items()
+                if all(s in k for s in subs) and "hbm_bytes_per_launch" in e]
+        if hits:
+            k, e = max(hits, key=lambda kv: kv[1]["hbm_bytes_per_launch"])
+            return {"traffic": round(e["hbm_bytes_per_launch"]), "traffic_unit": "bytes/launch",
+                    "traffic_source": os.path.relpath(f, ROOT) + " (2*FETCH_SIZE + WRITE_SIZE, rocprofv3 --pmc)",
+                    "traffic_kernel": k[:160], "pmc_mfma_util": e.get("mfma_util"),
+                    "pmc_lds_conflict_rate": e.get("lds_conflict_rate")}
+    return {"traffic": None, "traffic_note": f"no committed PMC profile of {subs} for {config}"}
 
 
 def main():
@@ -346,8 +359,9 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kt = {k: N.timing_stats(k) for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
-    ka = {k: N.timing_stats(k) for k in (N.TIMER_ATTN_FWD, N.TIMER_ATTN_BWD)}
+    allk = {k: N.timing_stats(k) for k in range(N.TIMER_N)}
+    kt = {k: allk[k] for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP, N.TIMER_CORE_WGRAD)}
+    ka = {k: allk[k] for k in (N.TIMER_ATTN_FWD, N.TIMER_ATTN_BWD)}
     N.timing_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -378,8 +392,31 @@ def main():
                           "flop_per_launch": v["work"] / max(v["launches"], 1),
                           "tflops": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12, 2),
                           "frac": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12 / peak, 4),
-                          "variant": v["variant"]}
+                          "variant": v["variant"], **pmc_traffic(args.config, world, v["variant"])}
                for k, v in kt.items() if v["launches"]}
+    # the rest of the step, by timer class (library-recorded HIP events of the
+    # last timed step): algorithmic FLOP where a GEMM dominates (tail classes
+    # priced at the fp32 peak: their operands are fp32), time only for glue
+    other = {N.TIMER_PACK: ("weight packing", None), N.TIMER_VISION_FWD: ("vision encoder fwd (conv1+conv2)", peak),
+             N.TIMER_TAIL_FWD: ("tail fwd (query pack, answer MLP, LSTMCell, heads)", PEAK_TFLOPS["fp32"]),
+             N.TIMER_TAIL_BWD: ("tail bwd", PEAK_TFLOPS["fp32"]), N.TIMER_CORE_DX: ("batched dx (conv2-output grad)", peak),
+             N.TIMER_VISION_BWD: ("vision bwd (conv2 wgrad+dgrad, conv1 wgrad)", peak),
+             N.TIMER_MISC: ("state copies, memsets, bias column sums", None)}
+    for k, (nm, pk) in other.items():
+        v = allk[k]
+        if not v["launches"]:
+            continue
+        e = {"ms": round(v["ms"], 4), "regions": v["launches"], "variant": v["variant"]}
+        if pk and v["work"] > 0:
+            e.update({"flop": v["work"], "tflops": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12, 2),
+                      "frac": round(v["work"] / max(v["ms"] * 1e-3, 1e-12) / 1e12 / pk, 4), "peak_tflops": pk})
+        if k == N.TIMER_CORE_DX:
+            e.update(pmc_traffic(args.config, world, v["variant"]))
+        kernels[nm] = e
+    timed_ms = sum(allk[k]["ms"] for k in allk)
+    coverage = {"timed_ms": round(timed_ms, 4), "ms_per_step": round(ms, 4), "frac": round(timed_ms / ms, 4),
+                "note": "sum of every timer class's HIP-event time in the last timed step / the average step; the "
+                        "remainder is launch gaps, host enqueue and the unattributed memsets"}
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -393,12 +430,13 @@ def main():
                    "heads": nq, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": names[dom], "variant": d["variant"], "achieved": round(achieved, 2),
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                     **pmc_traffic(args.config, dtype, world, names[dom]),
+                     **pmc_traffic(args.config, world, d["variant"]),
                      "flop_per_launch": per_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
                      "timed_launches": d["launches"], "timing": "HIP events around each launch of the last timed step"},
         "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
                          "frac": round(value * fpf / world / 1e12 / peak, 4)},
         "kernels": kernels,
+        "kernel_coverage": coverage,
         "hbm_kernels": attention_hbm(ka),
     }
     if world > 1:   # RCCL gradient all-reduce of the last timed step, per bucket

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 5
+#define AAA_ABI_VERSION 6
 
 enum aaa_status {
   AAA_OK = 0,
@@ -162,17 +162,29 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream);
  * are overwritten (not accumulated) by the phases that own them. */
 int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
 
-/* Health of the paired frame-resident ConvLSTM kernels (two cooperating
- * workgroups per frame, launched cooperatively; used when B is below the CU
- * count).  Their partner waits are bounded; a wait that times out is counted
- * in a word of pinned, device-mapped host memory and the kernel proceeds on a
- * stale partner half.  aaa_forward / aaa_backward consume pending counts at
- * entry and return AAA_E_STRANDED; aaa_pair_status synchronises ``stream``
- * (NULL: the device) and returns the count (>= 0; clear != 0 resets it).
- * aaa_debug_pair_spin bounds the wait to ``polls`` polls (0 = the default
- * 2^24, about 0.5 s) -- a test hook that makes the report path reachable. */
+/* Health of the multi-workgroup frame-resident ConvLSTM kernels (two or more
+ * cooperating workgroups per frame: the paired and band-mode bf16 kernels and
+ * the fp32 frame-group kernels, launched as ordinary grids that fit one
+ * residency wave of an idle chip).  Their partner waits are bounded by a
+ * deadline on the 100-MHz real-time counter (1 s + 20 ms per step after a
+ * workgroup's first wait); a wait that expires is counted in a word of
+ * pinned, device-mapped host memory and the kernel proceeds on a stale
+ * partner slice (later waits of that workgroup return at once, so a kernel
+ * whose partner never runs ends within about one budget).  aaa_forward /
+ * aaa_backward consume pending counts at entry and return AAA_E_STRANDED;
+ * aaa_pair_status synchronises ``stream`` (NULL: the device) and returns the
+ * count (>= 0; clear != 0 resets it).
+ * aaa_pair_flag enqueues on ``stream`` a copy of the pending count (as seen
+ * by the device at that point of the stream, not consumed) into dst[0] as a
+ * float: a learner puts it beside its gradients so the gradient all-reduce
+ * carries it to every rank and aaa_adam_step_guarded skips the update of a
+ * step whose gradients came from a stranded launch, with no host sync.
+ * aaa_debug_pair_spin is a TEST HOOK, not part of a production call
+ * sequence: it sets the wait budget to ``ticks`` 100-MHz ticks (0 = the
+ * default above) so the report path can be exercised. */
 int aaa_pair_status(hipStream_t stream, int clear);
-int aaa_debug_pair_spin(long polls);
+int aaa_pair_flag(float* dst, hipStream_t stream);
+int aaa_debug_pair_spin(long ticks);
 
 /* ---- optional kernel timing (benchmarks) ----
  * While enabled, the runtime records a hipEvent pair on the launch stream
@@ -185,19 +197,30 @@ enum aaa_timer {
   AAA_TIMER_CORE_WGRAD = 2,  /* ConvLSTM weight-gradient GEMM over all frames    */
   AAA_TIMER_ATTN_FWD = 3,    /* fused spatial-softmax attention readout (HBM)    */
   AAA_TIMER_ATTN_BWD = 4,    /* its backward (HBM)                               */
-  AAA_TIMER_N = 5
+  /* the rest of a learner iteration, so the classes cover the whole step
+     (work in FLOP where a GEMM dominates, 0 for the latency-bound glue):     */
+  AAA_TIMER_PACK = 5,        /* aaa_pack_weights (all packed layouts)            */
+  AAA_TIMER_VISION_FWD = 6,  /* frames -> conv1 -> conv2 (the vision encoder)    */
+  AAA_TIMER_TAIL_FWD = 7,    /* query pack, answer MLP, LSTMCell, heads          */
+  AAA_TIMER_TAIL_BWD = 8,    /* their backward (HEAD phase minus the attention)  */
+  AAA_TIMER_CORE_DX = 9,     /* batched conv2-output grad dx (when not fused)    */
+  AAA_TIMER_VISION_BWD = 10, /* conv2 wgrad + dgrad, conv1 wgrad, grad unpack    */
+  AAA_TIMER_MISC = 11,       /* state copies, memsets, bias column sums          */
+  AAA_TIMER_N = 12
 };
 int aaa_timing_enable(int on);
 int aaa_timing_read(int kind, double* total_ms, long* launches);
 /* The same read with the roofline inputs the runtime knows: the summed
- * algorithmic work of those launches (FLOP for the MFMA classes 0-2: 2*M*N*K
- * of each GEMM; bytes for the HBM classes 3-4: the fp32 tensors each frame
- * must move) and the kernel variant (tile / ring) dispatched last. */
+ * algorithmic work of those launches (FLOP for the MFMA classes 0-2 and 6-10:
+ * 2*M*N*K of each GEMM; bytes for the HBM classes 3-4: the fp32 tensors each
+ * frame must move; 0 for 5 and 11) and the kernel variant (tile / ring)
+ * dispatched last.  A "launch" of classes 5-11 is one timed region (a group
+ * of consecutive kernels of that class). */
 typedef struct aaa_timer_stats {
   double total_ms;
   long launches;
   double work;
-  char variant[96];
+  char variant[192];
 } aaa_timer_stats;
 int aaa_timing_stats(int kind, aaa_timer_stats* out);
 
@@ -218,6 +241,13 @@ typedef struct aaa_adam_hparams {
 int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* const* params,
                   const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream);
+/* The same update, skipped on the device when *guard != 0 (guard: one
+ * device float, e.g. the all-reduced aaa_pair_flag slot of the gradients):
+ * no parameter or moment is written and no host sync is needed. */
+int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* guard, int ntensors,
+                          float* const* params, const float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                          hipStream_t stream);
 
 /* ---- REINFORCE loss ----
  * finish_episode's loss (reference main_mp.py:62-77) for B independent

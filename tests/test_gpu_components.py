@@ -18,7 +18,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from helpers import assert_close, detinit
+from helpers import assert_close, detinit, rel_err
 from oracle import ref_cpu
 
 import attention
@@ -137,9 +137,7 @@ def test_conv_wgrad_ring_vs_oracle(cuda, monkeypatch, conv, pipe, H, W):
     from the bordered RGBx image, the 4x4/s2/p2 gather; 32 frames so the pixel
     counts are whole numbers of K tiles."""
     monkeypatch.setenv(f"AAA_CONV{conv}_WGRAD_PIPE", pipe)
-    # 168x168: 2 steps of 16 frames (a third bf16 step drifts one O element past 2e-2 of the
-    # emulated oracle, whatever the weight-gradient kernel: the forward is the same)
-    _vision_case(cuda, "bf16", H, W, *((4, 8) if H == 84 else (2, 16)))
+    _vision_case(cuda, "bf16", H, W, *((4, 8) if H == 84 else (4, 16)))
 
 
 def _vision_case(cuda, dt, H, W, T, B):
@@ -169,8 +167,28 @@ def _vision_case(cuda, dt, H, W, T, B):
         rloss = rloss + (routs[-1] * G[t]).sum()
     rloss.backward()
     tol = _tol(dt)
-    for t in range(T):
-        assert_close(outs[t].detach().cpu().numpy(), routs[t].detach().numpy(), tol, f"O[{t}]")
+    if dt == "bf16":
+        # O of the recurrent cell in bf16: elementwise within 2e-2 of the emulated
+        # oracle plus the bf16 envelope -- |emulated - fp32 reference| of that
+        # element, what the bf16 rounding itself moves it (a few saturating
+        # elements drift past a flat 2e-2 after several steps at 21x21)
+        P32 = ref_cpu.tensor_params({k: PARAMS[k] for k in CNN_KEYS + CELL_KEYS}, requires_grad=False)
+        st32, pp32 = None, None
+        with torch.no_grad():
+            for t in range(T):
+                h32, c32, pp32 = ref_cpu._vision_step(P32, X[t], st32, "fp32", pp32, "fp32")
+                st32 = (h32, c32)
+                x, r, r32 = (np.asarray(a, np.float64) for a in (outs[t].detach().cpu().numpy(),
+                                                                  routs[t].detach().numpy(),
+                                                                  h32.transpose(1, 3).numpy()))
+                assert rel_err(x, r) <= tol, f"O[{t}] norm-relative"
+                allow = tol * np.abs(r).max() + tol * np.abs(r) + np.abs(r - r32)
+                bad = np.abs(x - r) > allow
+                assert not bad.any(), (f"O[{t}]: {int(bad.sum())} elements beyond the bf16 envelope, worst excess "
+                                       f"{float((np.abs(x - r) - allow).max()):.3e}")
+    else:
+        for t in range(T):
+            assert_close(outs[t].detach().cpu().numpy(), routs[t].detach().numpy(), tol, f"O[{t}]")
     assert tuple(vis.vision_lstm.prev_hidden[0].shape) == (B, 128, ww, hh)
     assert_close(vis.vision_lstm.prev_hidden[1].detach().cpu().numpy(), state[1].detach().numpy(), tol, "c_T")
     g = _grads(vis)

@@ -1,0 +1,188 @@
+"""Co-residency of the multi-workgroup frame-resident ConvLSTM launches when
+another kernel holds CUs, and the stranded-launch guard of the optimizer.
+
+The recurrence (reference attention.py:117-125 over the unroll, and its
+autograd BPTT, main_mp.py:77) runs as grids of cooperating workgroups that
+must all be resident at once: the paired kernels (C4's per-GPU shape), the
+band-mode kernels (C5's per-GPU shape) and the fp32 frame-group kernels (C2).
+They launch as ordinary grids sized for an idle chip (csrc/common.h
+launch_resident), so a kernel already holding CUs -- e.g. an RCCL collective
+on another stream, which is what main_mp.py:182-184's Hogwild is replaced by
+-- delays some partners until it drains.  These tests keep a filler kernel
+(tests/native/filler.hip: 96 KB of LDS per workgroup, one per CU) resident on
+a second stream over k CUs while those launches run, and check that
+
+  * no partner wait times out (pair_status() == 0),
+  * logits, values and every gradient equal the unfilled run's,
+  * the slowdown is about the filler's lifetime (recorded in
+    gpurun_out/coresidency_<shape>.json), i.e. the partners wait, they are
+    not stranded.
+
+Learner.step's policy still never overlaps a collective with
+these launches; this pins what happens if something else does.
+"""
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import ROOT, detinit, rel_err
+import attention
+
+N = attention._pkg._native
+R = attention._pkg.runtime
+
+pytestmark = pytest.mark.gpu
+
+FILLER_LIB = os.path.join(ROOT, "tests", "native", "libaaa_filler.so")
+# shape -> (B, T, H, nq, dtype, variant substring of the forward and BPTT)
+SHAPES = {
+    "pairs_c4": (128, 20, 84, 4, "bf16", "2 WG per frame"),
+    "band_c5": (64, 50, 168, 8, "bf16", "band-mode"),
+    "f32group_c2": (32, 20, 84, 4, "fp32", "frame-group"),
+}
+
+
+def _filler():
+    if not os.path.isfile(FILLER_LIB):
+        pytest.fail(f"{FILLER_LIB} is missing: build it with `make -C <pkg>/csrc` (the test helper is not optional)")
+    lib = ctypes.CDLL(FILLER_LIB)
+    lib.aaa_test_filler.restype = ctypes.c_int
+    lib.aaa_test_filler.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+    return lib
+
+
+def _setup(cuda, B, T, H, nq, dtype):
+    runner = R.UnrollRunner(B, T, H, H, nq, 18, dtype, cuda, frames_u8=True)
+    params = detinit.deterministic_params(0, 18, nq)
+    flat = torch.cat([torch.from_numpy(np.asarray(v, np.float32)).reshape(-1) for v in params.values()]).to(cuda)
+    packed, ws = runner.new_packed(), runner.new_workspace()
+    runner.pack(flat, packed)
+    basis = attention.SpatialBasis(runner.h, runner.w).S.to(cuda).contiguous()
+    frames = torch.from_numpy(detinit.frames_u8(1234, (T, B, H, H, 3))).to(cuda)
+    dl = torch.from_numpy(detinit.cotangent(2, (T, B, 18))).to(cuda)
+    dv = torch.from_numpy(detinit.cotangent(3, (T, B, 18))).to(cuda)
+    return runner, flat, packed, basis, frames, ws, dl, dv
+
+
+def _run(args):
+    runner, flat, packed, basis, frames, ws, dl, dv = args
+    lg, vl, _, _, _ = runner.forward(flat, packed, basis, frames, ws, want_attn=False)
+    g, _, _ = runner.backward(flat, packed, basis, frames, ws, dl, dv)
+    return lg, vl, g
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_resident_launch_beside_filler(cuda, shape):
+    B, T, H, nq, dtype, var = SHAPES[shape]
+    lib = _filler()
+    args = _setup(cuda, B, T, H, nq, dtype)
+    N.pair_status(clear=True)
+    N.timing_enable(True)
+    try:
+        ref = _run(args)
+        fwd, bwd = N.timing_stats(N.TIMER_FWD_STEP), N.timing_stats(N.TIMER_BPTT_STEP)
+    finally:
+        N.timing_enable(False)
+    assert var in fwd["variant"] and var in bwd["variant"], (fwd["variant"], bwd["variant"])
+    ref = [t.clone() for t in ref]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _run(args)
+    torch.cuda.synchronize()
+    t_idle = time.perf_counter() - t0
+    assert N.pair_status(clear=True) == 0
+
+    side = torch.cuda.Stream(cuda)
+    sink = torch.zeros(4096, device=cuda)
+    rec = {"shape": shape, "B": B, "T": T, "frame": f"{H}x{H}", "dtype": dtype, "idle_ms": round(t_idle * 1e3, 3),
+           "variants": [fwd["variant"], bwd["variant"]], "runs": []}
+    for wgs, usec in ((32, 20000), (128, 20000), (256, 5000)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        assert lib.aaa_test_filler(wgs, usec, sink.data_ptr(), side.cuda_stream) == 0
+        time.sleep(0.002)          # the filler is dispatched (idle GPU) before the resident launches are enqueued
+        out = _run(args)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        stranded = N.pair_status(clear=True)
+        errs = {"logits": rel_err(out[0].cpu().numpy(), ref[0].cpu().numpy()),
+                "values": rel_err(out[1].cpu().numpy(), ref[1].cpu().numpy()),
+                "grads": rel_err(out[2].cpu().numpy(), ref[2].cpu().numpy())}
+        rec["runs"].append({"filler_cus": wgs, "filler_us": usec, "wall_ms": round(dt * 1e3, 3),
+                            "slowdown_ms": round((dt - t_idle) * 1e3, 3), "stranded": stranded,
+                            "rel_err": errs})
+        assert stranded == 0, rec
+        # forward: no atomics, identical; gradients: split-K atomics reorder fp32 sums
+        assert errs["logits"] <= 1e-6 and errs["values"] <= 1e-6, rec
+        assert errs["grads"] <= 1e-5, rec
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"coresidency_{shape}.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
+def test_guarded_adam_skips_stranded_step(cuda):
+    """A launch whose partner wait expired leaves its count in the report word;
+    aaa_pair_flag copies it (stream order, no sync) into the guard slot and
+    the guarded Adam then writes nothing.  A zero guard updates as usual."""
+    B, T, H, nq, dtype, _ = SHAPES["pairs_c4"]
+    args = _setup(cuda, B, T, H, nq, dtype)
+    n = args[0].n_params
+    gbuf = torch.zeros(n + 4, device=cuda)
+    guard = gbuf[n:n + 1]
+    p = torch.randn(n, device=cuda)
+    g = torch.randn(n, device=cuda)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    from aaa_amd.optim import adam_flat_
+    N.pair_status(clear=True)
+    N.debug_pair_spin(1)           # test hook: a one-tick partner wait budget strands the pairs
+    try:
+        runner, flat, packed, basis, frames, ws, dl, dv = args
+        runner.forward(flat, packed, basis, frames, ws, want_attn=False)
+        N.pair_flag(guard)         # before any API call consumes the report
+        before = p.clone()
+        adam_flat_(p, g, m, v, 1, guard=guard)
+        torch.cuda.synchronize()
+    finally:
+        N.debug_pair_spin(0)
+    assert float(guard.item()) > 0, "a one-tick partner wait never expired"
+    assert torch.equal(p, before) and float(m.abs().max()) == 0.0, "the guarded Adam updated a stranded step"
+    assert N.pair_status(clear=True) > 0
+    guard.zero_()
+    adam_flat_(p, g, m, v, 1, guard=guard)
+    torch.cuda.synchronize()
+    assert not torch.equal(p, before)
+
+
+def test_learner_stranded_step_leaves_params(cuda):
+    """Learner.train_step with stranded partners: either the backward's entry
+    check raises AAA_E_STRANDED (the forward's report was already visible) or
+    the guard slot skips the update -- the parameters never change; a clean
+    step afterwards updates them and check_health() is quiet."""
+    from aaa_amd.learner import Learner
+    B, T, H, nq, dtype, _ = SHAPES["pairs_c4"]
+    lr = Learner(B, T, H, H, nq, 18, dtype, cuda, frames_u8=True)
+    frames = torch.from_numpy(detinit.frames_u8(1234, (T, B, H, H, 3))).to(cuda)
+    dl = torch.from_numpy(detinit.cotangent(2, (T, B, 18))).to(cuda)
+    dv = torch.from_numpy(detinit.cotangent(3, (T, B, 18))).to(cuda)
+    before = lr.flat.clone()
+    N.pair_status(clear=True)
+    N.debug_pair_spin(1)
+    try:
+        try:
+            lr.train_step(frames, dl, dv)
+        except RuntimeError as e:
+            assert "status -5" in str(e), e
+        torch.cuda.synchronize()
+    finally:
+        N.debug_pair_spin(0)
+    assert torch.equal(lr.flat, before), "a stranded step reached the parameters"
+    N.pair_status(clear=True)
+    lr.train_step(frames, dl, dv)
+    torch.cuda.synchronize()
+    lr.check_health()
+    assert not torch.equal(lr.flat, before)

@@ -57,6 +57,25 @@ def _vs_fp32_reference(out, T, B, nq=4, H=84, W=84, what=""):
     assert_close(out[0].numpy(), rl.numpy(), 2e-2, what + "bf16 vs fp32 logits")
     assert_close(out[1].numpy(), rv.numpy(), 2e-2, what + "bf16 vs fp32 values")
     assert_close(out[2].numpy(), ra.numpy(), 2e-2, what + "bf16 vs fp32 attn")
+    return rl, rv, ra
+
+
+def _maps_close(at, ra, ra32, rtol, what):
+    """Attention maps elementwise, each (frame, query) map on its own scale:
+    |x - ref| <= rtol * max_p |ref_map| + rtol * |ref| + |ref - ref32|, where
+    ref is the bf16-emulated oracle and ref32 the fp32 reference -- the last
+    term is the bf16 envelope, what the bf16 rounding itself moves that
+    probability in the reference op sequence.  Norm-relative rtol as well."""
+    x, r, r32 = (np.asarray(t, np.float64) for t in (at, ra, ra32))
+    assert rel_err(x, r) <= rtol, f"{what}: norm-relative {rel_err(x, r):.3e}"
+    F = int(np.prod(x.shape[:2]))
+    nq = x.shape[-1]
+    xm, rm, r32m = (a.reshape(F, -1, nq) for a in (x, r, r32))
+    scale = np.abs(rm).max(axis=1, keepdims=True)
+    allow = rtol * scale + rtol * np.abs(rm) + np.abs(rm - r32m)
+    bad = np.abs(xm - rm) > allow
+    assert not bad.any(), (f"{what}: {int(bad.sum())} of {bad.size} probabilities beyond the per-map bf16 envelope; "
+                           f"worst excess {float((np.abs(xm - rm) - allow).max()):.3e}")
 
 
 def _run_unroll(agent, T, B, dev, scale=1.0, A=18, H=84, W=84, **kw):
@@ -427,11 +446,11 @@ def test_c5_full_size_bf16_vs_emulated_oracle(cuda):
     rl, rv, ra, _ = _oracle(T, B, nq=8, conv_mode="bf16", H=168, W=168)
     assert_close(lg.numpy(), rl.numpy(), 2e-2, "C5 bf16 logits")
     assert_close(vl.numpy(), rv.numpy(), 2e-2, "C5 bf16 values")
-    # attention maps over 441 positions are diffuse (max ~5e-3): after 50 bf16
-    # steps a few hundred of the 11.3M probabilities differ by ~3e-4 absolute,
-    # beyond the elementwise atol (2e-2 * max); the map is checked norm-relative
-    assert rel_err(at.numpy(), ra.numpy()) <= 2e-2, "C5 bf16 attn"
-    _vs_fp32_reference((lg, vl, at), T, B, nq=8, H=168, W=168, what="C5 ")
+    # attention maps over 441 positions are diffuse (max ~5e-3): each map is
+    # checked elementwise on its own scale, within the bf16 envelope measured
+    # against the fp32 reference (_maps_close)
+    _, _, ra32 = _vs_fp32_reference((lg, vl, at), T, B, nq=8, H=168, W=168, what="C5 ")
+    _maps_close(at.numpy(), ra.numpy(), ra32.numpy(), 2e-2, "C5 bf16 attn maps")
     # gradients norm-relative: over 3200 frames a handful of answer_processor.0
     # ReLU pre-activations sit within bf16 noise of 0 and flip, which moves single
     # weight-grad elements (the C2 fp32 test's kink) but not the norm

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.load().aaa_abi_version() == N.ABI_VERSION == 5
+    assert N.load().aaa_abi_version() == N.ABI_VERSION == 6
 
 
 @pytest.mark.parametrize("H,W,hw", [(84, 84, (11, 11)), (168, 168, (21, 21)), (210, 160, (27, 20))])
@@ -128,3 +128,27 @@ def test_actor_layout_refuses_readout_lds_overflow():
     assert N.grid(506, 506) == (64, 64)
     assert lib.aaa_actor_workspace_bytes(ctypes.byref(small)) > 0
     assert lib.aaa_actor_workspace_bytes(ctypes.byref(big)) == 0
+
+
+def test_timer_classes_match_header():
+    """Every timer class the header enumerates has its binding constant (the
+    bench reads all of them to attribute the whole step)."""
+    src = open(HEADER).read()
+    enum = dict((k, int(v)) for k, v in re.findall(r"AAA_TIMER_([A-Z_]+)\s*=\s*(\d+)", src))
+    assert enum.pop("N") == N.TIMER_N == 12
+    for name, val in enum.items():
+        assert getattr(N, "TIMER_" + name) == val, name
+
+
+def test_timing_stats_rejects_unknown_class():
+    lib = N.load()
+    s = N.TimerStats()
+    assert lib.aaa_timing_stats(N.TIMER_N, ctypes.byref(s)) == -1
+    assert lib.aaa_timing_stats(N.TIMER_MISC, ctypes.byref(s)) == 0 and s.launches == 0
+
+
+def test_debug_pair_spin_bounds():
+    lib = N.load()
+    assert lib.aaa_debug_pair_spin(-1) == -1
+    assert lib.aaa_debug_pair_spin(1 << 31) == -1
+    assert lib.aaa_debug_pair_spin(0) == 0

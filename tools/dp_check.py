@@ -10,12 +10,14 @@ against
   (1) a single-process backward of the full batch on the same kernels, and
   (2) the CPU oracle (oracle/ref_cpu.py) on the full batch: fp32 at 1e-4,
       bf16 at 2e-2 against the bf16-emulated oracle,
-and that the backward phases write only their own bucket (a phase never
-writes a bucket whose all-reduce an earlier phase already issued).
+and that no backward phase writes a gradient range whose all-reduce the
+learner's schedule (Learner.schedule: HEAD+CORE after CORE, VISION last)
+has already issued.
 
 Environment: AAA_DP_DTYPE fp32|bf16, AAA_DP_B rows per rank (bf16 at 32..128
 selects the paired frame-resident kernels, >= 160 the one-workgroup ones on a
-256-CU part), AAA_DP_T unroll length.  Prints one JSON line on rank 0; exit
+256-CU part; fp32 at 16..32 the frame-group kernels), AAA_DP_T unroll length,
+AAA_DP_H frame side (168: the band-mode kernels for bf16), AAA_DP_NQ heads.  Prints one JSON line on rank 0; exit
 status 1 on a mismatch.
 """
 import json
@@ -38,13 +40,13 @@ def rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-def oracle_grads(X, Gl, Gv, dtype, A):
+def oracle_grads(X, Gl, Gv, dtype, A, nq):
     """Per-tensor gradients of the CPU oracle on the full batch (fp32 reference
     op sequence, or its bf16-emulated form for the bf16 path)."""
     from oracle import ref_cpu
     torch.set_num_threads(int(os.environ.get("AAA_DP_ORACLE_THREADS", "16")))
-    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A))
-    lg, vl, _ = ref_cpu.unroll(P, X, conv_mode="bf16" if dtype == "bf16" else "fp32")
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A, nq))
+    lg, vl, _ = ref_cpu.unroll(P, X, nq=nq, conv_mode="bf16" if dtype == "bf16" else "fp32")
     ((lg * Gl).sum() + (vl * Gv).sum()).backward()
     return {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}
 
@@ -57,17 +59,19 @@ def main():
     dtype = os.environ.get("AAA_DP_DTYPE", "fp32")
     b = int(os.environ.get("AAA_DP_B", "2"))
     T = int(os.environ.get("AAA_DP_T", "3"))
+    H = int(os.environ.get("AAA_DP_H", "84"))       # square frames: 84 (11x11 grid) or 168 (21x21, band mode)
+    nq = int(os.environ.get("AAA_DP_NQ", "4"))
     A, Bt = 18, b * world
     tol = 2e-2 if dtype == "bf16" else 1e-4
-    X = torch.from_numpy(detinit.frames_u8(1234, (T, Bt, 84, 84, 3)).astype(np.float32))
+    X = torch.from_numpy(detinit.frames_u8(1234, (T, Bt, H, H, 3)).astype(np.float32))
     Gl = torch.from_numpy(detinit.normal(2, (T, Bt, A)))
     Gv = torch.from_numpy(detinit.normal(3, (T, Bt, A)))
     rows = slice(rank * b, (rank + 1) * b)
-    res = {"world": world, "backend": dist.get_backend(), "dtype": dtype, "B_per_rank": b, "T": T}
+    res = {"world": world, "backend": dist.get_backend(), "dtype": dtype, "B_per_rank": b, "T": T, "H": H, "nq": nq}
     ok = True
     grads_dp = None
     for overlap in (True, False):
-        lr = Learner(b, T, 84, 84, 4, A, dtype, dev)
+        lr = Learner(b, T, H, H, nq, A, dtype, dev)
         N.timing_enable(True)
         lr.step(X[:, rows].contiguous().to(dev), Gl[:, rows].contiguous().to(dev), Gv[:, rows].contiguous().to(dev),
                 overlap=overlap, comm_timing=True)
@@ -75,10 +79,10 @@ def main():
         variants = {k: N.timing_stats(k)["variant"] for k in (N.TIMER_FWD_STEP, N.TIMER_BPTT_STEP)}
         N.timing_enable(False)
         cs = lr.comm_stats()
-        assert len(cs["buckets"]) == 3 and all(x["allreduce_ms"] >= 0 for x in cs["buckets"]), cs
+        assert len(cs["buckets"]) == len(lr.schedule[overlap]) and all(x["allreduce_ms"] >= 0 for x in cs["buckets"]), cs
         assert N.pair_status(clear=True) == 0, "a paired kernel's partner wait timed out"
         if rank == 0:   # (1) single-process full batch, same weights
-            r = UnrollRunner(Bt, T, 84, 84, 4, A, dtype, dev)
+            r = UnrollRunner(Bt, T, H, H, nq, A, dtype, dev)
             pk, ws = r.new_packed(), r.new_workspace()
             r.pack(lr.flat, pk)
             r.forward(lr.flat, pk, lr.basis, X.to(dev), ws, want_attn=False)
@@ -92,10 +96,10 @@ def main():
             layout = (r.offsets, r.sizes)
         dist.barrier()
     if rank == 0:   # (2) the oracle on the full batch
-        ref = oracle_grads(X, Gl, Gv, dtype, A)
+        ref = oracle_grads(X, Gl, Gv, dtype, A, nq)
         offs, sizes = layout
         worst = 0.0
-        for (name, shape), o, n in zip(detinit.param_shapes(A), offs, sizes):
+        for (name, shape), o, n in zip(detinit.param_shapes(A, nq), offs, sizes):
             gr = ref[name].reshape(-1).float()
             gd = grads_dp[o:o + n]
             if float(gr.norm()) == 0.0:
@@ -106,14 +110,15 @@ def main():
         ok &= worst <= tol
         # (3) phase -> bucket write disjointness: poison the grads, run each
         # phase alone, and check that it changed nothing outside its bucket
-        r = UnrollRunner(b, T, 84, 84, 4, A, dtype, dev)   # (lr: the last learner; no new collective here)
+        r = UnrollRunner(b, T, H, H, nq, A, dtype, dev)   # (lr: the last learner; no new collective here)
         pk, ws = r.new_packed(), r.new_workspace()
         r.pack(lr.flat, pk)
         Xr = X[:, rows].contiguous().to(dev)
         r.forward(lr.flat, pk, lr.basis, Xr, ws, want_attn=False)
         gbuf = torch.full((r.n_params,), float("nan"), device=dev)
-        issued = []   # buckets whose all-reduce an earlier phase already started
-        for phase, (lo, hi) in zip((N.BWD_HEAD, N.BWD_CORE, N.BWD_VISION), lr.bounds):
+        issued = []   # ranges whose all-reduce the schedule has already started
+        sched = dict(lr.schedule[True])
+        for phase in (N.BWD_HEAD, N.BWD_CORE, N.BWD_VISION):
             before = gbuf.clone()
             r.backward(lr.flat, pk, lr.basis, Xr, ws, Gl[:, rows].contiguous().to(dev),
                        Gv[:, rows].contiguous().to(dev), grads=gbuf, phases=phase)
@@ -122,7 +127,7 @@ def main():
             bad = sum(int(changed[a:z].sum()) for a, z in issued)
             res[f"phase{phase}_writes_into_issued_buckets"] = bad
             ok &= bad == 0
-            issued.append((lo, hi))
+            issued += sched.get(phase, [])
         res["ok"] = bool(ok)
         print(json.dumps(res), flush=True)
     dist.barrier()

@@ -1,7 +1,7 @@
 // Microbenchmark of the bf16 frame-resident ConvLSTM BPTT (csrc/recur_bwd.h) on
 // random operands: the band kernel at config 5's shape (B = 64, T = 50, 21x21
 // grid, 4 bands) and the single-workgroup kernel at config 3's (B = 256, T = 20,
-// 11x11), plus the split-role kernel (csrc/recur_bwd_split.h) at both.  Device
+// 11x11), plus the split-role kernel (tools/ubench/recur_bwd_split.h, a rejected variant kept out of libaaa.so) at both.  Device
 // time per launch of the production kernels and of their ablations (ABL bits
 // in recur_bwd.h) and -- built with -DAAA_STAMPS -- per-step phase times.
 // Timing only: the results are not checked (tests/test_gpu_band.py,

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 5   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 6   # include/aaa.h AAA_ABI_VERSION
 E_STRANDED = -5   # AAA_E_STRANDED
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 
@@ -28,9 +28,13 @@ EXPORTS = (
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
-    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_debug_pair_spin",
+    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag", "aaa_debug_pair_spin",
+    "aaa_adam_step_guarded",
 )
+# include/aaa.h enum aaa_timer
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
+TIMER_PACK, TIMER_VISION_FWD, TIMER_TAIL_FWD, TIMER_TAIL_BWD, TIMER_CORE_DX, TIMER_VISION_BWD, TIMER_MISC = range(5, 12)
+TIMER_N = 12
 
 
 class Cfg(ctypes.Structure):
@@ -48,7 +52,7 @@ FLAG_FRAMES_U8 = 2
 
 class TimerStats(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("launches", ctypes.c_long), ("work", ctypes.c_double),
-                ("variant", ctypes.c_char * 96)]
+                ("variant", ctypes.c_char * 192)]
 
 
 class IO(ctypes.Structure):
@@ -118,6 +122,8 @@ def load(path: str = LIB_PATH):
             "aaa_timing_read": (I, [I, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]),
             "aaa_timing_stats": (I, [I, ctypes.POINTER(TimerStats)]),
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
+            "aaa_adam_step_guarded": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, P, I, P, P, P, P, P, P, P]),
+            "aaa_pair_flag": (I, [P, P]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
             "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
             "aaa_convlstm_packed_bytes": (S, [ctypes.POINTER(CellDesc)]),
@@ -217,7 +223,7 @@ def timing_read(kind: int):
 
 def timing_stats(kind: int) -> dict:
     """Kernel class ``kind`` since the last read: device ms, launches, the
-    launches' algorithmic work (FLOP for classes 0-2, bytes for 3-4) as the
+    launches' algorithmic work (FLOP for classes 0-2 and 6-10, bytes for 3-4) as the
     runtime accounts it, and the variant it dispatched."""
     s = TimerStats()
     check(load().aaa_timing_stats(kind, ctypes.byref(s)), "timing_stats")
@@ -234,13 +240,23 @@ def pair_status(clear: bool = True, stream=None) -> int:
     return n
 
 
-def debug_pair_spin(polls: int) -> None:
-    """Bound the paired kernels' partner wait to ``polls`` polls (0 = default).  Test hook."""
-    check(load().aaa_debug_pair_spin(int(polls)), "debug_pair_spin")
+def pair_flag(dst, stream=None) -> None:
+    """Enqueue a copy of the pending partner-timeout count into the one-element
+    fp32 device tensor ``dst`` (stream order, not consumed, no host sync)."""
+    check(load().aaa_pair_flag(dst.data_ptr(), stream if stream is not None else stream_ptr(dst.device)), "pair_flag")
 
 
-def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None) -> None:
-    """One fused Adam launch over lists of same-length fp32 device tensors (aaa_adam_step)."""
+def debug_pair_spin(ticks: int) -> None:
+    """TEST HOOK: bound the multi-workgroup kernels' partner wait to ``ticks``
+    100-MHz ticks after a workgroup's first wait (0 = the default budget)."""
+    check(load().aaa_debug_pair_spin(int(ticks)), "debug_pair_spin")
+
+
+def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None,
+              guard=None) -> None:
+    """One fused Adam launch over lists of same-length fp32 device tensors
+    (aaa_adam_step; with ``guard``, a one-element fp32 device tensor,
+    aaa_adam_step_guarded: no update when guard != 0)."""
     n = len(params)
     VP = ctypes.c_void_p * max(n, 1)
     def arr(ts):
@@ -249,6 +265,10 @@ def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp
     for group in (grads, exp_avg, exp_avg_sq) + ((max_exp_avg_sq,) if max_exp_avg_sq is not None else ()):
         assert len(group) == n
     mx = arr(max_exp_avg_sq)
-    check(load().aaa_adam_step(ctypes.byref(hp), int(step), n, arr(params), arr(grads), arr(exp_avg),
-                               arr(exp_avg_sq), mx, numel, stream if stream is not None else stream_ptr()),
-          "adam_step")
+    st = stream if stream is not None else stream_ptr()
+    if guard is not None:
+        check(load().aaa_adam_step_guarded(ctypes.byref(hp), int(step), guard.data_ptr(), n, arr(params), arr(grads),
+                                           arr(exp_avg), arr(exp_avg_sq), mx, numel, st), "adam_step_guarded")
+    else:
+        check(load().aaa_adam_step(ctypes.byref(hp), int(step), n, arr(params), arr(grads), arr(exp_avg),
+                                   arr(exp_avg_sq), mx, numel, st), "adam_step")

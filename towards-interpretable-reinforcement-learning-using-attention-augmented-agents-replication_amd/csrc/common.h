@@ -82,20 +82,30 @@ struct FastDiv {
 
 
 // Bounded wait of one lane for a partner workgroup's published step count
-// (the paired frame-resident kernels, recur.h / recur_bwd.h).  On timeout the
-// lane adds 1 to ``report`` -- a word of pinned host memory mapped into the
-// device (runtime.hip pair_report), so the host reads it with no copy -- and
-// returns: the kernel never hangs, and the host turns the report into
-// AAA_E_STRANDED at the next API call (or aaa_pair_status) instead of handing
-// back results computed from a stale partner half.
-__device__ __forceinline__ void pair_wait(const int* flag, int target, int* report, int spin) {
-  int n = 0;
+// (the multi-workgroup frame-resident kernels, recur*.h).  The bound is a
+// deadline on the 100-MHz real-time counter: ``budget`` ticks after this
+// workgroup's first wait that had to poll (``dl`` = 0 until then; the kernel
+// keeps it in one variable for all its waits).  Past the deadline the lane
+// adds 1 to ``report`` -- a word of pinned host memory mapped into the device
+// (rt_core.hip pair_report), so the host reads it with no copy -- and returns;
+// every later wait of that workgroup that is not satisfied at once returns
+// after one poll, so a kernel whose partner never arrives ends within about
+// ``budget`` ticks whatever its step count.  The host turns the report into
+// AAA_E_STRANDED at the next API call (or aaa_pair_status), and a guarded
+// optimizer step (aaa_pair_flag + aaa_adam_step_guarded) skips the update.
+__device__ __forceinline__ bool wait_expired(uint64_t& dl, int budget) {
+  const uint64_t now = __builtin_amdgcn_s_memrealtime();
+  if (!dl) dl = now + (uint64_t)(budget > 0 ? budget : 1);
+  return now >= dl;
+}
+
+__device__ __forceinline__ void pair_wait(const int* flag, int target, int* report, int budget, uint64_t& dl) {
   while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++n > spin) {
+    if (wait_expired(dl, budget)) {
       __hip_atomic_fetch_add(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
+    __builtin_amdgcn_s_sleep(1);
   }
 }
 
@@ -113,16 +123,16 @@ __device__ __forceinline__ void stagger_wait(int ticks) {
 
 // The same for several partners at once, by one wave: lane j polls flags[j]
 // for every bit j of ``mask`` (j < 64), all in one round trip per poll (a loop
-// of pair_wait calls pays one L2 round trip per partner, in sequence).  On
-// timeout one lane adds 1 to ``report`` and the wave returns.
+// of pair_wait calls pays one L2 round trip per partner, in sequence).  Past
+// the deadline one lane adds 1 to ``report`` and the wave returns.
 __device__ __forceinline__ void wave_wait_flags(const int* flags, unsigned long long mask, int target, int* report,
-                                                int spin) {
+                                                int budget, uint64_t& dl) {
   const int lane = (int)(threadIdx.x & 63);
   const bool mine = (mask >> lane) & 1ull;
-  for (int n = 0;; ++n) {
+  for (;;) {
     const int v = mine ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
     if (__all(v >= target)) return;
-    if (n >= spin) {
+    if (wait_expired(dl, budget)) {
       if (lane == 0) __hip_atomic_fetch_add(report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
@@ -133,7 +143,9 @@ __device__ __forceinline__ void wave_wait_flags(const int* flags, unsigned long 
 // Launch a paired kernel (two cooperating workgroups per frame) as an ordinary
 // dispatch whose whole grid fits one residency wave of the device: every
 // workgroup is placed at once on an idle chip, and the bounded partner waits
-// (pair_wait) report instead of hanging if a pair is ever not co-resident.
+// (pair_wait) report instead of hanging if a pair is ever not co-resident
+// (another kernel holding CUs: Learner.step never overlaps a collective with
+// these launches).
 // Not hipLaunchCooperativeKernel: ANY cooperative launch makes a process that
 // rocprofv3 profiles crash in exit() after the tool's finalisation -- a trivial
 // 256-workgroup kernel with no libaaa.so loaded reproduces it

@@ -21,10 +21,12 @@ struct AdamHost {
   double lr, beta1, beta2, eps, weight_decay;
   long step;
   int amsgrad, maximize;
+  const float* guard = nullptr;   // device float: skip the update when != 0
 };
 
 int adam_chunks(size_t numel);
 hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st);
+hipError_t pair_flag_launch(const int* report, float* dst, hipStream_t st);
 
 // loss.hip: REINFORCE (finish_episode) loss + logits cotangent, one workgroup per episode
 hipError_t reinforce_launch(int T, int B, int A, const float* logits, const int* actions, const float* rewards,

@@ -24,6 +24,7 @@ namespace aaa {
 struct AdamScalars {
   float wd, one_m_b1, b2, one_m_b2, step_size_neg, bc2_sqrt, eps;
   int amsgrad, maximize;
+  const float* guard;   // skip the whole update when *guard != 0 (aaa_adam_step_guarded), or nullptr
 };
 
 __device__ __forceinline__ float adam_elem(float& p, float g, float& m, float& v, float* vmax, const AdamScalars& s) {
@@ -47,6 +48,7 @@ constexpr int kAdamChunk = kAdamThreads * kAdamVec * 4;       // elements per wo
 // Workgroup -> (tensor, chunk) through the chunk prefix table; tensors whose
 // pointers are all 16-byte aligned use 16-byte vectors, the rest scalars.
 __global__ void __launch_bounds__(kAdamThreads) k_adam(AdamTable tab, AdamScalars s) {
+  if (s.guard && *s.guard != 0.f) return;   // gradients of a stranded launch: no update on any rank
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < tab.n && tab.chunk0[t + 1] <= b) ++t;
@@ -101,8 +103,20 @@ hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hip
   s.eps = (float)h.eps;
   s.amsgrad = h.amsgrad;
   s.maximize = h.maximize;
+  s.guard = h.guard;
   if (nchunks <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_adam, dim3(nchunks), dim3(kAdamThreads), 0, st, tab, s);
+  return hipGetLastError();
+}
+
+// The pending partner-timeout count of the frame-resident kernels (the pinned,
+// device-mapped report word) as one float, read in stream order.
+__global__ void k_pair_flag(const int* __restrict__ report, float* __restrict__ dst) {
+  if (threadIdx.x == 0) dst[0] = (float)__hip_atomic_load(report, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t pair_flag_launch(const int* report, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pair_flag, dim3(1), dim3(64), 0, st, report, dst);
   return hipGetLastError();
 }
 

@@ -91,7 +91,7 @@ struct RecFwdParams {
   int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed); band mode: [B][bands]
   int T, B, h, w, P;
   int* report;         // G = 2: partner-timeout report word (pinned host, device-mapped; pair_wait)
-  int spin;            // G = 2: partner-wait bound in polls
+  int spin;            // G = 2 / band: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;         // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
   // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
   // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     r1 = (band + 1) * p.h / kRecBands;
   }
   const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;   // partner-wait deadline (common.h wait_expired), set by the first wait that polls
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR) for the buffer soffsets
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (r1 - r0 + 2) * W2;
@@ -366,7 +367,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         if (wave == 0)   // the neighbour bands' flags, both in one poll
           wave_wait_flags(p.flags + b * kRecBands,
                           (band > 0 ? 1ull << (band - 1) : 0ull) | (band < kRecBands - 1 ? 1ull << (band + 1) : 0ull), t,
-                          p.report, p.spin);
+                          p.report, p.spin, wdl);
         barrier_lds();
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
         const int nh = p.w * 16;   // 16-B pieces of one grid row
@@ -385,7 +386,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     if constexpr (G == 2) {
       if (t > 0) {   // the partner's half of h_{t-1} (XH slot t) into the image, once it has published it
         if (tid == 0) {
-          pair_wait(p.flags + 2 * b + (1 - kh), t, p.report, p.spin);   // bounded: a stranded partner reports
+          pair_wait(p.flags + 2 * b + (1 - kh), t, p.report, p.spin, wdl);   // bounded: a stranded partner reports
           if constexpr (ABL & 16) {   // fenced hand-off (A/B only)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -84,7 +84,7 @@ struct RecBwdParams {
   int* flags;             // paired kernel: per (frame, half) count of published dZ steps ([2B], zeroed)
   int T, B, h, w, P;
   int* report;            // paired kernel: partner-timeout report word (pinned host, device-mapped; pair_wait)
-  int spin;               // paired kernel: partner-wait bound in polls
+  int spin;               // paired / band kernels: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;            // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
 };
 
@@ -144,6 +144,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     r1 = (band + 1) * p.h / kRecBands;
   }
   const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;   // partner-wait deadline (common.h wait_expired), set by the first wait that polls
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (r1 - r0 + 2) * W2;
@@ -385,7 +386,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       if (wave == 0)   // the neighbour bands' flags, both in one poll
         wave_wait_flags(p.flags + b * kRecBands,
                         ((band > 0 ? 1ull : 0ull) << (band - 1 + (band == 0))) | (band < kRecBands - 1 ? 2ull << band : 0ull),
-                        p.T - t, p.report, p.spin);
+                        p.T - t, p.report, p.spin, wdl);
       barrier_lds();
       const __amdgpu_buffer_rsrc_t rs =
           make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
@@ -605,6 +606,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 8 * 64];          // dc carry, lane-native [wave][g*2+j][lane]
   const int b = (int)blockIdx.x % p.B, kh = (int)blockIdx.x / p.B;
   const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;   // partner-wait deadline (common.h wait_expired), set by the first wait that polls
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2;
@@ -848,7 +850,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           }
         }
         if (ck == 0 && tid == 0) {   // the partner's dZ_t published? (the other waves load after the barrier)
-          pair_wait(p.flags + 2 * b + (1 - kh), p.T - t, p.report, p.spin);
+          pair_wait(p.flags + 2 * b + (1 - kh), p.T - t, p.report, p.spin, wdl);
         }
         barrier_lds();   // image c & 1 free for the partner's chunk; (ck = 1, 2) its refill complete
       }

@@ -74,7 +74,7 @@ struct RecBwdF32Params {
   float* xp;           // partial-dh exchange (b32_xpart_floats)
   int* flags;          // [B][8] count of published partial steps (zeroed by the caller)
   int* report;         // partner-timeout report word (pair_wait)
-  int spin;
+  int spin;           // partner-wait budget, 100-MHz ticks (pair_wait)
   int T, B, h, w, P;
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
 };
@@ -104,6 +104,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   const int b = xcd + 8 * (loc / G), kh = loc % G;
   if (b >= p.B) return;
   const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;   // partner-wait deadline (common.h wait_expired), set by the first wait that polls
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int rw = wave & 1, cw = wave >> 1;
@@ -284,7 +285,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     barrier_lds();
     if (tid == 0) __hip_atomic_store(p.flags + b * G + kh, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every wave waits for the seven partners, then sums their partials into its groups
-    if constexpr (!(ABL & 1)) wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), it + 1, p.report, p.spin);
+    if constexpr (!(ABL & 1)) wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), it + 1, p.report, p.spin, wdl);
     AAA_B32_STAMP(it, 2);
     f32x4 dhv[NG];
 #pragma unroll

@@ -77,7 +77,7 @@ struct RecF32Params {
   float* Gt;           // (T, B, P, 512) <- gate activations (i, f, c~, o)
   int* flags;          // [B][G] count of published h steps (zeroed by the caller)
   int* report;         // partner-timeout report word (pair_wait)
-  int spin;            // partner-wait bound in polls
+  int spin;            // partner-wait budget, 100-MHz ticks (pair_wait)
   int T, B, h, w, P;
   int h0_zero;         // slot 0's h part is zero (reset()): the t = 0 h-part is skipped
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
@@ -121,6 +121,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
   const int b = xcd + 8 * (loc / G), kh = loc % G;
   if (b >= p.B) return;   // padding group of the last XCD column (never a partner of a live frame)
   const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;   // partner-wait deadline (common.h wait_expired), set by the first wait that polls
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
@@ -245,7 +246,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
     const bool exch = G > 1 && t > 0 && !(ABL & 4);
     AAA_F32_STAMP(t, 0);
     auto partner_issue = [&] {
-      wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), t, p.report, p.spin);
+      wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), t, p.report, p.spin, wdl);
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
 #pragma unroll
       for (int n = 0; n < NPL; ++n) {

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -24,7 +25,6 @@
 #include "halo.h"
 #include "recur.h"
 #include "recur_bwd.h"
-#include "recur_bwd_split.h"
 #include "recur_f32.h"
 #include "recur_bwd_f32.h"
 #include "vision.h"
@@ -72,6 +72,16 @@ struct Layout {
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
 };
 
+// Algorithmic FLOP per frame of the other timer classes:
+// conv1 (K = 8*8*3) and conv2 (K = 4*4*32) forward; the answer MLP + LSTMCell
+// (zero state: W_ih only); their backward is twice that (dgrad + wgrad); the
+// conv2 wgrad + dgrad and conv1 wgrad of the vision backward.
+inline double vision_fwd_flop(const Layout& L) { return 2.0 * L.P1 * 32 * 192 + 2.0 * L.P * 64 * 512; }
+inline double tail_fwd_flop(const Layout& L) {
+  return 2.0 * ((double)L.ans_in * 512 + 512.0 * 256 + 256.0 * 1024);
+}
+inline double vision_bwd_flop(const Layout& L) { return 2.0 * (2.0 * L.P * 64 * 512) + 2.0 * L.P1 * 32 * 192; }
+
 // min_frames: the frames one launch must be able to address (a step's B for
 // the unroll; 1 for the frame-independent vision encoder entries).
 int build_layout(const aaa_cfg* c, Layout& L, int min_frames = 0);
@@ -87,7 +97,8 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // entry consumes pending reports and fails with AAA_E_STRANDED (the results of
 // the call that stranded are invalid); aaa_pair_status syncs a stream first.
 // Allocated once per process on first use, never freed (no HIP call at exit).
-extern long g_pair_spin;   // partner-wait bound in polls (aaa_debug_pair_spin)
+extern long g_pair_spin;   // partner-wait budget override in ticks (aaa_debug_pair_spin; 0 = default)
+int pair_budget(int T);    // partner-wait budget of a T-step launch, 100-MHz ticks
 int* pair_report(int dev);  // this device's report word, device-mapped (nullptr: cannot map)
 int pair_take();            // pending reports of the current device (consumed)
 int pair_peek();            // ... (left pending)
@@ -403,8 +414,8 @@ static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const Ep
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
   const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
   TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728,
-                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d", std::is_same<T, float>::value ? "fp32" : "bf16",
-                      ftile));
+                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d [kernel: EpiConvLstmFwd]",
+                      std::is_same<T, float>::value ? "fp32" : "bf16", ftile));
   if (ftile == 7)
     HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
   else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring

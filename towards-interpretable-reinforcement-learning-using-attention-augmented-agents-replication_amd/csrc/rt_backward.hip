@@ -189,7 +189,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // the other weight gradients doubled the output atomics for the same time:
     // profiles/r02/ab/wgrad_split.txt)
     const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, 512 / tiles)), rows / CW::BK));
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics", CW::BI, CW::BJ, CW::BK, ns));
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics [kernel: gemm_kernel+LdIm2colTB]", CW::BI, CW::BJ, CW::BK, ns));
     HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
   };
@@ -205,7 +205,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
                            1728, xh_bytes};
     EpiAtomicD ep{{gW, 1728, 512, 1728}};
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("LDS-DMA ring %dx%d BK%d, %d-deep", CW::BI, CW::BJ, CW::BK, NB));
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("LDS-DMA ring %dx%d BK%d, %d-deep [kernel: gemm_pipe_kernel+GIm2colT]", CW::BI, CW::BJ, CW::BK, NB));
     // split-K over pixels: about one resident wave of workgroups (fewer
     // passes of the output's atomics than the register path's ~1024)
     const int wgs = env_int("AAA_WGRAD_WGS", 256);
@@ -224,7 +224,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     EpiAtomicD ep{{gW, 1728, 512, 1728}};
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
-                   strf("LDS-DMA read-ahead ring %dx%d BK%d, %d-deep", CW::BI, CW::BJ, CW::BK, NB));
+                   strf("LDS-DMA read-ahead ring %dx%d BK%d, %d-deep [kernel: gemm_pipe_ra_kernel+GIm2colT]", CW::BI, CW::BJ, CW::BK, NB));
     const int wgs = env_int("AAA_WGRAD_WGS", 256);
     const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
     HIPCHK((launch_pipe_ra<CW, LA, LB, EpiAtomicD, NB>(pa, pb, ep, 512, 1728, rows, ns, s)));
@@ -435,13 +435,18 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
   LstmGrads core_unpack{};   // the ConvLSTM grads' reference tensors, unpacked with the vision grads when both run here
 
   if (phases & AAA_BWD_HEAD) {
-    HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
-    HIPCHK(hipMemsetAsync(ws + L.dQs, 0, L.ws - L.dQs, st));
-    HIPCHK(concat_dy(F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
+    {
+      TimerScope tim(AAA_TIMER_MISC, st, 0.0, "grad/accumulator memsets, cotangent concat");
+      HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
+      HIPCHK(hipMemsetAsync(ws + L.dQs, 0, L.ws - L.dQs, st));
+      HIPCHK(concat_dy(F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
+    }
     if (L.sc) {
       const int rc = head_backward_stateful(L, io, st);
       if (rc) return rc;
     } else {
+    std::unique_ptr<TimerScope> tail(new TimerScope(AAA_TIMER_TAIL_BWD, st, 2.0 * F * (tail_fwd_flop(L) + 2.0 * 256 * L.ldy),
+                                                    "heads + LSTMCell + answer MLP backward (fp32 GEMMs)"));
     {  // heads dgrad fused with the zero-state LSTMCell backward
       LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
       LRfj::Params pb{Wf(L.dY), L.ldy, F};
@@ -491,12 +496,14 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 512, L.ans_ld, F,
                                         wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), st)));
     }
+    tail.reset();
     // attention readout / softmax / logits backward, then the query MLP
     {
       TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)F * attn_bwd_bytes(P, L.nq), "k_attn_bwd, 1 WG per frame");
       HIPCHK(attn_bwd(Wf(L.Hs), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
                       Wf(L.dO), Wf(L.dQp), st));
     }
+    tail.reset(new TimerScope(AAA_TIMER_TAIL_BWD, st, 0.0, "bias column sums, query MLP backward, grad unpack"));
     {  // the bias grads of the heads, the LSTMCell and both answer layers, and dQ summed over frames: one launch
       ColSums cs;
       cs.add(Wf(L.dY), L.ldy, L.ldy, Wf(L.gbhd));
@@ -535,6 +542,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       if (rc) return rc;
     }
     if (!dx_fused) {  // dx_t for these steps: D[64][rows] = WdT[0:64] * gather(dZ)
+      TimerScope tim(AAA_TIMER_CORE_DX, s, 2.0 * rows * 64 * 4608, "batched dx (conv2-output grad), K=4608 [kernel: EpiStoreBiasT]");
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       const T* WdT = (const T*)(pk + L.k_WdTl);
       const uint32_t zb = (uint32_t)((size_t)rows * 512 * L.esz);
@@ -577,6 +585,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       }
     }
     if (!vision_here) return AAA_OK;
+    TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L), "conv2 wgrad + dgrad, conv1 wgrad");
     const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
     T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
     const int rows1 = F1 * L.P1;
@@ -598,6 +607,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     hipStream_t ax = aux_stream();
     hipStream_t os = ax ? ax : st;     // stream for the off-chain chunks
     const int cs = chunk_steps(L);
+    std::unique_ptr<TimerScope> misc(new TimerScope(AAA_TIMER_MISC, st, 0.0, "BPTT state in, last-step gate backward"));
     // ConvLSTM BPTT, t = T-1 .. 0
     if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
@@ -634,6 +644,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                                       Wf(L.Cst) + (size_t)t1 * M * 128, Wf(L.Cst) + (size_t)(t1 + 1) * M * 128,
                                       Wf(L.dC), Wt(L.dZ) + (size_t)t1 * M * 512,
                                       part ? part + (size_t)t1 * ntj * 512 : nullptr, st)));
+    misc.reset();
     const uint32_t dz_bytes = (uint32_t)((size_t)M * 512 * L.esz);  // one step slice of dZ
     const T* WdTh = (const T*)(pk + L.k_WdTl) + (size_t)64 * 4608;
     int done_hi = L.T;   // chunks [lo, done_hi) not yet issued
@@ -651,7 +662,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       if constexpr (!std::is_same<T, float>::value) {
         RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
                         Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), (int*)(ws + L.rflags),
-                        L.T, L.B, L.h, L.w, L.P, nullptr, (int)g_pair_spin, rec_stagger("AAA_REC_STAGGER_BWD")};
+                        L.T, L.B, L.h, L.w, L.P, nullptr, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_BWD")};
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));
@@ -664,14 +675,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
           TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 4608 * (128.0 * (L.T - 1 + (io->dh0 ? 1 : 0)) + 64.0 * L.T),
                          fb == kRecBands && !rec_fits(L.h, L.w)
                              ? strf("bf16 band-mode frame-resident BPTT + dx, %d steps per launch, %d bands per frame, "
-                                    "fp16 gates", L.T, fb)
-                             : strf("bf16 frame-resident BPTT + dx, %d steps per launch, %d WG per frame, fp16 gates",
-                                    L.T, fb));
-          // AAA_BWD_SPLIT=1: the split-role kernel (recur_bwd_split.h) for G = 1 and band mode
-          const bool split = fb != 2 && env_int("AAA_BWD_SPLIT", 0);
-          HIPCHK(fb == 2 ? convlstm_bwd_pairs(rp, st)
-                         : split ? convlstm_bwd_split(rp, fb != 1, st)
-                                 : (fb == 1 ? convlstm_bwd_frames(rp, st) : convlstm_bwd_band(rp, st)));
+                                    "fp16 gates [kernel: k_convlstm_bwd_frames<0, true]", L.T, fb)
+                             : strf("bf16 frame-resident BPTT + dx, %d steps per launch, %d WG per frame, fp16 gates "
+                                    "[kernel: %s]", L.T, fb, fb == 2 ? "k_convlstm_bwd_pairs" : "k_convlstm_bwd_frames<0, false"));
+          HIPCHK(fb == 2 ? convlstm_bwd_pairs(rp, st) : (fb == 1 ? convlstm_bwd_frames(rp, st) : convlstm_bwd_band(rp, st)));
         }
         HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
         dx_fused = true;
@@ -685,10 +692,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         int* rep = pair_report(dev);
         if (!rep) return fail(AAA_E_LAUNCH, "cannot map the frame-group report word");
         RecBwdF32Params rp{(const float*)(pk + L.k_Wb32), Wf(L.dO), Wf(L.Gt), Wf(L.Cst), Wf(L.dC), Wf(L.dZ),
-                           Wf(L.dZp), io->dh0, Wf(L.xpart), (int*)(ws + L.rflags), rep, (int)g_pair_spin,
+                           Wf(L.dZp), io->dh0, Wf(L.xpart), (int*)(ws + L.rflags), rep, pair_budget(L.T),
                            L.T, L.B, L.h, L.w, L.P, {}};
         TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
-                       strf("fp32 frame-group BPTT (dh rows), %d steps per launch, 8 WG per frame", L.T));
+                       strf("fp32 frame-group BPTT (dh rows), %d steps per launch, 8 WG per frame [kernel: k_convlstm_bwd_f32]", L.T));
         HIPCHK(convlstm_bwd_f32(rp, st));
       }
     }
@@ -699,7 +706,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       if (!prev && !io->dh0) break;
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
-      TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608, strf("%s dh dgrad + fused gate bwd, K=4608, AAA_BPTT_TILE %d%s", std::is_same<T, float>::value ? "fp32" : "bf16", bwd_tile, g16 ? ", fp16 gates" : ""));
+      TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608, strf("%s dh dgrad + fused gate bwd, K=4608, AAA_BPTT_TILE %d%s", std::is_same<T, float>::value ? "fp32" : "bf16", bwd_tile, g16 ? ", fp16 gates [kernel: EpiConvLstmBwd]" : " [kernel: EpiConvLstmBwd]"));
       auto step = [&](auto gtag) -> hipError_t {
         using GT = decltype(gtag);
         using EB = EpiConvLstmBwd<T, GT>;
@@ -791,6 +798,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       HIPCHK(e);
     }
     { const int rc0 = flush(0); if (rc0) return rc0; }
+    misc.reset(new TimerScope(AAA_TIMER_MISC, st, 0.0, "gate-bias column sums, state grads out, grad unpack"));
     // gate-bias gradient: column sum of the per-(step, tile) partials, or of dZ itself
     if (fb)   // per (step, frame[, pixel half]) partials
       HIPCHK(colsum<float>(Wf(L.dZp), 512, L.T * L.B * fb, 512, Wf(L.gbl), st));
@@ -812,6 +820,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
   }
 
   if (phases & AAA_BWD_VISION) {
+    TimerScope tim(AAA_TIMER_VISION_BWD, st, vision_here ? 0.0 : (double)F * vision_bwd_flop(L),
+                   "conv2 wgrad + dgrad, conv1 wgrad, grad unpack");
     if (!vision_here) {   // VISION alone: its chunk work over all frames, here
       const int rows1 = F * L.P1;
       constexpr bool f32 = std::is_same<T, float>::value;

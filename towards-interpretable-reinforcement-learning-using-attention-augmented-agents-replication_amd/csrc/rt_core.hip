@@ -197,7 +197,15 @@ int check_device() {
 static std::mutex g_pair_mu;
 static int* g_pair_host = nullptr;    // [64] words, one per device ordinal
 static int* g_pair_dev = nullptr;     // the same words, device-mapped
-long g_pair_spin = 1L << 24;   // partner-wait bound in polls (aaa_debug_pair_spin)
+long g_pair_spin = 0;   // partner-wait budget override, 100-MHz ticks (aaa_debug_pair_spin; 0 = pair_budget's)
+
+// Partner-wait budget of one multi-workgroup launch of T steps: 1 s plus 20 ms
+// per step (the slowest legitimate launch, C5's band BPTT, takes ~80 us per
+// step), so only a partner that is not running at all exhausts it.
+int pair_budget(int T) {
+  if (g_pair_spin > 0) return (int)std::min<long>(g_pair_spin, 0x7fffffffL);
+  return (int)std::min<long>(100000000L + 2000000L * (long)T, 0x7fffffffL);
+}
 
 int* pair_report(int dev) {
   std::lock_guard<std::mutex> lk(g_pair_mu);
@@ -305,7 +313,7 @@ hipError_t stream_order(hipStream_t from, hipStream_t to) {
 Timers g_timers;
 
 std::string strf(const char* fmt, ...) {
-  char buf[160];
+  char buf[256];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);

@@ -151,13 +151,16 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   const int F = L.F, M = L.B * L.P;
 
   {  // conv1 + conv2 over all T*B frames -> XH[:, :, 0:64] of every slot
+    TimerScope tim(AAA_TIMER_VISION_FWD, st, (double)F * vision_fwd_flop(L), "conv1 + conv2 (vision encoder)");
     const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st);
     if (rc) return rc;
   }
-  // initial state (reset(): zeros, attention.py:142-149) or carried state
-  HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
-  if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
-  else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  {  // initial state (reset(): zeros, attention.py:142-149) or carried state
+    TimerScope tim(AAA_TIMER_MISC, st, 0.0, "state in/out copies, memsets, bias column sums");
+    HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
+    if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
+  }
   if constexpr (std::is_same<T, float>::value) {
     if (const int G = f32_frames(L)) {   // one frame-group launch for all T steps, x-part included (recur_f32.h)
       HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)G * L.B * 4, st));
@@ -166,11 +169,11 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
       int* rep = pair_report(dev);
       if (!rep) return fail(AAA_E_LAUNCH, "cannot map the frame-group report word");
       RecF32Params rp{(const float*)(pk + L.k_Wf32), (const float*)(pk + L.k_bl), Wf(L.XH), Wf(L.Cst), Wf(L.Hs),
-                      Wf(L.Gt), (int*)(ws + L.rflags), rep, (int)g_pair_spin, L.T, L.B, L.h, L.w, L.P,
+                      Wf(L.Gt), (int*)(ws + L.rflags), rep, pair_budget(L.T), L.T, L.B, L.h, L.w, L.P,
                       io->h0 ? 0 : 1, {}};
       {
         TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
-                       strf("fp32 frame-group [x|h] recurrence, %d steps per launch, %d WG per frame", L.T, G));
+                       strf("fp32 frame-group [x|h] recurrence, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]", L.T, G));
         HIPCHK(convlstm_fwd_f32(rp, G, st));
       }
       return forward_tail<T>(L, io, st);
@@ -197,10 +200,10 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
           if (!rep) return fail(AAA_E_LAUNCH, "cannot map the band-mode report word");
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
                               Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
-                              rep, (int)g_pair_spin, rec_stagger("AAA_REC_STAGGER_FWD")};
+                              rep, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_FWD")};
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
-                         strf("bf16 band-mode frame-resident [x|h] recurrence, %d steps per launch, %d bands per frame",
-                              L.T, NBd));
+                         strf("bf16 band-mode frame-resident [x|h] recurrence, %d steps per launch, %d bands per frame "
+                              "[kernel: k_convlstm_fwd_frames+Lb1E]", L.T, NBd));
           HIPCHK(convlstm_fwd_frames_band<GT>(rp, st));
           return AAA_OK;
         }
@@ -214,9 +217,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
           }
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
                               Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
-                              rep, (int)g_pair_spin, rec_stagger("AAA_REC_STAGGER_FWD")};
+                              rep, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_FWD")};
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
-                         strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame", L.T, G));
+                         strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_frames+Lb0E]", L.T, G));
           HIPCHK(convlstm_fwd_frames<GT>(rp, G, st));
           return AAA_OK;
         }
@@ -283,7 +286,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                          Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
                          Wf(L.Gt) + (size_t)t * M * 512, M};
     const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
-    TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1152, strf("%s h-part step (x-part batched), K=1152, tile %d", std::is_same<T, float>::value ? "fp32" : "bf16", fwd_tile));
+    TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1152, strf("%s h-part step (x-part batched), K=1152, tile %d [kernel: EpiConvLstmFwd]", std::is_same<T, float>::value ? "fp32" : "bf16", fwd_tile));
     const T* WpH = (const T*)(pk + L.k_WpH);
     const T* xh = Wt(L.XH) + (size_t)t * M * 192;
     hipError_t e;
@@ -420,12 +423,16 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
   } else {
   // constant query (Q1) + fused attention readout over all T*B frames
   const float* Qc = (const float*)(pk + L.k_Q);
-  HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
+  {
+    TimerScope tim(AAA_TIMER_TAIL_FWD, st, 0.0, "query basis logits");
+    HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
+  }
   {
     TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld), "k_attn_fwd, 1 WG per frame");
     HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
                     Wf(L.ans), L.ans_ld, st));
   }
+  TimerScope tim(AAA_TIMER_TAIL_FWD, st, (double)F * tail_fwd_flop(L), "answer MLP + LSTMCell + heads (fp32 GEMMs)");
   if (io->attn) HIPCHK(hipMemcpyAsync(io->attn, Wf(L.Am), (size_t)F * P * L.nq * 4, hipMemcpyDeviceToDevice, st));
   using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
   using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;
@@ -448,6 +455,7 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     HIPCHK((tail_gemm(pa, pb, ep, 1024, F, 256, st)));
   }
   }
+  TimerScope tim(AAA_TIMER_TAIL_FWD, st, L.sc ? 0.0 : 2.0 * F * 256 * 2 * L.A, "policy/value heads + state out");
   {  // policy / values heads (attention.py:365-367), batched over all frames
     using LRf = LdRows<float, float, CF::BI, CF::BK, NTF>;
     using LRfj = LdRows<float, float, CF::BJ, CF::BK, NTF>;

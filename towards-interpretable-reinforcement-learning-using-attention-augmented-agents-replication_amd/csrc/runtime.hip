@@ -154,6 +154,7 @@ int aaa_pack_weights(const aaa_cfg* cfg, const float* params, void* packed, hipS
   if ((r = check_device())) return r;
   if (!params || !packed) return fail(AAA_E_ARG, "NULL params/packed");
   if (!aligned16(params) || !aligned16(packed)) return fail(AAA_E_ALIGN, "params/packed must be 16-byte aligned");
+  TimerScope tim(AAA_TIMER_PACK, stream, 0.0, "pack_all + fragment-order copies + query pack");
   return L.dt == AAA_BF16 ? pack_impl<__bf16>(L, params, (char*)packed, stream)
                           : pack_impl<float>(L, params, (char*)packed, stream);
 }
@@ -202,15 +203,35 @@ int aaa_pair_status(hipStream_t stream, int clear) {
   return clear ? pair_take() : pair_peek();
 }
 
-int aaa_debug_pair_spin(long polls) {
-  if (polls < 0 || polls > (1L << 30)) return fail(AAA_E_ARG, "pair spin bound must be in [0, 2^30] (0 = default)");
-  g_pair_spin = polls ? polls : (1L << 24);
+int aaa_pair_flag(float* dst, hipStream_t stream) {
+  if (!dst) return fail(AAA_E_ARG, "pair_flag: NULL dst");
+  int r = check_device();
+  if (r) return r;
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  const int* rep = pair_report(dev);
+  if (!rep) return fail(AAA_E_LAUNCH, "cannot map the partner-timeout report word");
+  HIPCHK(pair_flag_launch(rep, dst, stream));
+  return AAA_OK;
+}
+
+int aaa_debug_pair_spin(long ticks) {
+  if (ticks < 0 || ticks > 0x7fffffffL) return fail(AAA_E_ARG, "pair wait budget must be in [0, 2^31) ticks (0 = default)");
+  g_pair_spin = ticks;
   return AAA_OK;
 }
 
 int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* const* params,
                   const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream) {
+  return aaa_adam_step_guarded(hp, step, nullptr, ntensors, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq, numel,
+                               stream);
+}
+
+int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* guard, int ntensors,
+                          float* const* params, const float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                          hipStream_t stream) {
   if (!hp || ntensors < 0 || (ntensors > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel)))
     return fail(AAA_E_ARG, "adam: NULL argument");
   if (step < 1) return fail(AAA_E_ARG, "adam: step must be >= 1 (got %ld)", step);
@@ -220,7 +241,8 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
     return fail(AAA_E_ARG, "adam: invalid hyper-parameters");
   int r = check_device();
   if (r) return r;
-  AdamHost h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, step, hp->amsgrad ? 1 : 0, hp->maximize ? 1 : 0};
+  AdamHost h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, step, hp->amsgrad ? 1 : 0, hp->maximize ? 1 : 0,
+             guard};
   for (int t0 = 0; t0 < ntensors; t0 += kAdamMaxTensors) {
     AdamTable tab;
     memset(&tab, 0, sizeof tab);
