@@ -216,29 +216,38 @@ def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
             policy(obs[t])
         return finish()
 
-    episode(4).backward()                        # warm-up (allocations, code objects)
-    torch.cuda.synchronize()
-    base = torch.cuda.memory_allocated(dev)
-    torch.cuda.reset_peak_memory_stats(dev)
-    t0 = time.perf_counter()
-    loss = episode(T_ep)
-    t1 = time.perf_counter()
-    held = torch.cuda.memory_allocated(dev) - base
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    loss.backward()
-    e1.record()
-    torch.cuda.synchronize()
-    t2 = time.perf_counter()
-    peak = torch.cuda.max_memory_allocated(dev) - base
+    def measure():
+        episode(4).backward()                    # warm-up (allocations, code objects)
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated(dev)
+        torch.cuda.reset_peak_memory_stats(dev)
+        t0 = time.perf_counter()
+        loss = episode(T_ep)
+        t1 = time.perf_counter()
+        held = torch.cuda.memory_allocated(dev) - base
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        loss.backward()
+        e1.record()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        peak = torch.cuda.max_memory_allocated(dev) - base
+        return {"ms_per_step_host": round((t1 - t0) / T_ep * 1e3, 3),
+                "backward_ms_device": round(e0.elapsed_time(e1), 3), "backward_ms_host": round((t2 - t1) * 1e3, 3),
+                "episode_frames_per_s": round(T_ep / (t2 - t0), 1),
+                "graph_bytes_per_step": int(held // T_ep), "peak_bytes_per_step": int(peak // T_ep)}
+
+    agent.fuse_episode_backward = True
     out = {"pattern": "main_mp.py: T_ep x Policy.forward(obs) (B=1, 210x160, default basis, .item() per step) "
                       "-> finish_episode loss -> one loss.backward()",
-           "steps": T_ep, "ms_per_step_host": round((t1 - t0) / T_ep * 1e3, 3),
-           "backward_ms_device": round(e0.elapsed_time(e1), 3), "backward_ms_host": round((t2 - t1) * 1e3, 3),
-           "episode_frames_per_s": round(T_ep / (t2 - t0), 1),
-           "graph_bytes_per_step": int(held // T_ep), "peak_bytes_per_step": int(peak // T_ep),
+           "steps": T_ep, **measure(),
+           "path": "fused episode backward (episode.py): per-step forwards record into one episode; the backward "
+                   "re-runs it as 64-step unrolls from checkpointed states, one hand-written BPTT call each",
            "note": "graph_bytes_per_step x main_mp.py:151's max_steps (10,000) is the device memory one "
                    "full-length episode's autograd graph would hold"}
+    agent.fuse_episode_backward = False
+    out["per_step_path"] = {**measure(), "path": "one T=1 autograd node (own workspace) per step, T_ep backward calls"}
+    agent.fuse_episode_backward = True
     if cpu:
         from oracle import ref_cpu
         cores, _ = _cpu_threads()

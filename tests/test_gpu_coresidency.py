@@ -56,6 +56,33 @@ def _filler():
     return lib
 
 
+class strand_next_launch:
+    """Test hook: make the next multi-workgroup launch strand deterministically.
+    A filler holds half the CUs for 5 ms on a side stream while the partner-wait
+    budget is 100 us (aaa_debug_pair_spin), so the workgroups placed first give
+    up on partners that cannot be placed yet.  Restores the default budget."""
+
+    def __init__(self, cuda, cus=128, usec=5000, budget_ticks=10000):
+        self.cuda, self.cus, self.usec, self.budget = cuda, cus, usec, budget_ticks
+
+    def __enter__(self):
+        lib = _filler()
+        self.side = torch.cuda.Stream(self.cuda)
+        self.sink = torch.zeros(4096, device=self.cuda)
+        torch.cuda.synchronize()
+        N.debug_pair_spin(self.budget)
+        assert lib.aaa_test_filler(self.cus, self.usec, self.sink.data_ptr(), self.side.cuda_stream) == 0
+        time.sleep(0.002)
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            torch.cuda.synchronize()
+        finally:
+            N.debug_pair_spin(0)
+        return False
+
+
 def _setup(cuda, B, T, H, nq, dtype):
     runner = R.UnrollRunner(B, T, H, H, nq, 18, dtype, cuda, frames_u8=True)
     params = detinit.deterministic_params(0, 18, nq)
@@ -139,17 +166,13 @@ def test_guarded_adam_skips_stranded_step(cuda):
     m, v = torch.zeros_like(p), torch.zeros_like(p)
     from aaa_amd.optim import adam_flat_
     N.pair_status(clear=True)
-    N.debug_pair_spin(1)           # test hook: a one-tick partner wait budget strands the pairs
-    try:
-        runner, flat, packed, basis, frames, ws, dl, dv = args
+    runner, flat, packed, basis, frames, ws, dl, dv = args
+    before = p.clone()
+    with strand_next_launch(cuda):
         runner.forward(flat, packed, basis, frames, ws, want_attn=False)
         N.pair_flag(guard)         # before any API call consumes the report
-        before = p.clone()
         adam_flat_(p, g, m, v, 1, guard=guard)
-        torch.cuda.synchronize()
-    finally:
-        N.debug_pair_spin(0)
-    assert float(guard.item()) > 0, "a one-tick partner wait never expired"
+    assert float(guard.item()) > 0, "no partner wait expired beside the filler"
     assert torch.equal(p, before) and float(m.abs().max()) == 0.0, "the guarded Adam updated a stranded step"
     assert N.pair_status(clear=True) > 0
     guard.zero_()
@@ -159,7 +182,8 @@ def test_guarded_adam_skips_stranded_step(cuda):
 
 
 def test_learner_stranded_step_leaves_params(cuda):
-    """Learner.train_step with stranded partners: either the backward's entry
+    """Learner.train_step with stranded partners (a filler holds half the CUs
+    and the wait budget is 100 us): either the backward's entry
     check raises AAA_E_STRANDED (the forward's report was already visible) or
     the guard slot skips the update -- the parameters never change; a clean
     step afterwards updates them and check_health() is quiet."""
@@ -171,15 +195,11 @@ def test_learner_stranded_step_leaves_params(cuda):
     dv = torch.from_numpy(detinit.cotangent(3, (T, B, 18))).to(cuda)
     before = lr.flat.clone()
     N.pair_status(clear=True)
-    N.debug_pair_spin(1)
-    try:
+    with strand_next_launch(cuda):
         try:
             lr.train_step(frames, dl, dv)
         except RuntimeError as e:
             assert "status -5" in str(e), e
-        torch.cuda.synchronize()
-    finally:
-        N.debug_pair_spin(0)
     assert torch.equal(lr.flat, before), "a stranded step reached the parameters"
     N.pair_status(clear=True)
     lr.train_step(frames, dl, dv)

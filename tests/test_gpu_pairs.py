@@ -57,21 +57,19 @@ def test_paired_kernels_run_and_report_clean(cuda):
 
 
 def test_stranded_pair_is_reported(cuda):
-    """With the partner wait bounded to one poll, some wait times out: the
-    report word counts it, and the next API call fails with AAA_E_STRANDED
-    (once) instead of silently continuing."""
+    """With half the CUs held by a filler kernel and a 100-us partner-wait
+    budget, some wait expires: the report word counts it, and the next API
+    call fails with AAA_E_STRANDED (once) instead of silently continuing."""
+    from test_gpu_coresidency import strand_next_launch
     args = _setup(cuda)
     N.pair_status(clear=True)
-    N.debug_pair_spin(1)
-    try:
-        _run(cuda, *args)
-        n = N.pair_status(clear=False)
-    finally:
-        N.debug_pair_spin(0)
-    assert n > 0, "a one-poll partner wait never timed out"
-    runner, flat, packed, basis, frames, ws, dl = args
+    with strand_next_launch(cuda):
+        runner, flat, packed, basis, frames, ws, dl = args
+        runner.forward(flat, packed, basis, frames, ws, want_attn=False)
+    n = N.pair_status(clear=False)
+    assert n > 0, "no partner wait expired beside the filler"
     with pytest.raises(RuntimeError, match=r"status -5"):
         runner.forward(flat, packed, basis, frames, ws, want_attn=False)
     assert N.pair_status(clear=True) == 0   # consumed by the failing call
-    _run(cuda, *args)                       # default bound: clean again
+    _run(cuda, *args)                       # default budget: clean again
     assert N.pair_status(clear=True) == 0

@@ -152,3 +152,10 @@ def test_debug_pair_spin_bounds():
     assert lib.aaa_debug_pair_spin(-1) == -1
     assert lib.aaa_debug_pair_spin(1 << 31) == -1
     assert lib.aaa_debug_pair_spin(0) == 0
+
+
+def test_package_modules_import():
+    """Every host module of the package imports on a CPU-only box (no GPU call)."""
+    import importlib
+    for m in ("learner", "policy", "optim", "parallel", "reinforce", "runtime", "attention"):
+        importlib.import_module(f"aaa_amd.{m}")

@@ -373,18 +373,28 @@ class Agent(nn.Module):
         self._runners = {}
         self._basis = None
         self.last_attention = None
+        self._episode = None
+
+    # Per-step forward calls with autograd on record into one episode whose
+    # backward runs as multi-step BPTT calls (episode.py); False: one T=1
+    # autograd node with its own saved workspace per call.
+    fuse_episode_backward = True
 
     # -- reference API --------------------------------------------------------
     def reset(self):
         self.vision.reset()
         self.prev_output = None
         self.prev_hidden = None
+        self._episode = None
 
     def forward(self, X, prev_reward=None, prev_action=None, ts=0):
         """One step (attention.py:298-368): X (B, H, W, 3) -> logits, values (B, A)."""
         pr = None if prev_reward is None else prev_reward.reshape(1, -1)
         pa = None if prev_action is None else prev_action.reshape(1, -1)
-        logits, values, attn = self._step(X.unsqueeze(0), pr, pa)
+        if self._episode_eligible(X):
+            logits, values, attn = self._episode_step(X, pr, pa)
+        else:
+            logits, values, attn = self._step(X.unsqueeze(0), pr, pa)
         self.last_attention = attn[0]
         return logits[0], values[0]
 
@@ -400,6 +410,52 @@ class Agent(nn.Module):
         return logits, values, attn
 
     # -- internals ----------------------------------------------------------
+    def _episode_eligible(self, X):
+        return (self.fuse_episode_backward and torch.is_grad_enabled() and X.is_cuda and X.dim() == 4
+                and not (self.stateful_core or self.prev_hidden is not None)
+                and any(p.requires_grad for p in self.parameters()))
+
+    def _episode_step(self, X, pr, pa):
+        """One per-step call recorded into the open episode (episode.py): a new
+        episode after reset(), a parameter change, another geometry, or a
+        prev_hidden the episode did not set itself."""
+        from .episode import Episode, _EpisodeAnchorFn, _EpisodeStepFn
+        B, H, W, C = X.shape
+        if C != 3:
+            raise ValueError(f"frames must be (..., H, W, 3), got {tuple(X.shape)}")
+        params = list(self.parameters())
+        for p in params:
+            if p.device != X.device:
+                raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
+                                   f"call agent.to({X.device})")
+        u8 = X.dtype == torch.uint8
+        runner = self._runner(B, 1, H, W, X.device, False, u8)
+        S = self._basis_for(runner.h, runner.w, H, W, X.device)
+        flat, packed = self._packed_params(runner, params)
+        key = runner._pack_cache[0]
+        cell = self.vision.vision_lstm
+        ep = self._episode
+        if ep is None or ep.runner is not runner or ep.key != key or cell.prev_hidden is not ep.state_ref:
+            if cell.prev_hidden is None:
+                h0 = c0 = None
+                cell._peepholes(runner.w, runner.h, X.device)      # init_hidden's lazy zero peepholes (Q2)
+            else:
+                h0, c0 = (s.permute(0, 3, 2, 1) for s in cell.prev_hidden)
+                if tuple(h0.shape) != runner.state_shape() or tuple(c0.shape) != runner.state_shape():
+                    raise RuntimeError(f"carried ConvLSTM state {tuple(cell.prev_hidden[0].shape)} does not match "
+                                       f"this batch {(B, 128, runner.w, runner.h)}; call agent.reset()")
+            cell._check_peepholes(runner.w, runner.h)
+            ep = Episode(self, runner, flat, packed, key, S, h0, c0)
+            ep.anchor = _EpisodeAnchorFn.apply(ep, h0, c0, *params)
+            self._episode = ep
+        t = ep.record((X if u8 else X.float()).unsqueeze(0).contiguous(), pr, pa)
+        logits, values, attn, hT, cT = _EpisodeStepFn.apply(ep, t, ep.anchor)
+        cell.prev_hidden = (hT.permute(0, 3, 2, 1), cT.permute(0, 3, 2, 1))
+        ep.state_ref = cell.prev_hidden
+        if self.prev_output is None:   # Q1: the query input is created once and never updated
+            self.prev_output = torch.zeros(B, self.hidden_size, device=X.device)
+        return logits, values, attn
+
     def _step(self, X, pr, pa):
         if not X.is_cuda:
             raise RuntimeError("aaa: Agent runs only on the MI355X HIP path; move the agent and its "

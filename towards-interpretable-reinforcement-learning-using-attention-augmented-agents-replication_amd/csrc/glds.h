@@ -301,6 +301,13 @@ struct GIm2colT {
   // offset / origin steps of one x wrap and one y wrap
   int dix, diy, doff, xlim, xw, xwoff, ylim, yw, ywoff;
   int wofs;
+  // The pieces' pixel state advances by BK per issue instead of being derived
+  // from k0, so callers must call start(kb) once and then issue every K tile
+  // exactly once, in order (every pipe kernel of this file does).  Builds with
+  // -DAAA_DEBUG_LOADERS check that contract: a k0 out of sequence traps.
+#ifdef AAA_DEBUG_LOADERS
+  int knext = 0;
+#endif
   __device__ static bool ok_shape(const ConvGeo& g) { return g.Cin % VG == 0 && !g.transposed; }
   __device__ __forceinline__ GIm2colT(const Params& p, int row0) : g(p.g) {
     rs = make_rsrc(p.src, p.src_bytes);
@@ -332,6 +339,9 @@ struct GIm2colT {
   }
   __device__ __forceinline__ void start(int k0) {
     const int hw = g.Hout * g.Wout;
+#ifdef AAA_DEBUG_LOADERS
+    knext = k0;
+#endif
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const int m = k0 + kr[c];
@@ -343,7 +353,13 @@ struct GIm2colT {
     }
   }
   __device__ __forceinline__ void issue(T* lds, int k0) { issue_part(lds, k0, 0, 1); }
-  __device__ __forceinline__ void issue_part(T* lds, int, int part, int nparts) {
+  __device__ __forceinline__ void issue_part(T* lds, int k0, int part, int nparts) {
+#ifdef AAA_DEBUG_LOADERS
+    if (k0 != knext) __builtin_trap();   // out-of-order issue: the incremental gather would read wrong pixels
+    if (part == nparts - 1) knext += BK;
+#else
+    (void)k0;
+#endif
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       if (c % nparts != part) continue;

@@ -22,6 +22,20 @@ and the fused Adam skips the update on the device when it is non-zero
 (aaa_adam_step_guarded) -- gradients of a stranded launch never reach the
 parameters, with no host sync.  ``check_health()`` raises on it.
 """
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+from . import detinit
+from .attention import SpatialBasis
+from .optim import adam_flat_
+from .parallel import allreduce_buckets, bucket_bounds
+from .runtime import UnrollRunner
+
+
 class Learner:
     def __init__(self, B: int, T: int, H: int = 84, W: int = 84, nq: int = 4, A: int = 18,
                  dtype: str = "fp32", device=None, seed: int = 0, group=None, lr: float = 1e-3,

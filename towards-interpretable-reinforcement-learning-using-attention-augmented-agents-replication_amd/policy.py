@@ -139,6 +139,15 @@ class Policy(nn.Module):
         return int(action.item())
 
 
+def _actor_chain_fits(B, H, W, nq, A) -> bool:
+    """Whether aaa_actor_step accepts this geometry: its layout query returns 0
+    bytes (AAA_E_ARG) for what it refuses, e.g. a grid whose readout exceeds
+    the kernel's LDS; no device call."""
+    import ctypes
+    cfg = N.Cfg(B, 1, H, W, nq, A, N.F32, N.FLAG_FRAMES_U8)
+    return N.load().aaa_actor_workspace_bytes(ctypes.byref(cfg)) > 0
+
+
 class GraphActor:
     """One B-row environment step of the agent + action draw, captured once as
     a HIP graph and replayed per step (inference: test_model.py rollouts, or
@@ -170,13 +179,10 @@ class GraphActor:
         if chain and not eligible:
             raise ValueError("the actor chain needs an fp32 agent with the zero-state policy core and B <= 16")
         self.chain = eligible if chain is None else bool(chain)
-        if self.chain:
-            try:
-                r = ActorRunner(B, H, W, agent.num_queries, agent.num_actions, dev, frames_u8=True)
-            except RuntimeError:
-                if chain:   # asked for explicitly: the library's reason (e.g. the readout LDS of a large grid)
-                    raise
-                self.chain = False   # not applicable to this geometry: the learner's T=1 forward
+        if self.chain and chain is None and not _actor_chain_fits(B, H, W, agent.num_queries, agent.num_actions):
+            self.chain = False   # the geometry the chain refuses (its readout LDS): the learner's T=1 forward
+        if self.chain:   # any failure here (asked for, or a real HIP error) propagates
+            r = ActorRunner(B, H, W, agent.num_queries, agent.num_actions, dev, frames_u8=True)
         if self.chain:
             self.runner = r
             self._ws = r.new_workspace()
