@@ -24,6 +24,8 @@ Parity pinning: tests/test_oracle_golden.py checks this restatement against
 fixtures produced by importing the reference itself (tests/golden/gen_golden.py).
 
 ``conv_mode='bf16'`` is the bf16-emulated oracle (SURVEY.md §8c G7 analogue):
+the attention readout reads h_t rounded to bf16 (``h_store``, as the HIP
+bf16 path does since round 4), and
 every convolution rounds its GEMM operands to bf16 where the HIP kernels do
 (forward: activation and weight; dgrad: output-gradient and weight; wgrad:
 activation and output-gradient) and accumulates in fp32, and the ConvLSTM
@@ -164,17 +166,38 @@ def convlstm_cell(P, x, state, mode="fp32", peep=None, gate_store="fp32"):
     return h_new, c_new, peep
 
 
+class _RoundBf16(torch.autograd.Function):
+    """h_t as the HIP bf16 path hands it to the attention readout: rounded to
+    bf16 (it reads the bf16 copy the recurrence keeps for the next step's
+    h-conv and the weight gradient, csrc/recur.h), gradient straight through
+    (the readout's dO is added to dh of the fp32 h_t, csrc/recur_bwd.h)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        return _bf(h)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 def _vision_step(P, X_t, state, mode, peep, gate_store="fp32"):
     """Encoder + one ConvLSTM step in the reference's transposed orientation."""
     return convlstm_cell(P, vision_cnn(P, X_t, mode), state, mode, peep, gate_store)
 
 
-def _query(P, B, nq, hidden=256, prev_output=None):
+def _relu(x, probe):
+    return F.relu(x) if probe is None else _ProbedReLU.apply(x, probe, len(probe.pre))
+
+
+def _query(P, B, nq, hidden=256, prev_output=None, probe=None):
     """QueryNetwork on prev_output (attention.py:184-198,325-331): the zero
     tensor in the reference's reachable path (Q1), h_{t-1} in the stateful core."""
     z = prev_output if prev_output is not None else torch.zeros(B, hidden, dtype=P["query.model.0.weight"].dtype)
-    q = F.relu(F.linear(z, P["query.model.0.weight"], P["query.model.0.bias"]))
-    q = F.relu(F.linear(q, P["query.model.2.weight"], P["query.model.2.bias"]))
+    if prev_output is None:
+        probe = None          # a constant query: no kink moves
+    q = _relu(F.linear(z, P["query.model.0.weight"], P["query.model.0.bias"]), probe)
+    q = _relu(F.linear(q, P["query.model.2.weight"], P["query.model.2.bias"]), probe)
     q = F.linear(q, P["query.model.4.weight"], P["query.model.4.bias"])
     return q.reshape(-1, nq, 72)
 
@@ -205,7 +228,54 @@ def attention_readout(O, S, Q, prev_reward=None, prev_action=None):
     return A, answer
 
 
-def _head(P, O, S, nq, prev_reward, prev_action, core=None):
+class KinkProbe:
+    """The answer MLP's ReLU (attention.py:277-282) -- and, in the stateful
+    core, the query MLP's two (attention.py:184-198) -- as a probe of the
+    gradient's kinks.  The reference's gradient is discontinuous where a
+    pre-activation of answer_processor.0 crosses zero: a unit within a few
+    1e-6 of zero switches its whole frame's cotangent path on or off under
+    perturbations far below bf16's rounding (one such unit moves a T=20, B=3
+    ConvLSTM weight gradient by ~2% norm-relative -- measured on this oracle
+    by perturbing h_t by 1e-6 before its bf16 rounding).  ``unroll(...,
+    kinks=probe)`` records every probed pre-activation (in call order) and
+    lets the backward flip one unit's mask (``flip = (call, flat index)``):
+    ``near(eps)`` lists the units within eps of zero, so a test can bound the
+    gradient over every on/off choice of those units (tests/helpers.py
+    kink_envelope)."""
+
+    def __init__(self):
+        self.pre = []
+        self.flip = None
+
+    def near(self, eps, limit=8):
+        """(t, flat index, |pre|) of the units with |pre| < eps, nearest first."""
+        out = []
+        for t, x in enumerate(self.pre):
+            a = x.reshape(-1).abs()
+            for i in torch.nonzero(a < eps).reshape(-1).tolist():
+                out.append((t, i, float(a[i])))
+        return sorted(out, key=lambda u: u[2])[:limit]
+
+
+class _ProbedReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, probe, t):
+        ctx.save_for_backward(x)
+        ctx.probe, ctx.t = probe, t
+        probe.pre.append(x.detach().clone())
+        return x.clamp_min(0)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        m = (x > 0).to(g.dtype)
+        f = ctx.probe.flip
+        if f is not None and f[0] == ctx.t:
+            m.view(-1)[f[1]] = 1.0 - m.view(-1)[f[1]]
+        return g * m, None, None
+
+
+def _head(P, O, S, nq, prev_reward, prev_action, core=None, probe=None):
     """Attention readout + answer MLP + LSTMCell + heads (one frame batch).
 
     core=None: the reference's reachable path, zero-state LSTMCell and a query
@@ -214,9 +284,9 @@ def _head(P, O, S, nq, prev_reward, prev_action, core=None):
     holds a tensor: Q = query(h), LSTMCell from (h, c); returns the new (h, c).
     """
     B = O.shape[0]
-    Q = _query(P, B, nq, prev_output=None if core is None else core[0])
+    Q = _query(P, B, nq, prev_output=None if core is None else core[0], probe=probe)
     A, answer = attention_readout(O, S, Q, prev_reward, prev_action)
-    x = F.relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]))
+    x = _relu(F.linear(answer, P["answer_processor.0.weight"], P["answer_processor.0.bias"]), probe)
     x = F.linear(x, P["answer_processor.2.weight"], P["answer_processor.2.bias"])
     if core is None:
         zeros = torch.zeros(B, P["policy_core.weight_hh"].shape[1], dtype=O.dtype)
@@ -235,7 +305,8 @@ def _head(P, O, S, nq, prev_reward, prev_action, core=None):
 
 def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=None,
            state=None, S=None, conv_mode: str = "fp32", return_state: bool = False,
-           stateful_core: bool = False, core_state=None, gate_store=None):
+           stateful_core: bool = False, core_state=None, gate_store=None, h_store=None,
+           kinks: "KinkProbe | None" = None):
     """T-step unroll from ``reset()``: X is (T, B, H, W, 3) fp32 raw pixels.
 
     Returns logits (T,B,A), values (T,B,A), attention maps (T,B,h,w,nq)
@@ -248,6 +319,8 @@ def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=
     T, B = X.shape[0], X.shape[1]
     if gate_store is None:   # the HIP path's default: fp16 gate activations on the bf16 path
         gate_store = "fp16" if conv_mode == "bf16" else "fp32"
+    if h_store is None:      # the HIP bf16 path's readout reads its bf16 copy of h_t (_RoundBf16)
+        h_store = "bf16" if conv_mode == "bf16" else "fp32"
     if S is None:
         S = spatial_basis(*grid_of(X.shape[2], X.shape[3]))
     peep = None
@@ -259,13 +332,13 @@ def unroll(P: dict, X: torch.Tensor, nq: int = 4, prev_reward=None, prev_action=
     for t in range(T):
         hN, cN, peep = _vision_step(P, X[t], state, conv_mode, peep, gate_store)
         state = (hN, cN)
-        O = hN.transpose(1, 3)                                          # attention.py:181
+        O = (_RoundBf16.apply(hN) if h_store == "bf16" else hN).transpose(1, 3)   # attention.py:181
         r = None if prev_reward is None else prev_reward[t]
         a = None if prev_action is None else prev_action[t]
         if stateful_core:
-            lg, vl, A, core = _head(P, O, S, nq, r, a, core)
+            lg, vl, A, core = _head(P, O, S, nq, r, a, core, probe=kinks)
         else:
-            lg, vl, A = _head(P, O, S, nq, r, a)
+            lg, vl, A = _head(P, O, S, nq, r, a, probe=kinks)
         L.append(lg), Vv.append(vl), Am.append(A)
     out = (torch.stack(L), torch.stack(Vv), torch.stack(Am))
     if return_state:

@@ -131,7 +131,7 @@ def test_g7_bf16_emulation(golden):
     """G7 = the reference with its convs' operands rounded to bf16 (fp32 gates)."""
     g = golden("G7")
     P = _params()
-    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16", gate_store="fp32")
+    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16", gate_store="fp32", h_store="fp32")
     assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
     _loss_backward(P, lg, vl)
     _check_grads(P, g, 1e-4)
@@ -144,8 +144,22 @@ def test_fp16_gate_storage_emulation_is_a_small_backward_perturbation(golden):
     gradients within 1e-2 of it (measured ~1.4e-3; the HIP criterion is 2e-2)."""
     g = golden("G7")
     P = _params()
-    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16")
+    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16", h_store="fp32")
     assert_close(lg.detach().numpy(), g["logits"], RTOL, "logits")
+    _loss_backward(P, lg, vl)
+    _check_grads(P, g, 1e-2)
+
+
+def test_bf16_h_readout_emulation_is_a_small_perturbation(golden):
+    """The bf16 oracle's default also rounds h_t to bf16 where the attention
+    readout reads it (the HIP bf16 path reads its bf16 copy of h_t): outputs and
+    gradients stay within 1e-2 of G7 (the HIP criterion against the emulated
+    oracle is 2e-2; against the fp32 reference, test_gpu_parity's _vs_fp32_reference)."""
+    g = golden("G7")
+    P = _params()
+    lg, vl, A = ref_cpu.unroll(P, _frames(4, 2), conv_mode="bf16", h_store="bf16")
+    assert_close(lg.detach().numpy(), g["logits"], 1e-2, "logits")
+    assert_close(A.detach().numpy(), g["attn"], 1e-2, "attn")
     _loss_backward(P, lg, vl)
     _check_grads(P, g, 1e-2)
 

@@ -13,7 +13,6 @@
 #include <vector>
 #include "recur.h"
 #include "recur_bwd.h"
-#include "recur_bwd_split.h"
 
 using namespace aaa;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -110,13 +109,12 @@ static void bench(int B, int T, int h, int w, bool band) {
   RUN(1, "no A loads");
   RUN(4, "no MFMA");
   RUN(8, "no chunk-3 DMA");
+  RUN(128, "coalesced epilogue loads (same bytes)");
+  RUN(160, "coalesced epilogue loads, no dZ stores");
   if (band) RUN(16, "no halo exchange");
   timeit(band ? reinterpret_cast<const void*>(&k_convlstm_bwd_frames<0, true, true>)
               : reinterpret_cast<const void*>(&k_convlstm_bwd_frames<0, false, false>),
          grid, 256, p, band, reps, band ? "dO in the accumulators (band)" : "dO in the ring (frame)");
-  timeit(band ? reinterpret_cast<const void*>(&k_convlstm_bwd_split<true>)
-              : reinterpret_cast<const void*>(&k_convlstm_bwd_split<false>),
-         grid, 512, p, band, reps, "split roles (8 waves)");
   printf("timeout reports: %d\n", *hrep);
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -15,11 +16,26 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N).
+template <int I0, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I0 < N) {
+    f(std::integral_constant<int, I0>{});
+    static_for<I0 + 1, N>(f);
+  }
+}
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Accurate versions for the recurrent gate math (parity 1e-4 over 20 steps).
 __device__ __forceinline__ float sigm_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// bf16 -> fp32 (exact) of the low / high half of a dword holding two bf16
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ f32x4 bf4_f32(const u32x2& u) { return f32x4{bf_lo(u.x), bf_hi(u.x), bf_lo(u.y), bf_hi(u.y)}; }
 
 template <typename T> struct is_f32 { static constexpr bool value = false; };
 template <> struct is_f32<float> { static constexpr bool value = true; };

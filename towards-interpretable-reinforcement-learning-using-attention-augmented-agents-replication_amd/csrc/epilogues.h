@@ -283,7 +283,7 @@ template <typename T, typename GT = float>
 struct EpiConvLstmFwd {
   const float* cprev;  // [M][128]  c_{t-1}
   float* cnext;        // [M][128]  c_t
-  float* hout;         // [M][128]  h_t (fp32, attention input)
+  float* hout;         // [M][128]  h_t (fp32, the fp32 path's attention input), or null (bf16: readout_h reads XH)
   T* xhnext;           // [M][192]  slot t+1, channels 64..191 <- h_t (next step operand)
   GT* gates;           // [M][512]  in: Wx*x_t + b (fp32 only);  out: post-activation (i,f,c~,o)
   int Nj;              // M = B*P
@@ -311,7 +311,7 @@ struct EpiConvLstmFwd {
     float gi, gf, gc, go, c, h;
     GateFwd::run(p.zx[0] + v0, p.zx[1] + v1, p.zx[2] + v2, p.zx[3] + v3, p.cp, gi, gf, gc, go, c, h);
     cnext[(size_t)j * 128 + ch] = c;
-    hout[(size_t)j * 128 + ch] = h;
+    if (hout) hout[(size_t)j * 128 + ch] = h;
     xhnext[(size_t)j * 192 + 64 + ch] = (T)h;
     store_gates(gates + (size_t)j * 512 + i, f32x4{gi, gf, gc, go});
   }

@@ -47,12 +47,28 @@ hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hi
 // qs: per-frame query stride in floats (0 = one query for all frames, Q1);
 // SQ == NULL computes the basis half of the logits per frame.  addq adds the
 // answer row's Q-column gradient (dAns[f][184*nq ...]) into dQp.
-hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
+//
+// OSrc: h_t (the readout's O, frame rows of P pixels) as the readout reads it:
+// fp32 rows of 128 (Hs, the fp32 path) or the bf16 h half of the ConvLSTM's
+// [x | h] operand rows (XH, row pitch 192: the bf16 path keeps no fp32 copy).
+struct OSrc {
+  const void* p;
+  int bf16, ld;   // element type, row pitch in elements
+  OSrc frame(size_t f, int P) const {   // frame f's rows
+    return {(const char*)p + f * P * ld * (bf16 ? 2 : 4), bf16, ld};
+  }
+};
+inline OSrc o_f32(const float* Hs) { return {Hs, 0, 128}; }
+inline OSrc o_bf16(const __bf16* h, int ld) { return {h, 1, ld}; }
+hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, const float* pr,
                     const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
                     int qs = 0);
-hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
+// cqm: write dO in the channel-quad-major per-frame layout of the frame-resident BPTT (recur.h cqm4)
+hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, const float* dAns,
                     int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs = 0,
-                    int addq = 0);
+                    int addq = 0, int cqm = 0);
+// (nf, P, 128) fp32 slices: row-major -> channel-quad-major (to_cqm) or back
+hipError_t cqm_convert(const float* src, float* dst, int nf, int P, int to_cqm, hipStream_t st);
 hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int ans_in, int nq, const float* W2,
                      const float* W4, const float* q1, const float* q2, float* gW4, float* gb4, float* gW2,
                      float* gb2, float* gb0, hipStream_t st);
@@ -74,6 +90,7 @@ hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const
                          const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
+template <typename T> hipError_t xh_to_state(int M, const T* xh, float* h, hipStream_t st);
 template <typename T> hipError_t cell_xh(int M, const float* x, const float* h, T* xh, hipStream_t st);
 template <typename TI, typename TO> hipError_t cast(long n, const TI* src, TO* dst, hipStream_t st);
 template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, int K, T* dst, hipStream_t st);

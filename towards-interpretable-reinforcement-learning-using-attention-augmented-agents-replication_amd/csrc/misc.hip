@@ -79,23 +79,32 @@ k_query_sq(const float* __restrict__ S, const float* __restrict__ Q, int P, int 
 // key channels by the logit threads (one position each) and the first
 // kAttnPre positions of each readout thread's V slice straight into
 // registers -- so the frame's O rows stream in as one burst (no load phase
-// behind the softmax).  Readout thread (g, sl): 4-column group g of the 184
-// V columns (46 groups, 16 B per lane, consecutive lanes along a row),
-// position slice sl of 11; slices summed through LDS.
+// behind the softmax).
+//   fp32 O (TO = float, rows of 128): readout thread (g, sl) takes 4-column
+// group g of the 184 V columns (46 groups, 16 B per lane, consecutive lanes
+// along a row), position slice sl of SL; slices summed through LDS.
+//   bf16 O (TO = __bf16, the h half of the XH rows, pitch ``old``): waves 0-3
+// read O (30 groups of 4 channels, 8 B per lane), waves 4-7 read S (32 groups
+// of 2 channels, 8 B per lane), kAttnSlicesBf slices each -- one load width
+// for every lane (the prefetch is one straight-line burst) and the compute
+// branch is wave-uniform.
 constexpr int kAttnFwdThreads = 512;
 constexpr int kAttnSlices = 11;         // default position slices of the readout (46 * 11 = 506 threads)
-template <int NQ, int PRE, int SL = kAttnSlices>
+constexpr int kAttnSlicesBf = 8;        // bf16 O: 256 threads over 30 O groups / 32 S groups
+template <int NQ, int PRE, int SL, typename TO>
 __global__ void __launch_bounds__(kAttnFwdThreads) __attribute__((amdgpu_waves_per_eu(PRE > 0 || NQ > 4 ? 4 : 8)))
-k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
+k_attn_fwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa,
            int P, float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
+  constexpr bool BF = !std::is_same<TO, float>::value;
   constexpr int kAttnPre = PRE;   // V positions per readout thread loaded before the first wait
+  constexpr int NSL = BF ? kAttnSlicesBf : SL;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* L = sm;                         // P*NQ
   float* Qs = L + P * NQ;                // NQ*72
-  float* red = Qs + NQ * 72;             // SL * NQ * 184
+  float* red = Qs + NQ * 72;             // NSL * NQ * 184
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* O = Hs + (size_t)f * P * 128;
+  const TO* O = Hs + (size_t)f * P * old;
   const float* Qf = Q + (size_t)f * qs;   // qs = 0: one query for every frame (Q1)
   // the queries first (their LDS copy below then waits only for them), then
   // the first logit position's keys, then this thread's V slice head
@@ -105,29 +114,64 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   // position tid's keys and (constant query) basis logits: unconditional
   // loads from a clamped valid position, used only when tid < P
   const int p0 = min(tid, P - 1);
-  f32x4 k0 = *reinterpret_cast<const f32x4*>(O + p0 * 128);
-  f32x4 k1 = *reinterpret_cast<const f32x4*>(O + p0 * 128 + 4);
+  // key channels 0..7 of position p, raw (converted at their use, not here)
+  auto key_raw = [&](int p) {
+    if constexpr (BF) {
+      return *reinterpret_cast<const u32x4*>(O + (size_t)p * old);
+    } else {
+      struct { f32x4 a, b; } k{*reinterpret_cast<const f32x4*>(O + (size_t)p * old),
+                               *reinterpret_cast<const f32x4*>(O + (size_t)p * old + 4)};
+      return k;
+    }
+  };
+  const auto k0 = key_raw(p0);
   f32x4 sq[NQ / 4];
 #pragma unroll
   for (int j = 0; j < NQ / 4; ++j)
     sq[j] = SQ ? *reinterpret_cast<const f32x4*>(SQ + p0 * NQ + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool rd = tid < 46 * SL;
-  const int g = tid % 46, sl = tid / 46;
-  const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
-  const int ld = g < 30 ? 128 : 64;
-  f32x4 pre[kAttnPre > 0 ? kAttnPre : 1];
+  // readout slice of this thread: g = column group, sl = position slice
+  bool isO, rd;
+  int g, sl;
+  const char* src;   // column group g of position 0
+  size_t ldb;        // bytes per position
+  if constexpr (BF) {
+    isO = tid < 256;
+    const int t2 = isO ? tid : tid - 256;
+    g = isO ? t2 % 30 : t2 & 31;
+    sl = isO ? t2 / 30 : t2 >> 5;
+    rd = sl < NSL;
+    src = isO ? (const char*)(O + 8 + 4 * g) : (const char*)(S + 2 * g);
+    ldb = isO ? (size_t)old * 2 : 256;
+  } else {
+    isO = true;
+    rd = tid < 46 * SL;
+    g = tid % 46;
+    sl = tid / 46;
+    src = g < 30 ? (const char*)(O + 8 + 4 * g) : (const char*)(S + 4 * (g - 30));
+    ldb = g < 30 ? (size_t)old * 4 : 256;
+  }
+  using VR = typename std::conditional<BF, u32x2, f32x4>::type;   // one position's load of this lane
+  VR pre[kAttnPre > 0 ? kAttnPre : 1];
 #pragma unroll
   for (int i = 0; i < kAttnPre; ++i) {
     // unconditional load from a valid address (a select on the loaded value
     // would wait for it here); positions past P are skipped at their use
-    const int p = min(sl + i * SL, P - 1);
-    pre[i] = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
+    const int p = min(sl + i * NSL, P - 1);
+    pre[i] = *reinterpret_cast<const VR*>(src + (size_t)p * ldb);
   }
   if (tid < NQ * 72) Qs[tid] = qv0;
   if (tid + kAttnFwdThreads < NQ * 72) Qs[tid + kAttnFwdThreads] = qv1;
   __syncthreads();
   // logits: one thread per position, all NQ queries (its 8 key channels read once)
-  auto logits = [&](int p, const f32x4& ka, const f32x4& kb, const f32x4* sqp) {
+  auto logits = [&](int p, const auto& kr, const f32x4* sqp) {
+    f32x4 ka, kb;
+    if constexpr (BF) {
+      ka = bf4_f32(u32x2{kr.x, kr.y});
+      kb = bf4_f32(u32x2{kr.z, kr.w});
+    } else {
+      ka = kr.a;
+      kb = kr.b;
+    }
     float acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -153,15 +197,14 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
 #pragma unroll
     for (int q = 0; q < NQ; ++q) L[p * NQ + q] = acc[q];
   };
-  if (tid < P) logits(tid, k0, k1, sq);
+  if (tid < P) logits(tid, k0, sq);
   for (int p = tid + kAttnFwdThreads; p < P; p += kAttnFwdThreads) {   // grids past 512 positions
-    const f32x4 ka = *reinterpret_cast<const f32x4*>(O + p * 128);
-    const f32x4 kb = *reinterpret_cast<const f32x4*>(O + p * 128 + 4);
+    const auto kp = key_raw(p);
     f32x4 sp[NQ / 4];
 #pragma unroll
     for (int j = 0; j < NQ / 4; ++j)
       sp[j] = SQ ? *reinterpret_cast<const f32x4*>(SQ + p * NQ + 4 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
-    logits(p, ka, kb, sp);
+    logits(p, kp, sp);
   }
   __syncthreads();
   for (int q = wave; q < NQ; q += kAttnFwdThreads / 64) {
@@ -180,41 +223,54 @@ k_attn_fwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   }
   __syncthreads();
   // readout: the prefetched head of the slice, then the rest (large grids)
-  if (rd) {
-    float acc[NQ][4];
+  // CW channels of this lane: 4 (fp32; bf16 O) or 2 (bf16 path's S lanes)
+  auto readout = [&](auto cw) {
+    constexpr int CW = decltype(cw)::value;
+    auto cvt = [&](const VR& r) {
+      if constexpr (!BF) return r;
+      else if constexpr (CW == 4) return bf4_f32(r);
+      else return f32x4{__uint_as_float(r.x), __uint_as_float(r.y), 0.f, 0.f};
+    };
+    float acc[NQ][CW];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[q][0] = acc[q][1] = acc[q][2] = acc[q][3] = 0.f;
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
-    for (int i = 0; i < kAttnPre; ++i) {
-      const int p = sl + i * SL;
-      if (p < P) {
-        const f32x4 v = pre[i];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const float a = L[p * NQ + q];
-          acc[q][0] += a * v[0]; acc[q][1] += a * v[1]; acc[q][2] += a * v[2]; acc[q][3] += a * v[3];
-        }
-      }
-    }
-#pragma unroll 4
-    for (int p = sl + kAttnPre * SL; p < P; p += SL) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(src + (size_t)p * ld);
+      for (int k = 0; k < CW; ++k) acc[q][k] = 0.f;
+    auto fma_pos = [&](int p, const f32x4& v) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const float a = L[p * NQ + q];
-        acc[q][0] += a * v[0]; acc[q][1] += a * v[1]; acc[q][2] += a * v[2]; acc[q][3] += a * v[3];
-      }
-    }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      *reinterpret_cast<f32x4*>(red + (sl * NQ + q) * 184 + 4 * g) = f32x4{acc[q][0], acc[q][1], acc[q][2], acc[q][3]};
+        for (int k = 0; k < CW; ++k) acc[q][k] += a * v[k];
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < kAttnPre; ++i) {
+      const int p = sl + i * NSL;
+      if (p < P) fma_pos(p, cvt(pre[i]));
+    }
+#pragma unroll 4
+    for (int p = sl + kAttnPre * NSL; p < P; p += NSL)
+      fma_pos(p, cvt(*reinterpret_cast<const VR*>(src + (size_t)p * ldb)));
+    // column of this lane's first channel in the 184 V columns
+    const int col = BF ? (isO ? 4 * g : 120 + 2 * g) : 4 * g;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float* r = red + (sl * NQ + q) * 184 + col;
+      if constexpr (CW == 4) *reinterpret_cast<f32x4*>(r) = f32x4{acc[q][0], acc[q][1], acc[q][2], acc[q][3]};
+      else *reinterpret_cast<float2*>(r) = float2{acc[q][0], acc[q][1]};
+    }
+  };
+  if (rd) {
+    if (!BF || isO) readout(std::integral_constant<int, 4>{});   // wave-uniform (bf16: waves 0-3)
+    else readout(std::integral_constant<int, 2>{});
   }
   __syncthreads();
   float* arow = ans + (size_t)f * ans_ld;
   for (int i = tid; i < NQ * 184; i += kAttnFwdThreads) {
     float v = 0.f;
 #pragma unroll
-    for (int s2 = 0; s2 < SL; ++s2) v += red[s2 * NQ * 184 + i];
+    for (int s2 = 0; s2 < NSL; ++s2) v += red[s2 * NQ * 184 + i];
     arow[i] = v;
   }
   for (int i = tid; i < NQ * 72; i += kAttnFwdThreads) arow[NQ * 184 + i] = Qs[i];
@@ -243,11 +299,11 @@ __device__ uint64_t aaa_attn_stamps[16384 * 8];
 // Backward of the readout / softmax / logits for one frame: from da (the
 // answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
 // this frame's dQ (logits path, plus the answer row's Q columns when addq).
-template <int NQ>
+template <int NQ, typename TO>
 __global__ void __launch_bounds__(512)
-k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const float* __restrict__ Q, int qs,
+k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
-           float* __restrict__ dO, float* __restrict__ dQp) {
+           float* __restrict__ dO, float* __restrict__ dQp, int cqm) {
   constexpr int NT = 512, NW = NT / 64;
   constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT)
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -259,26 +315,42 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   float* red = ss + 8;           // G*NQ*72
   float* Vc = red + G * NQ * 72; // kAttnChunk * kVld
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* O = Hs + (size_t)f * P * 128;
+  constexpr bool BF = !std::is_same<TO, float>::value;
+  const TO* O = Hs + (size_t)f * P * old;
   AAA_AT_STAMP(0);
-  // V chunk pieces of this thread (16 B each, consecutive threads along a row),
-  // loaded into registers one chunk AHEAD of its LDS staging: chunk c+1's
-  // loads are in flight while chunk c's dot products run (the barriers below
-  // drain only the LDS counter), so the frame's V rows stream in behind the
-  // compute instead of one exposed load latency per chunk.
-  constexpr int VPT = (kAttnChunk * 46 + NT - 1) / NT;
-  f32x4 vr[VPT];
+  // V chunk pieces of this thread (consecutive threads along a row), loaded
+  // into registers one chunk AHEAD of its LDS staging: chunk c+1's loads are
+  // in flight while chunk c's dot products run (the barriers below drain only
+  // the LDS counter), so the frame's V rows stream in behind the compute
+  // instead of one exposed load latency per chunk.  fp32 O: 46 pieces of 16 B
+  // per position; bf16 O: 30 O pieces of 8 B (4 channels) and 16 S pieces of 16 B.
+  constexpr int VPT = BF ? (kAttnChunk * 30 + NT - 1) / NT : (kAttnChunk * 46 + NT - 1) / NT;
+  using VR = typename std::conditional<BF, u32x2, f32x4>::type;
+  VR vr[VPT];
+  f32x4 vs;   // bf16 O: this thread's S piece
+  static_assert(!BF || kAttnChunk * 16 <= NT, "one S piece per thread");
   auto vload = [&](int p0) {
-    const int nv = min(kAttnChunk, P - p0) * 46;
+    const int np = min(kAttnChunk, P - p0);
+    // one unconditional load from a selected address per piece (a load per
+    // branch would serialise them on the shared destination registers, and
+    // a select on the loaded value would wait for it right here); pieces
+    // past the chunk load a valid dummy the staging skips
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      // one unconditional load from a selected address (a load per branch
-      // would serialise them on the shared destination registers, and a
-      // select on the loaded value would wait for it right here)
-      const int i = tid + j * NT, pp = i / 46, g = i - pp * 46, p = p0 + pp;
-      const bool ok = i < nv;
-      const float* src = !ok ? S : (g < 30 ? O + p * 128 + 8 + 4 * g : S + p * 64 + 4 * (g - 30));
-      vr[j] = *reinterpret_cast<const f32x4*>(src);   // unused when !ok (the staging skips it)
+      for (int j = 0; j < VPT; ++j) {
+        const int i = tid + j * NT, pp = i / 30, g = i - pp * 30;
+        const TO* src = i < np * 30 ? O + (size_t)(p0 + pp) * old + 8 + 4 * g : O;
+        vr[j] = *reinterpret_cast<const u32x2*>(src);
+      }
+      const float* ss = tid < np * 16 ? S + (p0 + (tid >> 4)) * 64 + 4 * (tid & 15) : S;
+      vs = *reinterpret_cast<const f32x4*>(ss);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int i = tid + j * NT, pp = i / 46, g = i - pp * 46, p = p0 + pp;
+        const float* src = i >= np * 46 ? S : (g < 30 ? O + (size_t)p * old + 8 + 4 * g : S + p * 64 + 4 * (g - 30));
+        vr[j] = *reinterpret_cast<const f32x4*>(src);
+      }
     }
   };
   vload(0);
@@ -291,10 +363,19 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   // product from LDS (no cross-lane reductions).
   for (int p0 = 0; p0 < P; p0 += kAttnChunk) {
     const int np = min(kAttnChunk, P - p0);
+    if constexpr (BF) {
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) {
-      const int i = tid + j * NT, pp = i / 46, g = i - pp * 46;
-      if (i < np * 46) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = vr[j];
+      for (int j = 0; j < VPT; ++j) {
+        const int i = tid + j * NT, pp = i / 30, g = i - pp * 30;
+        if (i < np * 30) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = bf4_f32(vr[j]);
+      }
+      if (tid < np * 16) *reinterpret_cast<f32x4*>(Vc + (tid >> 4) * kVld + 120 + 4 * (tid & 15)) = vs;
+    } else {
+#pragma unroll
+      for (int j = 0; j < VPT; ++j) {
+        const int i = tid + j * NT, pp = i / 46, g = i - pp * 46;
+        if (i < np * 46) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = vr[j];
+      }
     }
     lds_barrier();
     if (p0 + kAttnChunk < P) vload(p0 + kAttnChunk);
@@ -328,10 +409,11 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
   }
   __syncthreads();
   AAA_AT_STAMP(3);
-  // dO: 16 B per thread, rows written by consecutive threads
+  // dO: 16 B per thread, rows written by consecutive threads (row-major) or
+  // each channel quad's pixels by consecutive threads (cqm: recur.h cqm4)
   float* dOf = dO + (size_t)f * P * 128;
   for (int i = tid; i < P * 32; i += NT) {
-    const int p = i >> 5, c4 = (i & 31) * 4;
+    const int p = cqm ? i % P : i >> 5, c4 = cqm ? (i / P) * 4 : (i & 31) * 4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (c4 < 8) {
 #pragma unroll
@@ -348,7 +430,7 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
         acc[0] += a * dd[0]; acc[1] += a * dd[1]; acc[2] += a * dd[2]; acc[3] += a * dd[3];
       }
     }
-    *reinterpret_cast<f32x4*>(dOf + p * 128 + c4) = acc;
+    *reinterpret_cast<f32x4*>(dOf + (cqm ? i * 4 : p * 128 + c4)) = acc;
   }
   AAA_AT_STAMP(4);
   // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] | S]: G position groups,
@@ -360,11 +442,18 @@ k_attn_bwd(const float* __restrict__ Hs, const float* __restrict__ S, const floa
     for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
     // K = [O[:8] | S] column c: one strided address stream per thread, loads
     // unrolled so several are in flight (not one latency per position)
-    const float* kp = c < 8 ? O + c : S + c - 8;
-    const int kld = c < 8 ? 128 : 64;
+    // (bf16 O: the dword holding channels c & ~1 and c | 1, its half picked)
+    const uint32_t* kp = c < 8 ? reinterpret_cast<const uint32_t*>(O + (BF ? (c & ~1) : c))
+                               : reinterpret_cast<const uint32_t*>(S + c - 8);
+    const int kld = c < 8 ? (BF ? old / 2 : old) : 64;   // in dwords
+    // the element as fp32 bits by a per-lane shift and mask (a select here
+    // compiles to a branch whose join waits for each load in turn)
+    const bool half = BF && c < 8;
+    const uint32_t ksh = half && !(c & 1) ? 16u : 0u, kmask = half ? 0xffff0000u : 0xffffffffu;
 #pragma unroll 8
     for (int p = g; p < P; p += G) {
-      const float k = kp[p * kld];
+      const uint32_t ku = kp[(size_t)p * kld];
+      const float k = __uint_as_float((ku << ksh) & kmask);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] += dA[p * NQ + q] * k;
     }
@@ -485,6 +574,20 @@ __global__ void k_concat_dy(int F, int A, int ldy, const float* dl, const float*
   }
 }
 
+// Per-frame (P, 128) fp32 state slices between row-major (the C ABI's h/c
+// tensors) and the channel-quad-major slices of the frame-resident kernels
+// (recur.h cqm4): 16 B (one channel quad of one pixel) per thread, pixels
+// fastest on the quad-major side.
+__global__ void k_cqm_convert(const float* __restrict__ src, float* __restrict__ dst, int nf, int P, int to_cqm) {
+  const long n = (long)nf * P * 32;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long f = i / ((long)P * 32);
+    const int r = (int)(i - f * P * 32), q = r / P, pp = r - q * P;
+    const size_t rm = (size_t)f * P * 128 + (size_t)pp * 128 + q * 4, cq = (size_t)f * P * 128 + (size_t)r * 4;
+    *reinterpret_cast<f32x4*>(dst + (to_cqm ? cq : rm)) = *reinterpret_cast<const f32x4*>(src + (to_cqm ? rm : cq));
+  }
+}
+
 // XH slot 0 channels 64..191 <- h0 (or zero)
 
 template <typename T>
@@ -494,6 +597,14 @@ __global__ void k_state_to_xh(int M, const float* h0, T* xh) {
     const int m = idx >> 7, ch = idx & 127;
     xh[(size_t)m * 192 + 64 + ch] = (T)(h0 ? h0[idx] : 0.f);
   }
+}
+
+// h_T (fp32 state out) <- the h half of XH slot T (the bf16 path's only copy of h_t)
+template <typename T>
+__global__ void k_xh_to_state(int M, const T* __restrict__ xh, float* __restrict__ h) {
+  const int n = M * 128;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x)
+    h[idx] = (float)xh[(size_t)(idx >> 7) * 192 + 64 + (idx & 127)];
 }
 
 // XH slot <- [x (64) | h (128)] of the standalone ConvLSTM cell (h NULL: the
@@ -659,7 +770,7 @@ __global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gat
     float gi, gf, gc, go, c, h;
     GateFwd::run(z[0], z[1], z[2], z[3], cprev[idx], gi, gf, gc, go, c, h);
     cnext[idx] = c;
-    hout[idx] = h;
+    if (hout) hout[idx] = h;   // null on the bf16 path (the readout reads xhnext)
     xhnext[(size_t)m * 192 + 64 + ch] = (T)h;
     *reinterpret_cast<f32x4*>(gates + (size_t)m * 512 + 4 * ch) = f32x4{gi, gf, gc, go};
   }
@@ -853,7 +964,7 @@ hipError_t query_sq(const float* S, const float* Q, int P, int nq, float* SQ, hi
   return hipGetLastError();
 }
 
-hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float* SQ, const float* pr,
+hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, const float* pr,
                     const float* pa, int F, int P, int nq, float* Am, float* ans, int ans_ld, hipStream_t st,
                     int qs) {
   // register prefetch of the V slice only on large grids (many positions per
@@ -862,42 +973,64 @@ hipError_t attn_fwd(const float* Hs, const float* S, const float* Q, const float
   static const int pre_env = getenv("AAA_ATTN_PRE") ? atoi(getenv("AAA_ATTN_PRE")) : -1;   // A/B override
   static const int sl_env = getenv("AAA_ATTN_SLICES") ? atoi(getenv("AAA_ATTN_SLICES")) : -1;
   const bool pre = pre_env >= 0 ? pre_env != 0 : P > 2 * kAttnSlices * 11;
-  const int sl = sl_env > 0 ? sl_env : kAttnSlices;
+  const int sl = O.bf16 ? kAttnSlicesBf : sl_env > 0 ? sl_env : kAttnSlices;
   const size_t sh = (size_t)(P * nq + nq * 72 + sl * nq * 184) * sizeof(float);
   if (sh > 160 * 1024) return hipErrorInvalidValue;
-  auto launch = [&](auto kern) {
+  if (O.bf16 ? (O.ld < 136 || O.ld % 8) : O.ld < 128 || O.ld % 4) return hipErrorInvalidValue;   // 16-B key loads
+  auto launch = [&](auto kern, auto* o) {
     if (sh > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sh);
-    hipLaunchKernelGGL(kern, dim3(F), dim3(kAttnFwdThreads), sh, st, Hs, S, Q, qs, SQ, pr, pa, P, Am, ans, ans_ld);
+    hipLaunchKernelGGL(kern, dim3(F), dim3(kAttnFwdThreads), sh, st, o, O.ld, S, Q, qs, SQ, pr, pa, P, Am, ans,
+                       ans_ld);
   };
   auto go = [&](auto slc) {
     constexpr int SL = decltype(slc)::value;
-    if (nq == 4) pre ? launch(k_attn_fwd<4, 8, SL>) : launch(k_attn_fwd<4, 0, SL>);
-    else if (nq == 8) pre ? launch(k_attn_fwd<8, 8, SL>) : launch(k_attn_fwd<8, 0, SL>);
+    if (O.bf16) {
+      const __bf16* o = (const __bf16*)O.p;
+      if (nq == 4) pre ? launch(k_attn_fwd<4, 8, SL, __bf16>, o) : launch(k_attn_fwd<4, 0, SL, __bf16>, o);
+      else if (nq == 8) pre ? launch(k_attn_fwd<8, 8, SL, __bf16>, o) : launch(k_attn_fwd<8, 0, SL, __bf16>, o);
+      return;
+    }
+    const float* o = (const float*)O.p;
+    if (nq == 4) pre ? launch(k_attn_fwd<4, 8, SL, float>, o) : launch(k_attn_fwd<4, 0, SL, float>, o);
+    else if (nq == 8) pre ? launch(k_attn_fwd<8, 8, SL, float>, o) : launch(k_attn_fwd<8, 0, SL, float>, o);
   };
   if (nq != 4 && nq != 8) return hipErrorInvalidValue;
-  if (sl == 8) go(std::integral_constant<int, 8>{});
+  if (O.bf16) go(std::integral_constant<int, 0>{});   // (SL unused: kAttnSlicesBf)
+  else if (sl == 8) go(std::integral_constant<int, 8>{});
   else if (sl == 5) go(std::integral_constant<int, 5>{});
   else if (sl == kAttnSlices) go(std::integral_constant<int, kAttnSlices>{});
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-hipError_t attn_bwd(const float* Hs, const float* S, const float* Q, const float* Am, const float* dAns,
-                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs, int addq) {
+hipError_t cqm_convert(const float* src, float* dst, int nf, int P, int to_cqm, hipStream_t st) {
+  hipLaunchKernelGGL(k_cqm_convert, dim3(nblk((long)nf * P * 32)), dim3(256), 0, st, src, dst, nf, P, to_cqm);
+  return hipGetLastError();
+}
+
+hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, const float* dAns,
+                    int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs, int addq,
+                    int cqm) {
   const int G = 7;   // k_attn_bwd's dQ position groups
   const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72 + kAttnChunk * kVld) * sizeof(float);
   if (sh > 160 * 1024) return hipErrorInvalidValue;
-  auto launch = [&](auto kern) {
+  if (O.bf16 ? (O.ld < 136 || O.ld % 4) : O.ld < 128 || O.ld % 4) return hipErrorInvalidValue;
+  auto launch = [&](auto kern, auto* o) {
     if (sh > 64 * 1024)   // large grids (168x168: P = 441, nq = 8) use more than the default 64 KiB
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sh);
-    hipLaunchKernelGGL(kern, dim3(F), dim3(512), sh, st, Hs, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp);
+    hipLaunchKernelGGL(kern, dim3(F), dim3(512), sh, st, o, O.ld, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp, cqm);
   };
-  if (nq == 4) launch(k_attn_bwd<4>);
-  else if (nq == 8) launch(k_attn_bwd<8>);
-  else return hipErrorInvalidValue;
+  if (nq != 4 && nq != 8) return hipErrorInvalidValue;
+  if (O.bf16) {
+    const __bf16* o = (const __bf16*)O.p;
+    nq == 4 ? launch(k_attn_bwd<4, __bf16>, o) : launch(k_attn_bwd<8, __bf16>, o);
+  } else {
+    const float* o = (const float*)O.p;
+    nq == 4 ? launch(k_attn_bwd<4, float>, o) : launch(k_attn_bwd<8, float>, o);
+  }
   return hipGetLastError();
 }
 
@@ -948,6 +1081,12 @@ hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, fl
 template <typename T>
 hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st) {
   hipLaunchKernelGGL(k_state_to_xh<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, h0, xh);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t xh_to_state(int M, const T* xh, float* h, hipStream_t st) {
+  hipLaunchKernelGGL(k_xh_to_state<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, xh, h);
   return hipGetLastError();
 }
 
@@ -1055,6 +1194,7 @@ template hipError_t cast<__bf16, float>(long, const __bf16*, float*, hipStream_t
 template hipError_t cast<float, float>(long, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<float>(int, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<__bf16>(int, const float*, __bf16*, hipStream_t);
+template hipError_t xh_to_state<__bf16>(int, const __bf16*, float*, hipStream_t);
 template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);
 template hipError_t pack_lstm_all<float>(const LstmPtrs&, float*, float*, float*, float*, float*, hipStream_t);

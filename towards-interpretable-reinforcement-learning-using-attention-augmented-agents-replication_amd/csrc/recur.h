@@ -43,6 +43,25 @@ constexpr int kRecHS = 136;         // h image pixel pitch (bf16): 128 + 8 pad (
 constexpr int kRecStg = 4608;       // per-wave epilogue staging bytes (16 px x 272 B gates; c + h 2 x 16 x 144 B)
 constexpr int kSC1 = 16;            // buffer load / store cache policy: sc1 (cross-workgroup hand-off bytes)
 
+// Channel-quad-major layout ("CQM") of the per-(frame, step) slices the
+// frame-resident forward writes and the frame-resident BPTT reads (the cell
+// state Cst, the gate activations Gt, the attention-path grad dO): inside a
+// frame's P x 128 slice, channel quad q = ch / 4 of pixel pp sits at
+// (q * P + pp) * 4 floats (Cst, dO) or (q * P + pp) * 16 fp16 (Gt: 4 channels
+// x 4 gates).  The BPTT epilogue's lanes hold 4 consecutive channels at 32
+// consecutive pixels, so each of its loads reads two contiguous 512-B runs
+// (c, dO) or 1-KB runs (gates) instead of 16 B of every 512-B pixel row, which
+// left the rest of each line to later loads (PMC: 2.4x the algorithmic bytes;
+// tools/ubench/bwband "coalesced epilogue loads" -14 % per launch).  Slices
+// keep their row-major positions and sizes; only their inside is permuted.
+__host__ __device__ __forceinline__ int cqm4(int pp, int ch, int P) { return ((ch >> 2) * P + pp) * 4 + (ch & 3); }
+__host__ __device__ __forceinline__ int cqmg(int pp, int ch, int P) { return ((ch >> 2) * P + pp) * 16 + (ch & 3) * 4; }
+// Which slices are channel-quad-major (cqm_layout's mask; the others row-major):
+constexpr int kCqmC = 1, kCqmG = 2, kCqmDO = 4;
+// offset of channel ch of pixel pp in a 128-channel fp32 slice / in a gate slice (4 gates per channel)
+__host__ __device__ __forceinline__ int slc4(int pp, int ch, int P, bool q) { return q ? cqm4(pp, ch, P) : pp * 128 + ch; }
+__host__ __device__ __forceinline__ int slcg(int pp, int ch, int P, bool q) { return q ? cqmg(pp, ch, P) : pp * 512 + ch * 4; }
+
 // k step ks of the x-first order -> element offset k of the [x|h] GEMM (k = tap*192 + c)
 __host__ __device__ constexpr int rec_k(int ks) {
   return ks < kRecKX ? (ks >> 2) * 192 + (ks & 3) * 16 : ((ks - kRecKX) >> 3) * 192 + 64 + ((ks - kRecKX) & 7) * 16;
@@ -86,13 +105,14 @@ struct RecFwdParams {
   const float* bias;   // [512] gate-interleaved x-conv biases
   __bf16* XH;          // (T+1, B, P, 192): slot t = [x_t | h_{t-1}]; writes h_t into slot t+1
   float* Cst;          // (T+1, B, P, 128): slot 0 = c_0 (read), slot t+1 <- c_t
-  float* Hs;           // (T, B, P, 128) <- h_t (fp32)
+  float* Hs;           // (T, B, P, 128) <- h_t (fp32), or null (the readout reads h_t from XH)
   GT* Gt;              // (T, B, P, 512) <- gate activations (i, f, c~, o)
   int* flags;          // G = 2: per (frame, half) count of published h steps ([2B], zeroed); band mode: [B][bands]
   int T, B, h, w, P;
   int* report;         // G = 2: partner-timeout report word (pinned host, device-mapped; pair_wait)
   int spin;            // G = 2 / band: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;         // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
+  int cqm;             // kCqmC / kCqmG: Cst / Gt slices channel-quad-major (cqm4 / cqmg) instead of row-major
   // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
   // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
   short colpp[128], colhb[128];
@@ -253,8 +273,9 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int pp = BAND ? (cb * 32 + r32 < Pb ? pix0 + cb * 32 + r32 : -1) : p.colpp[cb * 32 + r32];
+        const int ch = cbase + 8 * rb + 2 * g + hh;
         cw[(rb * 16 + cb * 4 + g) * 64] =
-            pp >= 0 ? p.Cst[((size_t)b * P + pp) * 128 + cbase + 8 * rb + 2 * g + hh] : 0.f;
+            pp >= 0 ? p.Cst[(size_t)b * P * 128 + slc4(pp, ch, P, p.cqm & kCqmC)] : 0.f;
       }
   __syncthreads();   // h image zeroed
   {  // h_0 (slot 0, channels 64..191) into the image (band mode: the band's rows and its halo rows)
@@ -475,13 +496,23 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
                 *reinterpret_cast<uint2*>(sw + pxl * GTP + (8 * rb + 2 * g + hl_) * 8) = uint2{gq[rb][g][0], gq[rb][g][1]};
           }
           constexpr int CG = GCH / 2, CC = GCH / 4;   // 16-B chunks per pixel row: gates, c / h
+          if (p.cqm & kCqmG) {   // quad-major: lane pairs walk the 16 pixels of one quad (512-B runs)
 #pragma unroll
-          for (int k = 0; k < NRB; ++k) {   // 1 KB each: 64 / CG pixel rows of 8 * GCH B
-            const int q = k * 64 + ln, px = q / CG, pix = scol[pbase + px];
-            const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * GTP + (q % CG) * 16);
-            if (pix >= 0)
-              *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * cbase) +
-                                        (q % CG) * 16) = v;
+            for (int k = 0; k < NRB; ++k) {
+              const int q = k * 64 + ln, hf = q & 1, px = (q >> 1) & 15, qi = q >> 5, pix = scol[pbase + px];
+              const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * GTP + (2 * qi + hf) * 16);
+              if (pix >= 0)
+                *reinterpret_cast<u32x4*>(p.Gt + rowt * 512 + ((size_t)(cbase / 4 + qi) * P + pix) * 16 + hf * 8) = v;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < NRB; ++k) {   // 1 KB each: 64 / CG pixel rows of 8 * GCH B
+              const int q = k * 64 + ln, px = q / CG, pix = scol[pbase + px];
+              const u32x4 v = *reinterpret_cast<const u32x4*>(sw + px * GTP + (q % CG) * 16);
+              if (pix >= 0)
+                *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(p.Gt + (rowt + pix) * 512 + 4 * cbase) +
+                                          (q % CG) * 16) = v;
+            }
           }
           // c_t and h_t: staging [16 px][GCH ch] fp32 at pixel pitch CHP (c), then (h) 16 * CHP B on
           if (mine) {
@@ -490,17 +521,23 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 #pragma unroll
               for (int g = 0; g < 4; ++g) {
                 *reinterpret_cast<float*>(sw + pxl * CHP + (8 * rb + 2 * g + hl_) * 4) = cv[rb][g];
-                *reinterpret_cast<float*>(sw + 16 * CHP + pxl * CHP + (8 * rb + 2 * g + hl_) * 4) = hv[rb][g];
+                if (p.Hs) *reinterpret_cast<float*>(sw + 16 * CHP + pxl * CHP + (8 * rb + 2 * g + hl_) * 4) = hv[rb][g];
               }
           }
 #pragma unroll
           for (int k = 0; k < NRB / 2; ++k) {   // 1 KB each of c and h: 64 / CC pixel rows of 4 * GCH B
             const int q = k * 64 + ln, px = q / CC, pix = scol[pbase + px];
-            const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * CHP + (q % CC) * 16);
-            const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 16 * CHP + px * CHP + (q % CC) * 16);
-            if (pix >= 0) {
-              *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + cbase + (q % CC) * 4) = vc;
-              *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + cbase + (q % CC) * 4) = vh;
+            if (p.cqm & kCqmC) {   // c quad-major: 16 lanes walk the 16 pixels of one quad (256-B runs)
+              const int pxq = q & 15, qi = q >> 4, pixq = scol[pbase + pxq];
+              const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + pxq * CHP + qi * 16);
+              if (pixq >= 0) *reinterpret_cast<u32x4*>(p.Cst + (rowt + M) * 128 + ((size_t)(cbase / 4 + qi) * P + pixq) * 4) = vc;
+            } else {
+              const u32x4 vc = *reinterpret_cast<const u32x4*>(sw + px * CHP + (q % CC) * 16);
+              if (pix >= 0) *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + cbase + (q % CC) * 4) = vc;
+            }
+            if (p.Hs) {
+              const u32x4 vh = *reinterpret_cast<const u32x4*>(sw + 16 * CHP + px * CHP + (q % CC) * 16);
+              if (pix >= 0) *reinterpret_cast<u32x4*>(p.Hs + (rowt + pix) * 128 + cbase + (q % CC) * 4) = vh;
             }
           }
         }

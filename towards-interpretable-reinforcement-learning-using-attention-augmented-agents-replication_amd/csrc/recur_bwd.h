@@ -69,7 +69,7 @@ __device__ __forceinline__ void gate_bwd_fast(float dh, const f32x4& g, float cp
   dc = dcc * gf;
 }
 
-struct RecBwdParams {
+struct RecBwdParams {   // dO, Gt, Cst: per-(frame, step) slices, channel-quad-major per cqm (recur.h cqm4)
   const __bf16* Wb;       // fragment-order W_h^T
   const float* dO;        // (T, B, P, 128) attention-path grad of h_t
   const _Float16* Gt;     // (T, B, P, 512) gate activations
@@ -86,6 +86,7 @@ struct RecBwdParams {
   int* report;            // paired kernel: partner-timeout report word (pinned host, device-mapped; pair_wait)
   int spin;               // paired / band kernels: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;            // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
+  int cqm = kCqmC | kCqmG | kCqmDO;   // which slices are channel-quad-major (recur.h kCqm*)
 };
 
 // Chunk images of the band kernel: image pixel ip (a (rows+2) x (w+2)
@@ -226,12 +227,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
-    if (col < Pb && !(ABL & 66)) {
-      const size_t row = (size_t)s * M + (size_t)b * P + pix0 + col;
-      const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g;
-      if constexpr (!DOACC) in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
-      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);         // c_{s-1}
-      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
+    if (col < Pb && !(ABL & 66)) {   // the slices are channel-quad-major (recur.h cqm4 / cqmg)
+      const size_t fr = (size_t)s * M + (size_t)b * P;
+      const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g, pp = pix0 + col;
+      if constexpr (!DOACC) in.dO = *reinterpret_cast<const f32x4*>(p.dO + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmDO));
+      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));   // c_{s-1}
+      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + fr * 512 + slcg(pp, ch, P, p.cqm & kCqmG));
       in.gt[0] = gp[0];
       in.gt[1] = gp[1];
     } else {
@@ -245,8 +246,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
     f32x4 v{0.f, 0.f, 0.f, 0.f};
     if (s >= 0 && col < Pb && !(ABL & 66))
-      v = *reinterpret_cast<const f32x4*>(p.dO + ((size_t)s * M + (size_t)b * P + pix0 + col) * 128 + 32 * wave +
-                                          4 * (ln >> 5) + 8 * g);
+      v = *reinterpret_cast<const f32x4*>(p.dO + ((size_t)s * M + (size_t)b * P) * 128 +
+                                          slc4(pix0 + col, 32 * wave + 4 * (ln >> 5) + 8 * g, P, p.cqm & kCqmDO));
     acc[cb][4 * g] = v[0]; acc[cb][4 * g + 1] = v[1]; acc[cb][4 * g + 2] = v[2]; acc[cb][4 * g + 3] = v[3];
   };
 
@@ -680,12 +681,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
     const int g = u >> 1, j = u & 1, pp = (cbA + j) * 32 + (ln & 31);
-    if (pp < P) {
-      const size_t row = (size_t)s * M + (size_t)b * P + pp;
+    if (pp < P) {   // channel-quad-major slices (recur.h cqm4 / cqmg)
+      const size_t fr = (size_t)s * M + (size_t)b * P;
       const int ch = 32 * hrb + 4 * (ln >> 5) + 8 * g;
-      in.dO = *reinterpret_cast<const f32x4*>(p.dO + row * 128 + ch);
-      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + row * 128 + ch);
-      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + row * 512 + 4 * ch);
+      in.dO = *reinterpret_cast<const f32x4*>(p.dO + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmDO));
+      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));
+      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + fr * 512 + slcg(pp, ch, P, p.cqm & kCqmG));
       in.gt[0] = gp[0];
       in.gt[1] = gp[1];
     } else {

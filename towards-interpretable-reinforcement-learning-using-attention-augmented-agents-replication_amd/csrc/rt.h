@@ -165,8 +165,14 @@ std::string strf(const char* fmt, ...);
 // Algorithmic bytes per frame of the fused attention readout kernels (fp32):
 // forward reads the frame's O rows (128 ch) and writes its map and answer row;
 // backward reads O, the map and the answer grad, writes dO and dQ.
-inline double attn_fwd_bytes(int P, int nq, int ans_ld) { return 4.0 * (128.0 * P + nq * P + ans_ld); }
-inline double attn_bwd_bytes(int P, int nq) { return 4.0 * (2.0 * 128 * P + nq * P + 184.0 * nq + 72.0 * nq); }
+// per frame: O read (oesz bytes per element: 4 fp32 Hs, 2 the bf16 XH copy), A and the answer row written
+inline double attn_fwd_bytes(int P, int nq, int ans_ld, int oesz = 4) {
+  return oesz * 128.0 * P + 4.0 * (nq * P + ans_ld);
+}
+// per frame: O read, dO written (fp32), A / da / Q read, dQ written
+inline double attn_bwd_bytes(int P, int nq, int oesz = 4) {
+  return oesz * 128.0 * P + 4.0 * (128.0 * P + nq * P + 184.0 * nq + 72.0 * nq);
+}
 
 // --------------------------------------------------------- tile configs ---
 // fp32 uses the exact v_mfma_f32_32x32x2_f32; bf16 v_mfma_f32_32x32x16_bf16 (fp32 accumulate).
@@ -440,6 +446,17 @@ int frames_g(const Layout& L, const char* env);
 int frames_band(const Layout& L);   // band mode (recur.h BAND): kRecBands, else 0
 int f32_frames(const Layout& L);    // fp32 frame-group G (recur_f32.h), else 0
 int frames_bwd(const Layout& L, bool g16);
+// Cst / Gt / dO slices channel-quad-major (recur.h cqm4): the frame-resident forward + BPTT pair
+int cqm_layout(const Layout& L);   // recur.h kCqm* mask of the channel-quad-major slices (0: all row-major)
+// h_t of all T*B frames as the attention readout reads it: the fp32 Hs slices
+// (fp32 path), or the h half of XH slots 1..T (bf16 path: no fp32 copy of h_t
+// is kept -- the readout reads the bf16 h the next step's conv and the weight
+// gradient read, oracle/ref_cpu.py h_store).  Frame f = t*B + b sits at
+// .frame(f, P) either way.
+inline OSrc readout_h(const Layout& L, char* ws) {
+  if (L.esz == 2) return o_bf16((const __bf16*)(ws + L.XH) + (size_t)L.B * L.P * 192 + 64, 192);
+  return o_f32((const float*)(ws + L.Hs));
+}
 int rec_stagger(const char* env);   // start offset of half the frames, 100-MHz ticks
 
 // ------------------------------------------------------- cross-unit paths --

@@ -356,9 +356,9 @@ static int head_backward_stateful(const Layout& L, const aaa_io* io, hipStream_t
     // readout / softmax / logits backward with this step's queries; dQ gets
     // the logits path plus the answer row's copy of Q
     {
-      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)B * attn_bwd_bytes(P, L.nq), "k_attn_bwd, per-frame query (stateful core)");
-      HIPCHK(attn_bwd(Wf(L.Hs) + f0 * P * 128, io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
-                      Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1));
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)B * attn_bwd_bytes(P, L.nq, L.esz), "k_attn_bwd, per-frame query (stateful core)");
+      HIPCHK(attn_bwd(readout_h(L, ws).frame(f0, P), io->basis, Wf(L.Qf) + f0 * qd, Wf(L.Am) + f0 * P * L.nq,
+                      Wf(L.dAns) + f0 * da, da, B, P, L.nq, Wf(L.dO) + f0 * P * 128, Wf(L.dQf) + f0 * qd, st, qd, 1, (cqm_layout(L) & kCqmDO) != 0));
     }
     {  // query MLP backward to its input h_{t-1}
       LTf::Params pa{prm + L.poff[Q4W], qd, qd};
@@ -499,9 +499,9 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     tail.reset();
     // attention readout / softmax / logits backward, then the query MLP
     {
-      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)F * attn_bwd_bytes(P, L.nq), "k_attn_bwd, 1 WG per frame");
-      HIPCHK(attn_bwd(Wf(L.Hs), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
-                      Wf(L.dO), Wf(L.dQp), st));
+      TimerScope tim(AAA_TIMER_ATTN_BWD, st, (double)F * attn_bwd_bytes(P, L.nq, L.esz), "k_attn_bwd, 1 WG per frame");
+      HIPCHK(attn_bwd(readout_h(L, ws), io->basis, (const float*)(pk + L.k_Q), Wf(L.Am), Wf(L.dAns), L.da, F, P, L.nq,
+                      Wf(L.dO), Wf(L.dQp), st, 0, 0, (cqm_layout(L) & kCqmDO) != 0));
     }
     tail.reset(new TimerScope(AAA_TIMER_TAIL_BWD, st, 0.0, "bias column sums, query MLP backward, grad unpack"));
     {  // the bias grads of the heads, the LSTMCell and both answer layers, and dQ summed over frames: one launch
@@ -662,7 +662,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       if constexpr (!std::is_same<T, float>::value) {
         RecBwdParams rp{(const __bf16*)(pk + L.k_Wbf), Wf(L.dO), (const _Float16*)(ws + L.Gt), Wf(L.Cst), io->dhT,
                         Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), (int*)(ws + L.rflags),
-                        L.T, L.B, L.h, L.w, L.P, nullptr, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_BWD")};
+                        L.T, L.B, L.h, L.w, L.P, nullptr, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_BWD"),
+                        cqm_layout(L)};
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));

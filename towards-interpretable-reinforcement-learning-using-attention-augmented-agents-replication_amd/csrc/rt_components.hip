@@ -451,7 +451,7 @@ int aaa_attn_fwd(int F, int h, int w, int nq, const float* O, const float* S, co
   if (!O || !S || !Q || !attn || !answer) return fail(AAA_E_ARG, "attn_fwd: O/S/Q/attn/answer must be set");
   if (!aligned16(O) || !aligned16(S)) return fail(AAA_E_ALIGN, "O and S must be 16-byte aligned");
   TimerScope tim(AAA_TIMER_ATTN_FWD, stream, (double)F * attn_fwd_bytes(h * w, nq, 256 * nq + 2), "k_attn_fwd (aaa_attn_fwd)");
-  HIPCHK(attn_fwd(O, S, Q, nullptr, prev_reward, prev_action, F, h * w, nq, attn, answer, 256 * nq + 2, stream,
+  HIPCHK(attn_fwd(o_f32(O), S, Q, nullptr, prev_reward, prev_action, F, h * w, nq, attn, answer, 256 * nq + 2, stream,
                   q_stride));
   return AAA_OK;
 }
@@ -464,7 +464,7 @@ int aaa_attn_bwd(int F, int h, int w, int nq, const float* O, const float* S, co
     return fail(AAA_E_ARG, "attn_bwd: O/S/Q/attn/danswer/dO/dQ must be set");
   if (!aligned16(O) || !aligned16(S) || !aligned16(dO)) return fail(AAA_E_ALIGN, "O, S, dO must be 16-byte aligned");
   TimerScope tim(AAA_TIMER_ATTN_BWD, stream, (double)F * attn_bwd_bytes(h * w, nq), "k_attn_bwd (aaa_attn_bwd)");
-  HIPCHK(attn_bwd(O, S, Q, attn, danswer, 256 * nq + 2, F, h * w, nq, dO, dQ, stream, q_stride, 1));
+  HIPCHK(attn_bwd(o_f32(O), S, Q, attn, danswer, 256 * nq + 2, F, h * w, nq, dO, dQ, stream, q_stride, 1));
   return AAA_OK;
 }
 

@@ -82,7 +82,7 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.Xp = take(F * (L.H + 2) * (L.W + 2) * 4 * e);  // frames as zero-bordered RGBx (conv1 operand type)
   L.Y1 = take(F * L.P1 * 32 * e);
   L.XH = take((size_t)(L.T + 1) * M * 192 * e);
-  L.Hs = take(F * P * 128 * 4);
+  L.Hs = take(e == 4 ? F * P * 128 * 4 : 0);   // fp32 h_t for the readout (bf16: it reads XH, readout_h)
   L.Cst = take((size_t)(L.T + 1) * M * 128 * 4);
   L.Gt = take(F * P * 512 * 4);
   L.SQ = take(P * L.nq * 4);
@@ -376,10 +376,16 @@ int f32_frames(const Layout& L) {
 // stagger_wait), in microseconds -> 100-MHz ticks.
 int rec_stagger(const char* env) { return 100 * env_int(env, 0); }
 // Band mode (recur_bwd.h BAND) wherever the forward runs in band mode: kRecBands.
+// Only behind a frame-resident forward: the two share the channel-quad-major
+// slices of Cst / Gt / dO (cqm_layout), which the per-step kernels do not read.
 int frames_bwd(const Layout& L, bool g16) {
   if (!g16) return 0;
   if (const int nb = frames_band(L)) return bw_band_fits(L.h, L.w) ? nb : 0;
-  return frames_g(L, "AAA_FRAMES_BWD");
+  return frames_fwd(L) ? frames_g(L, "AAA_FRAMES_BWD") : 0;
+}
+int cqm_layout(const Layout& L) {
+  static const int mask = env_int("AAA_CQM", kCqmC | kCqmG | kCqmDO) & 7;   // A/B: tools/gpu_ab.sh
+  return frames_bwd(L, gates_f16(L.dt, L.B * L.P)) != 0 ? mask : 0;
 }
 
 }  // namespace aaa

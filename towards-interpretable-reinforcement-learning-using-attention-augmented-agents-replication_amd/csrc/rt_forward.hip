@@ -149,6 +149,8 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   auto Wf = [&](size_t off) { return (float*)(ws + off); };
   auto Wt = [&](size_t off) { return (T*)(ws + off); };
   const int F = L.F, M = L.B * L.P;
+  // fp32 h_t slices for the readout: fp32 path only (bf16 reads XH, readout_h)
+  auto hs_out = [&](int t) { return L.esz == 4 ? Wf(L.Hs) + (size_t)t * M * 128 : (float*)nullptr; };
 
   {  // conv1 + conv2 over all T*B frames -> XH[:, :, 0:64] of every slot
     TimerScope tim(AAA_TIMER_VISION_FWD, st, (double)F * vision_fwd_flop(L), "conv1 + conv2 (vision encoder)");
@@ -158,7 +160,8 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   {  // initial state (reset(): zeros, attention.py:142-149) or carried state
     TimerScope tim(AAA_TIMER_MISC, st, 0.0, "state in/out copies, memsets, bias column sums");
     HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
-    if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    if (io->c0 && (cqm_layout(L) & kCqmC)) HIPCHK(cqm_convert(io->c0, Wf(L.Cst), L.B, L.P, 1, st));
+    else if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
   }
   if constexpr (std::is_same<T, float>::value) {
@@ -199,8 +202,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
           int* rep = pair_report(dev);
           if (!rep) return fail(AAA_E_LAUNCH, "cannot map the band-mode report word");
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
-                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
+                              nullptr, (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
                               rep, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_FWD")};
+          rp.cqm = cqm_layout(L);
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
                          strf("bf16 band-mode frame-resident [x|h] recurrence, %d steps per launch, %d bands per frame "
                               "[kernel: k_convlstm_fwd_frames+Lb1E]", L.T, NBd));
@@ -216,8 +220,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
             if (!(rep = pair_report(dev))) return fail(AAA_E_LAUNCH, "cannot map the paired-kernel report word");
           }
           RecFwdParams<GT> rp{(const __bf16*)(pk + L.k_Wfr), (const float*)(pk + L.k_bl), Wt(L.XH), Wf(L.Cst),
-                              Wf(L.Hs), (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
+                              nullptr, (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
                               rep, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_FWD")};
+          rp.cqm = cqm_layout(L);
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
                          strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_frames+Lb0E]", L.T, G));
           HIPCHK(convlstm_fwd_frames<GT>(rp, G, st));
@@ -226,7 +231,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
       }
       for (int t = 0; t < L.T; ++t) {   // ConvLSTM (attention.py:110-126), x- and h-part together
         EpiConvLstmFwd<T, GT> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
-                                 Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
+                                 hs_out(t), Wt(L.XH) + (size_t)(t + 1) * M * 192,
                                  (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
         const int rc = fused_step<T, GT>(WpXH, Wt(L.XH) + (size_t)t * M * 192, L.h, L.w, M, ep, st);
         if (rc) return rc;
@@ -278,12 +283,12 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   for (int t = 0; t < L.T; ++t) {  // ConvLSTM recurrence (attention.py:110-126): h-part only
     if (ax && t % cs == 0) HIPCHK(hipStreamWaitEvent(st, xev[t / cs], 0));   // x-part of steps [t, t+cs) done
     if (t == 0 && !io->h0) {       // zero state: gates come from the x-part alone
-      HIPCHK(gate_fwd_zx<T>(M, Wf(L.Cst), Wf(L.Gt), Wf(L.Cst) + (size_t)M * 128, Wf(L.Hs), Wt(L.XH) + (size_t)M * 192,
+      HIPCHK(gate_fwd_zx<T>(M, Wf(L.Cst), Wf(L.Gt), Wf(L.Cst) + (size_t)M * 128, hs_out(0), Wt(L.XH) + (size_t)M * 192,
                             st));
       continue;
     }
     EpiConvLstmFwd<T> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
-                         Wf(L.Hs) + (size_t)t * M * 128, Wt(L.XH) + (size_t)(t + 1) * M * 192,
+                         hs_out(t), Wt(L.XH) + (size_t)(t + 1) * M * 192,
                          Wf(L.Gt) + (size_t)t * M * 512, M};
     const ConvGeo g = ConvGeo{128, 192, 64, L.h, L.w, L.h, L.w, 3, 1, 1, 0}.prep();
     TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1152, strf("%s h-part step (x-part batched), K=1152, tile %d [kernel: EpiConvLstmFwd]", std::is_same<T, float>::value ? "fp32" : "bf16", fwd_tile));
@@ -377,8 +382,8 @@ static int forward_tail_stateful(const Layout& L, const aaa_io* io, hipStream_t 
     }
     // attention readout with this step's per-frame queries (basis logits in-kernel)
     {
-      TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)B * attn_fwd_bytes(P, L.nq, L.ans_ld), "k_attn_fwd, per-frame query (stateful core)");
-      HIPCHK(attn_fwd(Wf(L.Hs) + f0 * P * 128, io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
+      TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)B * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), "k_attn_fwd, per-frame query (stateful core)");
+      HIPCHK(attn_fwd(readout_h(L, ws).frame(f0, P), io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
                       io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
                       Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
     }
@@ -428,8 +433,8 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
   }
   {
-    TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld), "k_attn_fwd, 1 WG per frame");
-    HIPCHK(attn_fwd(Wf(L.Hs), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
+    TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), "k_attn_fwd, 1 WG per frame");
+    HIPCHK(attn_fwd(readout_h(L, ws), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
                     Wf(L.ans), L.ans_ld, st));
   }
   TimerScope tim(AAA_TIMER_TAIL_FWD, st, (double)F * tail_fwd_flop(L), "answer MLP + LSTMCell + heads (fp32 GEMMs)");
@@ -464,10 +469,13 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     EpiHeads ep{io->logits, io->values, (const float*)(pk + L.k_bhd), L.A, F};
     HIPCHK((tail_gemm(pa, pb, ep, 2 * L.A, F, 256, st)));
   }
-  if (io->hT)
+  if (io->hT && L.esz == 2)   // h_{T-1} from XH slot T (the bf16 path keeps no fp32 h_t)
+    HIPCHK(xh_to_state<__bf16>(M, (const __bf16*)(ws + L.XH) + (size_t)L.T * M * 192, io->hT, st));
+  else if (io->hT)
     HIPCHK(hipMemcpyAsync(io->hT, Wf(L.Hs) + (size_t)(L.T - 1) * M * 128, (size_t)M * 128 * 4,
                           hipMemcpyDeviceToDevice, st));
-  if (io->cT)
+  if (io->cT && (cqm_layout(L) & kCqmC)) HIPCHK(cqm_convert(Wf(L.Cst) + (size_t)L.T * M * 128, io->cT, L.B, P, 0, st));
+  else if (io->cT)
     HIPCHK(hipMemcpyAsync(io->cT, Wf(L.Cst) + (size_t)L.T * M * 128, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
   if (L.sc && io->core_hT)
     HIPCHK(hipMemcpyAsync(io->core_hT, Wf(L.CH) + (size_t)L.T * L.B * 256, (size_t)L.B * 256 * 4,
