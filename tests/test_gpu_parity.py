@@ -476,6 +476,41 @@ def test_c5_full_size_bf16_vs_emulated_oracle(cuda):
             assert e <= 2e-2, f"C5 bf16 /255 grad {n}: {e:.3e}"
 
 
+@pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
+def test_xp_chunks_ragged(cuda, monkeypatch, conv_dtype):
+    """conv1's bordered RGBx operand is rebuilt from the frames in chunks of
+    AAA_XP_CHUNK frames (forward layered conv1 and the backward's conv1 weight
+    gradient; csrc/rt_backward.hip conv1_wgrad_frames): 100 frames in chunks of
+    64 + 36 give the oracle's gradients, uint8 and fp32 frames."""
+    monkeypatch.setenv("AAA_XP_CHUNK", "64")
+    T, B = 20, 5
+    tol = RTOL if conv_dtype == "fp32" else 2e-2
+    ref = _oracle(T, B, conv_mode=conv_dtype)
+    _compare(_run_unroll(_agent(cuda, conv_dtype=conv_dtype), T, B, cuda), ref, tol, f"xp chunks {conv_dtype}: ")
+    ag = _agent(cuda, conv_dtype=conv_dtype)
+    X = torch.from_numpy(detinit.frames_u8(1234, (T, B, 84, 84, 3))).to(cuda)
+    ag.reset()
+    lg, vl, _ = ag.unroll(X)
+    Gl, Gv = _cot(T, B)
+    ((lg * Gl.to(cuda)).sum() + (vl * Gv.to(cuda)).sum()).backward()
+    torch.cuda.synchronize()
+    assert_close(_grads(ag)["vision.vision_cnn.0.weight"].numpy(), ref[3]["vision.vision_cnn.0.weight"].float().numpy(),
+                 tol, "uint8 frames conv1 grad", envelope=ref[4]["vision.vision_cnn.0.weight"].numpy() if len(ref) > 4 else None)
+
+
+def test_frames_modified_in_place_before_backward_raise(cuda):
+    """The backward reads the frames again (conv1's weight gradient): an
+    in-place change between forward and backward raises, as autograd does for
+    a saved tensor."""
+    ag = _agent(cuda)
+    X = _frames(2, 1).to(cuda)
+    ag.reset()
+    lg, _, _ = ag.unroll(X)
+    X.add_(1.0)
+    with pytest.raises(RuntimeError, match="inplace"):
+        lg.sum().backward()
+
+
 def test_repeat_is_deterministic_enough(cuda):
     """Two identical runs agree (atomics may reorder fp32 sums: ~1e-6)."""
     a = _run_unroll(_agent(cuda), 3, 4, cuda)

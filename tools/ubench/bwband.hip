@@ -145,8 +145,12 @@ static void phases_fwd(int nblk, int B, int T, int G, bool band) {
 }
 #endif
 
-// the bf16 frame-resident forward (recur.h): G = 1, G = 2 (paired) or band mode
-static void bench_fwd(int B, int T, int h, int w, int G, bool band) {
+// the bf16 frame-resident forward (recur.h): G = 1, G = 2 (paired) or band mode;
+// ABL ablations (timing only): 1 no A loads, 2 no epilogue HBM stores, 4 no MFMAs,
+// 8 no B fragment reads; cqm = the slice layout mask, hs = keep the fp32 h copy
+template <int ABL = 0>
+static void bench_fwd(int B, int T, int h, int w, int G, bool band, int cqm = 3, bool hs = false,
+                      const char* what = "production") {
   const int P = h * w;
   const size_t M = (size_t)B * P;
   RecFwdParams<_Float16> p{};
@@ -154,7 +158,8 @@ static void bench_fwd(int B, int T, int h, int w, int G, bool band) {
   p.bias = dev_rand<float>(512, 0.1f, 12);
   p.XH = dev_rand<__bf16>((size_t)(T + 1) * M * 192, 1.f, 13);
   p.Cst = dev_rand<float>((size_t)(T + 1) * M * 128, 1.f, 14);
-  p.Hs = dev_rand<float>((size_t)T * M * 128, 1.f, 15);
+  p.Hs = hs ? dev_rand<float>((size_t)T * M * 128, 1.f, 15) : nullptr;
+  p.cqm = cqm;
   p.Gt = dev_rand<_Float16>((size_t)T * M * 512, 1.f, 16);
   CK(hipMalloc(&p.flags, (size_t)B * kRecBands * 4));
   int* hrep = nullptr;
@@ -168,9 +173,9 @@ static void bench_fwd(int B, int T, int h, int w, int G, bool band) {
     p.colhb[c] = (short)((pp / w) * (w + 2) + pp % w);
   }
   const int grid = band ? 8 * kRecBands * ((B + 7) / 8) : G * B;
-  const void* k = band ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 1, 0, true>)
-                  : G == 2 ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 2, 0>)
-                           : reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 1, 0>);
+  const void* k = band ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 1, ABL, true>)
+                  : G == 2 ? reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 2, ABL>)
+                           : reinterpret_cast<const void*>(&k_convlstm_fwd_frames<_Float16, 1, ABL>);
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   double best = 1e30;
@@ -183,10 +188,10 @@ static void bench_fwd(int B, int T, int h, int w, int G, bool band) {
     float ms; CK(hipEventElapsedTime(&ms, a, b));
     if (r >= 2) best = std::min(best, (double)ms);
   }
-  printf("forward %s G=%d: B=%d T=%d %dx%d  best %8.1f us (%.1f us/step)\n", band ? "band" : "frame", G, B, T, h, w,
-         best * 1e3, best * 1e3 / T);
+  printf("forward %s G=%d: B=%d T=%d %dx%d  %-34s best %8.1f us (%.1f us/step)\n", band ? "band" : "frame", G, B, T,
+         h, w, what, best * 1e3, best * 1e3 / T);
 #ifdef AAA_STAMPS
-  phases_fwd(grid, B, T, G, band);
+  if (ABL == 0) phases_fwd(grid, B, T, G, band);
 #endif
   printf("timeout reports: %d\n", *hrep);
 }
@@ -197,6 +202,18 @@ int main(int argc, char** argv) {
   if (which == 0 || which == 3) bench(256, 20, 11, 11, false);
   if (which == 0 || which == 5) bench_fwd(64, 50, 21, 21, 1, true);
   if (which == 0 || which == 3) bench_fwd(256, 20, 11, 11, 1, false);
+  if (which == 6) {   // forward ablations at C3's shape
+    bench_fwd(256, 20, 11, 11, 1, false, 0, false, "row-major slices");
+    bench_fwd(256, 20, 11, 11, 1, false, 3, false, "quad-major c + gates");
+    bench_fwd(256, 20, 11, 11, 1, false, 3, true, "quad-major, fp32 h copy");
+    bench_fwd<2>(256, 20, 11, 11, 1, false, 3, false, "no epilogue HBM stores");
+    bench_fwd<1>(256, 20, 11, 11, 1, false, 3, false, "no A loads");
+    bench_fwd<4>(256, 20, 11, 11, 1, false, 3, false, "no MFMAs");
+    bench_fwd<8>(256, 20, 11, 11, 1, false, 3, false, "no B fragment reads");
+    bench_fwd(64, 50, 21, 21, 1, true, 0, false, "band row-major slices");
+    bench_fwd(64, 50, 21, 21, 1, true, 3, false, "band quad-major");
+    bench_fwd<2>(64, 50, 21, 21, 1, true, 3, false, "band no epilogue HBM stores");
+  }
   if (which == 0 || which == 4) bench_fwd(128, 20, 11, 11, 2, false);
   return 0;
 }

@@ -313,6 +313,7 @@ class _UnrollFn(torch.autograd.Function):
         logits, values, attn, hT, cT = out[:5]
         chT, ccT = out[5:] if runner.stateful_core else (None, None)
         ctx.runner, ctx.flat, ctx.packed, ctx.ws, ctx.S, ctx.X = runner, flat, packed, ws, S, X
+        ctx.Xv = X._version   # the backward rebuilds conv1's operand from these frames
         ctx.shapes = [p.shape for p in params]
         ctx.mark_non_differentiable(attn)
         return logits, values, attn, hT, cT, chT, ccT
@@ -320,6 +321,10 @@ class _UnrollFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dl, dv, _dattn, dhT, dcT, dchT=None, dccT=None):
         r = ctx.runner
+        if ctx.X._version != ctx.Xv:
+            raise RuntimeError("aaa: the frames of this unroll were modified by an inplace operation after the "
+                               "forward; the backward reads them again (conv1's weight gradient), as autograd "
+                               "would need them unchanged")
         want_state = bool(ctx.needs_input_grad[7] or ctx.needs_input_grad[8])
         if r.stateful_core:
             want_core = bool(ctx.needs_input_grad[9] or ctx.needs_input_grad[10])

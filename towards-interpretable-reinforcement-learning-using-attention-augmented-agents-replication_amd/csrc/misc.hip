@@ -282,9 +282,6 @@ k_attn_fwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
   }
 }
 
-constexpr int kAttnChunk = 32;   // positions per staged V chunk (attention backward)
-constexpr int kVld = 188;        // its row pitch in floats (184 + 4: 16-B aligned rows, spread banks)
-
 #ifdef AAA_STAMPS
 // Diagnostic builds only (tools/ubench/attn_stamps): per-workgroup phase stamps (s_memrealtime, 100 MHz).
 __device__ uint64_t aaa_attn_stamps[16384 * 8];
@@ -299,13 +296,33 @@ __device__ uint64_t aaa_attn_stamps[16384 * 8];
 // Backward of the readout / softmax / logits for one frame: from da (the
 // answer-gradient's readout part) to dO (grad of the ConvLSTM output h_t) and
 // this frame's dQ (logits path, plus the answer row's Q columns when addq).
+//
+// Latency-bound per frame (a few hundred KB of traffic), so every phase keeps
+// all 512 threads busy and issues its global loads up front:
+//  1. dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S]: 8 lanes per
+//     position, each streaming 16-B pieces of the V row straight from memory
+//     (no LDS staging, no barrier in the loop) against da from LDS; the 8
+//     partials meet in a 3-step transpose reduction (lane j ends with q = j).
+//     The same lanes park the position's key channels O[:8] in LDS (Kc).
+//  2. softmax backward: dlogit = A (dA - sum_p A dA).
+//  3. dO (16 B per thread): each thread's channel quad fixed, its NQ
+//     coefficients (da columns, or Q for the key channels) in registers, per
+//     position only the NQ weights (A or dlogit) read from LDS; row-major
+//     rows, or channel-quad-major slices (cqm, recur.h cqm4) in 1-KB runs.
+//  4. dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] (Kc) | S], G position
+//     groups reduced through LDS.
+// Pieces of a V row: O = 30 fp32 quads or 15 bf16 octets (one padding piece
+// pads them to a multiple of 8 lanes), then S = 16 fp32 quads.
 template <int NQ, typename TO>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))   // two frames per CU
 k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
            float* __restrict__ dO, float* __restrict__ dQp, int cqm) {
   constexpr int NT = 512, NW = NT / 64;
   constexpr int G = 7;             // position groups of the dQ reduction (7*72 <= NT)
+  constexpr bool BF = !std::is_same<TO, float>::value;
+  constexpr int NOP = BF ? 15 : 30, NOPP = BF ? 16 : 32;   // O pieces, padded to 8 lanes
+  constexpr int NK = (NOPP + 16) / 8, NKO = NOPP / 8;      // pieces per lane: all, O
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* A = sm;                 // P*NQ
   float* dA = A + P * NQ;        // P*NQ  (becomes dlogits)
@@ -313,87 +330,115 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
   float* Qs = da + NQ * 184;     // NQ*72
   float* ss = Qs + NQ * 72;      // NQ (padded to 8)
   float* red = ss + 8;           // G*NQ*72
-  float* Vc = red + G * NQ * 72; // kAttnChunk * kVld
+  float* Kc = red + G * NQ * 72; // P*8  key channels O[:8] as fp32
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr bool BF = !std::is_same<TO, float>::value;
   const TO* O = Hs + (size_t)f * P * old;
   AAA_AT_STAMP(0);
-  // V chunk pieces of this thread (consecutive threads along a row), loaded
-  // into registers one chunk AHEAD of its LDS staging: chunk c+1's loads are
-  // in flight while chunk c's dot products run (the barriers below drain only
-  // the LDS counter), so the frame's V rows stream in behind the compute
-  // instead of one exposed load latency per chunk.  fp32 O: 46 pieces of 16 B
-  // per position; bf16 O: 30 O pieces of 8 B (4 channels) and 16 S pieces of 16 B.
-  constexpr int VPT = BF ? (kAttnChunk * 30 + NT - 1) / NT : (kAttnChunk * 46 + NT - 1) / NT;
-  using VR = typename std::conditional<BF, u32x2, f32x4>::type;
-  VR vr[VPT];
-  f32x4 vs;   // bf16 O: this thread's S piece
-  static_assert(!BF || kAttnChunk * 16 <= NT, "one S piece per thread");
-  auto vload = [&](int p0) {
-    const int np = min(kAttnChunk, P - p0);
-    // one unconditional load from a selected address per piece (a load per
-    // branch would serialise them on the shared destination registers, and
-    // a select on the loaded value would wait for it right here); pieces
-    // past the chunk load a valid dummy the staging skips
-    if constexpr (BF) {
+  const int part = tid & 7, pl = tid >> 3;   // phase 1: 64 positions per pass, 8 lanes each
+  // the V pieces and key piece of position p: unconditional loads from valid
+  // (clamped) addresses; a padding piece is zeroed at its use
+  auto vload = [&](int p, u32x4 (&raw)[NK], u32x4& kraw) {
 #pragma unroll
-      for (int j = 0; j < VPT; ++j) {
-        const int i = tid + j * NT, pp = i / 30, g = i - pp * 30;
-        const TO* src = i < np * 30 ? O + (size_t)(p0 + pp) * old + 8 + 4 * g : O;
-        vr[j] = *reinterpret_cast<const u32x2*>(src);
-      }
-      const float* ss = tid < np * 16 ? S + (p0 + (tid >> 4)) * 64 + 4 * (tid & 15) : S;
-      vs = *reinterpret_cast<const f32x4*>(ss);
-    } else {
-#pragma unroll
-      for (int j = 0; j < VPT; ++j) {
-        const int i = tid + j * NT, pp = i / 46, g = i - pp * 46, p = p0 + pp;
-        const float* src = i >= np * 46 ? S : (g < 30 ? O + (size_t)p * old + 8 + 4 * g : S + p * 64 + 4 * (g - 30));
-        vr[j] = *reinterpret_cast<const f32x4*>(src);
-      }
+    for (int k = 0; k < NK; ++k) {
+      const int j = part + 8 * k;
+      const void* src;
+      if (k < NKO) src = O + (size_t)p * old + 8 + min(j, NOP - 1) * (BF ? 8 : 4);
+      else src = S + p * 64 + 4 * (j - NOPP);
+      raw[k] = *reinterpret_cast<const u32x4*>(src);
     }
+    kraw = *reinterpret_cast<const u32x4*>(O + (size_t)p * old + (BF ? 0 : 4 * (part & 1)));
   };
-  vload(0);
+  u32x4 raw[NK], kraw;
+  vload(min(pl, P - 1), raw, kraw);
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
   for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
+  __syncthreads();
   AAA_AT_STAMP(1);
-  // dA[p][q] = sum_c da[q][c] V[p][c], V = [O[8:128] | S], in chunks of
-  // kAttnChunk positions staged in LDS, then thread (p, q) takes its dot
-  // product from LDS (no cross-lane reductions).
-  for (int p0 = 0; p0 < P; p0 += kAttnChunk) {
-    const int np = min(kAttnChunk, P - p0);
-    if constexpr (BF) {
+  for (int p0 = 0; p0 < P; p0 += 64) {
+    const int p = p0 + pl;
+    // da's LDS reads stay inside the pass: hoisted out of the loop they would
+    // hold NQ x 184 / 8 floats per lane in registers (spills)
+    int opq = 0;
+    asm volatile("" : "+v"(opq));
+    const float* dap = da + opq;
+    float acc[NQ];
 #pragma unroll
-      for (int j = 0; j < VPT; ++j) {
-        const int i = tid + j * NT, pp = i / 30, g = i - pp * 30;
-        if (i < np * 30) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = bf4_f32(vr[j]);
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int j = part + 8 * k;
+      if (k < NKO && BF) {   // 8 bf16 channels of O
+        const float m = j < NOP ? 1.f : 0.f;
+        const f32x4 v0 = bf4_f32(u32x2{raw[k].x, raw[k].y}) * m, v1 = bf4_f32(u32x2{raw[k].z, raw[k].w}) * m;
+        const int c0 = 8 * min(j, NOP - 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const f32x4 d0 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
+          const f32x4 d1 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0 + 4);
+          acc[q] += v0[0] * d0[0] + v0[1] * d0[1] + v0[2] * d0[2] + v0[3] * d0[3] +
+                    v1[0] * d1[0] + v1[1] * d1[1] + v1[2] * d1[2] + v1[3] * d1[3];
+        }
+      } else {               // 4 fp32 channels (O quads of the fp32 path, or S)
+        const float m = k < NKO ? (j < NOP ? 1.f : 0.f) : 1.f;
+        const f32x4 v = __builtin_bit_cast(f32x4, raw[k]) * m;
+        const int c0 = k < NKO ? 4 * min(j, NOP - 1) : 120 + 4 * (j - NOPP);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const f32x4 d = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
+          acc[q] += v[0] * d[0] + v[1] * d[1] + v[2] * d[2] + v[3] * d[3];
+        }
       }
-      if (tid < np * 16) *reinterpret_cast<f32x4*>(Vc + (tid >> 4) * kVld + 120 + 4 * (tid & 15)) = vs;
+      // one piece's da reads at a time: the next piece's addresses depend on
+      // this piece's sums (scheduled all up front the reads need NK * NQ * 4
+      // registers and spill)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[q]));
+      asm volatile("" : "+v"(opq));
+      dap = da + opq;
+    }
+    const u32x4 kr = kraw;
+    if (p0 + 64 < P) vload(min(p + 64, P - 1), raw, kraw);   // the next pass's pieces in flight
+    // 3-step transpose reduction over the 8 lanes of the position: lane part
+    // ends with the total of q = part (NQ = 8) or part & 3 (NQ = 4)
+    float v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) v[q] = acc[q];
+    if constexpr (NQ == 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], 4, 64);
     } else {
 #pragma unroll
-      for (int j = 0; j < VPT; ++j) {
-        const int i = tid + j * NT, pp = i / 46, g = i - pp * 46;
-        if (i < np * 46) *reinterpret_cast<f32x4*>(Vc + pp * kVld + 4 * g) = vr[j];
+      for (int i = 0; i < 4; ++i) {
+        const bool up = part & 4;
+        const float keep = up ? v[i + 4] : v[i], send = up ? v[i] : v[i + 4];
+        v[i] = keep + __shfl_xor(send, 4, 64);
       }
     }
-    lds_barrier();
-    if (p0 + kAttnChunk < P) vload(p0 + kAttnChunk);
-    for (int i = tid; i < np * NQ; i += NT) {
-      const int pp = i / NQ, q = i - pp * NQ;
-      const f32x4* vrow = reinterpret_cast<const f32x4*>(Vc + pp * kVld);
-      const f32x4* dr = reinterpret_cast<const f32x4*>(da + q * 184);
-      float a0 = 0.f, a1 = 0.f;
-#pragma unroll 2
-      for (int g = 0; g < 46; ++g) {
-        const f32x4 v = vrow[g], d = dr[g];
-        a0 += v[0] * d[0] + v[1] * d[1];
-        a1 += v[2] * d[2] + v[3] * d[3];
-      }
-      dA[(p0 + pp) * NQ + q] = a0 + a1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool up = part & 2;
+      const float keep = up ? v[i + 2] : v[i], send = up ? v[i] : v[i + 2];
+      v[i] = keep + __shfl_xor(send, 2, 64);
     }
-    lds_barrier();
+    {
+      const bool up = part & 1;
+      const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
+      v[0] = keep + __shfl_xor(send, 1, 64);
+    }
+    if (p < P) {
+      if (part < NQ) dA[p * NQ + part] = v[0];
+      if constexpr (BF) {
+        if (part == 0) {
+          *reinterpret_cast<f32x4*>(Kc + p * 8) = bf4_f32(u32x2{kr.x, kr.y});
+          *reinterpret_cast<f32x4*>(Kc + p * 8 + 4) = bf4_f32(u32x2{kr.z, kr.w});
+        }
+      } else {
+        if (part < 2) *reinterpret_cast<u32x4*>(Kc + p * 8 + 4 * part) = kr;
+      }
+    }
   }
+  __syncthreads();
   AAA_AT_STAMP(2);
   // softmax backward: dlogit = A (dA - sum_p A dA)
   for (int q = wave; q < NQ; q += NW) {
@@ -409,51 +454,58 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
   }
   __syncthreads();
   AAA_AT_STAMP(3);
-  // dO: 16 B per thread, rows written by consecutive threads (row-major) or
-  // each channel quad's pixels by consecutive threads (cqm: recur.h cqm4)
+  // dO[p][c4..c4+3] = sum_q w[p][q] coef[q][0..3]: key channels (c4 < 8) w =
+  // dlogit, coef = Q[q][c4..]; the rest w = A, coef = da[q][c4-8..]
   float* dOf = dO + (size_t)f * P * 128;
-  for (int i = tid; i < P * 32; i += NT) {
-    const int p = cqm ? i % P : i >> 5, c4 = cqm ? (i / P) * 4 : (i & 31) * 4;
+  auto dO_pos = [&](int p, const f32x4 (&coef)[NQ], const float* W) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (c4 < 8) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const float d = dA[p * NQ + q];
-        const float* qq = Qs + q * 72 + c4;
-        acc[0] += d * qq[0]; acc[1] += d * qq[1]; acc[2] += d * qq[2]; acc[3] += d * qq[3];
-      }
-    } else {
+    for (int j = 0; j < NQ / 4; ++j) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(W + p * NQ + 4 * j);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const float a = A[p * NQ + q];
-        const float* dd = da + q * 184 + c4 - 8;
-        acc[0] += a * dd[0]; acc[1] += a * dd[1]; acc[2] += a * dd[2]; acc[3] += a * dd[3];
-      }
+      for (int i = 0; i < 4; ++i) acc += w[i] * coef[4 * j + i];
     }
-    *reinterpret_cast<f32x4*>(dOf + (cqm ? i * 4 : p * 128 + c4)) = acc;
+    return acc;
+  };
+  if (cqm) {   // quad-major: a wave per channel quad, lanes along the positions (1-KB stores)
+    for (int qd = wave; qd < 32; qd += NW) {
+      const int c4 = qd * 4;
+      f32x4 coef[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        coef[q] = *reinterpret_cast<const f32x4*>(c4 < 8 ? Qs + q * 72 + c4 : da + q * 184 + c4 - 8);
+      const float* W = c4 < 8 ? dA : A;
+      for (int p = lane; p < P; p += 64)
+        *reinterpret_cast<f32x4*>(dOf + ((size_t)qd * P + p) * 4) = dO_pos(p, coef, W);
+    }
+  } else {     // row-major: lanes along a row's 32 quads, 16 positions per pass (512-B stores)
+    const int qd = lane & 31, c4 = qd * 4;
+    f32x4 coef[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {   // both candidates read, then selected (no divergent branch)
+      const f32x4 cq = *reinterpret_cast<const f32x4*>(Qs + q * 72 + min(c4, 4));
+      const f32x4 cd = *reinterpret_cast<const f32x4*>(da + q * 184 + max(c4 - 8, 0));
+      coef[q] = c4 < 8 ? cq : cd;
+    }
+    for (int p = 2 * wave + (lane >> 5); p < P; p += 2 * NW) {
+      const f32x4 a = dO_pos(p, coef, A), d = dO_pos(p, coef, dA);
+      *reinterpret_cast<f32x4*>(dOf + (size_t)p * 128 + c4) = c4 < 8 ? d : a;
+    }
   }
   AAA_AT_STAMP(4);
-  // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] | S]: G position groups,
-  // every loaded K element feeds all NQ heads, partials reduced through LDS.
+  // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] (Kc) | S]: G position
+  // groups, every K element feeding all NQ heads, partials reduced through LDS
   if (tid < G * 72) {
     const int g = tid / 72, c = tid - g * 72;
     float acc[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
-    // K = [O[:8] | S] column c: one strided address stream per thread, loads
-    // unrolled so several are in flight (not one latency per position)
-    // (bf16 O: the dword holding channels c & ~1 and c | 1, its half picked)
-    const uint32_t* kp = c < 8 ? reinterpret_cast<const uint32_t*>(O + (BF ? (c & ~1) : c))
-                               : reinterpret_cast<const uint32_t*>(S + c - 8);
-    const int kld = c < 8 ? (BF ? old / 2 : old) : 64;   // in dwords
-    // the element as fp32 bits by a per-lane shift and mask (a select here
-    // compiles to a branch whose join waits for each load in turn)
-    const bool half = BF && c < 8;
-    const uint32_t ksh = half && !(c & 1) ? 16u : 0u, kmask = half ? 0xffff0000u : 0xffffffffu;
+    const float* ks = S + max(c - 8, 0);
+    const float* kc = Kc + min(c, 7);
 #pragma unroll 8
     for (int p = g; p < P; p += G) {
-      const uint32_t ku = kp[(size_t)p * kld];
-      const float k = __uint_as_float((ku << ksh) & kmask);
+      const float kS = ks[p * 64], kO = kc[p * 8];   // both read, then selected
+      const float k = c < 8 ? kO : kS;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] += dA[p * NQ + q] * k;
     }
@@ -1014,7 +1066,7 @@ hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, con
                     int da_ld, int F, int P, int nq, float* dO, float* dQp, hipStream_t st, int qs, int addq,
                     int cqm) {
   const int G = 7;   // k_attn_bwd's dQ position groups
-  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72 + kAttnChunk * kVld) * sizeof(float);
+  const size_t sh = (size_t)(2 * P * nq + nq * 184 + nq * 72 + 8 + G * nq * 72 + P * 8) * sizeof(float);
   if (sh > 160 * 1024) return hipErrorInvalidValue;
   if (O.bf16 ? (O.ld < 136 || O.ld % 4) : O.ld < 128 || O.ld % 4) return hipErrorInvalidValue;
   auto launch = [&](auto kern, auto* o) {

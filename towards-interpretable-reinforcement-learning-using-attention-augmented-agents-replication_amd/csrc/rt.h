@@ -62,6 +62,7 @@ struct Layout {
   int sc;   // stateful policy core (AAA_FLAG_STATEFUL_CORE)
   int fu8;  // frames are uint8 (AAA_FLAG_FRAMES_U8)
   int fchunk;   // frames per launch of the whole-batch conv GEMMs (< 2 GiB per descriptor, check_ranges)
+  int xpc;      // frames of the Xp chunk buffer (conv1's bordered RGBx operand, rebuilt per chunk)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
@@ -463,13 +464,13 @@ int rec_stagger(const char* env);   // start offset of half the frames, 100-MHz 
 template <typename T> int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st);
 template <typename T, typename OT>
 int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1, OT* out,
-               int out_ld, hipStream_t st);
+               int out_ld, hipStream_t st, bool xp_full = true);
 template <typename T> int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st);
 template <typename T>
 int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipStream_t s, bool aux);
 template <typename T>
-int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, const T* xp, T* dy1, int F, float* gW2,
-               float* gW1, float* gb1, hipStream_t s);
+int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, T* xp, T* dy1, int F, float* gW2,
+               float* gW1, float* gb1, hipStream_t s, const void* frames = nullptr);
 template <typename T> int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st);
 
 }  // namespace aaa

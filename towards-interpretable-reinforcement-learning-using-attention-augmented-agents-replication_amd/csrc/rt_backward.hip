@@ -287,19 +287,43 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
   return AAA_OK;
 }
 
+// conv1 weight gradient over n frames whose bordered RGBx image (Xp) is
+// rebuilt from the observation in chunks of L.xpc frames into the chunk
+// buffer xpbuf: the forward keeps no Xp, and each chunk is written and read
+// back while it sits in the memory-side cache (256 MB) instead of all F
+// frames' images round-tripping through HBM between the two passes.
+template <typename T>
+static int conv1_wgrad_frames(const Layout& L, const T* dy1, const void* frames, int n, T* xpbuf, float* gW,
+                              hipStream_t s) {
+  const size_t fb = (size_t)L.H * L.W * 3 * (L.fu8 ? 1 : 4);
+  for (int s0 = 0; s0 < n; s0 += L.xpc) {
+    const int m = std::min(L.xpc, n - s0);
+    const char* fr = (const char*)frames + (size_t)s0 * fb;
+    if (L.fu8) HIPCHK((frames_rgbx<T, uint8_t>(m, L.H, L.W, (const uint8_t*)fr, xpbuf, s)));
+    else HIPCHK((frames_rgbx<T, float>(m, L.H, L.W, (const float*)fr, xpbuf, s)));
+    const int rc = conv1_wgrad<T>(L, dy1 + (size_t)s0 * L.P1 * 32, xpbuf, m, gW, s);
+    if (rc) return rc;
+  }
+  return AAA_OK;
+}
+
 // Vision encoder backward over F frames in descriptor-sized chunks: conv2
 // weight grad (gW2 +=), conv2 dgrad -> dY1 with conv1's bias grad (gb1 +=),
-// conv1 weight grad (gW1 +=); accumulators zeroed by the caller.
+// conv1 weight grad (gW1 +=); accumulators zeroed by the caller.  frames:
+// xp is the L.xpc-frame chunk buffer rebuilt from them (conv1_wgrad_frames);
+// null: xp holds all F frames' images (the component entries).
 template <typename T>
-int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, const T* xp, T* dy1, int F,
-                      float* gW2, float* gW1, float* gb1, hipStream_t s) {
+int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, T* xp, T* dy1, int F,
+                      float* gW2, float* gW1, float* gb1, hipStream_t s, const void* frames) {
+  const size_t fb = (size_t)L.H * L.W * 3 * (L.fu8 ? 1 : 4);
   for (int f0 = 0; f0 < F; f0 += L.fchunk) {
     const int n = std::min(L.fchunk, F - f0);
     const T* d2 = dy2 + (size_t)f0 * L.P * 64;
     T* d1 = dy1 + (size_t)f0 * L.P1 * 32;
     int rc = conv2_wgrad<T>(L, d2, y1 + (size_t)f0 * L.P1 * 32, n, gW2, s);
     if (!rc) rc = conv2_dgrad<T>(L, pk, d2, d1, n, gb1, s);
-    if (!rc) rc = conv1_wgrad<T>(L, d1, xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, n, gW1, s);
+    if (!rc && frames) rc = conv1_wgrad_frames<T>(L, d1, (const char*)frames + (size_t)f0 * fb, n, xp, gW1, s);
+    else if (!rc) rc = conv1_wgrad<T>(L, d1, xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, n, gW1, s);
     if (rc) return rc;
   }
   return AAA_OK;
@@ -596,7 +620,9 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
       int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
-      if (!rc) rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
+      if (!rc)
+        rc = conv1_wgrad_frames<T>(L, dy1, (const char*)io->frames + (size_t)lo * L.B * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
+                                   F1, Wt(L.Xp), Wf(L.gWp1), s);
       if (rc) return rc;
       if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
@@ -828,7 +854,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       constexpr bool f32 = std::is_same<T, float>::value;
       {
         const int rc = vision_bwd<T>(L, pk, Wt(L.dY2), Wt(L.Y1), Wt(L.Xp), Wt(L.dY1), F, Wf(L.gWp2), Wf(L.gWp1),
-                                     grads + L.poff[C0B], st);
+                                     grads + L.poff[C0B], st, io->frames);
         if (rc) return rc;
         if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
@@ -842,10 +868,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
 
 template int lstm_wgrad<float>(const float*, const float*, int, int, int, float*, hipStream_t, bool);
 template int lstm_wgrad<__bf16>(const __bf16*, const __bf16*, int, int, int, float*, hipStream_t, bool);
-template int vision_bwd<float>(const Layout&, const char*, const float*, const float*, const float*, float*, int,
-                               float*, float*, float*, hipStream_t);
-template int vision_bwd<__bf16>(const Layout&, const char*, const __bf16*, const __bf16*, const __bf16*, __bf16*, int,
-                                float*, float*, float*, hipStream_t);
+template int vision_bwd<float>(const Layout&, const char*, const float*, const float*, float*, float*, int,
+                               float*, float*, float*, hipStream_t, const void*);
+template int vision_bwd<__bf16>(const Layout&, const char*, const __bf16*, const __bf16*, __bf16*, __bf16*, int,
+                                float*, float*, float*, hipStream_t, const void*);
 template int backward_impl<float>(const Layout&, const aaa_io*, int, hipStream_t);
 template int backward_impl<__bf16>(const Layout&, const aaa_io*, int, hipStream_t);
 

@@ -183,7 +183,7 @@ static int cnn_bwd_impl(const CnnLayout& CL, const char* pk, const float* dy2, f
   HIPCHK(hipMemsetAsync(gW1, 0, 32 * 256 * 4, st));
   HIPCHK(hipMemsetAsync(gW2, 0, 64 * 512 * 4, st));
   HIPCHK(colsum<float>(dy2, 64, N * L.P, 64, grads + L.poff[C1B], st));   // conv2 bias (fp32 grads)
-  const int rc = vision_bwd<T>(L, pk, dy2t, (const T*)(ws + CL.Y1), (const T*)(ws + CL.Xp), dY1, N, gW2, gW1,
+  const int rc = vision_bwd<T>(L, pk, dy2t, (const T*)(ws + CL.Y1), (T*)(ws + CL.Xp), dY1, N, gW2, gW1,
                                grads + L.poff[C0B], st);
   if (rc) return rc;
   if (std::is_same<T, float>::value && !env_int("AAA_CONV2_DGRAD_RING", 1))

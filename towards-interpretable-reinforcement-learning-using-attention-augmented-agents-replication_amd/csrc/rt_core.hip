@@ -79,7 +79,11 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   // workspace
   p = 0;
   const size_t F = L.F, P = L.P, M = (size_t)L.B * L.P;
-  L.Xp = take(F * (L.H + 2) * (L.W + 2) * 4 * e);  // frames as zero-bordered RGBx (conv1 operand type)
+  // frames as zero-bordered RGBx (conv1's operand type), a chunk of xpc frames at a time: rebuilt from the
+  // observation where conv1 (forward, layered path) or its weight gradient (backward) reads it, so it is
+  // written and read while it sits in the memory-side cache instead of round-tripping all F frames via HBM
+  L.xpc = (int)std::min<size_t>(F, (size_t)std::max(64, env_int("AAA_XP_CHUNK", 512)));
+  L.Xp = take((size_t)L.xpc * (L.H + 2) * (L.W + 2) * 4 * e);
   L.Y1 = take(F * L.P1 * 32 * e);
   L.XH = take((size_t)(L.T + 1) * M * 192 * e);
   L.Hs = take(e == 4 ? F * P * 128 * 4 : 0);   // fp32 h_t for the readout (bf16: it reads XH, readout_h)

@@ -50,39 +50,49 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
 // from the flat params (state_dict order: the vision tensors come first).
 template <typename T, typename OT>
 static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1,
-                      OT* out, int out_ld, hipStream_t st) {
+                      OT* out, int out_ld, hipStream_t st, bool xp_full) {
   using C = CfgFor<T>;
   constexpr int NT = C::NT;
   const int P = L.P;
   bool banded = false;   // bf16 frames too large for the frame-resident encoder: the banded conv1 (vision.h)
   if constexpr (std::is_same<T, __bf16>::value) {
     if (band_fits(L.H, L.W, L.H1, L.W1) && env_int("AAA_VIS_BAND", 1)) {
-      const VisBandParams bp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], Xp, Y1, F, L.H, L.W, L.H1, L.W1};
+      const VisBandParams bp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], xp_full ? Xp : nullptr, Y1, F,
+                             L.H, L.W, L.H1, L.W1};
       HIPCHK(L.fu8 ? vision_conv1_band<uint8_t>(bp, st) : vision_conv1_band<float>(bp, st));
       banded = true;
     }
   }
   if (!banded) {  // conv1 (attention.py:156-162): frames -> zero-bordered RGBx (Cin 4, pad 1 stored) -> Y1
-    if (L.fu8) HIPCHK((frames_rgbx<T, uint8_t>(F, L.H, L.W, (const uint8_t*)frames, Xp, st)));
-    else HIPCHK((frames_rgbx<T, float>(F, L.H, L.W, (const float*)frames, Xp, st)));
-    // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
-    constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
-    EpiStoreT<T> ep{Y1, 32, 32, F * L.P1, prm + L.poff[C0B], 0};
-    auto conv1 = [&](auto cfg) -> int {
-      using CP = decltype(cfg);
-      using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
-      using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
-      HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
-          typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
-          typename PB::Params{Xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), F * L.P1,
-                              (uint32_t)((size_t)F * (L.H + 2) * (L.W + 2) * 4 * L.esz)},
-          ep, 32, F * L.P1, 256, 1, st)));
-      return AAA_OK;
-    };
-    // K = 256 is four BK steps: a wider column tile does more MFMA work per DMA round trip (A/B: AAA_CONV1_TILE)
-    const int c1t = env_int("AAA_CONV1_TILE", 0);
-    const int rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
-    if (rc) return rc;
+    // xp_full: Xp holds all F frames (the component entries keep it for their backward);
+    // else Xp is the chunk buffer of L.xpc frames, rebuilt per chunk right before conv1 reads it
+    const size_t fb = (size_t)L.H * L.W * 3 * (L.fu8 ? 1 : 4), xb = (size_t)(L.H + 2) * (L.W + 2) * 4;
+    const int step = xp_full ? F : L.xpc;
+    for (int s0 = 0; s0 < F; s0 += step) {
+      const int n = std::min(step, F - s0);
+      const char* fr = (const char*)frames + (size_t)s0 * fb;
+      T* xp = xp_full ? Xp + (size_t)s0 * xb : Xp;
+      if (L.fu8) HIPCHK((frames_rgbx<T, uint8_t>(n, L.H, L.W, (const uint8_t*)fr, xp, st)));
+      else HIPCHK((frames_rgbx<T, float>(n, L.H, L.W, (const float*)fr, xp, st)));
+      // LDS-DMA ring, 32x128 tile over 4 waves (tools/ubench/conv_cfg: 62 vs 90 us register-staged)
+      constexpr int BKc = std::is_same<T, float>::value ? 32 : 64;
+      EpiStoreT<T> ep{Y1 + (size_t)s0 * L.P1 * 32, 32, 32, n * L.P1, prm + L.poff[C0B], 0};
+      auto conv1 = [&](auto cfg) -> int {
+        using CP = decltype(cfg);
+        using PA = GRowsB<T, CP::BI, CP::BK, CP::NT>;
+        using PB = GIm2colB<T, CP::BJ, CP::BK, CP::NT>;
+        HIPCHK((launch_pipe<CP, PA, PB, EpiStoreT<T>, 2>(
+            typename PA::Params{(const T*)(pk + L.k_Wp1), 256, 32},
+            typename PB::Params{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), n * L.P1,
+                                (uint32_t)((size_t)n * xb * L.esz)},
+            ep, 32, n * L.P1, 256, 1, st)));
+        return AAA_OK;
+      };
+      // K = 256 is four BK steps: a wider column tile does more MFMA work per DMA round trip (A/B: AAA_CONV1_TILE)
+      const int c1t = env_int("AAA_CONV1_TILE", 0);
+      const int rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
+      if (rc) return rc;
+    }
   }
   if constexpr (std::is_same<T, __bf16>::value && std::is_same<OT, __bf16>::value) {
     // after the banded conv1: the banded conv2 (vision.h), Y1 rows staged in LDS per band
@@ -114,12 +124,12 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
 
 template <typename T, typename OT>
 int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1,
-                      OT* out, int out_ld, hipStream_t st) {
+                      OT* out, int out_ld, hipStream_t st, bool xp_full) {
   if constexpr (std::is_same<T, __bf16>::value && std::is_same<OT, __bf16>::value) {
     // bf16: the frame-resident encoder (vision.h), one launch; AAA_VIS_FRAMES=0 -> the layered kernels
     if (vis_fits(L.H, L.W, L.H1, L.W1, L.h, L.w) && env_int("AAA_VIS_FRAMES", 1)) {
       VisFwdParams vp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], (const __bf16*)(pk + L.k_Wp2),
-                      prm + L.poff[C1B], Xp, Y1, out, out_ld, F, L.H, L.W, L.H1, L.W1, L.h, L.w};
+                      prm + L.poff[C1B], xp_full ? Xp : nullptr, Y1, out, out_ld, F, L.H, L.W, L.H1, L.W1, L.h, L.w};
       HIPCHK(L.fu8 ? vision_fwd_frames<uint8_t>(vp, device_cus(), st) : vision_fwd_frames<float>(vp, device_cus(), st));
       return AAA_OK;
     }
@@ -128,8 +138,9 @@ int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const v
     const int n = std::min(L.fchunk, F - f0);
     const int rc = vision_fwd_chunk<T, OT>(L, n, pk, prm,
                                            (const char*)frames + (size_t)f0 * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
-                                           Xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4, Y1 + (size_t)f0 * L.P1 * 32,
-                                           out + (size_t)f0 * L.P * out_ld, out_ld, st);
+                                           xp_full ? Xp + (size_t)f0 * (L.H + 2) * (L.W + 2) * 4 : Xp,
+                                           Y1 + (size_t)f0 * L.P1 * 32, out + (size_t)f0 * L.P * out_ld, out_ld, st,
+                                           xp_full);
     if (rc) return rc;
   }
   return AAA_OK;
@@ -154,7 +165,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
 
   {  // conv1 + conv2 over all T*B frames -> XH[:, :, 0:64] of every slot
     TimerScope tim(AAA_TIMER_VISION_FWD, st, (double)F * vision_fwd_flop(L), "conv1 + conv2 (vision encoder)");
-    const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st);
+    const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st, false);
     if (rc) return rc;
   }
   {  // initial state (reset(): zeros, attention.py:142-149) or carried state
@@ -489,11 +500,11 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
 template int pack_impl<float>(const Layout&, const float*, char*, hipStream_t);
 template int pack_impl<__bf16>(const Layout&, const float*, char*, hipStream_t);
 template int vision_fwd<float, float>(const Layout&, int, const char*, const float*, const void*, float*, float*,
-                                      float*, int, hipStream_t);
+                                      float*, int, hipStream_t, bool);
 template int vision_fwd<__bf16, __bf16>(const Layout&, int, const char*, const float*, const void*, __bf16*, __bf16*,
-                                        __bf16*, int, hipStream_t);
+                                        __bf16*, int, hipStream_t, bool);
 template int vision_fwd<__bf16, float>(const Layout&, int, const char*, const float*, const void*, __bf16*, __bf16*,
-                                       float*, int, hipStream_t);
+                                       float*, int, hipStream_t, bool);
 template int forward_impl<float>(const Layout&, const aaa_io*, hipStream_t);
 template int forward_impl<__bf16>(const Layout&, const aaa_io*, hipStream_t);
 

@@ -255,7 +255,7 @@ struct VisBandParams {
   const void* frames;   // (F, H, W, 3) uint8 or fp32
   const __bf16* Wc1;    // packed conv1 [32][256]
   const float* b1;      // [32]
-  __bf16* Xp;           // (F, H+2, W+2, 4) <- bordered RGBx rows 0 .. 4*H1+3
+  __bf16* Xp;           // (F, H+2, W+2, 4) <- bordered RGBx rows 0 .. 4*H1+3, or null
   __bf16* Y1;           // (F, H1*W1, 32) <- conv1 output
   int F, H, W, H1, W1;
 };
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256) k_vision_conv1_band(VisBandParams p) {
     }
   }
   __syncthreads();
-  {  // the rows this band owns into Xp (16 B = 2 pixels per store)
+  if (p.Xp) {  // the rows this band owns into Xp (16 B = 2 pixels per store)
     const int rows = 4 * ny + (y0 + ny == p.H1 ? 4 : 0);
     u32x4* xo = reinterpret_cast<u32x4*>(p.Xp + ((size_t)f * (p.H + 2) + r0) * Wp * 4);
     const int n = rows * Wp / 2;
