@@ -476,6 +476,26 @@ def test_c5_full_size_bf16_vs_emulated_oracle(cuda):
             assert e <= 2e-2, f"C5 bf16 /255 grad {n}: {e:.3e}"
 
 
+def test_f32_split6_accuracy(cuda, monkeypatch):
+    """The fp32 path's ConvLSTM weight gradient and batched dx on the bf16 MFMA
+    with three-way split operands (gemm.h SPLIT6, AAA_F32_SPLIT6=1) are as
+    accurate as on the fp32 MFMA: against the exact (fp64) evaluation of the
+    reference op sequence, every gradient's error stays within 2x (+1e-7) of
+    the fp32-MFMA run's, and both within the 1e-4 criterion."""
+    T, B = 20, 8
+    torch.set_num_threads(16)
+    ref = _oracle(T, B, dtype=torch.float64)
+    errs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("AAA_F32_SPLIT6", mode)
+        out = _run_unroll(_agent(cuda), T, B, cuda)
+        _compare(out, ref, RTOL, f"split6={mode}: ")
+        errs[mode] = {n: rel_err(out[3][n].numpy().astype(np.float64), ref[3][n].numpy())
+                      for n in ref[3] if float(ref[3][n].norm()) > 0}
+    worse = {n: (errs["1"][n], errs["0"][n]) for n in errs["0"] if errs["1"][n] > 2 * errs["0"][n] + 1e-7}
+    assert not worse, f"split6 less accurate than the fp32 MFMA (err6, err32): {worse}"
+
+
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_xp_chunks_ragged(cuda, monkeypatch, conv_dtype):
     """conv1's bordered RGBx operand is rebuilt from the frames in chunks of

@@ -399,6 +399,30 @@ template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
 struct GemmCfgS3 : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, WK_> {
   static constexpr bool SPLIT3 = true;
 };
+// fp32 operands at fp32 accuracy on the bf16 MFMA (configs with SPLIT6): x =
+// hi + mid + lo, each bf16 (8 + 8 + 8 mantissa bits cover fp32's 24), and a.b
+// accumulated as the six products with i + j <= 2 (hh, hm, mh, hl, lh, mm) --
+// the dropped ml, lm, ll are ~2^-24 of the product, the size of an fp32
+// rounding.  Six 32x32x16 bf16 MFMAs (6 x 32 cycles) per 16-k step instead of
+// eight 32x32x2 fp32 ones (8 x 64): the fp32 path's large GEMMs
+// (tests/test_gpu_parity.py test_f32_split6_accuracy: the error against the
+// fp64 evaluation stays that of the fp32 MFMA).
+template <class C, class = void> struct split6_of : std::false_type {};
+template <class C> struct split6_of<C, std::enable_if_t<C::SPLIT6>> : std::true_type {};
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
+struct GemmCfgS6 : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, WK_> {
+  static constexpr bool SPLIT3 = true, SPLIT6 = true;
+};
+__device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    hi[e] = (__bf16)x[e];
+    const float r = x[e] - (float)hi[e];
+    mid[e] = (__bf16)r;
+    lo[e] = (__bf16)(r - (float)mid[e]);
+  }
+}
+
 __device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -473,7 +497,25 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
         for (int a = 0; a < MI; ++a) frag_f32<TA>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
 #pragma unroll
         for (int b = 0; b < MJ; ++b) frag_f32<TB>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
-        if constexpr (split3_of<C>::value) {
+        if constexpr (split6_of<C>::value) {
+          // as SPLIT3 below, with a three-way split; smallest products first
+          bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
+#pragma unroll
+          for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
+#pragma unroll
+          for (int a = 0; a < MI; ++a)
+#pragma unroll
+            for (int b = 0; b < MJ; ++b) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+            }
+        } else if constexpr (split3_of<C>::value) {
           // the 8 k of a lane's fp32 fragment are the 8 k of the bf16 operand layout
           // (lane (r32, h): k 8h .. 8h+7 of the 16-k step)
           bf16x8 ah[MI], al[MI], bh[MJ], bl[MJ];

@@ -656,13 +656,32 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
         for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
 #pragma unroll
         for (int b = 0; b < MJ; ++b) frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+        if constexpr (split6_of<C>::value) {   // fp32 at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+          bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
+          for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
 #pragma unroll
           for (int a = 0; a < MI; ++a)
 #pragma unroll
-            for (int b = 0; b < MJ; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < MJ; ++b) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int a = 0; a < MI; ++a)
+#pragma unroll
+              for (int b = 0; b < MJ; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+        }
         }
         if constexpr (ILV == 1) {
           if (pf && s2 == 0) la.issue(st, kn);

@@ -459,6 +459,8 @@ inline OSrc readout_h(const Layout& L, char* ws) {
   return o_f32((const float*)(ws + L.Hs));
 }
 int rec_stagger(const char* env);   // start offset of half the frames, 100-MHz ticks
+// fp32 path: its large GEMMs on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+bool f32_split6();
 
 // ------------------------------------------------------- cross-unit paths --
 template <typename T> int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st);

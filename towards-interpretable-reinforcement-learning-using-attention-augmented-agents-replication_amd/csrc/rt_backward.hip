@@ -189,7 +189,9 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // the other weight gradients doubled the output atomics for the same time:
     // profiles/r02/ab/wgrad_split.txt)
     const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, 512 / tiles)), rows / CW::BK));
-    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("register-staged %dx%d BK%d, %d-way split-K atomics [kernel: gemm_kernel+LdIm2colTB]", CW::BI, CW::BJ, CW::BK, ns));
+    TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
+                   strf("register-staged %dx%d BK%d%s, %d-way split-K atomics [kernel: gemm_kernel+LdIm2colTB]", CW::BI,
+                        CW::BJ, CW::BK, split6_of<CW>::value ? " (fp32 as bf16x6 split products)" : "", ns));
     HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
   };
@@ -274,6 +276,11 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
         break;
       default: rc = wgrad_lstm_pipe(GemmCfg<T, 128, 128, WBK, 2, 2>{}, I2{}, I0{}); break;
     }
+    if (rc) return rc;
+  } else if (std::is_same<T, float>::value && f32_split6()) {
+    // fp32: the register-staged 128x128 tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+    using CS6 = std::conditional_t<std::is_same<T, float>::value, GemmCfgS6<128, 128, 32, 2, 2>, CfgWFor<T>>;
+    const int rc = wgrad_lstm(CS6{});
     if (rc) return rc;
   } else {
     // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
@@ -575,7 +582,9 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // gradient summed from the tile in the epilogue (no column-sum pass)
         EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
         using ED = EpiStoreBiasT<float>;
-        switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
+        if (f32_split6())   // the same ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+          HIPCHK((step_gemm<GemmCfgS6<64, 64, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+        else switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
           case -1: HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
           case 1: HIPCHK((step_gemm<Cfg64For<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
           case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED, 3, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;

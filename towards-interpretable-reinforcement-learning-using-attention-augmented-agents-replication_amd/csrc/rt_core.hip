@@ -379,6 +379,7 @@ int f32_frames(const Layout& L) {
 // Start offset of half the frames of the bf16 frame-resident kernels (common.h
 // stagger_wait), in microseconds -> 100-MHz ticks.
 int rec_stagger(const char* env) { return 100 * env_int(env, 0); }
+bool f32_split6() { return env_int("AAA_F32_SPLIT6", 0) != 0; }
 // Band mode (recur_bwd.h BAND) wherever the forward runs in band mode: kRecBands.
 // Only behind a frame-resident forward: the two share the channel-quad-major
 // slices of Cst / Gt / dO (cqm_layout), which the per-step kernels do not read.
