@@ -92,7 +92,9 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 // ABL (diagnostic builds only, tools/ubench/f32rec): bit 0 = no partner waits,
 // bit 1 = no MFMAs, bit 3 = no exchange (partials neither stored nor loaded).
 // Production launches use 0.
-template <int ABL = 0>
+// S6: the MFMAs on the bf16 MFMA at fp32 accuracy, two quads per k-step with
+// three-way split operands (as recur_f32.h S6, gemm.h SPLIT6).
+template <int ABL = 0, bool S6 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_bwd_f32(RecBwdF32Params p) {
   constexpr int G = 8, NG = 2;                   // NG: (pixel, 4-channel) groups per thread (484 <= 512)
@@ -232,6 +234,62 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       }
     };
     f32x4 bfr[2][2];
+    if constexpr (S6) {
+      f32x4 bp[4][2];   // B fragments of two pairs of quads
+      ldb(0, 0, bp[0]);
+      ldb(0, 1, bp[1]);
+      for (int tap = 0; tap < 9; ++tap) {
+        int qt = tap * 8;
+        asm volatile("" : "+s"(qt));
+#pragma unroll
+        for (int q8 = 0; q8 < 8; q8 += 2) {
+          const int pb = (q8 >> 1) & 1, nb = pb ^ 1;
+          float a8[2][8];
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              a8[r][e] = af[q8][r][e];
+              a8[r][4 + e] = af[q8 + 1][r][e];
+            }
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            af[(q8 + PD - 1) % PD][r] = lda(qt + q8 + PD - 1, r);
+            af[q8][r] = lda(qt + q8 + PD, r);
+          }
+          if (q8 < 6) {
+            ldb(tap, q8 + 2, bp[2 * nb]);
+            ldb(tap, q8 + 3, bp[2 * nb + 1]);
+          } else if (tap < 8) {
+            ldb(tap + 1, 0, bp[2 * nb]);
+            ldb(tap + 1, 1, bp[2 * nb + 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          bf16x8 bh[2], bm[2], bl[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const float b8[8] = {bp[2 * pb][c][0],     bp[2 * pb][c][1],     bp[2 * pb][c][2],     bp[2 * pb][c][3],
+                                 bp[2 * pb + 1][c][0], bp[2 * pb + 1][c][1], bp[2 * pb + 1][c][2], bp[2 * pb + 1][c][3]};
+            split3_bf16(b8, bh[c], bm[c], bl[c]);
+          }
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            bf16x8 ah, am, al;
+            split3_bf16(a8[r], ah, am, al);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[c], acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[c], acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[c], acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[c], acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[c], acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[c], acc[r][c], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
     ldb(0, 0, bfr[0]);
     for (int tap = 0; tap < 9; ++tap) {
       int qt = tap * 8;
@@ -256,6 +314,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
             }
         __builtin_amdgcn_sched_barrier(0);
       }
+    }
     }
     AAA_B32_STAMP(it, 1);
     // partial dh: lane (r32, hh) of tile (r, c), element 4g + e = channel
@@ -349,7 +408,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   }
 }
 
-inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st) {
+inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 = false) {
   if (!f32_rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0 ||
       !p.part || !p.xp)
     return hipErrorInvalidValue;
@@ -357,7 +416,9 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st) {
     const int pp = c < p.P ? c : p.P - 1;
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
-  return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>), f32_grid(p.B, 8), 256, p, st);
+  return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true>)
+                            : reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>),
+                         f32_grid(p.B, 8), 256, p, st);
 }
 
 }  // namespace aaa

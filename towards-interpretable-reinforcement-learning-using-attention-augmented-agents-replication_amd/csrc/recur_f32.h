@@ -106,7 +106,12 @@ __device__ uint64_t aaa_f32_clocks[512 * 64 * 5];   // s_memtime (shader clock) 
 // ABL (diagnostic builds only, tools/ubench/f32rec; production launches use 0):
 // bit 0 = no epilogue (gate math, stores), bit 1 = no epilogue HBM stores,
 // bit 2 = no partner exchange, bit 3 = no MFMAs.
-template <int G, int ABL = 0>
+// S6: the MFMAs on the bf16 MFMA at fp32 accuracy (gemm.h SPLIT6): two quads
+// (16 channels) per v_mfma_f32_32x32x16_bf16 k-step -- lane half hh's 8 k-slots
+// are channels 4hh..4hh+3 of the first quad, then of the second, in the same
+// order for A and B -- each operand split three ways, six MFMAs (6 x 32
+// cycles) where the fp32 MFMA takes eight (8 x 64).
+template <int G, int ABL = 0, bool S6 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_fwd_f32(RecF32Params p) {
   constexpr int NRB = 16 / G, RPW = NRB / 2;       // row blocks per workgroup / per wave
@@ -240,7 +245,47 @@ k_convlstm_fwd_f32(RecF32Params p) {
           }
       __builtin_amdgcn_sched_barrier(0);
     };
+    // S6: quads qn, qn + 1 (slot even: PD is even), B fragments of both in b0 / b1
+    auto pair = [&](int qn, int slot, f32x4 (&b0)[2], f32x4 (&b1)[2], auto&& load_next_b) {
+      float a8[RPW][8];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a8[r][e] = af[slot][r][e];
+          a8[r][4 + e] = af[slot + 1][r][e];
+        }
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        af[(slot + PD - 1) % PD][r] = lda(qn + PD - 1, r);
+        af[slot][r] = lda(qn + PD, r);
+      }
+      load_next_b();
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 bh[2], bm[2], bl[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float b8[8] = {b0[c][0], b0[c][1], b0[c][2], b0[c][3], b1[c][0], b1[c][1], b1[c][2], b1[c][3]};
+        split3_bf16(b8, bh[c], bm[c], bl[c]);
+      }
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        bf16x8 ah, am, al;
+        split3_bf16(a8[r], ah, am, al);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[c], acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[c], acc[r][c], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
     f32x4 bfr[2][2];
+    f32x4 bp[4][2];   // S6: B fragments of two pairs of quads
     // partners' slices of h_{t-1} (XH slot t): loaded into registers mid x-part
     u32x4 pv[NPL];
     const bool exch = G > 1 && t > 0 && !(ABL & 4);
@@ -269,18 +314,39 @@ k_convlstm_fwd_f32(RecF32Params p) {
     };
 
     // ---- x-part: 9 taps x 8 quads over the x image
-    ldb(xim, 256, 0, 0, bfr[0]);
+    if constexpr (S6) {
+      ldb(xim, 256, 0, 0, bp[0]);
+      ldb(xim, 256, 0, 2, bp[1]);
+    } else {
+      ldb(xim, 256, 0, 0, bfr[0]);
+    }
     for (int tap = 0; tap < 9; ++tap) {
       const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
       int qt = tap * 8;
       asm volatile("" : "+s"(qt));
       if (tap == 2 && exch) partner_issue();
+      if constexpr (S6) {
 #pragma unroll
-      for (int c8 = 0; c8 < 8; ++c8)
-        quad(qt + c8, c8 % PD, bfr[c8 & 1], [&] {
-          if (c8 < 7) ldb(xim, 256, toff, 2 * (c8 + 1), bfr[(c8 + 1) & 1]);
-          else if (tap < 8) ldb(xim, 256, tn, 0, bfr[0]);
-        });
+        for (int c8 = 0; c8 < 8; c8 += 2) {
+          const int pb = (c8 >> 1) & 1, nb = pb ^ 1;
+          pair(qt + c8, c8 % PD, bp[2 * pb], bp[2 * pb + 1], [&] {
+            if (c8 < 6) {
+              ldb(xim, 256, toff, 2 * (c8 + 2), bp[2 * nb]);
+              ldb(xim, 256, toff, 2 * (c8 + 3), bp[2 * nb + 1]);
+            } else if (tap < 8) {
+              ldb(xim, 256, tn, 0, bp[2 * nb]);
+              ldb(xim, 256, tn, 2, bp[2 * nb + 1]);
+            }
+          });
+        }
+      } else {
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8)
+          quad(qt + c8, c8 % PD, bfr[c8 & 1], [&] {
+            if (c8 < 7) ldb(xim, 256, toff, 2 * (c8 + 1), bfr[(c8 + 1) & 1]);
+            else if (tap < 8) ldb(xim, 256, tn, 0, bfr[0]);
+          });
+      }
     }
     const bool hpart = t > 0 || !p.h0_zero;
     if (exch) partner_store();
@@ -288,17 +354,38 @@ k_convlstm_fwd_f32(RecF32Params p) {
     AAA_F32_STAMP(t, 1);
     if (hpart) {
       // ---- h-part: 9 taps x 16 quads over the h image
-      ldb(him, 512, 0, 0, bfr[0]);
+      if constexpr (S6) {
+        ldb(him, 512, 0, 0, bp[0]);
+        ldb(him, 512, 0, 2, bp[1]);
+      } else {
+        ldb(him, 512, 0, 0, bfr[0]);
+      }
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
         int qt = kF32QX + tap * 16;
         asm volatile("" : "+s"(qt));
+        if constexpr (S6) {
 #pragma unroll
-        for (int c16 = 0; c16 < 16; ++c16)
-          quad(qt + c16, c16 % PD, bfr[c16 & 1], [&] {
-            if (c16 < 15) ldb(him, 512, toff, 2 * (c16 + 1), bfr[(c16 + 1) & 1]);
-            else if (tap < 8) ldb(him, 512, tn, 0, bfr[0]);
-          });
+          for (int c16 = 0; c16 < 16; c16 += 2) {
+            const int pb = (c16 >> 1) & 1, nb = pb ^ 1;
+            pair(qt + c16, c16 % PD, bp[2 * pb], bp[2 * pb + 1], [&] {
+              if (c16 < 14) {
+                ldb(him, 512, toff, 2 * (c16 + 2), bp[2 * nb]);
+                ldb(him, 512, toff, 2 * (c16 + 3), bp[2 * nb + 1]);
+              } else if (tap < 8) {
+                ldb(him, 512, tn, 0, bp[2 * nb]);
+                ldb(him, 512, tn, 2, bp[2 * nb + 1]);
+              }
+            });
+          }
+        } else {
+#pragma unroll
+          for (int c16 = 0; c16 < 16; ++c16)
+            quad(qt + c16, c16 % PD, bfr[c16 & 1], [&] {
+              if (c16 < 15) ldb(him, 512, toff, 2 * (c16 + 1), bfr[(c16 + 1) & 1]);
+              else if (tap < 8) ldb(him, 512, tn, 0, bfr[0]);
+            });
+        }
       }
     } else {   // the prefetched A quads are the h-part's: restart the stream at quad 0
 #pragma unroll
@@ -391,15 +478,17 @@ inline int f32_rec_g(int B, int cus) {
   return 0;
 }
 
-inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st) {
+inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool s6 = false) {
   if (!f32_rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
     return hipErrorInvalidValue;
   for (int c = 0; c < 128; ++c) {
     const int pp = c < p.P ? c : p.P - 1;
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
-  const void* k = G == 8   ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>)
-                  : G == 4 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4>)
+  const void* k = G == 8   ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true>)
+                                 : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>))
+                  : G == 4 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4, 0, true>)
+                                 : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4>))
                            : nullptr;
   if (!k) return hipErrorInvalidValue;
   return launch_resident(k, f32_grid(p.B, G), 256, p, st);

@@ -730,9 +730,11 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         RecBwdF32Params rp{(const float*)(pk + L.k_Wb32), Wf(L.dO), Wf(L.Gt), Wf(L.Cst), Wf(L.dC), Wf(L.dZ),
                            Wf(L.dZp), io->dh0, Wf(L.xpart), (int*)(ws + L.rflags), rep, pair_budget(L.T),
                            L.T, L.B, L.h, L.w, L.P, {}};
+        const bool s6 = f32_split6();
         TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
-                       strf("fp32 frame-group BPTT (dh rows), %d steps per launch, 8 WG per frame [kernel: k_convlstm_bwd_f32]", L.T));
-        HIPCHK(convlstm_bwd_f32(rp, st));
+                       strf("fp32 frame-group BPTT (dh rows)%s, %d steps per launch, 8 WG per frame [kernel: k_convlstm_bwd_f32]",
+                            s6 ? " (bf16x6 split products)" : "", L.T));
+        HIPCHK(convlstm_bwd_f32(rp, st, s6));
       }
     }
     for (int t = (fb || fb32) ? -1 : t1; t >= 0; --t) {

@@ -186,9 +186,11 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                       Wf(L.Gt), (int*)(ws + L.rflags), rep, pair_budget(L.T), L.T, L.B, L.h, L.w, L.P,
                       io->h0 ? 0 : 1, {}};
       {
+        const bool s6 = f32_split6();
         TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
-                       strf("fp32 frame-group [x|h] recurrence, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]", L.T, G));
-        HIPCHK(convlstm_fwd_f32(rp, G, st));
+                       strf("fp32 frame-group [x|h] recurrence%s, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]",
+                            s6 ? " (bf16x6 split products)" : "", L.T, G));
+        HIPCHK(convlstm_fwd_f32(rp, G, st, s6));
       }
       return forward_tail<T>(L, io, st);
     }
