@@ -297,13 +297,22 @@ static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const 
 // g_tail3 (set per forward / backward call of the bf16 path, TailPrecision):
 // the same tiles with fp32 operands split into bf16 pairs on the bf16 MFMA
 // (gemm.h GemmCfgS3), ~1e-5 relative per product.
-extern thread_local bool g_tail3;
+// g_tail6 (set per call of the fp32 path when f32_split6()): the three-way
+// split at fp32 accuracy (gemm.h GemmCfgS6).
+extern thread_local bool g_tail3, g_tail6;
 struct TailPrecision {
-  bool prev;
-  explicit TailPrecision(bool split3) : prev(g_tail3) { g_tail3 = split3; }
-  ~TailPrecision() { g_tail3 = prev; }
+  bool prev3, prev6;
+  explicit TailPrecision(bool split3, bool split6 = false) : prev3(g_tail3), prev6(g_tail6) {
+    g_tail3 = split3;
+    g_tail6 = split6;
+  }
+  ~TailPrecision() {
+    g_tail3 = prev3;
+    g_tail6 = prev6;
+  }
 };
 template <class C> struct S3Of { using type = GemmCfgS3<C::BI, C::BJ, C::BK, C::WI, C::WJ, C::WK>; };
+template <class C> struct S6Of { using type = GemmCfgS6<C::BI, C::BJ, C::BK, C::WI, C::WJ, C::WK>; };
 
 template <template <typename, typename, int, int, int> class LA_,
           template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
@@ -312,6 +321,13 @@ static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, in
   const int mode = env_int("AAA_HEAD_TILE", 0);
   const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
   auto splitk = [&](auto cfg0) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
+    if (g_tail6) {
+      using C = typename S6Of<decltype(cfg0)>::type;
+      using A = LA_<float, float, C::BI, C::BK, C::NT>;
+      using B = LB_<float, float, C::BJ, C::BK, C::NT>;
+      return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows},
+                                  typename B::Params{pb.src, pb.ld, pb.nrows}, ep, Mi, Nj, K, nsplit, st);
+    }
     if (g_tail3) {
       using C = typename S3Of<decltype(cfg0)>::type;
       using A = LA_<float, float, C::BI, C::BK, C::NT>;
@@ -330,7 +346,7 @@ static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, in
   if (mode == 5) return splitk(CFK4B{});
   if (mode == 0 && tiles < 192) return splitk(CFK4{});
   if (mode == 1 || (mode == 0 && tiles >= 192)) return splitk(CF{});
-  if (g_tail3) return splitk(CF32{});
+  if (g_tail3 || g_tail6) return splitk(CF32{});
   using C = CF32;
   using A = LA_<float, float, C::BI, C::BK, C::NT>;
   using B = LB_<float, float, C::BJ, C::BK, C::NT>;

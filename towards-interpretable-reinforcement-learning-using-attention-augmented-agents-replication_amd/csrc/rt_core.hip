@@ -6,7 +6,7 @@
 namespace aaa {
 
 thread_local std::string g_err;
-thread_local bool g_tail3 = false;
+thread_local bool g_tail3 = false, g_tail6 = false;
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];

@@ -153,7 +153,8 @@ template <typename T>
 int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
   using C = CfgFor<T>;
   // bf16 path: the fp32 tail GEMMs on the bf16 MFMA with split operands (AAA_TAIL_SPLIT3=0: fp32 MFMA)
-  TailPrecision tail_prec(std::is_same<T, __bf16>::value && env_int("AAA_TAIL_SPLIT3", 1));
+  TailPrecision tail_prec(std::is_same<T, __bf16>::value && env_int("AAA_TAIL_SPLIT3", 1),
+                          std::is_same<T, float>::value && f32_split6());
   char* ws = (char*)io->workspace;
   const char* pk = (const char*)io->packed;
   const float* prm = io->params;
