@@ -123,6 +123,12 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
                          (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
   EpiStore<true> ep{gW, 512, 64, 512};
   const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
+  if constexpr (std::is_same<T, float>::value) {
+    if (f32_split6()) {   // the same tile at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+      HIPCHK((launch_gemm<typename S6Of<C>::type, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
+      return AAA_OK;
+    }
+  }
   HIPCHK((launch_gemm<C, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
   return AAA_OK;
 }
@@ -140,6 +146,13 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
                            (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
     EpiStore<true> ep{gW, 256, 32, 256};
     const int tiles = cdiv(32, C3::BI) * cdiv(256, C3::BJ);
+    if constexpr (std::is_same<T, float>::value) {
+      if (f32_split6()) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+        HIPCHK((launch_gemm<typename S6Of<C3>::type, LA, LB>(pa, pb, ep, 32, 256, rows1,
+                                                            wgrad_splits(tiles, rows1, C3::BK), s)));
+        return AAA_OK;
+      }
+    }
     HIPCHK((launch_gemm<C3, LA, LB>(pa, pb, ep, 32, 256, rows1, wgrad_splits(tiles, rows1, C3::BK), s)));
     return AAA_OK;
   };

@@ -90,7 +90,13 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
       };
       // K = 256 is four BK steps: a wider column tile does more MFMA work per DMA round trip (A/B: AAA_CONV1_TILE)
       const int c1t = env_int("AAA_CONV1_TILE", 0);
-      const int rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
+      int rc;
+      if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+        if (f32_split6()) rc = conv1(GemmCfgS6<32, 128, BKc, 1, 4>{});
+        else rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
+      } else {
+        rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
+      }
       if (rc) return rc;
     }
   }
@@ -109,7 +115,11 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
     EpiStoreT<OT> ep{out, out_ld, 64, F * P, prm + L.poff[C1B], 0};
     const uint32_t y1b = (uint32_t)((size_t)F * L.P1 * 32 * L.esz);
     if constexpr (32 % C::BK == 0) {   // LDS-DMA ring (tools/ubench/conv_cfg: 62 vs 67 us)
-      HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g, F * P, y1b, ep, 64, 512, st)));
+      if (std::is_same<T, float>::value && f32_split6())   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+        HIPCHK((step_gemm<std::conditional_t<std::is_same<T, float>::value, typename S6Of<C>::type, C>, true>(
+            (const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g, F * P, y1b, ep, 64, 512, st)));
+      else
+        HIPCHK((step_gemm<C, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g, F * P, y1b, ep, 64, 512, st)));
     } else if (pipe_batched()) {   // bf16: a BK=32 ring, one 4x4 tap row's 32 channels per K tile
       HIPCHK((step_gemm<GemmCfg<T, 64, 128, 32, 2, 2>, true>((const T*)(pk + L.k_Wp2), 512, 64, (const T*)Y1, g,
                                                            F * P, y1b, ep, 64, 512, st)));
