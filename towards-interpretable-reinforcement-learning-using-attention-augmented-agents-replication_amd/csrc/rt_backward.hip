@@ -643,9 +643,11 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     }
     {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
       int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
-      if (!rc)
+      if (!rc && L.xpc < L.F)   // Xp chunk buffer: rebuilt from the observation
         rc = conv1_wgrad_frames<T>(L, dy1, (const char*)io->frames + (size_t)lo * L.B * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
                                    F1, Wt(L.Xp), Wf(L.gWp1), s);
+      else if (!rc)
+        rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
       if (rc) return rc;
       if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
@@ -879,7 +881,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       constexpr bool f32 = std::is_same<T, float>::value;
       {
         const int rc = vision_bwd<T>(L, pk, Wt(L.dY2), Wt(L.Y1), Wt(L.Xp), Wt(L.dY1), F, Wf(L.gWp2), Wf(L.gWp1),
-                                     grads + L.poff[C0B], st, io->frames);
+                                     grads + L.poff[C0B], st, L.xpc < L.F ? io->frames : nullptr);
         if (rc) return rc;
         if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }

@@ -79,10 +79,12 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   // workspace
   p = 0;
   const size_t F = L.F, P = L.P, M = (size_t)L.B * L.P;
-  // frames as zero-bordered RGBx (conv1's operand type), a chunk of xpc frames at a time: rebuilt from the
-  // observation where conv1 (forward, layered path) or its weight gradient (backward) reads it, so it is
-  // written and read while it sits in the memory-side cache instead of round-tripping all F frames via HBM
-  L.xpc = (int)std::min<size_t>(F, (size_t)std::max(64, env_int("AAA_XP_CHUNK", 512)));
+  // frames as zero-bordered RGBx (conv1's operand type): all F frames, written by the forward's encoder
+  // and read by conv1's weight gradient; AAA_XP_CHUNK=n (A/B) keeps a chunk of n frames instead, rebuilt
+  // from the observation right before conv1 (layered forward) or its weight gradient reads it (measured
+  // slower: C3 vision backward 0.368 -> 0.666 ms for -0.03 ms in the forward)
+  const int xc = env_int("AAA_XP_CHUNK", 0);
+  L.xpc = xc > 0 ? (int)std::min<size_t>(F, (size_t)std::max(64, xc)) : (int)F;
   L.Xp = take((size_t)L.xpc * (L.H + 2) * (L.W + 2) * 4 * e);
   L.Y1 = take(F * L.P1 * 32 * e);
   L.XH = take((size_t)(L.T + 1) * M * 192 * e);
@@ -379,7 +381,8 @@ int f32_frames(const Layout& L) {
 // Start offset of half the frames of the bf16 frame-resident kernels (common.h
 // stagger_wait), in microseconds -> 100-MHz ticks.
 int rec_stagger(const char* env) { return 100 * env_int(env, 0); }
-bool f32_split6() { return env_int("AAA_F32_SPLIT6", 0) != 0; }
+// default on: C2 150.6k -> 175.6k frames/s (profiles/r04/ab_split6); AAA_F32_SPLIT6=0 restores the fp32 MFMA
+bool f32_split6() { return env_int("AAA_F32_SPLIT6", 1) != 0; }
 // Band mode (recur_bwd.h BAND) wherever the forward runs in band mode: kRecBands.
 // Only behind a frame-resident forward: the two share the channel-quad-major
 // slices of Cst / Gt / dO (cqm_layout), which the per-step kernels do not read.

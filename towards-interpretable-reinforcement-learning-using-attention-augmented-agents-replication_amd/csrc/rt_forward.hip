@@ -176,7 +176,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
 
   {  // conv1 + conv2 over all T*B frames -> XH[:, :, 0:64] of every slot
     TimerScope tim(AAA_TIMER_VISION_FWD, st, (double)F * vision_fwd_flop(L), "conv1 + conv2 (vision encoder)");
-    const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st, false);
+    const int rc = vision_fwd<T, T>(L, F, pk, prm, io->frames, Wt(L.Xp), Wt(L.Y1), Wt(L.XH), 192, st, L.xpc >= F);
     if (rc) return rc;
   }
   {  // initial state (reset(): zeros, attention.py:142-149) or carried state
