@@ -77,6 +77,7 @@ struct RecBwdF32Params {
   int spin;           // partner-wait budget, 100-MHz ticks (pair_wait)
   int T, B, h, w, P;
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
+  const u32x2* Wb6 = nullptr;   // S6: the three-way split of Wb (recur_f32.h k_split_frag)
 };
 
 #ifdef AAA_STAMPS
@@ -185,10 +186,24 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   constexpr int PD = kB32PD;
   static_assert(kB32Q % PD == 0 && PD == 8, "slot = q8");
   f32x4 af[PD][2];
+  // S6: the pre-split stream (recur_f32.h k_split_frag), part p of chunk group g at (g * 3 + p) * 512 B
+  const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wb6, S6 ? (uint32_t)(8 * kB32QP * 4 * 3 * 512) : 0u);
+  auto lda6 = [&](int q, int r, int part) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         rsw6, lane * 8, (((kh * kB32QP + q) * 4 + 2 * rw + r) * 3 + part) * 512, 0));
+  };
+  u32x2 a6[S6 ? PD : 1][2][3];
 #pragma unroll
   for (int s = 0; s < PD - 1; ++s)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) af[s][r] = lda(s, r);
+    for (int r = 0; r < 2; ++r) {
+      if constexpr (S6) {
+#pragma unroll
+        for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6(s, r, part);
+      } else {
+        af[s][r] = lda(s, r);
+      }
+    }
 
   // the dgrad is the transposed conv: tap (ky, kx) of W^T (packed in the forward's
   // orientation) reads dZ at (y + 1 - ky, x + 1 - kx) (ConvGeo transposed gather)
@@ -244,19 +259,20 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
 #pragma unroll
         for (int q8 = 0; q8 < 8; q8 += 2) {
           const int pb = (q8 >> 1) & 1, nb = pb ^ 1;
-          float a8[2][8];
+          bf16x8 a3[2][3];
 #pragma unroll
           for (int r = 0; r < 2; ++r)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              a8[r][e] = af[q8][r][e];
-              a8[r][4 + e] = af[q8 + 1][r][e];
-            }
+            for (int part = 0; part < 3; ++part)
+              a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8][r][part].x, a6[q8][r][part].y,
+                                                             a6[q8 + 1][r][part].x, a6[q8 + 1][r][part].y});
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            af[(q8 + PD - 1) % PD][r] = lda(qt + q8 + PD - 1, r);
-            af[q8][r] = lda(qt + q8 + PD, r);
-          }
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int part = 0; part < 3; ++part) {
+              a6[(q8 + PD - 1) % PD][r][part] = lda6(qt + q8 + PD - 1, r, part);
+              a6[q8][r][part] = lda6(qt + q8 + PD, r, part);
+            }
           if (q8 < 6) {
             ldb(tap, q8 + 2, bp[2 * nb]);
             ldb(tap, q8 + 3, bp[2 * nb + 1]);
@@ -274,8 +290,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
           }
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
-            bf16x8 ah, am, al;
-            split3_bf16(a8[r], ah, am, al);
+            const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
               acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[c], acc[r][c], 0, 0, 0);

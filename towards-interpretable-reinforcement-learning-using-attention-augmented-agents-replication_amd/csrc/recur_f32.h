@@ -63,6 +63,45 @@ static __global__ void __launch_bounds__(256) k_pack_wf32(const float* __restric
   *reinterpret_cast<f32x4*>(Wf + (size_t)c * 4) = *reinterpret_cast<const f32x4*>(W + (size_t)row * 1728 + k);
 }
 
+// S6 (bf16x6) copy of a fragment-order fp32 weight stream: chunk c = g * 64 + lane
+// (16 B = 4 fp32) -> three 8-B parts (hi, mid, lo: 4 bf16 each, gemm.h split3_bf16's
+// split) at [(g * 3 + part) * 64 + lane], so a wave's load of one part is 512 contiguous
+// bytes and the kernels assemble their bf16x8 operands from two quads without VALU work.
+static __global__ void __launch_bounds__(256) k_split_frag(const f32x4* __restrict__ src, u32x2* __restrict__ dst,
+                                                           int nchunks) {
+  const int c = blockIdx.x * 256 + (int)threadIdx.x;
+  if (c >= nchunks) return;
+  const f32x4 x = src[c];
+  u32x2 part[3];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    uint32_t h2[2], m2[2], l2[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float v = x[2 * e + k];
+      const __bf16 hi = (__bf16)v;
+      const float r = v - (float)hi;
+      const __bf16 mid = (__bf16)r;
+      const __bf16 lo = (__bf16)(r - (float)mid);
+      h2[k] = __builtin_bit_cast(uint16_t, hi);
+      m2[k] = __builtin_bit_cast(uint16_t, mid);
+      l2[k] = __builtin_bit_cast(uint16_t, lo);
+    }
+    part[0][e] = h2[0] | (h2[1] << 16);
+    part[1][e] = m2[0] | (m2[1] << 16);
+    part[2][e] = l2[0] | (l2[1] << 16);
+  }
+  const int g = c >> 6, lane = c & 63;
+#pragma unroll
+  for (int p = 0; p < 3; ++p) dst[(g * 3 + p) * 64 + lane] = part[p];
+}
+
+inline hipError_t split_frag(const float* src, void* dst, int nchunks, hipStream_t st) {
+  hipLaunchKernelGGL(k_split_frag, dim3((nchunks + 255) / 256), dim3(256), 0, st,
+                     reinterpret_cast<const f32x4*>(src), reinterpret_cast<u32x2*>(dst), nchunks);
+  return hipGetLastError();
+}
+
 inline hipError_t pack_wf32(const float* W, float* Wf, hipStream_t st) {
   hipLaunchKernelGGL(k_pack_wf32, dim3((16 * kF32QP * 64 + 255) / 256), dim3(256), 0, st, W, Wf);
   return hipGetLastError();
@@ -81,6 +120,7 @@ struct RecF32Params {
   int T, B, h, w, P;
   int h0_zero;         // slot 0's h part is zero (reset()): the t = 0 h-part is skipped
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
+  const u32x2* Wf6 = nullptr;   // S6: the three-way split of Wf (k_split_frag)
 };
 
 // Blocks of the launch: 8 * G * ceil(B / 8) (XCD-local frame groups).
@@ -195,10 +235,27 @@ k_convlstm_fwd_f32(RecF32Params p) {
   };
   constexpr int PD = kF32PD;
   f32x4 af[PD][RPW];
+  // S6: the pre-split stream, quad q's part p of row block rb at ((rb * kF32QP + q) * 3 + p) * 512 B
+  const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wf6, S6 ? (uint32_t)(16 * kF32QP * 3 * 512) : 0u);
+  auto lda6 = [&](int q, int r, int part) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         rsw6, lane * 8, (((rbg0 + r) * kF32QP + q) * 3 + part) * 512, 0));
+  };
+  u32x2 a6[S6 ? PD : 1][RPW][3];
+  auto preload = [&] {
 #pragma unroll
-  for (int s = 0; s < PD - 1; ++s)
+    for (int s = 0; s < PD - 1; ++s)
 #pragma unroll
-    for (int r = 0; r < RPW; ++r) af[s][r] = lda(s, r);
+      for (int r = 0; r < RPW; ++r) {
+        if constexpr (S6) {
+#pragma unroll
+          for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6(s, r, part);
+        } else {
+          af[s][r] = lda(s, r);
+        }
+      }
+  };
+  preload();
   __syncthreads();   // h_{-1} image written; this wave's x DMA is waited for below
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave's x_0 DMA landed
@@ -245,21 +302,23 @@ k_convlstm_fwd_f32(RecF32Params p) {
           }
       __builtin_amdgcn_sched_barrier(0);
     };
-    // S6: quads qn, qn + 1 (slot even: PD is even), B fragments of both in b0 / b1
+    // S6: quads qn, qn + 1 (slot even: PD is even), B fragments of both in b0 / b1;
+    // the A operand's parts come pre-split (k_split_frag): two quads' 8-B parts side by side
     auto pair = [&](int qn, int slot, f32x4 (&b0)[2], f32x4 (&b1)[2], auto&& load_next_b) {
-      float a8[RPW][8];
+      bf16x8 a3[RPW][3];
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a8[r][e] = af[slot][r][e];
-          a8[r][4 + e] = af[slot + 1][r][e];
-        }
+        for (int part = 0; part < 3; ++part)
+          a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[slot][r][part].x, a6[slot][r][part].y,
+                                                         a6[slot + 1][r][part].x, a6[slot + 1][r][part].y});
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) {
-        af[(slot + PD - 1) % PD][r] = lda(qn + PD - 1, r);
-        af[slot][r] = lda(qn + PD, r);
-      }
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+          a6[(slot + PD - 1) % PD][r][part] = lda6(qn + PD - 1, r, part);
+          a6[slot][r][part] = lda6(qn + PD, r, part);
+        }
       load_next_b();
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 bh[2], bm[2], bl[2];
@@ -270,8 +329,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
       }
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
-        bf16x8 ah, am, al;
-        split3_bf16(a8[r], ah, am, al);
+        const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[c], acc[r][c], 0, 0, 0);
@@ -388,10 +446,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
         }
       }
     } else {   // the prefetched A quads are the h-part's: restart the stream at quad 0
-#pragma unroll
-      for (int s = 0; s < PD - 1; ++s)
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) af[s][r] = lda(s, r);
+      preload();
     }
     barrier_lds();   // every wave is done with h_{t-1}: the epilogue overwrites its own channels
     AAA_F32_STAMP(t, 2);

@@ -747,6 +747,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                            Wf(L.dZp), io->dh0, Wf(L.xpart), (int*)(ws + L.rflags), rep, pair_budget(L.T),
                            L.T, L.B, L.h, L.w, L.P, {}};
         const bool s6 = f32_split6();
+        rp.Wb6 = (const u32x2*)(pk + L.k_Wb6);
         TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
                        strf("fp32 frame-group BPTT (dh rows)%s, %d steps per launch, 8 WG per frame [kernel: k_convlstm_bwd_f32]",
                             s6 ? " (bf16x6 split products)" : "", L.T));

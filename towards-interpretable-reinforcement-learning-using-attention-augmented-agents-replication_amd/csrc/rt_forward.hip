@@ -36,6 +36,8 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
   } else {   // the fp32 frame-group recurrence's fragment order (recur_f32.h)
     HIPCHK(pack_wf32((const float*)(pk + L.k_WpXH), (float*)(pk + L.k_Wf32), st));
     HIPCHK(pack_wb32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wb32), st));
+    HIPCHK(split_frag((const float*)(pk + L.k_Wf32), pk + L.k_Wf6, 16 * kF32QP * 64, st));
+    HIPCHK(split_frag((const float*)(pk + L.k_Wb32), pk + L.k_Wb6, 8 * kB32QP * 4 * 64, st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
@@ -198,6 +200,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
                       io->h0 ? 0 : 1, {}};
       {
         const bool s6 = f32_split6();
+        rp.Wf6 = (const u32x2*)(pk + L.k_Wf6);
         TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
                        strf("fp32 frame-group [x|h] recurrence%s, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]",
                             s6 ? " (bf16x6 split products)" : "", L.T, G));
