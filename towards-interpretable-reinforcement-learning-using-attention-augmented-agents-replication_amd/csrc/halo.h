@@ -37,6 +37,12 @@ struct HaloCfg {
   static constexpr int HMAX = HMAX_;              // halo rows (>= FR*(h+2)*(w+2) + 1 zero row)
 };
 
+// fp32 at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6): three-way split operands, six products
+template <int BI_, int BJ_, int CK_, int WI_, int WJ_, int FR_, int HMAX_>
+struct HaloCfgS6 : HaloCfg<float, BI_, BJ_, CK_, WI_, WJ_, FR_, HMAX_> {
+  static constexpr bool SPLIT3 = true, SPLIT6 = true;
+};
+
 struct HaloParams {
   const void* wt;       // weights [Mi][9*Cin] (row stride ldw elements), tap-major k
   int ldw, Mi;
@@ -187,13 +193,32 @@ __global__ void __launch_bounds__(C::NT) conv3_halo_kernel(HaloParams p, EP ep, 
           bfr[b][0] = x[0]; bfr[b][1] = x[1]; bfr[b][2] = x[2]; bfr[b][3] = x[3];
           bfr[b][4] = y[0]; bfr[b][5] = y[1]; bfr[b][6] = y[2]; bfr[b][7] = y[3];
         }
+        if constexpr (split6_of<C>::value) {
+          bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
+          for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
 #pragma unroll
           for (int a = 0; a < MI; ++a)
 #pragma unroll
-            for (int b = 0; b < MJ; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+            for (int b = 0; b < MJ; ++b) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+            for (int a = 0; a < MI; ++a)
+#pragma unroll
+              for (int b = 0; b < MJ; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+        }
       } else {
         bf16x8 af[MI], bfr[MJ];
 #pragma unroll

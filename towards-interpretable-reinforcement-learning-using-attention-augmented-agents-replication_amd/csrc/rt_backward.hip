@@ -36,6 +36,9 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     const int fr = env_int("AAA_DGRAD2_FR", std::is_same<T, float>::value ? 1 : 2);
     if (env_int("AAA_DGRAD2_HALO", 1)) {
       if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{});
+      if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+        if (f32_split6() && fits(1, 128, 192)) return halo4(HaloCfgS6<128, 128, CKd, 2, 2, 1, 192>{});
+      }
       if (fits(1, 128, 192)) return halo4(HaloCfg<T, 128, 128, CKd, 2, 2, 1, 192>{});
       // bf16, grids up to 21x21 (168x168 frames, C5): one frame per 512-column tile of 8 waves,
       // 32-channel chunks (two LDS images of 23x23 pixels), the epilogue in two column chunks
@@ -596,7 +599,13 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // gradient summed from the tile in the epilogue (no column-sum pass)
         EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
         using ED = EpiStoreBiasT<float>;
-        if (f32_split6())   // the same ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+        using HF6 = HaloCfgS6<64, 128, 32, 1, 2, 1, 176>;   // one 11x11 frame per tile, its dZ image in LDS
+        if (f32_split6() && halo_fits<HF6>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+          // small grids: the halo-staged conv (every dZ element read once per channel chunk, not
+          // once per tap as the ring's gather does) on the bf16 MFMA with three-way split operands
+          const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
+          HIPCHK((launch_halo<HF6>(hp, ep, s)));
+        } else if (f32_split6())   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
           HIPCHK((step_gemm<GemmCfgS6<64, 64, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
         else switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
           case -1: HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
