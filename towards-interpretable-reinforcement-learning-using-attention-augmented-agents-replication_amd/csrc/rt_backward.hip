@@ -600,9 +600,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
         using ED = EpiStoreBiasT<float>;
         using HF6 = HaloCfgS6<64, 128, 32, 1, 2, 1, 176>;   // one 11x11 frame per tile, its dZ image in LDS
-        if (f32_split6() && halo_fits<HF6>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
-          // small grids: the halo-staged conv (every dZ element read once per channel chunk, not
-          // once per tap as the ring's gather does) on the bf16 MFMA with three-way split operands
+        if (f32_split6() && halo_fits<HF6>(L.h, L.w, 512) && env_int("AAA_HALO_DX_F32", 0)) {
+          // A/B only: the halo-staged conv (every dZ element read once per channel chunk, not once
+          // per tap as the ring's gather does) on split operands -- C2 478 vs 370 us for the ring
+          // (profiles/r04/ab/halo_dx_f32_c2_*.json: 2 waves per 64x128 tile, one frame each)
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HF6>(hp, ep, s)));
         } else if (f32_split6())   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
