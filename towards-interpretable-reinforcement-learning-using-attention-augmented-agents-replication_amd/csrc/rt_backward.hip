@@ -295,8 +295,18 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     if (rc) return rc;
   } else if (std::is_same<T, float>::value && f32_split6()) {
     // fp32: the register-staged 128x128 tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
-    using CS6 = std::conditional_t<std::is_same<T, float>::value, GemmCfgS6<128, 128, 32, 2, 2>, CfgWFor<T>>;
-    const int rc = wgrad_lstm(CS6{});
+    // AAA_WGRAD_S6_TILE (A/B): 0 = 128x128, 1 = 128x256, 2 = 256x128 (4 waves: fewer operand splits per
+    // MFMA), 3 = 256x256 (8 waves of 128x64), the default: C2 842 / 936 / 832 / 729 us
+    // (profiles/r04/ab/split6_tiles_c2_*.json)
+    auto s6 = [&](auto cfg) {
+      using CS6 = std::conditional_t<std::is_same<T, float>::value, decltype(cfg), CfgWFor<T>>;
+      return wgrad_lstm(CS6{});
+    };
+    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 3);
+    const int rc = tile6 == 1   ? s6(GemmCfgS6<128, 256, 32, 2, 2>{})
+                   : tile6 == 2 ? s6(GemmCfgS6<256, 128, 32, 2, 2>{})
+                   : tile6 == 3 ? s6(GemmCfgS6<256, 256, 32, 2, 4>{})
+                                : s6(GemmCfgS6<128, 128, 32, 2, 2>{});
     if (rc) return rc;
   } else {
     // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
@@ -606,9 +616,19 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
           // (profiles/r04/ab/halo_dx_f32_c2_*.json: 2 waves per 64x128 tile, one frame each)
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HF6>(hp, ep, s)));
-        } else if (f32_split6())   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
-          HIPCHK((step_gemm<GemmCfgS6<64, 64, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
-        else switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
+        } else if (f32_split6()) {   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+          // A/B: 0 = 64x64, 1 = 64x128 (the default: C2 355 / 344 / 373 us), 2 = 64x64 BK64
+          switch (env_int("AAA_DX_S6_TILE", 1)) {
+            case 1:
+              HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+              break;
+            case 2:
+              HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+              break;
+            default:
+              HIPCHK((step_gemm<GemmCfgS6<64, 64, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+          }
+        } else switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
           case -1: HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
           case 1: HIPCHK((step_gemm<Cfg64For<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
           case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED, 3, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
