@@ -183,7 +183,7 @@ def dropin_api(cfg, dev, frames, dl, dv, steps, flat):
             "path": "attention.Agent.unroll + loss.backward() (autograd .grad), same frames and weights"}
 
 
-def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
+def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True, per_step=True):
     """The reference's own call pattern (main_mp.py:49-59, 62-80): one episode of
     T_ep per-step ``Policy.forward(observation)`` calls -- B = 1, Seaquest's
     210x160 frames, the default 27x20 spatial basis, the ``.item()`` host sync
@@ -225,7 +225,7 @@ def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
         return finish()
 
     def measure():
-        episode(4).backward()                    # warm-up (allocations, code objects)
+        episode(T_ep).backward()                 # warm-up (code objects; the segment workspace's allocator block)
         torch.cuda.synchronize()
         base = torch.cuda.memory_allocated(dev)
         torch.cuda.reset_peak_memory_stats(dev)
@@ -253,9 +253,10 @@ def episode_leg(dev, T_ep=64, H=210, W=160, cpu=True):
                    "re-runs it as 64-step unrolls from checkpointed states, one hand-written BPTT call each",
            "note": "graph_bytes_per_step x main_mp.py:151's max_steps (10,000) is the device memory one "
                    "full-length episode's autograd graph would hold"}
-    agent.fuse_episode_backward = False
-    out["per_step_path"] = {**measure(), "path": "one T=1 autograd node (own workspace) per step, T_ep backward calls"}
-    agent.fuse_episode_backward = True
+    if per_step:
+        agent.fuse_episode_backward = False
+        out["per_step_path"] = {**measure(), "path": "one T=1 autograd node (own workspace) per step, T_ep backward calls"}
+        agent.fuse_episode_backward = True
     if cpu:
         from oracle import ref_cpu
         cores, _ = _cpu_threads()

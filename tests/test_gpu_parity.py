@@ -119,11 +119,13 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
 
 # Every per-step tile variant of the ConvLSTM forward / BPTT GEMMs (runtime.hip
 # step_tile: 0 64x64, 1/2 split-K, 3 BK=128 split-K, 4-6 the LDS-DMA ring of
-# glds.h, 9 the 64x32 BPTT ring, 10-18 the 32x32 / 64x32 / 64x64 ring variants) must give the same answer;
+# glds.h, 9 the 64x32 BPTT ring, 10-18 the 32x32 / 64x32 / 64x64 ring variants, 27-29 the fp32
+# split-product BPTT rings -- bf16 maps them to 4) must give the same answer;
 # B=5 makes B*P = 605 pixels (ragged tiles).
 @pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 4), (7, 7), (4, 8), (4, 9),
                                      (6, 10), (6, 11), (12, 12), (14, 13), (17, 15), (18, 16),
-                                     (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24), (25, 16), (26, 16)])
+                                     (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24), (25, 16), (26, 16),
+                                     (4, 27), (4, 28), (4, 29), (4, 30), (4, 31)])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")   # the per-step launches (the frame-resident kernel: below)
@@ -154,10 +156,13 @@ def test_fused_x_part_both_ways(cuda, monkeypatch, fused, conv_dtype):
 
 
 # Every tile of the fused [x | h] forward step (runtime.hip AAA_FUSED_TILE: 4 128x64 8 waves,
-# 7 64x64, 8/10 3-stage rings, 9 128x128 4 waves (bf16 default), 11 2-way split-K, 12 128x64 4 waves).
-@pytest.mark.parametrize("tile", ["4", "7", "8", "9", "10", "11", "12"])
+# 7 64x64, 8/10 3-stage rings, 9 128x128 4 waves (bf16 default), 11 2-way split-K, 12 128x64 4 waves,
+# 13-16 the fp32 split-product tiles, 17/18 their split-K forms (K-slice partials + gate_fwd_zx)).
+@pytest.mark.parametrize("tile", ["4", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16", "17", "18"])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
+    if conv_dtype == "bf16" and int(tile) >= 13:
+        pytest.skip("fp32 split-product tiles (the bf16 path refuses them: test_fused_split_tiles_refuse_bf16)")
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")
     monkeypatch.setenv("AAA_FUSED_X", "1")
     monkeypatch.setenv("AAA_FUSED_TILE", tile)
@@ -167,6 +172,37 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
     else:
         _compare(_run_unroll(_agent(cuda, conv_dtype="bf16"), T, B, cuda), _oracle(T, B, conv_mode="bf16"), 2e-2,
                  f"bf16 fused tile {tile}: ")
+
+
+@pytest.mark.parametrize("tile,ns", [("30", "2"), ("30", "3"), ("30", "8"), ("31", "5")])
+def test_bptt_splitk_slices(cuda, monkeypatch, tile, ns):
+    """Split-K BPTT (fp32 tiles 30/31): K-slice partials of the dh dgrad summed
+    by the gate backward; slice counts that do not divide K's 64-deep tiles
+    evenly (3, 5) leave a short last slice."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
+    monkeypatch.setenv("AAA_BPTT_TILE", tile)
+    monkeypatch.setenv("AAA_BPTT_SPLITK", ns)
+    T, B = 4, 3
+    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"split-K tile {tile} x{ns}: ")
+
+
+@pytest.mark.parametrize("tile,ns", [("17", "2"), ("17", "4"), ("18", "4")])
+def test_fused_splitk_slices(cuda, monkeypatch, tile, ns):
+    """Split-K fused forward step: 2 and 4 K slices (27 k-tiles of 64: ragged)."""
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
+    monkeypatch.setenv("AAA_FUSED_X", "1")
+    monkeypatch.setenv("AAA_FUSED_TILE", tile)
+    monkeypatch.setenv("AAA_FUSED_SPLITK", ns)
+    T, B = 3, 2
+    _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"fused split-K {tile} x{ns}: ")
+
+
+def test_fused_split_tiles_refuse_bf16(cuda, monkeypatch):
+    monkeypatch.setenv("AAA_FRAMES_FWD", "0")
+    monkeypatch.setenv("AAA_FRAMES_BAND", "0")
+    monkeypatch.setenv("AAA_FUSED_TILE", "13")
+    with pytest.raises(RuntimeError, match="split-product"):
+        _run_unroll(_agent(cuda, conv_dtype="bf16"), 2, 2, cuda)
 
 
 # The frame-resident bf16 recurrence (csrc/recur.h: one workgroup per frame for

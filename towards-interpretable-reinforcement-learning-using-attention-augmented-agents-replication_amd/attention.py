@@ -401,7 +401,9 @@ class Agent(nn.Module):
         else:
             logits, values, attn = self._step(X.unsqueeze(0), pr, pa)
         self.last_attention = attn[0]
-        return logits[0], values[0]
+        # squeeze, not [0]: the same (B, A) view, but its backward is a view too
+        # (select_backward allocates zeros and copies: two launches per step)
+        return logits.squeeze(0), values.squeeze(0)
 
     # -- added API ----------------------------------------------------------
     def unroll(self, X, prev_reward=None, prev_action=None):

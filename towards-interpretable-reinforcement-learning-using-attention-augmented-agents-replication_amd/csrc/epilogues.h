@@ -36,6 +36,20 @@ struct EpiStoreT {
   }
 };
 
+// Split-K partial of a D^T store: K slice z of the launch writes
+// out[z*sls + j*ld + i..i+3] (glds.h with_z calls set_z); a later kernel sums
+// the slices in a fixed order (deterministic, unlike atomics).
+struct EpiSliceT {
+  float* out;
+  int ld, Mi, Nj;
+  size_t sls;
+  __device__ __forceinline__ void set_z(int z) { out += (size_t)z * sls; }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    store4(out + (size_t)j * ld + i, v0, v1, v2, v3);
+  }
+};
+
 // Stride-2 conv dgrad, one parity class (py, px): column j = (frame, a, b) of
 // the class grid (Ha x Wa) lands at output pixel (2a+py, 2b+px) of H1 x W1.
 struct EpiStoreParity {

@@ -82,6 +82,21 @@ template <class EP, class = void> struct has_acc : std::false_type {};
 template <class EP> struct has_acc<EP, std::void_t<typename EP::Acc>> : std::true_type {};
 template <class EP, bool> struct acc_of { using type = int; };
 template <class EP> struct acc_of<EP, true> { using type = typename EP::Acc; };
+// Epilogues that store one partial per K slice (EpiSliceT): the kernel hands
+// them the workgroup's slice index before any use (set_z on a local copy).
+template <class EP, class = void> struct has_set_z : std::false_type {};
+template <class EP>
+struct has_set_z<EP, std::void_t<decltype(std::declval<EP&>().set_z(0))>> : std::true_type {};
+template <class EP>
+__device__ __forceinline__ EP with_z(const EP& ep, int tz) {
+  if constexpr (has_set_z<EP>::value) {
+    EP e = ep;
+    e.set_z(tz);
+    return e;
+  } else {
+    return ep;
+  }
+}
 
 #ifdef AAA_STAMPS
 // Diagnostic builds only (tools/ubench): per-workgroup phase timestamps
@@ -564,7 +579,7 @@ __device__ __forceinline__ void staged_epilogue(const EP& ep, T* smem, const f32
 // loader's pieces spread evenly over the k steps (loaders with issue_part).
 template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, int ILV = 0>
 __global__ void __launch_bounds__(C::NT)
-gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
+gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, int kchunk, TileMap tm) {
   using T = typename C::type;
   constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ, WK = C::WK;
   constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
@@ -590,6 +605,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, i
   const int kb = tz * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke) return;
+  const EP ep = with_z(ep_, tz);
 
   LA la(pa, i0);
   LB lb(pb, j0);

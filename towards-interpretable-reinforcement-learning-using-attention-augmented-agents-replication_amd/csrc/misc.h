@@ -87,7 +87,8 @@ hipError_t colsum_multi(ColSums c, int M, hipStream_t st);
 template <typename TI> hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st);
 template <typename TZ, typename GT>
 hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const GT* gates, const float* cprev,
-                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st);
+                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st, int nsl = 1,
+                         size_t sls = 0);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
 template <typename T> hipError_t xh_to_state(int M, const T* xh, float* h, hipStream_t st);
@@ -97,7 +98,8 @@ template <typename T> hipError_t pack_conv(const float* w, int Cout, int Cin, in
 template <typename T>
 hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T* WpXH, hipStream_t st);
 template <typename T>
-hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st);
+hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st,
+                       const float* zs = nullptr, int nsl = 0, size_t sls = 0, const float* bias = nullptr);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);
 template <typename T, typename TI> hipError_t frames_rgbx(int F, int H, int W, const TI* x, T* y, hipStream_t st);
 template <typename T> hipError_t pack_conv2_classes(const float* w2, T* dst, hipStream_t st);

@@ -583,11 +583,14 @@ __global__ void k_colsum(const TI* __restrict__ X, int ld, int M, int N, int row
 // One workgroup per tile of ``bj`` pixels (the BPTT GEMM's column tile), 128
 // channels x 4 pixel lanes; dz is stored as TZ and, when ``part`` is set, the
 // tile's fp32 gate-bias partials go to part[tile][512] (EpiConvLstmBwd::flush).
+// nsl > 1: dhT holds nsl split-K partials (stride sls floats) of the BPTT dgrad
+// (EpiSliceT), summed in slice order -- the gate backward of any step t-1 of a
+// split-K BPTT chain (rt_backward.hip tiles 30/31).
 template <typename TZ, typename GT>
 __global__ void __launch_bounds__(512)
 k_gate_bwd_last(int M, int bj, const float* __restrict__ dO, const float* __restrict__ dhT,
                 const GT* __restrict__ gates, const float* __restrict__ cprev, const float* __restrict__ ccur,
-                float* dC, TZ* dz, float* part) {
+                float* dC, TZ* dz, float* part, int nsl, size_t sls) {
   __shared__ f32x4 red[4][128];
   const int ch = threadIdx.x & 127, sl = threadIdx.x >> 7;
   const int m0 = blockIdx.x * bj, m1 = min(M, m0 + bj);
@@ -595,7 +598,10 @@ k_gate_bwd_last(int M, int bj, const float* __restrict__ dO, const float* __rest
 #pragma unroll 4
   for (int m = m0 + sl; m < m1; m += 4) {
     const size_t idx = (size_t)m * 128 + ch;
-    const float dh = dO[idx] + (dhT ? dhT[idx] : 0.f);
+    float dh = dO[idx];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)   // <= kBpttSplitMax slices, summed in order
+      if (k < nsl) dh += dhT[k * sls + idx];
     const f32x4 g = load_gates(gates + (size_t)m * 512 + 4 * ch);
     float dc = dC[idx], di, df, dcg, dout;
     gate_bwd(dh, g, cprev[idx], ccur[idx], dc, di, df, dcg, dout);
@@ -812,13 +818,28 @@ __global__ void k_pack_lstm_all(LstmPtrs L, T* WpX, T* WpH, float* bl, T* WdT, T
 }
 
 // Step 0 from a zero state: the gates come from the batched x-part alone.
+// nsl > 0 (the split-K fused step, rt.h fused_step tiles 17/18): the gate
+// pre-activations are bias + the nsl K-slice partials zs[k*sls + m*512 + ..]
+// (EpiSliceT), summed in slice order, instead of ``gates``' contents.
 template <typename T>
 __global__ void k_gate_fwd_zx(int M, const float* __restrict__ cprev, float* gates, float* cnext, float* hout,
-                              T* xhnext) {
+                              T* xhnext, const float* __restrict__ zs, int nsl, size_t sls,
+                              const float* __restrict__ bias) {
   const int n = M * 128;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
     const int m = idx >> 7, ch = idx & 127;
-    const f32x4 z = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
+    f32x4 z;
+    if (nsl > 0) {
+      z = *reinterpret_cast<const f32x4*>(bias + 4 * ch);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < nsl) {
+          const f32x4 u = *reinterpret_cast<const f32x4*>(zs + k * sls + (size_t)m * 512 + 4 * ch);
+          z[0] += u[0]; z[1] += u[1]; z[2] += u[2]; z[3] += u[3];
+        }
+    } else {
+      z = *reinterpret_cast<const f32x4*>(gates + (size_t)m * 512 + 4 * ch);
+    }
     float gi, gf, gc, go, c, h;
     GateFwd::run(z[0], z[1], z[2], z[3], cprev[idx], gi, gf, gc, go, c, h);
     cnext[idx] = c;
@@ -1119,9 +1140,9 @@ hipError_t colsum(const TI* X, int ld, int M, int N, float* out, hipStream_t st)
 
 template <typename TZ, typename GT>
 hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const GT* gates, const float* cprev,
-                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st) {
+                         const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st, int nsl, size_t sls) {
   hipLaunchKernelGGL((k_gate_bwd_last<TZ, GT>), dim3((M + bj - 1) / bj), dim3(512), 0, st, M, bj, dO, dhT, gates,
-                     cprev, ccur, dC, dz, part);
+                     cprev, ccur, dC, dz, part, dhT ? nsl : 0, sls);
   return hipGetLastError();
 }
 
@@ -1173,9 +1194,10 @@ hipError_t pack_lstm_all(const LstmPtrs& L, T* WpX, T* WpH, T* WdT, float* bl, T
 
 template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext,
-                       hipStream_t st) {
+                       hipStream_t st, const float* zs, int nsl, size_t sls, const float* bias) {
+  if (nsl > 0 && (!zs || !bias || nsl > 8)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_gate_fwd_zx<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, cprev, gates, cnext, hout,
-                     xhnext);
+                     xhnext, zs, nsl, sls, bias);
   return hipGetLastError();
 }
 
@@ -1224,13 +1246,13 @@ hipError_t unpack_conv1_rgbx(const float* g, float* dst, hipStream_t st) {
 template hipError_t colsum<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t colsum<__bf16>(const __bf16*, int, int, int, float*, hipStream_t);
 template hipError_t gate_bwd_last<float, float>(int, int, const float*, const float*, const float*, const float*,
-                                                const float*, float*, float*, float*, hipStream_t);
+                                                const float*, float*, float*, float*, hipStream_t, int, size_t);
 template hipError_t gate_bwd_last<__bf16, float>(int, int, const float*, const float*, const float*, const float*,
-                                                 const float*, float*, __bf16*, float*, hipStream_t);
+                                                 const float*, float*, __bf16*, float*, hipStream_t, int, size_t);
 template hipError_t gate_bwd_last<float, _Float16>(int, int, const float*, const float*, const _Float16*,
-                                                   const float*, const float*, float*, float*, float*, hipStream_t);
+                                                   const float*, const float*, float*, float*, float*, hipStream_t, int, size_t);
 template hipError_t gate_bwd_last<__bf16, _Float16>(int, int, const float*, const float*, const _Float16*,
-                                                    const float*, const float*, float*, __bf16*, float*, hipStream_t);
+                                                    const float*, const float*, float*, __bf16*, float*, hipStream_t, int, size_t);
 template hipError_t frames_rgbx<float, float>(int, int, int, const float*, float*, hipStream_t);
 template hipError_t frames_rgbx<__bf16, float>(int, int, int, const float*, __bf16*, hipStream_t);
 template hipError_t frames_rgbx<float, uint8_t>(int, int, int, const uint8_t*, float*, hipStream_t);
@@ -1251,8 +1273,10 @@ template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStr
 template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);
 template hipError_t pack_lstm_all<float>(const LstmPtrs&, float*, float*, float*, float*, float*, hipStream_t);
 template hipError_t pack_lstm_all<__bf16>(const LstmPtrs&, __bf16*, __bf16*, __bf16*, float*, __bf16*, hipStream_t);
-template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t);
-template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t);
+template hipError_t gate_fwd_zx<float>(int, const float*, float*, float*, float*, float*, hipStream_t, const float*, int, size_t,
+                                         const float*);
+template hipError_t gate_fwd_zx<__bf16>(int, const float*, float*, float*, float*, __bf16*, hipStream_t, const float*, int, size_t,
+                                         const float*);
 
 template <typename T>
 hipError_t pack_all(const PackAll<T>& a, hipStream_t st) {

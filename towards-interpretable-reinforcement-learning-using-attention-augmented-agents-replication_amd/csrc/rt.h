@@ -67,7 +67,7 @@ struct Layout {
   size_t poff[NPARAM], psz[NPARAM], ptotal;
   size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_Wf6, k_Wb6, k_WdTl, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
-  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags, xpart;
+  size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags, xpart, dhs;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;
   // stateful core: state slots, per-step query activations, [answer | h] rows, their grads
   size_t CH, CC, AOX, Qf, q1s, q2s, dAOX, dQf, dq2s, dq1s, dhc, dcc, gWihhp;
@@ -221,11 +221,14 @@ static int chunk_steps(const Layout& L) {
   const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : L.T);
   return std::max(1, std::min({c, L.T, L.fchunk / L.B}));
 }
+bool f32_split6();   // fp32 path: large GEMMs as bf16x6 split products (rt_core.hip)
 static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = false) {
   const int v = env_int(env, -1);
   if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
-    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || (v >= 19 && v <= 24);
+    const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || (v >= 19 && v <= 24) ||
+                           (v >= 27 && v <= 31);
     if (v >= 19 && v <= 24 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
+    if (v >= 27 && v <= 31 && bf16) return 4;    // 27-31: fp32 split-product BPTT tiles (30/31 split-K)
     const bool fwd_only = v == 14 || v == 17 || v == 18 || v == 25 || v == 26;
     return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
   }
@@ -238,8 +241,23 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
   // per CU whose barriers are not in step (51.6 vs 54.4 us for 64x32 BK128, 54.6 vs 55.9 for
   // 32x64); 64x64 BK64 forward 47.4 us (32x64 / 32x32 / 64x32 split-K rings: 52-55 us)
   // (bench.py kernel table, tools/ab_bptt.sh)
-  if (bptt) return out_tiles32 < 1024 ? 16 : (out_tiles32 < 1536 ? 1 : 0);
+  // fp32 with f32_split6(): below 1024 tiles (the B=1 episode / actor: 68) the split-product
+  // twin of 16, tile 27 (C2 itself runs the frame-group BPTT, recur_bwd_f32.h)
+  if (bptt) return out_tiles32 < 1024 ? (f32_split6() ? 27 : 16) : (out_tiles32 < 1536 ? 1 : 0);
   return out_tiles32 < 1024 ? 5 : 6;
+}
+
+// Split-K BPTT (fp32 tiles 30/31): K slices of the per-step dh dgrad, summed by
+// the gate backward (misc.hip k_gate_bwd_last).  Only where the step has few
+// output tiles (the B=1 episode: 4 x 17), so the partials stay small.
+constexpr int kBpttSplitMax = 8;
+constexpr int kSplitBj = 8;   // pixels per gate-backward workgroup (and gate-bias partial row) of the split-K chain
+static bool bptt_splitk_fits(int M) { return 4L * ((M + 31) / 32) < 1024; }
+static int bptt_splitk() { return std::max(2, std::min(kBpttSplitMax, env_int("AAA_BPTT_SPLITK", 4))); }
+// K slices launch_pipe actually runs for a requested nsplit (glds.h: whole BK tiles per slice)
+inline int splitk_slices(int K, int BK, int nsplit) {
+  const int kc = ((K + nsplit - 1) / nsplit + BK - 1) / BK * BK;
+  return (K + kc - 1) / kc;
 }
 
 // fp16 gate-activation storage (halves the step epilogues' largest stream):
@@ -274,13 +292,14 @@ constexpr bool pipe_even() {
 // otherwise the register-staged kernel (which can convert fp32 -> bf16).
 template <class CK, bool PIPE, typename T, typename G, class EP, int NBUF = 2, bool ILV = false>
 static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const ConvGeo& g, int M, uint32_t src_bytes,
-                            const EP& ep, int Mi, int K, hipStream_t st) {
+                            const EP& ep, int Mi, int K, hipStream_t st, int nsplit = 1) {
   if constexpr (PIPE && pipe_even<CK>() && std::is_same<G, T>::value) {
     using LA = GRowsB<T, CK::BI, CK::BK, CK::NT>;
     using LB = GIm2colB<T, CK::BJ, CK::BK, CK::NT>;
     return launch_pipe<CK, LA, LB, EP, NBUF, ILV>(typename LA::Params{W, ldw, wrows},
-                                                  typename LB::Params{src, g, M, src_bytes}, ep, Mi, M, K, 1, st);
+                                                  typename LB::Params{src, g, M, src_bytes}, ep, Mi, M, K, nsplit, st);
   } else {
+    if (nsplit != 1) return hipErrorInvalidValue;   // split-K: ring tiles only
     using LA = LdRowsB<T, T, CK::BI, CK::BK, CK::NT>;
     using LB = LdIm2colB<G, T, CK::BJ, CK::BK, CK::NT>;
     return launch_gemm<CK, LA, LB>(typename LA::Params{W, ldw, wrows}, typename LB::Params{src, g, M, src_bytes}, ep,
@@ -429,16 +448,70 @@ static int wgrad_splits(int tiles, int K, int BK) {
 // epilogue ``ep``.  Tile: AAA_FUSED_TILE, default bf16 128x128 of 4 waves
 // (64x64 per wave; tools/ab_fused.sh), fp32 (small M only, e.g. the B=1 actor
 // and the standalone cell) 128x64 of 8 waves.
+// zpart (fp32, B*P < 8192: Layout::dhs) enables the split-K tiles 17/18: K-slice
+// partials of the gate pre-activations, then the cell in gate_fwd_zx.
+static int fused_splitk() { return std::max(2, std::min(4, env_int("AAA_FUSED_SPLITK", 3))); }
+// Ring depth of the split-K launches (2-4 stages: tiles in flight per workgroup; their few
+// k-steps per slice are latency-bound, not MFMA-bound).  AAA_SPLITK_NBUF.
+static int splitk_nbuf() { return std::max(2, std::min(4, env_int("AAA_SPLITK_NBUF", 2))); }
+template <class CK, class EP, typename T>
+static hipError_t step_gemm_splitk(const T* W, int ldw, int wrows, const T* src, const ConvGeo& g, int M,
+                                   uint32_t src_bytes, const EP& ep, int Mi, int K, hipStream_t st, int nsplit,
+                                   bool ilv = false) {
+  switch (splitk_nbuf() * 2 + (ilv ? 1 : 0)) {
+    case 4: return step_gemm<CK, true, T, T, EP, 2, false>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+    case 5: return step_gemm<CK, true, T, T, EP, 2, true>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+    case 6: return step_gemm<CK, true, T, T, EP, 3, false>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+    case 7: return step_gemm<CK, true, T, T, EP, 3, true>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+    case 8: return step_gemm<CK, true, T, T, EP, 4, false>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+    default: return step_gemm<CK, true, T, T, EP, 4, true>(W, ldw, wrows, src, g, M, src_bytes, ep, Mi, K, st, nsplit);
+  }
+}
 template <typename T, typename GT>
 static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const EpiConvLstmFwd<T, GT>& ep,
-                      hipStream_t st) {
+                      hipStream_t st, float* zpart = nullptr) {
   using EF = EpiConvLstmFwd<T, GT>;
   const ConvGeo g = ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
-  const int ftile = env_int("AAA_FUSED_TILE", std::is_same<T, float>::value ? 4 : 9);
+  constexpr bool f32 = std::is_same<T, float>::value;
+  // fp32 with f32_split6(): the split-product tiles 13-16 (bf16x6 on the bf16
+  // MFMA), default 13 = 32x64 BK64 with a 4-way in-WG split-K -- 144 WGs of 8
+  // waves at the B=1 episode's 27x20 grid instead of 36 of the 128x64 tile
+  const int ftile = env_int("AAA_FUSED_TILE", f32 ? (f32_split6() ? 13 : 4) : 9);
   TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728,
-                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d [kernel: EpiConvLstmFwd]",
-                      std::is_same<T, float>::value ? "fp32" : "bf16", ftile));
+                 strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d%s [kernel: EpiConvLstmFwd]", f32 ? "fp32" : "bf16",
+                      ftile, f32 && ftile >= 13 && ftile <= 16 ? " (bf16x6 split products)" : ""));
+  if (ftile == 17 || ftile == 18) {   // split-K (bf16x6 split products)
+    if constexpr (!f32 || !std::is_same<GT, float>::value) {
+      return fail(AAA_E_ARG, "AAA_FUSED_TILE %d: fp32 split-product tiles only", ftile);
+    } else {
+      if (!zpart || !ep.bias) return fail(AAA_E_ARG, "AAA_FUSED_TILE %d: split-K needs B*P < 8192 (got %d)", ftile, M);
+      const int ns = splitk_slices(1728, 64, fused_splitk());
+      const EpiSliceT es{zpart, 512, 512, M, (size_t)M * 512};
+      if (ftile == 17)
+        HIPCHK((step_gemm_splitk<GemmCfgS6<32, 64, 64, 1, 2, 4>>(WpXH, 1728, 512, xht, g, M, xh_bytes, es, 512, 1728,
+                                                                 st, ns)));
+      else
+        HIPCHK((step_gemm_splitk<GemmCfgS6<64, 64, 64, 2, 2, 2>>(WpXH, 1728, 512, xht, g, M, xh_bytes, es, 512, 1728,
+                                                                 st, ns)));
+      HIPCHK(gate_fwd_zx<T>(M, ep.cprev, ep.gates, ep.cnext, ep.hout, ep.xhnext, st, zpart, ns, (size_t)M * 512,
+                            ep.bias));
+      return AAA_OK;
+    }
+  }
+  if (ftile >= 13 && ftile <= 16) {
+    if constexpr (!f32) return fail(AAA_E_ARG, "AAA_FUSED_TILE %d: fp32 split-product tiles only", ftile);
+    else if (ftile == 13)
+      HIPCHK((step_gemm<GemmCfgS6<32, 64, 64, 1, 2, 4>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+    else if (ftile == 14)
+      HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+    else if (ftile == 15)
+      HIPCHK((step_gemm<GemmCfgS6<128, 64, 32, 4, 2>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
+    else
+      HIPCHK((step_gemm<GemmCfgS6<32, 32, 64, 1, 1, 4>, true, T, T, EF, 3>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep,
+                                                                             512, 1728, st)));
+    return AAA_OK;
+  }
   if (ftile == 7)
     HIPCHK((step_gemm<CfgFor<T>, true>(WpXH, 1728, 512, xht, g, M, xh_bytes, ep, 512, 1728, st)));
   else if (ftile == 8)   // 128x64, 8 waves, 3-stage ring

@@ -698,14 +698,17 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     const int bwd_tile = step_tile((long)(128 / 32) * cdiv(M, 32), "AAA_BPTT_TILE", true, L.dt == AAA_BF16);
     // pipe (glds.h) tiles reduce the gate-bias partials in their epilogue;
     // the register-staged ones leave the bias to a column sum over dZ
-    const int bj = bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 || bwd_tile == 22 || bwd_tile == 23 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64));
+    // (split-K tiles 30/31: the gate backward kernel's pixel tile, kSplitBj -- finer than the GEMM's, so
+    // that kernel spreads over the chip)
+    const int bj = bwd_tile == 30 || bwd_tile == 31 ? kSplitBj : (bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 || bwd_tile == 22 || bwd_tile == 23 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64)));
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
                       (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 || bwd_tile >= 19 ||
                       (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>()) ||
                       (bwd_tile == 10 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 4>>()) ||
                       ((bwd_tile == 11 || bwd_tile == 12 || bwd_tile == 16) && pipe_even<GemmCfg<T, 32, 32, 64, 1, 1, 4>>()) ||
                       (bwd_tile == 13 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 8>>()) ||
-                      (bwd_tile == 15 && pipe_even<GemmCfg<T, 64, 32, 64, 2, 1, 4>>());
+                      (bwd_tile == 15 && pipe_even<GemmCfg<T, 64, 32, 64, 2, 1, 4>>()) ||
+                      (bwd_tile >= 27 && bwd_tile <= 31);   // fp32 split-product tiles (ring only)
     const int ntj = cdiv(M, bj);
     float* part = pipe ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
@@ -792,6 +795,27 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       const ConvGeo g = ConvGeo{512, 512, 0, L.h, L.w, L.h, L.w, 3, 1, 1, 1}.prep();
       const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608, strf("%s dh dgrad + fused gate bwd, K=4608, AAA_BPTT_TILE %d%s", std::is_same<T, float>::value ? "fp32" : "bf16", bwd_tile, g16 ? ", fp16 gates [kernel: EpiConvLstmBwd]" : " [kernel: EpiConvLstmBwd]"));
+      if constexpr (std::is_same<T, float>::value) {
+        if ((bwd_tile == 30 || bwd_tile == 31) && prev) {   // split-K: K-slice partials, then the gate backward
+          if (!L.dhs) return fail(AAA_E_ARG, "AAA_BPTT_TILE %d: split-K needs B*P < 8192 (got %d)", bwd_tile, M);
+          const int bk = bwd_tile == 30 ? 64 : 128;
+          const int ns = splitk_slices(4608, bk, bptt_splitk());   // as launch_pipe rounds it
+          float* dhp = Wf(L.dhs);
+          const EpiSliceT es{dhp, 128, 128, M, (size_t)M * 128};
+          if (bwd_tile == 30)   // tile 27's shape
+            HIPCHK((step_gemm_splitk<GemmCfgS6<32, 32, 64, 1, 1, 4>>(WdTh, 4608, 128, dzt, g, M, dz_bytes, es, 128,
+                                                                     4608, st, ns)));
+          else                  // tile 28's shape (interleaved DMA)
+            HIPCHK((step_gemm_splitk<GemmCfgS6<32, 32, 128, 1, 1, 8>>(WdTh, 4608, 128, dzt, g, M, dz_bytes, es, 128,
+                                                                      4608, st, ns, true)));
+          HIPCHK((gate_bwd_last<T, float>(M, bj, Wf(L.dO) + (size_t)(t - 1) * M * 128, dhp,
+                                          Wf(L.Gt) + (size_t)(t - 1) * M * 512, Wf(L.Cst) + (size_t)(t - 1) * M * 128,
+                                          Wf(L.Cst) + (size_t)t * M * 128, Wf(L.dC), Wt(L.dZ) + (size_t)(t - 1) * M * 512,
+                                          part ? part + (size_t)(t - 1) * ntj * 512 : nullptr, st, ns,
+                                          (size_t)M * 128)));
+          continue;
+        }
+      }
       auto step = [&](auto gtag) -> hipError_t {
         using GT = decltype(gtag);
         using EB = EpiConvLstmBwd<T, GT>;
@@ -832,7 +856,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                                                                        4608, st);
         } else {
           // tiles 19-24 other than 22 exist for fp16 gate storage only: fail loudly, never fall back
-          if (bwd_tile >= 19 && bwd_tile != 22) return hipErrorInvalidValue;
+          if (bwd_tile >= 19 && bwd_tile <= 24 && bwd_tile != 22) return hipErrorInvalidValue;
           switch (bwd_tile) {
             case 1: return step_gemm<CfgKFor<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
             case 2: return step_gemm<CfgK4For<T>, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
@@ -875,6 +899,28 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
             case 16:   // 32x32, BK64, 4-way in-WG split-K, 3-stage ring, DMA issued before the MFMAs
               return step_gemm<GemmCfg<T, 32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, false>(WdTh, 4608, 128, dzt, g, M,
                                                                                          dz_bytes, ep, 128, 4608, st);
+            // 27-29: fp32 as bf16x6 split products (gemm.h SPLIT6) on the small-batch shapes
+            case 27:   // tile 16's shape
+              if constexpr (!std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfgS6<32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, false>(WdTh, 4608, 128, dzt, g,
+                                                                                              M, dz_bytes, ep, 128,
+                                                                                              4608, st);
+            case 28:   // 32x32, BK128, 8-way in-WG split-K (8 waves), 2-stage ring
+              if constexpr (!std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfgS6<32, 32, 128, 1, 1, 8>, true, T, T, EB, 2, true>(WdTh, 4608, 128, dzt, g,
+                                                                                              M, dz_bytes, ep, 128,
+                                                                                              4608, st);
+            case 30:   // split-K tiles: t = 0 (dh0) takes tile 27
+            case 31:
+              if constexpr (!std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfgS6<32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, false>(WdTh, 4608, 128, dzt, g,
+                                                                                              M, dz_bytes, ep, 128,
+                                                                                              4608, st);
+            case 29:   // 64x32, BK128, 4-way in-WG split-K, 3-stage ring
+              if constexpr (!std::is_same<T, float>::value) return hipErrorInvalidValue;
+              else return step_gemm<GemmCfgS6<64, 32, 128, 2, 1, 4>, true, T, T, EB, 3, true>(WdTh, 4608, 128, dzt, g,
+                                                                                              M, dz_bytes, ep, 128,
+                                                                                              4608, st);
             default: return step_gemm<C, false>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ep, 128, 4608, st);
           }
         }

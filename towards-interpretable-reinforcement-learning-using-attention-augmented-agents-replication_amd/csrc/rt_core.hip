@@ -110,12 +110,18 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.dQp = take(F * L.qd * 4);
   L.dC = take(M * 128 * 4);
   L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
-  L.dZp = take((size_t)L.T * std::max((M + 31) / 32, 2 * (size_t)L.B) * 512 * 4);  // gate-bias partials per (step, column tile | frame half)
+  // gate-bias partials per (step, column tile | frame half); the fp32 split-K chain's tiles are kSplitBj pixels
+  const size_t zp_rows = std::max({(M + 31) / 32, 2 * (size_t)L.B,
+                                   L.esz == 4 && bptt_splitk_fits(M) ? (M + kSplitBj - 1) / kSplitBj : 0});
+  L.dZp = take((size_t)L.T * zp_rows * 512 * 4);
   L.dY2 = take(F * P * 64 * e);       // conv-input grads in the operand type of the GEMMs reading them
   L.dY1 = take(F * L.P1 * 32 * e);
   L.dxb = take((size_t)L.B * 64 * 4);   // conv2 bias-gradient partials per frame (frame-resident BPTT)
   L.rflags = take((size_t)8 * L.B * 4);   // hand-off flags of the multi-workgroup frame kernels ([B][G], G <= 8)
   L.xpart = take(L.esz == 4 && rec_fits(L.h, L.w) ? b32_xpart_floats(L.B) * 4 : 0);   // fp32 frame-group BPTT exchange
+  // split-K partials: BPTT dh (<= kBpttSplitMax x 128 per pixel) or the fused forward step's gates (<= 4 x 512)
+  // (0 = none: the split-K tiles then fail loudly)
+  L.dhs = L.esz == 4 && bptt_splitk_fits(M) ? take((size_t)std::max(kBpttSplitMax * 128, 4 * 512) * M * 4) : 0;
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);

@@ -260,7 +260,8 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
         EpiConvLstmFwd<T, GT> ep{Wf(L.Cst) + (size_t)t * M * 128, Wf(L.Cst) + (size_t)(t + 1) * M * 128,
                                  hs_out(t), Wt(L.XH) + (size_t)(t + 1) * M * 192,
                                  (GT*)(ws + L.Gt) + (size_t)t * M * 512, M, (const float*)(pk + L.k_bl)};
-        const int rc = fused_step<T, GT>(WpXH, Wt(L.XH) + (size_t)t * M * 192, L.h, L.w, M, ep, st);
+        const int rc = fused_step<T, GT>(WpXH, Wt(L.XH) + (size_t)t * M * 192, L.h, L.w, M, ep, st,
+                                         L.dhs ? Wf(L.dhs) : nullptr);
         if (rc) return rc;
       }
       return AAA_OK;

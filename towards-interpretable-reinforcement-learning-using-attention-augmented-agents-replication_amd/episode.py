@@ -76,7 +76,9 @@ class _EpisodeStepFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dl, dv, _dattn, dh, dc):
         ctx.ep.stash(ctx.t, dl, dv, dh, dc)
-        return None, None, torch.zeros((), device=ctx.ep.device)
+        # no cotangent for the anchor: the edge alone orders its backward after
+        # this node (a zeros() here cost a fill + an accumulate launch per step)
+        return None, None, None
 
 
 class Episode:
