@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 6
+#define AAA_ABI_VERSION 7
 
 enum aaa_status {
   AAA_OK = 0,
@@ -155,6 +155,34 @@ int aaa_pack_weights(const aaa_cfg* cfg, const float* params, void* packed, hipS
 
 /* T-step forward from reset(); replaces T calls of Agent.forward. */
 int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream);
+
+/* Forward phases (aaa_forward_phases).  Skipping CORE leaves the ConvLSTM
+ * recurrence out: its per-step products -- gate activations, c_t, h_t of
+ * every step -- must already be in the workspace (aaa_core_import), as the
+ * fused episode backward does with the products each per-step call of the
+ * episode exported (episode.py).  VISION and TAIL always run. */
+enum aaa_fwd_phase {
+  AAA_FWD_VISION = 1,  /* conv1 + conv2 over all T*B frames                   */
+  AAA_FWD_CORE = 2,    /* the ConvLSTM recurrence                             */
+  AAA_FWD_TAIL = 4,    /* attention readout, answer MLP, LSTMCell, heads      */
+  AAA_FWD_ALL = 7
+};
+/* aaa_forward with a phase mask: AAA_FWD_ALL, or AAA_FWD_VISION |
+ * AAA_FWD_TAIL (fp32 configs).  Replaces the recomputation half of the
+ * reference's per-step graph (main_mp.py:54 -> attention.py:110-126). */
+int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
+
+/* The ConvLSTM products of steps [t0, t0+n) between an aaa_forward workspace
+ * and flat fp32 buffers: gates (n, B*h*w, 512) post-activation (i, f, c~, o
+ * interleaved per channel), c (n, B*h*w, 128) = c_t, h (n, B*h*w, 128) = h_t
+ * (pixel-major, channel fastest).  Export reads a workspace aaa_forward
+ * filled; import writes one for aaa_forward_phases without CORE (and the h
+ * half of the [x | h] operand slots).  fp32 configs only; device pointers,
+ * stream-ordered, no host sync. */
+int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, float* gates, float* c, float* h,
+                    hipStream_t stream);
+int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const float* gates, const float* c,
+                    const float* h, hipStream_t stream);
 
 /* Backward of the loss sum(logits*dlogits)+sum(values*dvalues) (+ state
  * cotangents) through the saved activations of the matching aaa_forward.

@@ -68,11 +68,16 @@ def _cmp(a, b, tol, what):
             assert rel_err(a[n].numpy(), b[n].numpy()) <= tol, f"{what} {n}: {rel_err(a[n].numpy(), b[n].numpy()):.3e}"
 
 
-@pytest.mark.parametrize("T,B,seg,u8,extras", [(9, 2, 4, True, False), (7, 3, 64, False, True), (70, 1, 64, True, True)])
-def test_episode_matches_per_step_path(cuda, monkeypatch, T, B, seg, u8, extras):
+@pytest.mark.parametrize("T,B,seg,u8,extras,store", [(9, 2, 4, True, False, "1"), (7, 3, 64, False, True, "1"),
+                                                    (70, 1, 64, True, True, "1"), (9, 2, 4, True, False, "0"),
+                                                    (37, 1, 64, True, False, "1")])
+def test_episode_matches_per_step_path(cuda, monkeypatch, T, B, seg, u8, extras, store):
     """Segments of 4 (3 segments, ragged last), one segment, and 70 steps over
-    the default 64-step segment; uint8 and fp32 frames; prev_reward/action."""
+    the default 64-step segment; uint8 and fp32 frames; prev_reward/action;
+    the kept ConvLSTM products (16-step blocks, a ragged last block at 37) or
+    the recomputed recurrence (AAA_EPISODE_STORE=0)."""
     monkeypatch.setattr(E, "EPISODE_SEGMENT", seg)
+    monkeypatch.setenv("AAA_EPISODE_STORE", store)
     X = _frames(T, B)
     Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
     Gv = torch.from_numpy(detinit.normal(3, (T, B, A)))
@@ -160,9 +165,13 @@ def test_parameter_change_starts_new_episode(cuda, monkeypatch):
     _cmp(gf, gr, 1e-5, "parameter change")
 
 
-def test_episode_memory_per_step(cuda):
-    """The graph of a 210x160 episode keeps well under 1 MB per step (frames +
-    a state checkpoint every 64 steps), not a T=1 workspace per step."""
+@pytest.mark.parametrize("store", ["1", "0"])
+def test_episode_memory_per_step(cuda, monkeypatch, store):
+    """The graph of a 210x160 episode keeps a bounded amount per step, not a
+    T=1 workspace (12.6 MB): frames + a state checkpoint every 64 steps (< 1 MB
+    with AAA_EPISODE_STORE=0), plus the ConvLSTM products the backward imports
+    instead of re-running the recurrence (1.66 MB, in 16-step blocks: < 3 MB)."""
+    monkeypatch.setenv("AAA_EPISODE_STORE", store)
     ag = attention.Agent(A).to(cuda)
     detinit.load_into(ag, detinit.deterministic_params(0, A))
     ag.to(cuda)
@@ -178,7 +187,7 @@ def test_episode_memory_per_step(cuda):
         loss = loss + lg.sum()
     torch.cuda.synchronize()
     per_step = (torch.cuda.memory_allocated(cuda) - base) / (T - 1)
-    assert per_step < 1 << 20, per_step
+    assert per_step < (3 << 20 if store == "1" else 1 << 20), per_step
     loss.backward()
 
 
@@ -193,3 +202,50 @@ def test_inplace_modified_frames_raise(cuda):
     X[1].add_(1)          # the frames of step 1 change under the recorded episode
     with pytest.raises(RuntimeError, match="modified in place"):
         loss.backward()
+
+
+@pytest.mark.parametrize("u8", [True, False])
+def test_core_import_replaces_the_recurrence(cuda, u8):
+    """aaa_core_export of a full forward's ConvLSTM products, imported in two
+    pieces into a fresh workspace, then aaa_forward_phases without CORE: the
+    same logits bit for bit and the same gradients (up to the wgrad atomics'
+    summation order) as the full forward + backward."""
+    from aaa_amd import _native as N
+    T, B = 5, 2
+    ag = _agent(cuda, False)
+    r = ag._runner(B, T, 84, 84, cuda, False, u8)
+    S = ag._basis_for(r.h, r.w, 84, 84, cuda)
+    flat, packed = ag._packed_params(r, list(ag.parameters()))
+    X = _frames(T, B).to(cuda)
+    X = X if u8 else X.float()
+    dl = torch.from_numpy(detinit.normal(2, (T, B, A))).to(cuda)
+    dv = torch.from_numpy(detinit.normal(3, (T, B, A))).to(cuda)
+    ws1 = r.new_workspace()
+    l1, v1, _, _, _ = r.forward(flat, packed, S, X, ws1, want_attn=False)
+    core = [torch.empty(s, device=cuda) for s in r.core_shapes(T)]
+    r.core_export(ws1, 0, T, *core)
+    g1, _, _ = r.backward(flat, packed, S, X, ws1, dl, dv)
+    ws2 = r.new_workspace()
+    for t0, n in ((0, 2), (2, 3)):
+        r.core_import(ws2, t0, n, *(x[t0:t0 + n] for x in core))
+    l2, v2, _, _, _ = r.forward(flat, packed, S, X, ws2, want_attn=False, phases=N.FWD_VISION | N.FWD_TAIL)
+    g2, _, _ = r.backward(flat, packed, S, X, ws2, dl, dv)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(v1, v2)
+    assert rel_err(g2.cpu().numpy(), g1.cpu().numpy()) < 1e-6
+    with pytest.raises(ValueError, match="contiguous fp32"):
+        r.core_import(ws2, 0, 2, core[0][:1], core[1][:2], core[2][:2])
+
+
+def test_core_transfer_refuses_bf16_and_bad_ranges(cuda):
+    ag = _agent(cuda, False, dtype="bf16")
+    r = ag._runner(2, 3, 84, 84, cuda, False, True)
+    ws = r.new_workspace()
+    core = [torch.empty(s, device=cuda) for s in r.core_shapes(3)]
+    with pytest.raises(RuntimeError, match="fp32 configs only"):
+        r.core_export(ws, 0, 3, *core)
+    agf = _agent(cuda, False)
+    rf = agf._runner(2, 3, 84, 84, cuda, False, True)
+    core = [torch.empty(s, device=cuda) for s in rf.core_shapes(2)]
+    with pytest.raises(RuntimeError, match="steps"):
+        rf.core_export(rf.new_workspace(), 2, 2, *core)

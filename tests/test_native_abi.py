@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.load().aaa_abi_version() == N.ABI_VERSION == 6
+    assert N.load().aaa_abi_version() == N.ABI_VERSION == 7
 
 
 @pytest.mark.parametrize("H,W,hw", [(84, 84, (11, 11)), (168, 168, (21, 21)), (210, 160, (27, 20))])

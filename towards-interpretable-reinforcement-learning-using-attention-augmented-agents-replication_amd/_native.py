@@ -15,9 +15,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 6   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 7   # include/aaa.h AAA_ABI_VERSION
 E_STRANDED = -5   # AAA_E_STRANDED
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
+FWD_VISION, FWD_CORE, FWD_TAIL, FWD_ALL = 1, 2, 4, 7
 
 # Every symbol include/aaa.h declares (checked by tests/test_native_abi.py).
 EXPORTS = (
@@ -29,7 +30,7 @@ EXPORTS = (
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
     "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag", "aaa_debug_pair_spin",
-    "aaa_adam_step_guarded",
+    "aaa_adam_step_guarded", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
 )
 # include/aaa.h enum aaa_timer
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
@@ -114,6 +115,9 @@ def load(path: str = LIB_PATH):
             "aaa_pack_weights": (I, [CP, P, P, P]),
             "aaa_forward": (I, [CP, ctypes.POINTER(IO), P]),
             "aaa_backward": (I, [CP, ctypes.POINTER(IO), I, P]),
+            "aaa_forward_phases": (I, [CP, ctypes.POINTER(IO), I, P]),
+            "aaa_core_export": (I, [CP, P, I, I, P, P, P, P]),
+            "aaa_core_import": (I, [CP, P, I, I, P, P, P, P]),
             "aaa_conv2d_nhwc": (I, [ctypes.POINTER(ConvDesc), P, P, P, P, P]),
             "aaa_conv2d_nhwc_dgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),
             "aaa_conv2d_nhwc_wgrad": (I, [ctypes.POINTER(ConvDesc), P, P, P, P]),

@@ -405,6 +405,16 @@ class Agent(nn.Module):
         # (select_backward allocates zeros and copies: two launches per step)
         return logits.squeeze(0), values.squeeze(0)
 
+    def act_episode(self, X, sampler, ts=0):
+        """Policy.act's step (forward + action draw, policy.py) as one node of the
+        open episode when the fused episode backward applies: (action, log_prob),
+        else None (the caller then runs forward() and samples itself)."""
+        if not self._episode_eligible(X):
+            return None
+        logits, values, attn, action, logp = self._episode_step(X, None, None, sampler)
+        self.last_attention = attn[0]
+        return action, logp
+
     # -- added API ----------------------------------------------------------
     def unroll(self, X, prev_reward=None, prev_action=None):
         """T steps in one call: X (T, B, H, W, 3) -> logits, values (T, B, A), attn (T, B, h, w, nq).
@@ -422,11 +432,11 @@ class Agent(nn.Module):
                 and not (self.stateful_core or self.prev_hidden is not None)
                 and any(p.requires_grad for p in self.parameters()))
 
-    def _episode_step(self, X, pr, pa):
+    def _episode_step(self, X, pr, pa, sampler=None):
         """One per-step call recorded into the open episode (episode.py): a new
         episode after reset(), a parameter change, another geometry, or a
         prev_hidden the episode did not set itself."""
-        from .episode import Episode, _EpisodeAnchorFn, _EpisodeStepFn
+        from .episode import Episode, _EpisodeActFn, _EpisodeAnchorFn, _EpisodeStepFn
         B, H, W, C = X.shape
         if C != 3:
             raise ValueError(f"frames must be (..., H, W, 3), got {tuple(X.shape)}")
@@ -456,11 +466,16 @@ class Agent(nn.Module):
             ep.anchor = _EpisodeAnchorFn.apply(ep, h0, c0, *params)
             self._episode = ep
         t = ep.record((X if u8 else X.float()).unsqueeze(0).contiguous(), pr, pa)
-        logits, values, attn, hT, cT = _EpisodeStepFn.apply(ep, t, ep.anchor)
+        if sampler is None:
+            logits, values, attn, hT, cT = _EpisodeStepFn.apply(ep, t, ep.anchor)
+        else:
+            logits, values, attn, hT, cT, action, logp = _EpisodeActFn.apply(ep, t, ep.anchor, sampler)
         cell.prev_hidden = (hT.permute(0, 3, 2, 1), cT.permute(0, 3, 2, 1))
         ep.state_ref = cell.prev_hidden
         if self.prev_output is None:   # Q1: the query input is created once and never updated
             self.prev_output = torch.zeros(B, self.hidden_size, device=X.device)
+        if sampler is not None:
+            return logits, values, attn, action, logp
         return logits, values, attn
 
     def _step(self, X, pr, pa):

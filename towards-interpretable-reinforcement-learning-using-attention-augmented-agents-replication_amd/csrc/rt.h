@@ -241,9 +241,10 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
   // per CU whose barriers are not in step (51.6 vs 54.4 us for 64x32 BK128, 54.6 vs 55.9 for
   // 32x64); 64x64 BK64 forward 47.4 us (32x64 / 32x32 / 64x32 split-K rings: 52-55 us)
   // (bench.py kernel table, tools/ab_bptt.sh)
-  // fp32 with f32_split6(): below 1024 tiles (the B=1 episode / actor: 68) the split-product
-  // twin of 16, tile 27 (C2 itself runs the frame-group BPTT, recur_bwd_f32.h)
-  if (bptt) return out_tiles32 < 1024 ? (f32_split6() ? 27 : 16) : (out_tiles32 < 1536 ? 1 : 0);
+  // fp32 with f32_split6(): below 1024 tiles (the B=1 episode / actor: 68) the split-K
+  // split-product tile 31 (15.0 + 5.6 us per step vs 37 us for the fp32 tile 16 at the
+  // episode's 27x20 grid; C2 itself runs the frame-group BPTT, recur_bwd_f32.h)
+  if (bptt) return out_tiles32 < 1024 ? (f32_split6() ? 31 : 16) : (out_tiles32 < 1536 ? 1 : 0);
   return out_tiles32 < 1024 ? 5 : 6;
 }
 
@@ -474,10 +475,12 @@ static int fused_step(const T* WpXH, const T* xht, int h, int w, int M, const Ep
   const ConvGeo g = ConvGeo{192, 192, 0, h, w, h, w, 3, 1, 1, 0}.prep();
   const uint32_t xh_bytes = (uint32_t)((size_t)M * 192 * sizeof(T));
   constexpr bool f32 = std::is_same<T, float>::value;
-  // fp32 with f32_split6(): the split-product tiles 13-16 (bf16x6 on the bf16
-  // MFMA), default 13 = 32x64 BK64 with a 4-way in-WG split-K -- 144 WGs of 8
-  // waves at the B=1 episode's 27x20 grid instead of 36 of the 128x64 tile
-  const int ftile = env_int("AAA_FUSED_TILE", f32 ? (f32_split6() ? 13 : 4) : 9);
+  // fp32 with f32_split6(): the split-product tiles 13-18 (bf16x6 on the bf16
+  // MFMA): default 18 = 64x64 BK64 2-way in-WG split-K x 3 K slices + gate_fwd_zx
+  // (B=1 episode step, 27x20 grid: 16.2 + 5.0 us vs 68 us for the fp32 128x64
+  // tile, 23 us for 13 = 32x64 4-way in-WG; tools/gpu_episode_ab.sh), 13 where
+  // there is no split-K scratch
+  const int ftile = env_int("AAA_FUSED_TILE", f32 ? (f32_split6() ? (zpart ? 18 : 13) : 4) : 9);
   TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728,
                  strf("%s fused [x|h] step, K=1728, AAA_FUSED_TILE %d%s [kernel: EpiConvLstmFwd]", f32 ? "fp32" : "bf16",
                       ftile, f32 && ftile >= 13 && ftile <= 16 ? " (bf16x6 split products)" : ""));
@@ -556,7 +559,7 @@ template <typename T> int pack_impl(const Layout& L, const float* prm, char* pk,
 template <typename T, typename OT>
 int vision_fwd(const Layout& L, int F, const char* pk, const float* prm, const void* frames, T* Xp, T* Y1, OT* out,
                int out_ld, hipStream_t st, bool xp_full = true);
-template <typename T> int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st);
+template <typename T> int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases);
 template <typename T>
 int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipStream_t s, bool aux);
 template <typename T>

@@ -162,7 +162,7 @@ template <typename T>
 static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st);
 
 template <typename T>
-int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
+int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) {
   using C = CfgFor<T>;
   // bf16 path: the fp32 tail GEMMs on the bf16 MFMA with split operands (AAA_TAIL_SPLIT3=0: fp32 MFMA)
   TailPrecision tail_prec(std::is_same<T, __bf16>::value && env_int("AAA_TAIL_SPLIT3", 1),
@@ -188,6 +188,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st) {
     else if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
     else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
   }
+  // no CORE (aaa_forward_phases, fp32): the recurrence's products are already in
+  // Gt / Cst / Hs / XH (aaa_core_import)
+  if (!(phases & AAA_FWD_CORE)) return forward_tail<T>(L, io, st);
   if constexpr (std::is_same<T, float>::value) {
     if (const int G = f32_frames(L)) {   // one frame-group launch for all T steps, x-part included (recur_f32.h)
       HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)G * L.B * 4, st));
@@ -522,7 +525,7 @@ template int vision_fwd<__bf16, __bf16>(const Layout&, int, const char*, const f
                                         __bf16*, int, hipStream_t, bool);
 template int vision_fwd<__bf16, float>(const Layout&, int, const char*, const float*, const void*, __bf16*, __bf16*,
                                        float*, int, hipStream_t, bool);
-template int forward_impl<float>(const Layout&, const aaa_io*, hipStream_t);
-template int forward_impl<__bf16>(const Layout&, const aaa_io*, hipStream_t);
+template int forward_impl<float>(const Layout&, const aaa_io*, hipStream_t, int);
+template int forward_impl<__bf16>(const Layout&, const aaa_io*, hipStream_t, int);
 
 }  // namespace aaa

@@ -180,7 +180,60 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream) {
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, false))) return r;
   if ((r = pair_check())) return r;
-  return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream) : forward_impl<float>(L, io, stream);
+  return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream, AAA_FWD_ALL)
+                          : forward_impl<float>(L, io, stream, AAA_FWD_ALL);
+}
+
+int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream) {
+  Layout L;
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if (phases != AAA_FWD_ALL && phases != (AAA_FWD_VISION | AAA_FWD_TAIL))
+    return fail(AAA_E_ARG, "forward phases %d: AAA_FWD_ALL or AAA_FWD_VISION | AAA_FWD_TAIL", phases);
+  if (!(phases & AAA_FWD_CORE) && L.dt != AAA_F32) return fail(AAA_E_ARG, "skipping the core: fp32 configs only");
+  if ((r = check_device())) return r;
+  if ((r = check_io(L, io, false))) return r;
+  if ((r = pair_check())) return r;
+  return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream, phases) : forward_impl<float>(L, io, stream, phases);
+}
+
+// The recurrence's per-step products in the fp32 workspace (rt_core.hip
+// build_layout): Gt [T][M][512], Cst [T+1][M][128] (slot t+1 = c_t), Hs
+// [T][M][128] (= h_t), XH [T+1][M][192] (channels 64.. of slot t+1 = h_t).
+static int core_xfer_check(const aaa_cfg* cfg, Layout& L, const void* ws, int t0, int n) {
+  int r = build_layout(cfg, L);
+  if (r) return r;
+  if (L.dt != AAA_F32) return fail(AAA_E_ARG, "core export/import: fp32 configs only");
+  if (cqm_layout(L)) return fail(AAA_E_ARG, "core export/import: channel-quad-major slices unsupported");
+  if (!ws || t0 < 0 || n < 1 || t0 + n > L.T) return fail(AAA_E_ARG, "core export/import: steps [%d, %d) of T=%d", t0, t0 + n, L.T);
+  return check_device();
+}
+
+int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, float* gates, float* c, float* h,
+                    hipStream_t st) {
+  Layout L;
+  if (int r = core_xfer_check(cfg, L, workspace, t0, n)) return r;
+  const char* ws = (const char*)workspace;
+  const size_t M = (size_t)L.B * L.P;
+  if (gates) HIPCHK(hipMemcpyAsync(gates, ws + L.Gt + (size_t)t0 * M * 512 * 4, (size_t)n * M * 512 * 4, hipMemcpyDeviceToDevice, st));
+  if (c) HIPCHK(hipMemcpyAsync(c, ws + L.Cst + (size_t)(t0 + 1) * M * 128 * 4, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  if (h) HIPCHK(hipMemcpyAsync(h, ws + L.Hs + (size_t)t0 * M * 128 * 4, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  return AAA_OK;
+}
+
+int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const float* gates, const float* c,
+                    const float* h, hipStream_t st) {
+  Layout L;
+  if (int r = core_xfer_check(cfg, L, workspace, t0, n)) return r;
+  if (!gates || !c || !h) return fail(AAA_E_ARG, "core import: gates, c and h are required");
+  char* ws = (char*)workspace;
+  const size_t M = (size_t)L.B * L.P;
+  HIPCHK(hipMemcpyAsync(ws + L.Gt + (size_t)t0 * M * 512 * 4, gates, (size_t)n * M * 512 * 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(ws + L.Cst + (size_t)(t0 + 1) * M * 128 * 4, c, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(ws + L.Hs + (size_t)t0 * M * 128 * 4, h, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  // slots t0+1 .. t0+n of XH are n*M consecutive 192-channel rows: one launch
+  HIPCHK(state_to_xh<float>((int)(n * M), h, (float*)(ws + L.XH) + (size_t)(t0 + 1) * M * 192, st));
+  return AAA_OK;
 }
 
 int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream) {

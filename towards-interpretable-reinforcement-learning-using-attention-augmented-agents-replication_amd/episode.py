@@ -31,16 +31,30 @@ The result is the gradient of the same loss through the same op sequence
 (the recomputed forward runs the same kernels as the per-step one at this
 batch, up to summation order).  The memory kept per step is the frames plus
 ``2 * B*h*w*128*4 / seg`` bytes of state.
+
+fp32 agents also keep each step's ConvLSTM products (gate activations, c_t,
+h_t: ``B*h*w*768*4`` bytes, 1.66 MB at 210x160) exported from the per-step
+workspace (``aaa_core_export``); the segment's re-run then imports them and
+skips the recurrence (``aaa_forward_phases`` without CORE) -- the 64
+sequential step launches that dominated the recomputation -- and runs only
+the batched vision encoder and tail.  AAA_EPISODE_STORE=0 recomputes instead.
 """
 from __future__ import annotations
 
+import os
+
 import torch
+
+from . import _native as N
 
 __all__ = ["Episode", "EPISODE_SEGMENT"]
 
 # Steps per recomputed segment (memory of one segment's workspace is live
 # only inside the anchor's backward; the state is checkpointed every EPISODE_SEGMENT steps).
 EPISODE_SEGMENT = 64
+# Steps per block of the kept ConvLSTM products (allocated as the episode
+# grows; one aaa_core_import per block in the backward).
+STORE_BLOCK = 16
 
 
 class _EpisodeAnchorFn(torch.autograd.Function):
@@ -81,6 +95,29 @@ class _EpisodeStepFn(torch.autograd.Function):
         return None, None, None
 
 
+class _EpisodeActFn(torch.autograd.Function):
+    """_EpisodeStepFn plus Policy.act's draw (policy.py): one node per step
+    instead of two.  The log-prob's cotangent is stashed with the draw's
+    Jacobian and folded into dlogits per segment in one batched product
+    (backward_all), instead of one sampler backward launch per step."""
+
+    @staticmethod
+    def forward(ctx, ep, t, anchor, sampler):
+        from .policy import _sample_raw
+        ctx.set_materialize_grads(False)
+        ctx.ep, ctx.t = ep, t
+        logits, values, attn, hT, cT = ep.forward_step(t)
+        action, logp, jac = _sample_raw(logits[0], sampler.seed, sampler.counter)
+        ep.jac[t] = jac
+        ctx.mark_non_differentiable(attn, action)
+        return logits, values, attn, hT, cT, action, logp
+
+    @staticmethod
+    def backward(ctx, dl, dv, _dattn, dh, dc, _daction, dlogp):
+        ctx.ep.stash(ctx.t, dl, dv, dh, dc, dlogp)
+        return None, None, None, None
+
+
 class Episode:
     """The per-step calls of one episode (from reset(), a carried state or a
     parameter change) of one Agent geometry and parameter version."""
@@ -96,6 +133,12 @@ class Episode:
         self.ckpt = {0: (h, c)}                    # segment start -> ConvLSTM state entering it
         self.cur = (h, c)
         self.cot, self.ext = {}, {}
+        self.cotp, self.jac = {}, {}               # log-prob cotangents / draw Jacobians (_EpisodeActFn)
+        # step block t // STORE_BLOCK -> (gates, c, h) of its steps (fp32: aaa_core_export), or None (recompute)
+        self.store = {} if (runner.cfg.dtype == N.F32 and os.environ.get("AAA_EPISODE_STORE", "1") != "0") else None
+        self.blk = max(1, min(self.seg, STORE_BLOCK))
+        while self.seg % self.blk:   # blocks never straddle a segment
+            self.blk -= 1
         self.state_ref = None                      # the prev_hidden tuple this episode last set
         self.anchor = None
 
@@ -113,10 +156,18 @@ class Episode:
         self.cur = (hT, cT)
         if (t + 1) % self.seg == 0:
             self.ckpt[t + 1] = (hT, cT)
+        if self.store is not None:
+            k, i = divmod(t, self.blk)
+            if k not in self.store:
+                self.store[k] = tuple(torch.empty(s, device=self.device) for s in r.core_shapes(self.blk))
+            g, c, h = self.store[k]
+            r.core_export(self.ws, 0, 1, g[i:i + 1], c[i:i + 1], h[i:i + 1])
         return logits, values, attn, hT, cT
 
     # -- backward -------------------------------------------------------------
-    def stash(self, t, dl, dv, dh, dc):
+    def stash(self, t, dl, dv, dh, dc, dlogp=None):
+        if dlogp is not None:
+            self.cotp[t] = _add(self.cotp.get(t), dlogp)
         if dl is not None or dv is not None:
             pl, pv = self.cot.get(t, (None, None))
             self.cot[t] = (_add(pl, dl), _add(pv, dv))
@@ -143,7 +194,7 @@ class Episode:
         A, B = r.A, r.B
         for k, t0 in reversed(list(enumerate(starts))):
             t1 = min(n, t0 + self.seg)
-            live = any(t in self.cot for t in range(t0, t1)) or dh is not None or dc is not None
+            live = any(t in self.cot or t in self.cotp for t in range(t0, t1)) or dh is not None or dc is not None
             need_state = k > 0 or want_state
             if not live:                  # no cotangent reaches this segment or anything before it through it
                 dh = dc = None
@@ -156,15 +207,28 @@ class Episode:
             pa = _stack([self.steps[t][3] for t in range(t0, t1)], (1, B), self.device)
             dl = _stack([self.cot.get(t, (None, None))[0] for t in range(t0, t1)], (1, B, A), self.device, zero=True)
             dv = _stack([self.cot.get(t, (None, None))[1] for t in range(t0, t1)], (1, B, A), self.device, zero=True)
+            if any(t in self.cotp for t in range(t0, t1)):   # dlogits += jac * dlogp, all steps at once
+                J = torch.stack([self.jac[t] for t in range(t0, t1)])
+                G = _stack([self.cotp.get(t) for t in range(t0, t1)], (1, B), self.device, zero=True)
+                dl = torch.addcmul(dl, J, G.unsqueeze(-1))
             h0, c0 = self.ckpt[t0]
             ws = ru.new_workspace()
-            ru.forward(self.flat, self.packed, self.basis, frames, ws, pr, pa, h0, c0, want_attn=False)
+            if self.store is not None:   # the recorded products: no recurrence re-run
+                for b0 in range(t0, t1, self.blk):
+                    nb = min(self.blk, t1 - b0)
+                    sg, sc, sh = self.store[b0 // self.blk]
+                    ru.core_import(ws, b0 - t0, nb, sg[:nb], sc[:nb], sh[:nb])
+                ru.forward(self.flat, self.packed, self.basis, frames, ws, pr, pa, h0, c0, want_attn=False,
+                           phases=N.FWD_VISION | N.FWD_TAIL)
+            else:
+                ru.forward(self.flat, self.packed, self.basis, frames, ws, pr, pa, h0, c0, want_attn=False)
             g, dh, dc = ru.backward(self.flat, self.packed, self.basis, frames, ws, dl, dv, dh, dc,
                                     want_state_grads=need_state)
             total += g
             del ws
         self.cot.clear()
         self.ext.clear()
+        self.cotp.clear()
         return total, dh, dc
 
 

@@ -32,18 +32,25 @@ from . import _native as N
 __all__ = ["Policy", "sample_actions", "ActionSampler", "GraphActor"]
 
 
+def _sample_raw(logits, seed, counter):
+    """aaa_sample_actions on (B, A) fp32 logits -> (actions int32 (B,), log_prob (B,),
+    jac (B, A) = d log_prob / d logits); no autograd."""
+    B, A = logits.shape
+    lg = logits.detach().contiguous()
+    actions = torch.empty(B, dtype=torch.int32, device=lg.device)
+    logp = torch.empty(B, dtype=torch.float32, device=lg.device)
+    jac = torch.empty(B, A, dtype=torch.float32, device=lg.device)
+    N.check(N.load().aaa_sample_actions(B, A, lg.data_ptr(), int(seed) & (2**64 - 1),
+                                        None if counter is None else counter.data_ptr(),
+                                        actions.data_ptr(), logp.data_ptr(), jac.data_ptr(),
+                                        N.stream_ptr(lg.device)), "sample_actions")
+    return actions, logp, jac
+
+
 class _SampleFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, seed, counter):
-        B, A = logits.shape
-        lg = logits.detach().contiguous()
-        actions = torch.empty(B, dtype=torch.int32, device=lg.device)
-        logp = torch.empty(B, dtype=torch.float32, device=lg.device)
-        jac = torch.empty(B, A, dtype=torch.float32, device=lg.device)
-        N.check(N.load().aaa_sample_actions(B, A, lg.data_ptr(), int(seed) & (2**64 - 1),
-                                            None if counter is None else counter.data_ptr(),
-                                            actions.data_ptr(), logp.data_ptr(), jac.data_ptr(),
-                                            N.stream_ptr(lg.device)), "sample_actions")
+        actions, logp, jac = _sample_raw(logits, seed, counter)
         ctx.save_for_backward(jac)
         ctx.mark_non_differentiable(actions)
         return actions, logp
@@ -126,10 +133,16 @@ class Policy(nn.Module):
     def act(self, observation, ts: int = 0):
         """One step without a host sync: returns (action int32 (1,), log_prob (1,)) on the device."""
         state = self._upload(observation)
-        logits, _ = self.agent(state, ts=ts)
-        if self._sampler is None or self._sampler.counter.device != logits.device:
-            self._sampler = ActionSampler(self._seed, logits.device)
-        action, logp = self._sampler(logits)
+        dev = state.device
+        if self._sampler is None or self._sampler.counter.device != dev:
+            self._sampler = ActionSampler(self._seed, dev)
+        act_episode = getattr(self.agent, "act_episode", None)
+        out = act_episode(state, self._sampler, ts=ts) if act_episode is not None else None
+        if out is not None:   # the step and its draw as ONE episode node (episode.py _EpisodeActFn)
+            action, logp = out
+        else:
+            logits, _ = self.agent(state, ts=ts)
+            action, logp = self._sampler(logits)
         self.saved_log_probs.append(logp)
         return action, logp
 

@@ -59,10 +59,11 @@ class UnrollRunner:
         return io
 
     def forward(self, flat_params, packed, basis, frames, workspace, prev_reward=None, prev_action=None,
-                h0=None, c0=None, want_attn=True, want_state=False, core=None):
+                h0=None, c0=None, want_attn=True, want_state=False, core=None, phases=N.FWD_ALL):
         """Returns (logits, values, attn, hT, cT); a stateful-core runner also
         returns the core state (core_hT, core_cT) (B, 256), starting from
-        ``core`` = (h0, c0) or zeros."""
+        ``core`` = (h0, c0) or zeros.  ``phases`` = FWD_VISION | FWD_TAIL skips
+        the ConvLSTM recurrence (its products imported first: core_import)."""
         T, B, A = self.T, self.B, self.A
         dev = self.device
         self._check_frames(frames)
@@ -81,10 +82,33 @@ class UnrollRunner:
                          core_hT=torch.empty(B, 256, device=dev), core_cT=torch.empty(B, 256, device=dev))
         io = self._io(params=flat_params, packed=packed, basis=basis, frames=frames,
                       logits=logits, values=values, attn=attn, hT=hT, cT=cT, workspace=workspace, **keep, **extra)
-        N.check(self.lib.aaa_forward(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(dev)), "forward")
+        if phases == N.FWD_ALL:
+            N.check(self.lib.aaa_forward(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(dev)), "forward")
+        else:
+            N.check(self.lib.aaa_forward_phases(ctypes.byref(self.cfg), ctypes.byref(io), int(phases),
+                                                N.stream_ptr(dev)), "forward_phases")
         if self.stateful_core:
             return logits, values, attn, hT, cT, extra["core_hT"], extra["core_cT"]
         return logits, values, attn, hT, cT
+
+    def core_shapes(self, n):
+        """Shapes of n steps' (gates, c, h) for core_export / core_import."""
+        M = self.B * self.h * self.w
+        return (n, M, 512), (n, M, 128), (n, M, 128)
+
+    def core_export(self, workspace, t0, n, gates, c, h):
+        """Steps [t0, t0+n) of the recurrence's products (fp32 runners) -> gates, c, h (core_shapes)."""
+        for x, shp in zip((gates, c, h), self.core_shapes(n)):
+            _check_out(x, shp)
+        N.check(self.lib.aaa_core_export(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
+                                         N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_export")
+
+    def core_import(self, workspace, t0, n, gates, c, h):
+        """The inverse of core_export, into a workspace for forward(phases=FWD_VISION | FWD_TAIL)."""
+        for x, shp in zip((gates, c, h), self.core_shapes(n)):
+            _check_out(x, shp)
+        N.check(self.lib.aaa_core_import(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
+                                         N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_import")
 
     def backward(self, flat_params, packed, basis, frames, workspace, dlogits, dvalues=None, dhT=None,
                  dcT=None, grads=None, want_state_grads=False, phases=N.BWD_ALL, dcore=None, want_core_grads=False):
@@ -120,6 +144,13 @@ class UnrollRunner:
             raise ValueError(f"frames must be contiguous {dt} {exp}, got {tuple(frames.shape)} {frames.dtype}")
         if frames.device != self.device and frames.device.type != "cuda":
             raise RuntimeError("frames must be on the GPU")
+
+
+def _check_out(t, shape):
+    if (t is None or tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or not t.is_contiguous()
+            or t.device.type != "cuda"):
+        raise ValueError(f"expected a contiguous fp32 device tensor {tuple(shape)}, got "
+                         f"{None if t is None else (tuple(t.shape), t.dtype, t.device)}")
 
 
 def _f32(t, shape):
