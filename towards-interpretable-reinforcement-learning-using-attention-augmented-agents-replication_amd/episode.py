@@ -246,5 +246,11 @@ def _stack(items, shape, device, zero=False):
     (zeros with ``zero``)."""
     if all(x is None for x in items):
         return torch.zeros((len(items), *shape[1:]), device=device) if zero else None
+    n = 1
+    for d in shape:
+        n *= d
+    d0 = items[0].dim() if items[0] is not None else -1
+    if all(x is not None and x.numel() == n and x.dtype == torch.float32 and x.dim() == d0 for x in items):
+        return torch.cat(items).reshape((len(items), *shape[1:]))   # one launch, no per-item ops
     out = [torch.zeros(shape, device=device) if x is None else x.reshape(shape).float() for x in items]
     return torch.cat(out) if len(out) > 1 else out[0]
