@@ -132,13 +132,19 @@ struct ConvGeo {
   int Hin, Win, Hout, Wout;
   int KW, stride, pad;
   int transposed;  // 0: forward gather, 1: dgrad (transposed-conv) gather
-  FastDiv dCin, dKW, dWout, dHW;  // filled by prep()
+  // K order: 0 = tap-major (k = tap * Cin + ci); cmaj = BK > 0: channel-chunk-major,
+  // k = (ci / BK) * taps * BK + tap * BK + ci % BK -- the taps of one channel chunk
+  // adjacent in K, so a tile's 3x3 re-reads of the same rows hit in L2 (glds.h
+  // GIm2colB only; the A operand must be packed in the same order, reorder_cmaj)
+  int cmaj;
+  FastDiv dCin, dKW, dWout, dHW, dTaps;  // filled by prep()
   ConvGeo prep() const {
     ConvGeo g = *this;
     g.dCin = FastDiv((uint32_t)Cin);
     g.dKW = FastDiv((uint32_t)KW);
     g.dWout = FastDiv((uint32_t)Wout);
     g.dHW = FastDiv((uint32_t)(Hout * Wout));
+    g.dTaps = FastDiv((uint32_t)(KW * KW));
     return g;
   }
 };

@@ -194,8 +194,15 @@ struct GIm2colB {
   // The tap's own offset is negative for the transposed gather, so vo carries
   // it (kOOB lanes stay kOOB), and soff = ci0 >= 0 only.
   __device__ __forceinline__ void issue(T* lds, int k0) {
-    const int tap = __builtin_amdgcn_readfirstlane((int)g.dCin.div(k0));
-    const int ci0 = k0 - tap * g.Cin;
+    int tap, ci0;
+    if (g.cmaj) {   // channel-chunk-major K (ConvGeo::cmaj == BK, whole taps)
+      const int blk = k0 / BK, q = __builtin_amdgcn_readfirstlane((int)g.dTaps.div(blk));
+      tap = blk - q * (int)g.dTaps.d;
+      ci0 = q * BK;
+    } else {
+      tap = __builtin_amdgcn_readfirstlane((int)g.dCin.div(k0));
+      ci0 = k0 - tap * g.Cin;
+    }
     const int ky = __builtin_amdgcn_readfirstlane((int)g.dKW.div(tap));
     const int kx = tap - ky * g.KW;
     const int tv = (g.transposed ? -(ky * g.Win + kx) : (ky * g.Win + kx)) * g.cs;

@@ -101,6 +101,9 @@ template <typename T>
 hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, float* hout, T* xhnext, hipStream_t st,
                        const float* zs = nullptr, int nsl = 0, size_t sls = 0, const float* bias = nullptr);
 hipError_t pack_f32(const F32Pack& p, hipStream_t st);
+// Channel-chunk-major copy of conv-GEMM rows (ConvGeo::cmaj): row r's K = taps x Cin
+// (tap-major) -> dst[r][(c / BK) * taps * BK + tap * BK + c % BK]
+hipError_t reorder_cmaj(const float* src, int rows, int Cin, int taps, int BK, float* dst, hipStream_t st);
 template <typename T, typename TI> hipError_t frames_rgbx(int F, int H, int W, const TI* x, T* y, hipStream_t st);
 template <typename T> hipError_t pack_conv2_classes(const float* w2, T* dst, hipStream_t st);
 template <typename T> hipError_t pack_conv1_rgbx(const float* w, T* dst, hipStream_t st);

@@ -1201,6 +1201,23 @@ hipError_t gate_fwd_zx(int M, const float* cprev, float* gates, float* cnext, fl
   return hipGetLastError();
 }
 
+__global__ void k_reorder_cmaj(const float* __restrict__ src, int rows, int Cin, int taps, int BK,
+                               float* __restrict__ dst) {
+  const long K = (long)taps * Cin, n = (long)rows * K;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / K;
+    const int k = (int)(i - r * K), tap = k / Cin, c = k - tap * Cin;
+    dst[r * K + (long)(c / BK) * taps * BK + tap * BK + c % BK] = src[i];
+  }
+}
+
+hipError_t reorder_cmaj(const float* src, int rows, int Cin, int taps, int BK, float* dst, hipStream_t st) {
+  if (Cin % BK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reorder_cmaj, dim3(nblk((long)rows * taps * Cin)), dim3(256), 0, st, src, rows, Cin, taps, BK,
+                     dst);
+  return hipGetLastError();
+}
+
 hipError_t pack_f32(const F32Pack& p, hipStream_t st) {
   long n = 512L * p.ans_ld + 1024L * 256 + 1024 + (long)p.ldy * 256 + p.ldy + (p.Wihhp ? 1024L * 512 : 0);
   hipLaunchKernelGGL(k_pack_f32, dim3(nblk(n)), dim3(256), 0, st, p);

@@ -114,7 +114,8 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   const int P = p.P, W2 = p.w + 2;
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
-  auto sw16 = [](int q, int ip) { return (q ^ (ip & 15)) << 4; };
+  // 16-B chunk q of image pixel (y, x) at slot q ^ (key & 15), key = y * w + x (recur_f32.h)
+  auto sw16 = [](int q, int key) { return (q ^ (key & 15)) << 4; };
   // exchange slot of (buffer, destination, source): [128 px][16 ch]
   auto xslot = [&](int buf, int dst, int src) {
     return p.xp + ((((size_t)buf * p.B + b) * 8 + dst) * 8 + src) * 128 * 16;
@@ -168,16 +169,20 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
           const f32x4 z = *reinterpret_cast<const f32x4*>(p.dZ + ((size_t)(p.T - 1) * M + (size_t)b * P + px) * 512 +
                                                           64 * kh + 16 * cq + 4 * e);
           bs[e] += z;
-          *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(4 * cq + e, ip)) = z;
+          *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(4 * cq + e, px)) = z;
         }
       }
     }
     bias_flush(p.T - 1, bs);   // (its barrier also completes the image)
   }
 
-  int hb[2];
+  int hb[2], sb[2];   // sb: swizzle key of the window's top-left pixel
 #pragma unroll
-  for (int c = 0; c < 2; ++c) hb[c] = p.colhb[32 * (2 * cw + c) + r32];
+  for (int c = 0; c < 2; ++c) {
+    const int col = 32 * (2 * cw + c) + r32;
+    hb[c] = p.colhb[col];
+    sb[c] = (col < P ? col : P - 1) - p.w - 1;
+  }
   const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(8 * kB32QP * 4 * 1024));
   auto lda = [&](int q, int r) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -208,6 +213,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   // the dgrad is the transposed conv: tap (ky, kx) of W^T (packed in the forward's
   // orientation) reads dZ at (y + 1 - ky, x + 1 - kx) (ConvGeo transposed gather)
   auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + 2 - tap % 3; };
+  auto tapkey = [&](int tap) { return (2 - tap / 3) * p.w + 2 - tap % 3; };
   const int nsteps = p.T - 1 + (p.dh0 ? 1 : 0);   // dgrads: dZ_{T-1} .. dZ_1 (+ dZ_0 for dh0)
   for (int it = 0; it < nsteps; ++it) {
     const int s = p.T - 1 - it;   // this dgrad reads dZ_s and yields dh_{s-1}
@@ -220,11 +226,12 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
-    int hbs[2];
+    int hbs[2], sbs[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       hbs[c] = hb[c];
-      asm volatile("" : "+v"(hbs[c]));
+      sbs[c] = sb[c];
+      asm volatile("" : "+v"(hbs[c]), "+v"(sbs[c]));
     }
     // gate-backward inputs of step s-1, loaded at the start (they land under the K loop)
     f32x4 gpre[NG][7];
@@ -241,11 +248,11 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       }
     }
     auto ldb = [&](int tap, int q8, f32x4 (&bf)[2]) {
-      const int toff = tapoff(tap);
+      const int toff = tapoff(tap), tk = tapkey(tap);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int ip = hbs[c] + toff;
-        bf[c] = *reinterpret_cast<const f32x4*>(zim + ip * 256 + sw16(2 * q8 + hh, ip));
+        bf[c] = *reinterpret_cast<const f32x4*>(zim + ip * 256 + sw16(2 * q8 + hh, sbs[c] + tk));
       }
     };
     f32x4 bfr[2][2];
@@ -406,7 +413,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
         const f32x4 z{di, df, dcg, dout};
         bs[e] += z;
         const int q = 4 * cq + e;   // 16-B chunk (4 rows) of the workgroup's 64 rows
-        *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(q, ip)) = z;
+        *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(q, px)) = z;
         *reinterpret_cast<f32x4*>(zo + 4 * q) = z;
       }
     }

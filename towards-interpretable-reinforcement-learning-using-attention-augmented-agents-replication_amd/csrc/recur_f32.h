@@ -26,8 +26,12 @@
 // ds_read_b128 of the B image and one 16-B load of the fragment-order weights
 // (k_pack_wf32) feed four MFMAs.
 //
-// LDS images (zero border), 16-B chunk q of image pixel ip at slot q ^ (ip & 15)
-// (16 consecutive pixels of a fragment read hit 16 distinct bank groups):
+// LDS images (zero border), 16-B chunk q of image pixel (y, x) at slot q ^ (key & 15),
+// key = y * w + x (border pixels: y or x = -1 / h or w): consecutive columns --
+// the lanes of a fragment read -- have consecutive keys under every tap, row ends
+// included, so 8 consecutive lanes hit 8 distinct bank groups (keyed by the bordered
+// index ip instead, the 2-pixel jump at each row end collided: PMC conflict rate
+// 0.54 on the C2 forward):
 //   x image: 169 pixels x 64 fp32 (256 B),  DMA-filled from XH slot t+1 under the epilogue
 //   h image: 169 pixels x 128 fp32 (512 B), own channels from the epilogue, the
 //            partners' from XH slot t.
@@ -174,7 +178,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
   const int rw = wave & 1, cw = wave >> 1;
   const int rbg0 = kh * NRB + rw * RPW;            // the wave's first global row block
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
-  auto sw16 = [](int q, int ip) { return (q ^ (ip & 15)) << 4; };
+  auto sw16 = [](int q, int key) { return (q ^ (key & 15)) << 4; };
   unsigned char* stg = stgall + wave * kF32STG;
 
   {  // zero both images (borders stay zero)
@@ -186,12 +190,12 @@ k_convlstm_fwd_f32(RecF32Params p) {
   __syncthreads();
   // x image of step t by LDS-DMA (XH slot t, channels 0..63): piece i of 44
   // covers image bytes [1024 i, 1024 i + 1024) = pixels 4i + lane / 16, slot
-  // lane % 16, which holds chunk slot ^ (ip & 15); border pixels land as zeros.
+  // lane % 16, which holds chunk slot ^ (key & 15); border pixels land as zeros.
   auto dma_x = [&](int t) {
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
     for (int i = wave; i < kF32XB / 1024; i += 4) {
-      const int ip = i * 4 + (lane >> 4), q = (lane & 15) ^ (ip & 15);
-      const int py = ip / W2 - 1, px = ip % W2 - 1;
+      const int ip = i * 4 + (lane >> 4);
+      const int py = ip / W2 - 1, px = ip % W2 - 1, q = (lane & 15) ^ ((py * p.w + px) & 15);
       const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
       dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 4) * 4) : kOOB);
     }
@@ -201,7 +205,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
     const float* src = p.XH + (size_t)b * P * 192 + 64;
     for (int i = tid; i < P * 32; i += 256) {
       const int px = i >> 5, q = i & 31, ip = hidx(px);
-      *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(q, ip)) = *reinterpret_cast<const u32x4*>(src + (size_t)px * 192 + q * 4);
+      *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(q, px)) = *reinterpret_cast<const u32x4*>(src + (size_t)px * 192 + q * 4);
     }
   }
 
@@ -210,12 +214,13 @@ k_convlstm_fwd_f32(RecF32Params p) {
   // rbg0 + r = gate e of channel 8 (rbg0 + r) + 2g + hh, at column 32 (2cw + c) + r32
   f32x4 bz[RPW][4];
   float cst[RPW][2][4];
-  int pcol[2], hb[2];
+  int pcol[2], hb[2], sb[2];   // sb: swizzle key of the window's top-left pixel
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int col = 32 * (2 * cw + c) + r32;
     pcol[c] = col < P ? col : -1;
     hb[c] = p.colhb[col];
+    sb[c] = (col < P ? col : P - 1) - p.w - 1;
   }
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
@@ -268,19 +273,21 @@ k_convlstm_fwd_f32(RecF32Params p) {
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
-    int hbs[2];
+    int hbs[2], sbs[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       hbs[c] = hb[c];
-      asm volatile("" : "+v"(hbs[c]));
+      sbs[c] = sb[c];
+      asm volatile("" : "+v"(hbs[c]), "+v"(sbs[c]));
     }
-    auto tapoff = [&](int tap) { return (tap / 3) * W2 + tap % 3; };
+    // a tap's image-pixel offset and swizzle-key offset, packed (key offset << 16 | pixel offset)
+    auto tapoff = [&](int tap) { return (((tap / 3) * p.w + tap % 3) << 16) | ((tap / 3) * W2 + tap % 3); };
     // B fragments of a quad: image pixel hbs[c] + toff, 16-B chunk q (x: 0..15, h: 0..31) + hh
     auto ldb = [&](const unsigned char* img, int pitch, int toff, int q, f32x4 (&bf)[2]) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int ip = hbs[c] + toff;
-        bf[c] = *reinterpret_cast<const f32x4*>(img + ip * pitch + sw16(q + hh, ip));
+        const int ip = hbs[c] + (toff & 0xffff);
+        bf[c] = *reinterpret_cast<const f32x4*>(img + ip * pitch + sw16(q + hh, sbs[c] + (toff >> 16)));
       }
     };
     // one quad: A prefetch PD-1 ahead, next B fragments, 4 k-steps x RPW x 2 MFMAs
@@ -366,7 +373,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
         const int pj = rem / CPG, kq = (pj < kh ? pj : pj + 1) * CPG + rem % CPG;
         if (px < P) {
           const int ip = hidx(px);
-          *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(kq, ip)) = pv[n];
+          *reinterpret_cast<u32x4*>(him + ip * 512 + sw16(kq, px)) = pv[n];
         }
       }
     };
@@ -480,7 +487,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
           *reinterpret_cast<f32x4*>(stg + r32 * kF32GP + 16 * chl) = f32x4{gi, gf, gc, go};
           *reinterpret_cast<float*>(stg + kF32SG + r32 * 48 + 4 * chl) = cc;
           *reinterpret_cast<float*>(stg + kF32SG + 32 * 48 + r32 * 48 + 4 * chl) = h;
-          if (pp >= 0) *reinterpret_cast<float*>(him + ip * 512 + sw16(ch >> 2, ip) + (ch & 3) * 4) = h;
+          if (pp >= 0) *reinterpret_cast<float*>(him + ip * 512 + sw16(ch >> 2, pp) + (ch & 3) * 4) = h;
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -511,7 +518,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + (rowt + M) * 192, (uint32_t)(P * 192 * 4));
       for (int i = tid; i < P * CPG; i += 256) {
         const int px = i / CPG, q = kh * CPG + i % CPG, ip = hidx(px);
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + ip * 512 + sw16(q, ip)), rs,
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + ip * 512 + sw16(q, px)), rs,
                                                (uint32_t)((px * 192 + 64 + q * 4) * 4), 0, kSC1);
       }
     }

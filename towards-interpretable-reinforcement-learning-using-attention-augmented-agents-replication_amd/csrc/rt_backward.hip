@@ -617,10 +617,31 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HF6>(hp, ep, s)));
         } else if (f32_split6()) {   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
-          // A/B: 0 = 64x64, 1 = 64x128 (the default: C2 355 / 344 / 373 us), 2 = 64x64 BK64
+          // A/B: 0 = 64x64, 1 = 64x128 (C2 355 / 344 / 373 us), 2 = 64x64 BK64, 3 = 64x128 with the K
+          // order channel-chunk-major (ConvGeo::cmaj: a chunk's 9 taps adjacent, so the 3x3 re-reads of
+          // dZ rows hit in L2 -- tap-major, the launch fetched 1.2 GB for 158 MB of dZ, PMC)
           switch (env_int("AAA_DX_S6_TILE", 1)) {
+            case 3: {   // (A/B only: measured no faster, 365 vs 353 us -- the ring is not fetch-bound)
+              HIPCHK(reorder_cmaj(WdT, 64, 512, 9, 32, (float*)(pk + L.k_WdTc), s));   // its weights, re-laid here
+              ConvGeo gc = g;
+              gc.cmaj = 32;
+              HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>((const T*)(pk + L.k_WdTc), 4608, 64, dz, gc,
+                                                                             rows, zb, ep, 64, 4608, s)));
+              break;
+            }
             case 1:
               HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+              break;
+            // 4-6: one wave per 64 rows (MI = 2: each split B fragment feeds 2x6 MFMAs, each split A fragment
+            // 2-4 x 6), 2 / 4 waves side by side
+            case 4:
+              HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 1, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+              break;
+            case 5:
+              HIPCHK((step_gemm<GemmCfgS6<64, 256, 32, 1, 4>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+              break;
+            case 6:
+              HIPCHK((step_gemm<GemmCfgS6<64, 256, 32, 1, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
             case 2:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
