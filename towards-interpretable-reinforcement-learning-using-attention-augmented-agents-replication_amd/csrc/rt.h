@@ -313,7 +313,8 @@ static hipError_t step_gemm(const T* W, int ldw, int wrows, const G* src, const 
 // tile with a 4-way in-WG split-K (8 waves per WG: the serial K loop of these
 // long-K, few-tile GEMMs is what they wait on; C2 4.487 -> 4.414 ms per
 // iteration vs the plain 32x64 tile, tools/ab_head.sh).  AAA_HEAD_TILE=1 forces
-// 64x64, =2 the plain 32x64, =3/4/5 the 2-way / 4-way / 4-way BK128 split-K tiles.
+// 64x64, =2 the plain 32x64, =3/4/5 the 2-way / 4-way / 4-way BK128 split-K tiles.  (128x128 and 64x128
+// tiles, fewer split fragments per MFMA, measured slower: C2 tail 190 -> 370 / 290 us, C3 367 -> 536 / 433.)
 // g_tail3 (set per forward / backward call of the bf16 path, TailPrecision):
 // the same tiles with fp32 operands split into bf16 pairs on the bf16 MFMA
 // (gemm.h GemmCfgS3), ~1e-5 relative per product.

@@ -617,6 +617,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HF6>(hp, ep, s)));
         } else if (f32_split6()) {   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
+          // (one wave per 64 rows -- 64x128 of 2 waves, 64x256 of 2 / 4 -- measured slower: 380-395 vs 360 us)
           // A/B: 0 = 64x64, 1 = 64x128 (C2 355 / 344 / 373 us), 2 = 64x64 BK64, 3 = 64x128 with the K
           // order channel-chunk-major (ConvGeo::cmaj: a chunk's 9 taps adjacent, so the 3x3 re-reads of
           // dZ rows hit in L2 -- tap-major, the launch fetched 1.2 GB for 158 MB of dZ, PMC)
@@ -632,17 +633,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
             case 1:
               HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
-            // 4-6: one wave per 64 rows (MI = 2: each split B fragment feeds 2x6 MFMAs, each split A fragment
-            // 2-4 x 6), 2 / 4 waves side by side
-            case 4:
-              HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 1, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
-              break;
-            case 5:
-              HIPCHK((step_gemm<GemmCfgS6<64, 256, 32, 1, 4>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
-              break;
-            case 6:
-              HIPCHK((step_gemm<GemmCfgS6<64, 256, 32, 1, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
-              break;
+
             case 2:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
