@@ -155,6 +155,30 @@ struct GRowsB {
   }
 };
 
+// A operand of the split-product (SPLIT6) ring pre-split into three bf16
+// planes (hi, mid, lo: split_planes) -- fp32 weights whose split the kernel
+// would otherwise redo per fragment read: three GRowsB<bf16> stages side by
+// side in the fp32 stage's place (ELEMS in float units: 1.5 x BI x BK).
+template <int R, int BK, int NT>
+struct GRows3B {
+  using P1 = GRowsB<__bf16, R, BK, NT>;
+  static constexpr bool KC = true, PRESPLIT = true;
+  static constexpr int PER = 3 * P1::PER;
+  static constexpr int ELEMS = 3 * R * BK / 2;
+  struct Params { const __bf16* src; int ld; int nrows; size_t plane; };   // plane p at src + p * plane
+  P1 pl[3];
+  __device__ __forceinline__ GRows3B(const Params& p, int row0)
+      : pl{P1(typename P1::Params{p.src, p.ld, p.nrows}, row0),
+           P1(typename P1::Params{p.src + p.plane, p.ld, p.nrows}, row0),
+           P1(typename P1::Params{p.src + 2 * p.plane, p.ld, p.nrows}, row0)} {}
+  __device__ __forceinline__ void issue(float* lds, int k0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pl[q].issue(reinterpret_cast<__bf16*>(lds) + q * R * BK, k0);
+  }
+};
+template <class LD, class = void> struct presplit_of : std::false_type {};
+template <class LD> struct presplit_of<LD, std::enable_if_t<LD::PRESPLIT>> : std::true_type {};
+
 // Implicit-GEMM gather (rows = output pixels, k = (tap, ci)); same geometry
 // rules as LdIm2colB, whose per-pixel setup it shares.
 template <typename T, int R, int BK, int NT>
@@ -675,14 +699,27 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
         const int kofs = 16 * (s2 * WK + wk) + 8 * h;
         float af[MI][8], bfr[MJ][8];
         if constexpr (MF) {
+        if constexpr (!presplit_of<LA>::value) {
 #pragma unroll
-        for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+          for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+        }
 #pragma unroll
         for (int b = 0; b < MJ; ++b) frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
         if constexpr (split6_of<C>::value) {   // fp32 at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
           bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
+          if constexpr (presplit_of<LA>::value) {   // A's parts straight from its three bf16 planes
+            const __bf16* Ab = reinterpret_cast<const __bf16*>(Ac);
 #pragma unroll
-          for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+            for (int a = 0; a < MI; ++a) {
+              const int r = wi * WTI + a * 32 + r32;
+              ah[a] = frag_sw<BK>(Ab, r, kofs);
+              am[a] = frag_sw<BK>(Ab + BI * BK, r, kofs);
+              al[a] = frag_sw<BK>(Ab + 2 * BI * BK, r, kofs);
+            }
+          } else {
+#pragma unroll
+            for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+          }
 #pragma unroll
           for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
 #pragma unroll

@@ -104,6 +104,8 @@ hipError_t pack_f32(const F32Pack& p, hipStream_t st);
 // Channel-chunk-major copy of conv-GEMM rows (ConvGeo::cmaj): row r's K = taps x Cin
 // (tap-major) -> dst[r][(c / BK) * taps * BK + tap * BK + c % BK]
 hipError_t reorder_cmaj(const float* src, int rows, int Cin, int taps, int BK, float* dst, hipStream_t st);
+// fp32 -> three bf16 planes (hi, mid, lo; gemm.h split3_bf16's split): dst[p * n + i]
+hipError_t split_planes(const float* src, long n, __bf16* dst, hipStream_t st);
 template <typename T, typename TI> hipError_t frames_rgbx(int F, int H, int W, const TI* x, T* y, hipStream_t st);
 template <typename T> hipError_t pack_conv2_classes(const float* w2, T* dst, hipStream_t st);
 template <typename T> hipError_t pack_conv1_rgbx(const float* w, T* dst, hipStream_t st);

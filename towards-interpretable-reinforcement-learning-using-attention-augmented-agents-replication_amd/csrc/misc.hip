@@ -1218,6 +1218,23 @@ hipError_t reorder_cmaj(const float* src, int rows, int Cin, int taps, int BK, f
   return hipGetLastError();
 }
 
+__global__ void k_split_planes(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = src[i];
+    const __bf16 hi = (__bf16)x;
+    const float r = x - (float)hi;
+    const __bf16 mid = (__bf16)r;
+    dst[i] = hi;
+    dst[n + i] = mid;
+    dst[2 * n + i] = (__bf16)(r - (float)mid);
+  }
+}
+
+hipError_t split_planes(const float* src, long n, __bf16* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_split_planes, dim3(nblk(n)), dim3(256), 0, st, src, n, dst);
+  return hipGetLastError();
+}
+
 hipError_t pack_f32(const F32Pack& p, hipStream_t st) {
   long n = 512L * p.ans_ld + 1024L * 256 + 1024 + (long)p.ldy * 256 + p.ldy + (p.Wihhp ? 1024L * 512 : 0);
   hipLaunchKernelGGL(k_pack_f32, dim3(nblk(n)), dim3(256), 0, st, p);

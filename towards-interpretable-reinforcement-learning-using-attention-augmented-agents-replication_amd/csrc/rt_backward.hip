@@ -621,7 +621,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
           // A/B: 0 = 64x64, 1 = 64x128 (C2 355 / 344 / 373 us), 2 = 64x64 BK64, 3 = 64x128 with the K
           // order channel-chunk-major (ConvGeo::cmaj: a chunk's 9 taps adjacent, so the 3x3 re-reads of
           // dZ rows hit in L2 -- tap-major, the launch fetched 1.2 GB for 158 MB of dZ, PMC)
-          switch (env_int("AAA_DX_S6_TILE", 1)) {
+          // default 4: 1 with the weights pre-split (C2 340 vs 357 us, profiles/r04/ab/README.md)
+          switch (env_int("AAA_DX_S6_TILE", 4)) {
             case 3: {   // (A/B only: measured no faster, 365 vs 353 us -- the ring is not fetch-bound)
               HIPCHK(reorder_cmaj(WdT, 64, 512, 9, 32, (float*)(pk + L.k_WdTc), s));   // its weights, re-laid here
               ConvGeo gc = g;
@@ -633,6 +634,15 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
             case 1:
               HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
+            case 4: {   // 64x128 with the weights pre-split (k_WdT6 planes): only dZ is split in the loop
+              using C6 = GemmCfgS6<64, 128, 32, 2, 2>;
+              using LA3 = GRows3B<64, 32, C6::NT>;
+              using LBx = GIm2colB<float, 128, 32, C6::NT>;
+              HIPCHK((launch_pipe<C6, LA3, LBx, ED, 2>(
+                  typename LA3::Params{(const __bf16*)(pk + L.k_WdT6), 4608, 64, (size_t)64 * 4608},
+                  typename LBx::Params{dz, g, rows, zb}, ep, 64, rows, 4608, 1, s)));
+              break;
+            }
 
             case 2:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));

@@ -63,6 +63,7 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.k_Wfr = take(e == 2 ? (size_t)16 * kRecKSP * 64 * 16 : 0);   // its fragment-order copy (frame-resident recurrence, recur.h)
   L.k_WdTl = take(192 * 4608 * e);
   L.k_WdTc = take(e == 4 ? 64 * 4608 * 4 : 0);   // its dx rows channel-chunk-major (BK 32: the fp32 dx ring, cmaj)
+  L.k_WdT6 = take(e == 4 ? 3 * 64 * 4608 * 2 : 0);   // its dx rows as three bf16 planes (the split6 dx ring's A)
   L.k_Wbf = take(e == 2 ? (size_t)6 * kBwKSP * 64 * 16 : 0);   // fragment-order [W_h^T | W_x^T] (frame-resident BPTT)
   L.k_Wf32 = take(e == 4 ? (size_t)16 * kF32QP * 64 * 16 : 0);   // fp32 fragment-order [x|h] (frame-group recurrence, recur_f32.h)
   L.k_Wb32 = take(e == 4 ? (size_t)8 * kB32QP * 4 * 64 * 16 : 0);   // fp32 fragment-order W_h^T (frame-group BPTT, recur_bwd_f32.h)

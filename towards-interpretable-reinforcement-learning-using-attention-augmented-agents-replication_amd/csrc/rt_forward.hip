@@ -38,6 +38,7 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
     HIPCHK(pack_wb32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wb32), st));
     HIPCHK(split_frag((const float*)(pk + L.k_Wf32), pk + L.k_Wf6, 16 * kF32QP * 64, st));
     HIPCHK(split_frag((const float*)(pk + L.k_Wb32), pk + L.k_Wb6, 8 * kB32QP * 4 * 64, st));
+    HIPCHK(split_planes((const float*)(pk + L.k_WdTl), 64L * 4608, (__bf16*)(pk + L.k_WdT6), st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
