@@ -125,7 +125,7 @@ def test_unroll_vs_oracle_fp32(cuda, T, B):
 @pytest.mark.parametrize("fwd,bwd", [(0, 0), (1, 1), (2, 2), (3, 3), (4, 4), (5, 5), (6, 6), (7, 4), (7, 7), (4, 8), (4, 9),
                                      (6, 10), (6, 11), (12, 12), (14, 13), (17, 15), (18, 16),
                                      (4, 19), (4, 20), (4, 21), (4, 22), (4, 23), (4, 24), (25, 16), (26, 16),
-                                     (4, 27), (4, 28), (4, 29), (4, 30), (4, 31)])
+                                     (4, 27), (4, 28), (4, 29), (4, 30), (4, 31), (4, 32), (4, 33)])
 @pytest.mark.parametrize("conv_dtype", ["fp32", "bf16"])
 def test_step_tile_variants(cuda, monkeypatch, fwd, bwd, conv_dtype):
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")   # the per-step launches (the frame-resident kernel: below)
@@ -174,10 +174,12 @@ def test_fused_step_tiles(cuda, monkeypatch, tile, conv_dtype):
                  f"bf16 fused tile {tile}: ")
 
 
-@pytest.mark.parametrize("tile,ns", [("30", "2"), ("30", "3"), ("30", "8"), ("31", "5")])
+@pytest.mark.parametrize("tile,ns", [("30", "2"), ("30", "3"), ("30", "8"), ("31", "5"), ("32", "3"), ("33", "4"),
+                                     ("33", "8")])
 def test_bptt_splitk_slices(cuda, monkeypatch, tile, ns):
     """Split-K BPTT (fp32 tiles 30/31): K-slice partials of the dh dgrad summed
-    by the gate backward; slice counts that do not divide K's 64-deep tiles
+    by the gate backward (30/31) or by the tile's last-arriving slice inside the
+    GEMM (32/33, EpiSliceFix); slice counts that do not divide K's 64-deep tiles
     evenly (3, 5) leave a short last slice."""
     monkeypatch.setenv("AAA_FRAMES_FWD", "0")
     monkeypatch.setenv("AAA_BPTT_TILE", tile)

@@ -84,6 +84,74 @@ template <class EP, bool> struct acc_of { using type = int; };
 template <class EP> struct acc_of<EP, true> { using type = typename EP::Acc; };
 // Epilogues that store one partial per K slice (EpiSliceT): the kernel hands
 // them the workgroup's slice index before any use (set_z on a local copy).
+// EpiSliceT with the tile finished in the kernel (stream-K fixup): every K
+// slice stores its partial, and the workgroup whose slice arrives last at the
+// tile's counter (cnt[ti * ntj + tj], zeroed once, reset by that workgroup)
+// sums the nz partials in slice order and runs the inner epilogue ``in`` on
+// them (gemm_pipe_kernel calls fixup<C> after the staged epilogue): one launch
+// per split-K step instead of a GEMM and a separate summing kernel.  Hand-off
+// without fences (an agent-scope release would write back the whole L2):
+// write-through (sc1) partial stores, every wave's vmcnt(0), a workgroup
+// barrier, ONE lane's agent-scope add to the tile's counter, and the last
+// workgroup -- told by the value its add returned -- takes one agent acquire
+// and reads the partials with sc1 loads behind a barrier (MI355X_MICROARCH.md
+// consumer rule; the hand-off table's row 1 without the acquire would do for
+// fresh buffers, but these are rewritten every step).
+template <class IN>
+struct EpiSliceFix {
+  static constexpr bool kFixup = true;
+  static constexpr int kSc1 = 16;   // buffer cache policy: sc1
+  float* out;        // slice 0 of the partials; slice s at out + s * sls (floats)
+  int ld, Mi, Nj;
+  size_t sls;
+  int nz, ntj;
+  int* cnt;
+  IN in;
+  int z = 0;
+  __device__ __forceinline__ void set_z(int z_) { z = z_; }
+  __device__ __forceinline__ void operator()(int i, int j, float v0, float v1, float v2, float v3) const {
+    if (j >= Nj || i >= Mi) return;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(out, (uint32_t)((size_t)nz * sls * 4));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4{v0, v1, v2, v3}), rs,
+                                           (uint32_t)(((size_t)z * sls + (size_t)j * ld + i) * 4), 0, kSc1);
+  }
+  template <class C>
+  __device__ __forceinline__ void fixup(void* lds, int i0, int j0, int ti, int tj) const {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores retired
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(lds);
+    if (threadIdx.x == 0) {
+      const int old = __hip_atomic_fetch_add(cnt + ti * ntj + tj, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == nz - 1) {
+        __hip_atomic_store(cnt + ti * ntj + tj, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the partial buffers are reused every step: drop this CU's / XCD's stale copies (one
+        // agent acquire by the last workgroup; the barrier below holds the others until it completes)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *last = old == nz - 1;
+    }
+    __syncthreads();
+    if (!*last) return;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(out, (uint32_t)((size_t)nz * sls * 4));
+    constexpr int G4 = C::BI / 4;
+    for (int c = (int)threadIdx.x; c < G4 * C::BJ; c += C::NT) {
+      const int i = i0 + 4 * (c % G4), j = j0 + c / G4;
+      if (j >= Nj || i >= Mi) continue;
+      const uint32_t o = (uint32_t)(((size_t)j * ld + i) * 4);
+      f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kSc1));
+      for (int k = 1; k < nz; ++k) {
+        const f32x4 u = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + (uint32_t)((size_t)k * sls * 4), 0, kSc1));
+        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+      }
+      in(i, j, v[0], v[1], v[2], v[3]);
+    }
+  }
+};
+
+template <class EP, class = void> struct has_fixup : std::false_type {};
+template <class EP> struct has_fixup<EP, std::enable_if_t<EP::kFixup>> : std::true_type {};
 template <class EP, class = void> struct has_set_z : std::false_type {};
 template <class EP>
 struct has_set_z<EP, std::void_t<decltype(std::declval<EP&>().set_z(0))>> : std::true_type {};
@@ -826,6 +894,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
     return;
   }
   staged_epilogue<C, EP, PL>(ep, smem, acc, i0, j0, BJ, tj, pre);
+  if constexpr (has_fixup<EP>::value) ep.template fixup<C>(smem, i0, j0, ti, tj);
   AAA_STAMP(3);
 }
 

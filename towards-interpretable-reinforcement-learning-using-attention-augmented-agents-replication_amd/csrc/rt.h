@@ -226,9 +226,9 @@ static int step_tile(long out_tiles32, const char* env, bool bptt, bool bf16 = f
   const int v = env_int(env, -1);
   if (v >= 0) {   // 7, 8: bf16 only; 9-11, 13, 15, 16: BPTT only; 14, 17, 18: forward only
     const bool bptt_only = v == 9 || v == 10 || v == 11 || v == 13 || v == 15 || v == 16 || (v >= 19 && v <= 24) ||
-                           (v >= 27 && v <= 31);
+                           (v >= 27 && v <= 33);
     if (v >= 19 && v <= 24 && !bf16) return 4;   // 19-24: bf16 BPTT tiles (fp16 gate storage)
-    if (v >= 27 && v <= 31 && bf16) return 4;    // 27-31: fp32 split-product BPTT tiles (30/31 split-K)
+    if (v >= 27 && v <= 33 && bf16) return 4;    // 27-33: fp32 split-product BPTT tiles (30-33 split-K)
     const bool fwd_only = v == 14 || v == 17 || v == 18 || v == 25 || v == 26;
     return ((v == 7 || v == 8) && !bf16) || (bptt_only && !bptt) || (fwd_only && bptt) ? 4 : v;
   }

@@ -722,7 +722,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     // the register-staged ones leave the bias to a column sum over dZ
     // (split-K tiles 30/31: the gate backward kernel's pixel tile, kSplitBj -- finer than the GEMM's, so
     // that kernel spreads over the chip)
-    const int bj = bwd_tile == 30 || bwd_tile == 31 ? kSplitBj : (bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 || bwd_tile == 22 || bwd_tile == 23 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64)));
+    const int bj = bwd_tile >= 30 && bwd_tile <= 33 ? kSplitBj : (bwd_tile == 7 || bwd_tile == 19 || bwd_tile == 20 ? 128 : (bwd_tile == 21 || bwd_tile == 22 || bwd_tile == 23 ? 64 : (bwd_tile >= 9 && bwd_tile != 14 ? 32 : 64)));
     const bool pipe = (bwd_tile == 4 && pipe_even<CfgK4BFor<T>>()) || (bwd_tile == 5 && pipe_even<CfgK4For<T>>()) ||
                       (bwd_tile == 6 && pipe_even<C>()) || bwd_tile == 7 || bwd_tile == 8 || bwd_tile >= 19 ||
                       (bwd_tile == 9 && pipe_even<GemmCfg<T, 64, 32, 128, 2, 1, 4>>()) ||
@@ -731,8 +731,11 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                       (bwd_tile == 13 && pipe_even<GemmCfg<T, 32, 32, 128, 1, 1, 8>>()) ||
                       (bwd_tile == 15 && pipe_even<GemmCfg<T, 64, 32, 64, 2, 1, 4>>()) ||
                       (bwd_tile >= 27 && bwd_tile <= 31);   // fp32 split-product tiles (ring only)
+    const bool fixk = bwd_tile == 32 || bwd_tile == 33;   // split-K finished in the GEMM: bias from dZ's column sum
+    if (fixk && L.dhs)   // the fixup counters (self-resetting; zeroed per call in case a launch was abandoned)
+      HIPCHK(hipMemsetAsync(ws + L.dhs + (size_t)std::max(kBpttSplitMax * 128, 4 * 512) * M * 4, 0, 4096, st));
     const int ntj = cdiv(M, bj);
-    float* part = pipe ? Wf(L.dZp) : nullptr;
+    float* part = pipe && !fixk ? Wf(L.dZp) : nullptr;
     const bool g16 = gates_f16(L.dt, M);
     const int fb = frames_bwd(L, g16);   // the whole chain in one frame-resident launch (workgroups per frame)
     // fp32: the frame-group BPTT (recur_bwd_f32.h, G = 8) behind the forward's frame-group kernel
@@ -818,6 +821,25 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       const T* dzt = Wt(L.dZ) + (size_t)t * M * 512;
       TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608, strf("%s dh dgrad + fused gate bwd, K=4608, AAA_BPTT_TILE %d%s", std::is_same<T, float>::value ? "fp32" : "bf16", bwd_tile, g16 ? ", fp16 gates [kernel: EpiConvLstmBwd]" : " [kernel: EpiConvLstmBwd]"));
       if constexpr (std::is_same<T, float>::value) {
+        if (fixk && prev) {   // split-K, the last slice of each tile runs the gate backward (EpiSliceFix)
+          if (!L.dhs) return fail(AAA_E_ARG, "AAA_BPTT_TILE %d: split-K needs B*P < 8192 (got %d)", bwd_tile, M);
+          const int bk = bwd_tile == 32 ? 64 : 128;
+          const int ns = splitk_slices(4608, bk, bptt_splitk());
+          float* dhp = Wf(L.dhs);
+          int* cnt = (int*)(ws + L.dhs + (size_t)std::max(kBpttSplitMax * 128, 4 * 512) * M * 4);
+          using EB = EpiConvLstmBwd<T, float>;
+          const EB eb{nullptr, (const float*)(ws + L.Gt) + (size_t)(t - 1) * M * 512, Wf(L.Cst) + (size_t)(t - 1) * M * 128,
+                      Wf(L.Cst) + (size_t)t * M * 128, Wf(L.dO) + (size_t)(t - 1) * M * 128, Wf(L.dC),
+                      Wt(L.dZ) + (size_t)(t - 1) * M * 512, nullptr, 1, M, 64, nullptr};
+          const EpiSliceFix<EB> ef{dhp, 128, 128, M, (size_t)M * 128, ns, cdiv(M, 32), cnt, eb};
+          if (bwd_tile == 32)
+            HIPCHK((step_gemm_splitk<GemmCfgS6<32, 32, 64, 1, 1, 4>>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ef, 128,
+                                                                     4608, st, ns)));
+          else
+            HIPCHK((step_gemm_splitk<GemmCfgS6<32, 32, 128, 1, 1, 8>>(WdTh, 4608, 128, dzt, g, M, dz_bytes, ef, 128,
+                                                                      4608, st, ns, true)));
+          continue;
+        }
         if ((bwd_tile == 30 || bwd_tile == 31) && prev) {   // split-K: K-slice partials, then the gate backward
           if (!L.dhs) return fail(AAA_E_ARG, "AAA_BPTT_TILE %d: split-K needs B*P < 8192 (got %d)", bwd_tile, M);
           const int bk = bwd_tile == 30 ? 64 : 128;
@@ -934,6 +956,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                                                                                               4608, st);
             case 30:   // split-K tiles: t = 0 (dh0) takes tile 27
             case 31:
+            case 32:
+            case 33:
               if constexpr (!std::is_same<T, float>::value) return hipErrorInvalidValue;
               else return step_gemm<GemmCfgS6<32, 32, 64, 1, 1, 4>, true, T, T, EB, 3, false>(WdTh, 4608, 128, dzt, g,
                                                                                               M, dz_bytes, ep, 128,

@@ -123,7 +123,8 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.xpart = take(L.esz == 4 && rec_fits(L.h, L.w) ? b32_xpart_floats(L.B) * 4 : 0);   // fp32 frame-group BPTT exchange
   // split-K partials: BPTT dh (<= kBpttSplitMax x 128 per pixel) or the fused forward step's gates (<= 4 x 512)
   // (0 = none: the split-K tiles then fail loudly)
-  L.dhs = L.esz == 4 && bptt_splitk_fits(M) ? take((size_t)std::max(kBpttSplitMax * 128, 4 * 512) * M * 4) : 0;
+  // (+ 4 KB: the split-K tiles' fixup counters, EpiSliceFix, after the partials)
+  L.dhs = L.esz == 4 && bptt_splitk_fits(M) ? take((size_t)std::max(kBpttSplitMax * 128, 4 * 512) * M * 4 + 4096) : 0;
   {
     const size_t sc = L.sc ? 1 : 0, B = L.B;
     L.CH = take(sc * (L.T + 1) * B * 256 * 4);
