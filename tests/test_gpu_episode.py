@@ -249,3 +249,20 @@ def test_core_transfer_refuses_bf16_and_bad_ranges(cuda):
     core = [torch.empty(s, device=cuda) for s in rf.core_shapes(2)]
     with pytest.raises(RuntimeError, match="steps"):
         rf.core_export(rf.new_workspace(), 2, 2, *core)
+
+
+def test_bf16_episode_recomputes_and_matches_per_step_path(cuda, monkeypatch):
+    """bf16 agents keep no ConvLSTM products (the store is fp32-only): the
+    fused backward re-runs the recurrence and must still give the per-step
+    path's gradients (same bf16 kernels and rounding points)."""
+    monkeypatch.setattr(E, "EPISODE_SEGMENT", 4)
+    T, B = 6, 2
+    X = _frames(T, B)
+    Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
+    Gv = torch.from_numpy(detinit.normal(3, (T, B, A)))
+    ag = _agent(cuda, True, dtype="bf16")
+    lf, gf = _episode(ag, X, Gl, Gv, cuda)
+    assert ag._episode.store is None
+    lr_, gr = _episode(_agent(cuda, False, dtype="bf16"), X, Gl, Gv, cuda)
+    assert torch.equal(lf, lr_)
+    _cmp(gf, gr, 2e-2, "bf16 fused vs per-step")
