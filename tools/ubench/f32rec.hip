@@ -22,9 +22,9 @@ static float* dev_rand(size_t n, float scale, unsigned seed) {
   return d;
 }
 
-template <int G, int ABL>
+template <int G, int ABL, bool S6 = false>
 static double run(RecF32Params p, int reps, const char* name) {
-  const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_f32<G, ABL>);
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_f32<G, ABL, S6>);
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   double best = 1e30, sum = 0;
@@ -89,9 +89,9 @@ static void phases(int G, int B, int T) {
 }
 #endif
 
-template <int ABL>
+template <int ABL, bool S6 = false>
 static double run_bwd(RecBwdF32Params p, int reps, const char* name) {
-  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_f32<ABL>);
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_f32<ABL, S6>);
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   double best = 1e30, sum = 0;
@@ -169,6 +169,15 @@ int main(int argc, char** argv) {
   run<8, 5>(p, reps, "no epilogue, no exchange");
   run<8, 13>(p, reps, "no epilogue/exchange/MFMA");
   run<4, 0>(p, reps, "production");
+  {  // the split-product (bf16x6) kernel, the production fp32 path since round 4
+    void* w6;
+    CK(hipMalloc(&w6, (size_t)16 * kF32QP * 64 * 24));
+    CK(split_frag(p.Wf, w6, 16 * kF32QP * 64, 0));
+    p.Wf6 = reinterpret_cast<const u32x2*>(w6);
+    run<8, 0, true>(p, reps, "S6 production");
+    run<8, 16, true>(p, reps, "S6 no B split (hi only)");
+    run<8, 1, true>(p, reps, "S6 no epilogue");
+  }
   {  // the frame-group BPTT at the same shape
     RecBwdF32Params q{};
     q.Wb = dev_rand((size_t)8 * kB32QP * 4 * 256, 0.02f, 7);
@@ -190,6 +199,13 @@ int main(int argc, char** argv) {
     run_bwd<1>(q, reps, "no partner waits");
     run_bwd<9>(q, reps, "no exchange");
     run_bwd<11>(q, reps, "no exchange, no MFMA");
+    void* w6;
+    CK(hipMalloc(&w6, (size_t)8 * kB32QP * 4 * 64 * 24));
+    CK(split_frag(q.Wb, w6, 8 * kB32QP * 4 * 64, 0));
+    q.Wb6 = reinterpret_cast<const u32x2*>(w6);
+    run_bwd<0, true>(q, reps, "S6 production");
+    run_bwd<16, true>(q, reps, "S6 no B split (hi only)");
+
   }
   printf("timeout reports: %d\n", *hrep);
   return 0;

@@ -91,7 +91,8 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 #endif
 
 // ABL (diagnostic builds only, tools/ubench/f32rec): bit 0 = no partner waits,
-// bit 1 = no MFMAs, bit 3 = no exchange (partials neither stored nor loaded).
+// bit 1 = no MFMAs, bit 3 = no exchange (partials neither stored nor loaded),
+// bit 4 (S6) = no three-way split of the B fragments (hi only).
 // Production launches use 0.
 // S6: the MFMAs on the bf16 MFMA at fp32 accuracy, two quads per k-step with
 // three-way split operands (as recur_f32.h S6, gemm.h SPLIT6).
@@ -293,7 +294,14 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
           for (int c = 0; c < 2; ++c) {
             const float b8[8] = {bp[2 * pb][c][0],     bp[2 * pb][c][1],     bp[2 * pb][c][2],     bp[2 * pb][c][3],
                                  bp[2 * pb + 1][c][0], bp[2 * pb + 1][c][1], bp[2 * pb + 1][c][2], bp[2 * pb + 1][c][3]};
-            split3_bf16(b8, bh[c], bm[c], bl[c]);
+            if constexpr ((ABL & 16) != 0) {   // ablation: hi part only (the split's VALU cost)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) bh[c][e] = (__bf16)b8[e];
+              bm[c] = bh[c];
+              bl[c] = bh[c];
+            } else {
+              split3_bf16(b8, bh[c], bm[c], bl[c]);
+            }
           }
 #pragma unroll
           for (int r = 0; r < 2; ++r) {

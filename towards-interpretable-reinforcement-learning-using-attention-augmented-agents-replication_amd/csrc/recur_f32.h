@@ -149,7 +149,8 @@ __device__ uint64_t aaa_f32_clocks[512 * 64 * 5];   // s_memtime (shader clock) 
 
 // ABL (diagnostic builds only, tools/ubench/f32rec; production launches use 0):
 // bit 0 = no epilogue (gate math, stores), bit 1 = no epilogue HBM stores,
-// bit 2 = no partner exchange, bit 3 = no MFMAs.
+// bit 2 = no partner exchange, bit 3 = no MFMAs, bit 4 (S6) = no three-way
+// split of the B fragments (hi part only: the split's cost, wrong numerics).
 // S6: the MFMAs on the bf16 MFMA at fp32 accuracy (gemm.h SPLIT6): two quads
 // (16 channels) per v_mfma_f32_32x32x16_bf16 k-step -- lane half hh's 8 k-slots
 // are channels 4hh..4hh+3 of the first quad, then of the second, in the same
@@ -332,7 +333,14 @@ k_convlstm_fwd_f32(RecF32Params p) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const float b8[8] = {b0[c][0], b0[c][1], b0[c][2], b0[c][3], b1[c][0], b1[c][1], b1[c][2], b1[c][3]};
-        split3_bf16(b8, bh[c], bm[c], bl[c]);
+        if constexpr ((ABL & 16) != 0) {   // ablation: hi part only (the split's VALU cost, wrong numerics)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bh[c][e] = (__bf16)b8[e];
+          bm[c] = bh[c];
+          bl[c] = bh[c];
+        } else {
+          split3_bf16(b8, bh[c], bm[c], bl[c]);
+        }
       }
 #pragma unroll
       for (int r = 0; r < RPW; ++r) {
