@@ -22,9 +22,9 @@ static float* dev_rand(size_t n, float scale, unsigned seed) {
   return d;
 }
 
-template <int G, int ABL, bool S6 = false>
+template <int G, int ABL, bool S6 = false, bool WIDE = false, int PDW = kF32PD>
 static double run(RecF32Params p, int reps, const char* name) {
-  const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_f32<G, ABL, S6>);
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_fwd_f32<G, ABL, S6, WIDE, PDW>);
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   double best = 1e30, sum = 0;
@@ -89,9 +89,9 @@ static void phases(int G, int B, int T) {
 }
 #endif
 
-template <int ABL, bool S6 = false>
+template <int ABL, bool S6 = false, int PDS = kB32PD>
 static double run_bwd(RecBwdF32Params p, int reps, const char* name) {
-  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_f32<ABL, S6>);
+  const void* k = reinterpret_cast<const void*>(&k_convlstm_bwd_f32<ABL, S6, PDS>);
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   double best = 1e30, sum = 0;
@@ -174,9 +174,21 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&w6, (size_t)16 * kF32QP * 64 * 24));
     CK(split_frag(p.Wf, w6, 16 * kF32QP * 64, 0));
     p.Wf6 = reinterpret_cast<const u32x2*>(w6);
-    run<8, 0, true>(p, reps, "S6 production");
-    run<8, 16, true>(p, reps, "S6 no B split (hi only)");
-    run<8, 1, true>(p, reps, "S6 no epilogue");
+    for (int rep = 0; rep < 2; ++rep) {   // the arms twice, in opposite orders (clock drift)
+      if (rep == 1) {
+        run<8, 0, true, true, 4>(p, reps, "S6 WIDE, 4 A quads in flight (production)");
+        run<8, 0, true, false, 4>(p, reps, "S6, 4 A quads in flight");
+        run<8, 0, true, true>(p, reps, "S6 WIDE (1 wave per column block)");
+      }
+      run<8, 0, true>(p, reps, "S6 2 column blocks per wave, 8 in flight");
+      run<8, 16, true>(p, reps, "S6 no B split (hi only)");
+      run<8, 1, true>(p, reps, "S6 no epilogue");
+      if (rep == 0) {
+        run<8, 0, true, true>(p, reps, "S6 WIDE (1 wave per column block)");
+        run<8, 0, true, false, 4>(p, reps, "S6, 4 A quads in flight");
+        run<8, 0, true, true, 4>(p, reps, "S6 WIDE, 4 A quads in flight (production)");
+      }
+    }
   }
   {  // the frame-group BPTT at the same shape
     RecBwdF32Params q{};
@@ -203,8 +215,12 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&w6, (size_t)8 * kB32QP * 4 * 64 * 24));
     CK(split_frag(q.Wb, w6, 8 * kB32QP * 4 * 64, 0));
     q.Wb6 = reinterpret_cast<const u32x2*>(w6);
-    run_bwd<0, true>(q, reps, "S6 production");
-    run_bwd<16, true>(q, reps, "S6 no B split (hi only)");
+    for (int rep = 0; rep < 2; ++rep) {
+      if (rep == 1) run_bwd<0, true, 4>(q, reps, "S6, 4 A quads in flight (production)");
+      run_bwd<0, true>(q, reps, "S6, 8 A quads in flight");
+      run_bwd<16, true>(q, reps, "S6 no B split (hi only)");
+      if (rep == 0) run_bwd<0, true, 4>(q, reps, "S6, 4 A quads in flight (production)");
+    }
 
   }
   printf("timeout reports: %d\n", *hrep);

@@ -96,7 +96,8 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 // Production launches use 0.
 // S6: the MFMAs on the bf16 MFMA at fp32 accuracy, two quads per k-step with
 // three-way split operands (as recur_f32.h S6, gemm.h SPLIT6).
-template <int ABL = 0, bool S6 = false>
+// PDS: the S6 kernel's A quads in flight (4 or 8).
+template <int ABL = 0, bool S6 = false, int PDS = kB32PD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_bwd_f32(RecBwdF32Params p) {
   constexpr int G = 8, NG = 2;                   // NG: (pixel, 4-channel) groups per thread (484 <= 512)
@@ -189,8 +190,8 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                          rsw, lane * 16, ((kh * kB32QP + q) * 4 + 2 * rw + r) * 1024, 0));
   };
-  constexpr int PD = kB32PD;
-  static_assert(kB32Q % PD == 0 && PD == 8, "slot = q8");
+  constexpr int PD = S6 ? PDS : kB32PD;
+  static_assert(kB32Q % PD == 0 && 8 % PD == 0 && PD >= 4 && PD <= kB32PD, "slot = q8 % PD");
   f32x4 af[PD][2];
   // S6: the pre-split stream (recur_f32.h k_split_frag), part p of chunk group g at (g * 3 + p) * 512 B
   const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wb6, S6 ? (uint32_t)(8 * kB32QP * 4 * 3 * 512) : 0u);
@@ -272,14 +273,14 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
           for (int r = 0; r < 2; ++r)
 #pragma unroll
             for (int part = 0; part < 3; ++part)
-              a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8][r][part].x, a6[q8][r][part].y,
-                                                             a6[q8 + 1][r][part].x, a6[q8 + 1][r][part].y});
+              a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8 % PD][r][part].x, a6[q8 % PD][r][part].y,
+                                                             a6[q8 % PD + 1][r][part].x, a6[q8 % PD + 1][r][part].y});
 #pragma unroll
           for (int r = 0; r < 2; ++r)
 #pragma unroll
             for (int part = 0; part < 3; ++part) {
               a6[(q8 + PD - 1) % PD][r][part] = lda6(qt + q8 + PD - 1, r, part);
-              a6[q8][r][part] = lda6(qt + q8 + PD, r, part);
+              a6[q8 % PD][r][part] = lda6(qt + q8 + PD, r, part);
             }
           if (q8 < 6) {
             ldb(tap, q8 + 2, bp[2 * nb]);
@@ -446,7 +447,8 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 =
     const int pp = c < p.P ? c : p.P - 1;
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
-  return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true>)
+  // S6: 4 A quads in flight (tools/ubench/f32rec: 3% under 8, fewer registers parked in AGPRs)
+  return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4>)
                             : reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>),
                          f32_grid(p.B, 8), 256, p, st);
 }

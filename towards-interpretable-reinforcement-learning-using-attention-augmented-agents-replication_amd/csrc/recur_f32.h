@@ -156,10 +156,18 @@ __device__ uint64_t aaa_f32_clocks[512 * 64 * 5];   // s_memtime (shader clock) 
 // are channels 4hh..4hh+3 of the first quad, then of the second, in the same
 // order for A and B -- each operand split three ways, six MFMAs (6 x 32
 // cycles) where the fp32 MFMA takes eight (8 x 64).
-template <int G, int ABL = 0, bool S6 = false>
+//
+// WIDE (S6, G = 8 only): wave w takes both row blocks and column block w, so each
+// B fragment is split by one wave instead of two (the split is VALU work the MFMAs
+// wait on: tools/ubench/f32rec "S6 no B split"), at twice the per-wave A stream
+// (the four waves of a workgroup then read the same A quads).  PDW: A quads in flight.
+template <int G, int ABL = 0, bool S6 = false, bool WIDE = false, int PDW = kF32PD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_fwd_f32(RecF32Params p) {
-  constexpr int NRB = 16 / G, RPW = NRB / 2;       // row blocks per workgroup / per wave
+  static_assert(!WIDE || (S6 && G == 8), "WIDE: the S6 kernel at G = 8");
+  constexpr int NRB = 16 / G;                      // row blocks per workgroup
+  constexpr int RPW = WIDE ? NRB : NRB / 2;        // ... per wave
+  constexpr int NCB = WIDE ? 1 : 2;                // column blocks per wave
   constexpr int CPG = 32 / G;                      // 16-B h chunks (4 channels) per workgroup slice
   constexpr int NPL = (128 * (G - 1) * CPG + 255) / 256;   // partner chunks per thread (P <= 128)
   static_assert(G == 4 || G == 8, "G");
@@ -176,7 +184,8 @@ k_convlstm_fwd_f32(RecF32Params p) {
   const int r32 = lane & 31, hh = lane >> 5;
   const int P = p.P, W2 = p.w + 2, NPH = (p.h + 2) * W2;
   const size_t M = (size_t)p.B * P;
-  const int rw = wave & 1, cw = wave >> 1;
+  const int rw = WIDE ? 0 : wave & 1;
+  auto cbk = [&](int c) { return WIDE ? wave : 2 * (wave >> 1) + c; };   // the wave's column block c
   const int rbg0 = kh * NRB + rw * RPW;            // the wave's first global row block
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
   auto sw16 = [](int q, int key) { return (q ^ (key & 15)) << 4; };
@@ -212,13 +221,13 @@ k_convlstm_fwd_f32(RecF32Params p) {
 
   // per-lane state: bias of the lane's rows, c of its (pixel, channel) pairs
   // tile (r, c) lane (r32, hh): element 4g + e = row 8g + 4hh + e of row block
-  // rbg0 + r = gate e of channel 8 (rbg0 + r) + 2g + hh, at column 32 (2cw + c) + r32
+  // rbg0 + r = gate e of channel 8 (rbg0 + r) + 2g + hh, at column 32 cbk(c) + r32
   f32x4 bz[RPW][4];
-  float cst[RPW][2][4];
-  int pcol[2], hb[2], sb[2];   // sb: swizzle key of the window's top-left pixel
+  float cst[RPW][NCB][4];
+  int pcol[NCB], hb[NCB], sb[NCB];   // sb: swizzle key of the window's top-left pixel
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int col = 32 * (2 * cw + c) + r32;
+  for (int c = 0; c < NCB; ++c) {
+    const int col = 32 * cbk(c) + r32;
     pcol[c] = col < P ? col : -1;
     hb[c] = p.colhb[col];
     sb[c] = (col < P ? col : P - 1) - p.w - 1;
@@ -230,7 +239,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
       const int ch = 8 * (rbg0 + r) + 2 * g + hh;
       bz[r][g] = *reinterpret_cast<const f32x4*>(p.bias + 4 * ch);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) cst[r][c][g] = pcol[c] >= 0 ? p.Cst[((size_t)b * P + pcol[c]) * 128 + ch] : 0.f;
+      for (int c = 0; c < NCB; ++c) cst[r][c][g] = pcol[c] >= 0 ? p.Cst[((size_t)b * P + pcol[c]) * 128 + ch] : 0.f;
     }
 
   // A stream: the wave's RPW row blocks, quad q at soffset (rb * kF32QP + q) * 1 KB
@@ -239,7 +248,8 @@ k_convlstm_fwd_f32(RecF32Params p) {
     return __builtin_bit_cast(f32x4,
                               __builtin_amdgcn_raw_buffer_load_b128(rsw, lane * 16, ((rbg0 + r) * kF32QP + q) * 1024, 0));
   };
-  constexpr int PD = kF32PD;
+  constexpr int PD = S6 ? PDW : kF32PD;
+  static_assert(8 % PD == 0 && PD >= 4 && PD <= kF32PD, "PD");   // slot = quad % PD; a pair never wraps
   f32x4 af[PD][RPW];
   // S6: the pre-split stream, quad q's part p of row block rb at ((rb * kF32QP + q) * 3 + p) * 512 B
   const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wf6, S6 ? (uint32_t)(16 * kF32QP * 3 * 512) : 0u);
@@ -267,16 +277,16 @@ k_convlstm_fwd_f32(RecF32Params p) {
   __syncthreads();   // every wave's x_0 DMA landed
 
   for (int t = 0; t < p.T; ++t) {
-    f32x16 acc[RPW][2];
+    f32x16 acc[RPW][NCB];
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < NCB; ++c)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
-    int hbs[2], sbs[2];
+    int hbs[NCB], sbs[NCB];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < NCB; ++c) {
       hbs[c] = hb[c];
       sbs[c] = sb[c];
       asm volatile("" : "+v"(hbs[c]), "+v"(sbs[c]));
@@ -284,15 +294,15 @@ k_convlstm_fwd_f32(RecF32Params p) {
     // a tap's image-pixel offset and swizzle-key offset, packed (key offset << 16 | pixel offset)
     auto tapoff = [&](int tap) { return (((tap / 3) * p.w + tap % 3) << 16) | ((tap / 3) * W2 + tap % 3); };
     // B fragments of a quad: image pixel hbs[c] + toff, 16-B chunk q (x: 0..15, h: 0..31) + hh
-    auto ldb = [&](const unsigned char* img, int pitch, int toff, int q, f32x4 (&bf)[2]) {
+    auto ldb = [&](const unsigned char* img, int pitch, int toff, int q, f32x4 (&bf)[NCB]) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NCB; ++c) {
         const int ip = hbs[c] + (toff & 0xffff);
         bf[c] = *reinterpret_cast<const f32x4*>(img + ip * pitch + sw16(q + hh, sbs[c] + (toff >> 16)));
       }
     };
     // one quad: A prefetch PD-1 ahead, next B fragments, 4 k-steps x RPW x 2 MFMAs
-    auto quad = [&](int qn, int slot, f32x4 (&bc)[2], auto&& load_next_b) {
+    auto quad = [&](int qn, int slot, f32x4 (&bc)[NCB], auto&& load_next_b) {
 #pragma unroll
       for (int r = 0; r < RPW; ++r) af[(slot + PD - 1) % PD][r] = lda(qn + PD - 1, r);
       load_next_b();
@@ -302,7 +312,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
+          for (int c = 0; c < NCB; ++c) {
             if constexpr (ABL & 8)
               acc[r][c][j] += af[slot][r][j] * bc[c][j];
             else
@@ -312,7 +322,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
     };
     // S6: quads qn, qn + 1 (slot even: PD is even), B fragments of both in b0 / b1;
     // the A operand's parts come pre-split (k_split_frag): two quads' 8-B parts side by side
-    auto pair = [&](int qn, int slot, f32x4 (&b0)[2], f32x4 (&b1)[2], auto&& load_next_b) {
+    auto pair = [&](int qn, int slot, f32x4 (&b0)[NCB], f32x4 (&b1)[NCB], auto&& load_next_b) {
       bf16x8 a3[RPW][3];
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
@@ -329,9 +339,9 @@ k_convlstm_fwd_f32(RecF32Params p) {
         }
       load_next_b();
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 bh[2], bm[2], bl[2];
+      bf16x8 bh[NCB], bm[NCB], bl[NCB];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NCB; ++c) {
         const float b8[8] = {b0[c][0], b0[c][1], b0[c][2], b0[c][3], b1[c][0], b1[c][1], b1[c][2], b1[c][3]};
         if constexpr ((ABL & 16) != 0) {   // ablation: hi part only (the split's VALU cost, wrong numerics)
 #pragma unroll
@@ -346,7 +356,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
       for (int r = 0; r < RPW; ++r) {
         const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < NCB; ++c) {
           acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[c], acc[r][c], 0, 0, 0);
           acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[c], acc[r][c], 0, 0, 0);
           acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[c], acc[r][c], 0, 0, 0);
@@ -357,8 +367,8 @@ k_convlstm_fwd_f32(RecF32Params p) {
       }
       __builtin_amdgcn_sched_barrier(0);
     };
-    f32x4 bfr[2][2];
-    f32x4 bp[4][2];   // S6: B fragments of two pairs of quads
+    f32x4 bfr[2][NCB];
+    f32x4 bp[4][NCB];   // S6: B fragments of two pairs of quads
     // partners' slices of h_{t-1} (XH slot t): loaded into registers mid x-part
     u32x4 pv[NPL];
     const bool exch = G > 1 && t > 0 && !(ABL & 4);
@@ -477,7 +487,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NCB; ++c) {
         const int pp = pcol[c];
         if constexpr ((ABL & 1) != 0) {   // keep the accumulators alive, no epilogue work
           if (pp < 0) *reinterpret_cast<float*>(him) = acc[r][c][0] + acc[r][c][15];
@@ -500,7 +510,7 @@ k_convlstm_fwd_f32(RecF32Params p) {
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!(ABL & 2)) {
-          const int col0 = 32 * (2 * cw + c);
+          const int col0 = 32 * cbk(c);
 #pragma unroll
           for (int k = 0; k < 4; ++k) {   // Gt: 32 pixels x 8 chunks of 16 B (rows 32 rbg .. + 32)
             const int q = k * 64 + lane, px = q >> 3, ch16 = q & 7, pix = col0 + px;
@@ -555,7 +565,9 @@ inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool 
     const int pp = c < p.P ? c : p.P - 1;
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
-  const void* k = G == 8   ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true>)
+  // G = 8, S6: the WIDE mapping with 4 A quads in flight (tools/ubench/f32rec: 7-10% under
+  // the two-column-block mapping with 8, most of it from the shallower prefetch)
+  const void* k = G == 8   ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true, true, 4>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>))
                   : G == 4 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4, 0, true>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4>))
