@@ -87,6 +87,7 @@ struct RecBwdParams {   // dO, Gt, Cst: per-(frame, step) slices, channel-quad-m
   int spin;               // paired / band kernels: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;            // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
   int cqm = kCqmC | kCqmG | kCqmDO;   // which slices are channel-quad-major (recur.h kCqm*)
+  int rowpad = 0;         // single-workgroup kernel: 16-B slots after each image row (0 or 14: bw_rowpad)
 };
 
 // Chunk images of the band kernel: image pixel ip (a (rows+2) x (w+2)
@@ -102,6 +103,13 @@ struct RecBwdParams {   // dO, Gt, Cst: per-(frame, step) slices, channel-quad-m
 // (C3 BPTT 1340 -> 1358 us, C4 paired 756 -> 790; profiles/r03/ab/swizzle.txt).
 __device__ __forceinline__ int bw_fz(int ip, int W2) { return (ip - 2 * (ip / W2)) & 15; }
 constexpr int kBwIBS = 47104;   // swizzled chunk image bytes: 184 px x 256 B (46 whole 1-KB DMA pieces)
+// The single-workgroup kernel's row-padded images: pixel ip at byte 272 ip + 16 rowpad (ip / W2).
+// With rowpad = 14 the slot group of (pixel, slot j) is (ip - 2 (ip / W2) + j) mod 16 = bw_fz + j:
+// a B-fragment read's consecutive columns stay on consecutive bank groups across grid-row ends
+// (272-B rows alone skip two groups at every row end), and a tap and a k step still move the
+// address by a wave-uniform amount and an immediate -- window columns never cross an image row.
+constexpr int kBwIBP = 49152;   // row-padded chunk image bytes (48 whole 1-KB DMA pieces)
+inline int bw_rowpad(int h, int w) { return (h + 2) * (17 * (w + 2) + 14) * 16 <= kBwIBP ? 14 : 0; }
 
 #ifdef AAA_STAMPS
 // Diagnostic builds only (tools/ubench/bwband): per (workgroup, step) phase stamps
@@ -133,7 +141,8 @@ template <int ABL = 0, bool BAND = false, bool DOACC = !BAND>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
   constexpr bool SWZ = BAND;             // swizzled 256-B pixel rows (band) or 272-B rows
   constexpr int PIT = SWZ ? 256 : 272;   // image pixel pitch (bytes)
-  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBS];   // chunk images (0: chunks 0, 2; 1: 1, 3)
+  constexpr int IMG = SWZ ? kBwIBS : kBwIBP;   // bytes per chunk image
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * IMG];   // chunk images (0: chunks 0, 2; 1: 1, 3)
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];          // dc carry, lane-native [wave][g*4+cb][lane]
   int b = (int)blockIdx.x, band = 0, r0 = 0, r1 = p.h;   // band mode: this workgroup's grid rows [r0, r1)
   if constexpr (BAND) {
@@ -152,10 +161,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   const int Pb = (r1 - r0) * p.w, pix0 = r0 * p.w;   // the band's pixels (the whole frame without BAND)
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w - r0 + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
+  const int rp = SWZ ? 0 : p.rowpad;   // (the host checked that the padded image fits: bw_rowpad)
+  auto pixb = [&](int ip) { return SWZ ? ip * PIT : 272 * ip + 16 * rp * (ip / W2); };   // image pixel -> byte
+  const int RS = 17 * W2 + rp;         // unswizzled: 16-B slots per image row
 
   {  // zero the images (borders and pads stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < 2 * kBwIBS / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < 2 * IMG / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   // chunk c (rows 128c .. 128c+127) of dZ_t from HBM into image c & 1, whole
   // 1-KB pieces of 4 image pixels; borders and the tail read outside the
@@ -163,14 +175,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto dma_chunk = [&](int t, int c) {
     const __amdgpu_buffer_rsrc_t rs =
         make_rsrc(p.dZ + ((size_t)t * M + (size_t)b * P) * 512, (uint32_t)(P * 512 * 2));
-    for (int i = wave; i < (SWZ ? (NPH + 3) >> 2 : kBwIB / 1024); i += 4) {
-      const int sl = i * 64 + lane, ip = SWZ ? sl >> 4 : sl / 17, iy = ip / W2, ix = ip - iy * W2;
-      const int q = SWZ ? sl & 15 : sl - 17 * ip;   // 16-B slot of the pixel row (17: the pad)
-      const int py = r0 + iy - 1, px = ix - 1, lq = SWZ ? q ^ ((ip - 2 * iy) & 15) : q;
-      const bool v = (SWZ || q < 16) && ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
-      const uint32_t vo = v ? (uint32_t)(((py * p.w + px) * 512 + 128 * c + lq * 8) * 2) : kOOB;
-      if constexpr (BAND) dma16_sc1(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
-      else dma16(rs, zim + (c & 1) * kBwIBS + i * 1024, vo);
+    for (int i = wave; i < (SWZ ? (NPH + 3) >> 2 : ((r1 - r0 + 2) * RS + 63) >> 6); i += 4) {
+      const int sl = i * 64 + lane;
+      int iy, ix, q;   // image row, column, 16-B slot of the pixel row (unswizzled: 16 = the pixel pad, ix = W2 the row pad)
+      if constexpr (SWZ) {
+        iy = (sl >> 4) / W2;
+        ix = (sl >> 4) - iy * W2;
+        q = (sl & 15) ^ (((sl >> 4) - 2 * iy) & 15);
+      } else {
+        iy = sl / RS;
+        const int rem = sl - iy * RS;
+        ix = rem / 17;
+        q = rem - 17 * ix;
+      }
+      const int py = r0 + iy - 1, px = ix - 1;
+      const bool v = q < 16 && iy < r1 - r0 + 2 && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
+      const uint32_t vo = v ? (uint32_t)(((py * p.w + px) * 512 + 128 * c + q * 8) * 2) : kOOB;
+      if constexpr (BAND) dma16_sc1(rs, zim + (c & 1) * IMG + i * 1024, vo);
+      else dma16(rs, zim + (c & 1) * IMG + i * 1024, vo);
     }
   };
 
@@ -314,7 +336,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             *reinterpret_cast<bf16x8*>(zo + 8) = z1;
           }
           if (wave < 2) {   // chunk w of the next step's B operand: rows 4(ch - 32w) + gate = slots 4g + 2hq, +1
-            unsigned char* zi = zim + wave * kBwIBS + hidx(pp) * PIT;
+            unsigned char* zi = zim + wave * IMG + pixb(hidx(pp));
             const int fz = SWZ ? (col + p.w + 1) & 15 : 0, s0 = 4 * g + 2 * hq;
             *reinterpret_cast<bf16x8*>(zi + ((s0 ^ fz) << 4)) = z0;
             *reinterpret_cast<bf16x8*>(zi + (((s0 + 1) ^ fz) << 4)) = z1;
@@ -409,7 +431,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           const int gy = (k >> 1) ? r1 : r0 - 1, iy = (k >> 1) ? r1 - r0 + 1 : 0, gx = j >> 4;
           if (i < 4 * nh && (unsigned)gy < (unsigned)p.h) {
             const int ip = iy * W2 + gx + 1, fz = (iy * p.w + gx + 1) & 15;
-            *reinterpret_cast<u32x4*>(zim + (k & 1) * kBwIBS + ip * 256 + (((j & 15) ^ fz) << 4)) = v[r];
+            *reinterpret_cast<u32x4*>(zim + (k & 1) * IMG + ip * 256 + (((j & 15) ^ fz) << 4)) = v[r];
           }
         }
       }
@@ -432,27 +454,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     int hbs[4], fbs[4];
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
-      hbs[cb] = hb[cb];
+      hbs[cb] = SWZ ? hb[cb] : pixb(hb[cb]);   // unswizzled: the window's top-left pixel as a byte offset
       fbs[cb] = fb[cb];
       asm volatile("" : "+v"(hbs[cb]), "+v"(fbs[cb]));
     }
     // transposed gather: output pixel q reads dZ at q - d(tap): image offset (2-ky)*W2 + (2-kx),
     // bw_fz offset (2-ky)*w + (2-kx).  Per tap and column block: the byte address of the
     // lane's pixel row or'ed with its swizzled slot for c16 = 0; row group c16 xors in c16 << 5.
-    // (unswizzled: the lane's part hbs * PIT + hh * 16 is per step, the tap's offset wave-uniform, the row
+    // (unswizzled: the lane's part hbs + hh * 16 is per step, the tap's offset wave-uniform, the row
     // group an immediate; tb then carries the tap offset only)
     auto bases = [&](int tap, int (&tb)[4]) {
       const int ky = tap / 3, kx = tap - 3 * ky;
       const int toff = (2 - ky) * W2 + (2 - kx), tf = (2 - ky) * p.w + (2 - kx);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
-        tb[cb] = SWZ ? ((hbs[cb] + toff) << 8) | (((((fbs[cb] + tf) & 15) ^ hh)) << 4) : toff * PIT;
+        tb[cb] = SWZ ? ((hbs[cb] + toff) << 8) | (((((fbs[cb] + tf) & 15) ^ hh)) << 4) : toff * PIT + 16 * rp * (2 - ky);
     };
     auto ldb = [&](const unsigned char* img, const int (&tb)[4], int c16, bf16x8 (&bf)[4]) {
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
         bf[cb] = SWZ ? *reinterpret_cast<const bf16x8*>(img + (tb[cb] ^ (c16 << 5)))
-                     : *reinterpret_cast<const bf16x8*>(img + tb[0] + hbs[cb] * PIT + hh * 16 + c16 * 32);
+                     : *reinterpret_cast<const bf16x8*>(img + tb[0] + hbs[cb] + hh * 16 + c16 * 32);
     };
     constexpr int BD = 4;   // B fragment ring: BD-1 k steps of lookahead (LDS latency vs 4 MFMAs per k step); divides 8
     bf16x8 bfr[BD][4];
@@ -463,7 +485,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       constexpr int XC = decltype(xc)::value;
   #pragma unroll 1
       for (int ck = 0; ck < 4; ++ck) {
-        const unsigned char* img = zim + (ck & 1) * kBwIBS;
+        const unsigned char* img = zim + (ck & 1) * IMG;
         if (ck == 1 || ck == 2) {   // every wave is done with image ck-1 and every wave's dZ_t stores have
                                     // retired (its later A loads did): refill it with chunk ck+1 from HBM
           if constexpr (!(ABL & 8)) dma_chunk(t, ck + 1);
@@ -603,7 +625,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 // Launched as one residency wave (launch_resident); the spins are bounded and reported.
 template <int ABL = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_pairs(RecBwdParams p) {
-  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIB];   // chunk images (c & 1)
+  __shared__ __attribute__((aligned(16))) unsigned char zim[2 * kBwIBP];   // chunk images (c & 1)
   __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 8 * 64];          // dc carry, lane-native [wave][g*2+j][lane]
   const int b = (int)blockIdx.x % p.B, kh = (int)blockIdx.x / p.B;
   const int tid = (int)threadIdx.x, lane = tid & 63;
@@ -615,10 +637,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   const int hrb = 2 * kh + (wave & 1);   // the wave's h row block (channels 32 hrb ..) = the dZ chunk it produces
   const int cbA = 2 * (wave >> 1);       // its column blocks cbA, cbA + 1
   auto hidx = [&](int pp) { return (pp / p.w + 1) * W2 + pp % p.w + 1; };
+  // row-padded images as in k_convlstm_bwd_frames (kBwIBP; the host checked bw_rowpad)
+  const int rp = p.rowpad;
+  auto pixb = [&](int ip) { return 272 * ip + 16 * rp * (ip / W2); };   // image pixel -> byte
 
   {  // zero the images (borders and pads stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < 2 * kBwIB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < 2 * kBwIBP / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   // the partner's chunk c of dZ_t: sc1 loads of the P x 256 B into registers
   // (issued at the start of a chunk), then into image c & 1 (three taps later)
@@ -637,7 +662,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
     for (int r = 0; r < NPR; ++r) {
       const int i = tid + 256 * r, px = i >> 4, q = i & 15;
-      if (px < P) *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIB + hidx(px) * (kBwIP * 2) + q * 16) = v[r];
+      if (px < P) *reinterpret_cast<u32x4*>(zim + (c & 1) * kBwIBP + pixb(hidx(px)) + q * 16) = v[r];
     }
   };
 
@@ -747,7 +772,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
           const uint32_t zo = (uint32_t)((pp * 512 + 4 * ch) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, kSC1);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo + 16, 0, kSC1);
-          unsigned char* zi = zim + (wave & 1) * kBwIB + hidx(pp) * (kBwIP * 2) + (4 * (ch - 32 * hrb)) * 2;
+          unsigned char* zi = zim + (wave & 1) * kBwIBP + pixb(hidx(pp)) + (4 * (ch - 32 * hrb)) * 2;
           *reinterpret_cast<bf16x8*>(zi) = z0;
           *reinterpret_cast<bf16x8*>(zi + 16) = z1;
         }
@@ -797,14 +822,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     int hbs[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      hbs[j] = hb[j];
+      hbs[j] = pixb(hb[j]);   // the window's top-left pixel as a byte offset
       asm volatile("" : "+v"(hbs[j]));
     }
-    auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + (2 - tap % 3); };
+    // a tap's byte offset (window columns never cross an image row: the row pad is per tap row)
+    auto tapoff = [&](int tap) { return ((2 - tap / 3) * W2 + (2 - tap % 3)) * 272 + 16 * rp * (2 - tap / 3); };
     auto ldb = [&](const unsigned char* img, int toff, int c16, bf16x8 (&bf)[2]) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        bf[j] = *reinterpret_cast<const bf16x8*>(img + (hbs[j] + toff) * (kBwIP * 2) + c16 * 32 + hh * 16);
+        bf[j] = *reinterpret_cast<const bf16x8*>(img + hbs[j] + toff + c16 * 32 + hh * 16);
     };
     constexpr int BD = 4;
     bf16x8 bfr[BD][2];
@@ -814,7 +840,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll 1
       for (int ck = 0; ck < 4; ++ck) {
         const int c = (ck + 2 * kh) & 3;   // own chunks first, then the partner's
-        const unsigned char* img = zim + (c & 1) * kBwIB;
+        const unsigned char* img = zim + (c & 1) * kBwIBP;
         u32x4 pv[NPR];
         const bool refill = ck == 1 || ck == 2;   // the partner's chunk c+1 into the image chunk ck-1 freed
         if (refill) pld(t, (c + 1) & 3, pv);
@@ -922,14 +948,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 }
 
 inline hipError_t convlstm_bwd_pairs(const RecBwdParams& p, hipStream_t st) {
-  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
+  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0 ||
+      (p.rowpad && p.rowpad != bw_rowpad(p.h, p.w)))
     return hipErrorInvalidValue;
   RecBwdParams q = p;
   return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_pairs<0>), 2 * p.B, 256, q, st);
 }
 
 inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {
-  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1) return hipErrorInvalidValue;
+  if (!rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || (p.rowpad && p.rowpad != bw_rowpad(p.h, p.w)))
+    return hipErrorInvalidValue;
 #ifdef AAA_ABLATION   // diagnostic builds only (tools/ubench): the product library never reads AAA_RECB_ABL
   const char* e = getenv("AAA_RECB_ABL");
   switch (e ? atoi(e) : 0) {

@@ -773,6 +773,9 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                         Wf(L.dC), Wt(L.dZ), Wf(L.dZp), io->dh0, Wt(L.dY2), Wf(L.dxb), (int*)(ws + L.rflags),
                         L.T, L.B, L.h, L.w, L.P, nullptr, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_BWD"),
                         cqm_layout(L)};
+        // single-workgroup and paired kernels: row-padded images (recur_bwd.h kBwIBP) where they fit
+        // (C3 LDS bank conflicts 52.8 -> 10.0 %: profiles/r04/ab/rowpad_c3/); AAA_BW_ROWPAD=0 (A/B): 272-B rows only
+        rp.rowpad = fb <= 2 && env_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));
