@@ -199,12 +199,13 @@ def test_fused_splitk_slices(cuda, monkeypatch, tile, ns):
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"fused split-K {tile} x{ns}: ")
 
 
-@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4", "5"])
 def test_dx_split6_tiles(cuda, monkeypatch, tile):
     """The fp32 batched dx (conv2-output grad) ring tiles on split products:
     64x64, 64x128, 64x64 BK64, 64x128 with the channel-chunk-major K order
     (ConvGeo::cmaj, reorder_cmaj weights), 64x128 with the weights pre-split
-    into bf16 planes (GRows3B); B=5 -> ragged column tiles."""
+    into bf16 planes (GRows3B), and the same with dZ pre-split too
+    (GIm2colB3 over split_planes); B=5 -> ragged column tiles."""
     monkeypatch.setenv("AAA_DX_S6_TILE", tile)
     T, B = 3, 5
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"dx tile {tile}: ")

@@ -244,6 +244,11 @@ struct GRows3B {
     for (int q = 0; q < 3; ++q) pl[q].issue(reinterpret_cast<__bf16*>(lds) + q * R * BK, k0);
   }
 };
+// B operand of the split-product ring as an implicit-GEMM gather over three
+// bf16 planes of the fp32 source (split_planes): each element is split once
+// instead of once per tap its window reads it.
+template <int R, int BK, int NT>
+struct GIm2colB3;
 template <class LD, class = void> struct presplit_of : std::false_type {};
 template <class LD> struct presplit_of<LD, std::enable_if_t<LD::PRESPLIT>> : std::true_type {};
 
@@ -318,6 +323,25 @@ struct GIm2colB {
       const bool v = (vmask[c] >> (tap + dt[c])) & 1ull;
       dma16a(rs, lds + c * NT * VG + wofs, v ? (uint32_t)((base[c] + toff) * (int)sizeof(T)) : kOOB);
     }
+  }
+};
+
+template <int R, int BK, int NT>
+struct GIm2colB3 {
+  using P1 = GIm2colB<__bf16, R, BK, NT>;
+  static constexpr bool KC = true, PRESPLIT = true;
+  static constexpr int PER = 3 * P1::PER;
+  static constexpr int ELEMS = 3 * R * BK / 2;
+  struct Params { const __bf16* src; ConvGeo g; int nrows; uint32_t src_bytes; size_t plane; };   // plane p at src + p * plane
+  P1 pl[3];
+  __device__ static bool ok_shape(const ConvGeo& g) { return P1::ok_shape(g); }
+  __device__ __forceinline__ GIm2colB3(const Params& p, int row0)
+      : pl{P1(typename P1::Params{p.src, p.g, p.nrows, p.src_bytes}, row0),
+           P1(typename P1::Params{p.src + p.plane, p.g, p.nrows, p.src_bytes}, row0),
+           P1(typename P1::Params{p.src + 2 * p.plane, p.g, p.nrows, p.src_bytes}, row0)} {}
+  __device__ __forceinline__ void issue(float* lds, int k0) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pl[q].issue(reinterpret_cast<__bf16*>(lds) + q * R * BK, k0);
   }
 };
 
@@ -771,8 +795,10 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
 #pragma unroll
           for (int a = 0; a < MI; ++a) frag_any<LA, BI, BK>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
         }
+        if constexpr (!presplit_of<LB>::value) {
 #pragma unroll
-        for (int b = 0; b < MJ; ++b) frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+          for (int b = 0; b < MJ; ++b) frag_any<LB, BJ, BK>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+        }
         if constexpr (split6_of<C>::value) {   // fp32 at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
           bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
           if constexpr (presplit_of<LA>::value) {   // A's parts straight from its three bf16 planes
@@ -788,8 +814,19 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
 #pragma unroll
             for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
           }
+          if constexpr (presplit_of<LB>::value) {   // B's parts straight from its three bf16 planes
+            const __bf16* Bb = reinterpret_cast<const __bf16*>(Bc);
 #pragma unroll
-          for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
+            for (int b = 0; b < MJ; ++b) {
+              const int r = wj * WTJ + b * 32 + r32;
+              bh[b] = frag_sw<BK>(Bb, r, kofs);
+              bm[b] = frag_sw<BK>(Bb + BJ * BK, r, kofs);
+              bl[b] = frag_sw<BK>(Bb + 2 * BJ * BK, r, kofs);
+            }
+          } else {
+#pragma unroll
+            for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
+          }
 #pragma unroll
           for (int a = 0; a < MI; ++a)
 #pragma unroll

@@ -643,6 +643,18 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                   typename LBx::Params{dz, g, rows, zb}, ep, 64, rows, 4608, 1, s)));
               break;
             }
+            case 5: {   // (A/B) case 4 with dZ pre-split too (L.dZ6 planes, bit-identical to the in-loop split)
+              if (!L.dZ6) return fail(AAA_E_ARG, "AAA_DX_S6_TILE=5 set after the workspace was laid out");
+              using C6 = GemmCfgS6<64, 128, 32, 2, 2>;
+              using LA3 = GRows3B<64, 32, C6::NT>;
+              using LB3 = GIm2colB3<128, 32, C6::NT>;
+              __bf16* z6 = (__bf16*)Wf(L.dZ6);
+              HIPCHK(split_planes(dz, (long)rows * 512, z6, s));
+              HIPCHK((launch_pipe<C6, LA3, LB3, ED, 2>(
+                  typename LA3::Params{(const __bf16*)(pk + L.k_WdT6), 4608, 64, (size_t)64 * 4608},
+                  typename LB3::Params{z6, g, rows, zb / 2, (size_t)rows * 512}, ep, 64, rows, 4608, 1, s)));
+              break;
+            }
 
             case 2:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));

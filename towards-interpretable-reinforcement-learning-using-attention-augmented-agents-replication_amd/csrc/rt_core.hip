@@ -112,6 +112,8 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.dQp = take(F * L.qd * 4);
   L.dC = take(M * 128 * 4);
   L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
+  // (A/B, AAA_DX_S6_TILE=5) fp32 dZ as three bf16 planes for the batched dx (0 = none)
+  L.dZ6 = take(e == 4 && env_int("AAA_DX_S6_TILE", 4) == 5 ? F * P * 512 * 6 : 0);
   // gate-bias partials per (step, column tile | frame half); the fp32 split-K chain's tiles are kSplitBj pixels
   const size_t zp_rows = std::max({(M + 31) / 32, 2 * (size_t)L.B,
                                    L.esz == 4 && bptt_splitk_fits(M) ? (M + kSplitBj - 1) / kSplitBj : 0});
