@@ -327,6 +327,9 @@ def main():
                          "(cast on the host as main_mp.py:53 does)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B check only: time the steps without the library's per-kernel HIP events")
+    ap.add_argument("--timed-steps", type=int, default=1,
+                    help="how many of the last timed steps carry the library's per-kernel HIP events "
+                         "(1: the last step only, ~0.4 %% of the run's time; K: every timed step)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -363,7 +366,7 @@ def main():
     # live in the LAST timed step only: an event pair around every launch of
     # every step costs ~7 % of the step time at C2 (4.85 vs 4.54 ms/step,
     # tools/ab_timing.sh), so the sample keeps that cost to 1/K of it.
-    timed = 0 if args.no_kernel_timing else 1
+    timed = 0 if args.no_kernel_timing else max(1, min(args.timed_steps, args.steps))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -456,9 +459,18 @@ def main():
                      "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                      **pmc_traffic(args.config, world, d["variant"]),
                      "flop_per_launch": per_launch, "avg_launch_us": round(avg_ms * 1e3, 2),
-                     "timed_launches": d["launches"], "timing": "HIP events around each launch of the last timed step"},
+                     "timed_launches": d["launches"],
+                     "timing": f"HIP events around each launch of the last {timed} timed step(s)",
+                     **({"peak_fp32_mfma": PEAK_TFLOPS["fp32"],
+                         "frac_vs_fp32_mfma": round(achieved / PEAK_TFLOPS["fp32"], 4),
+                         "peak_note": "bound = the bf16 MFMA running six split products per fp32 product "
+                                      "(bf16 dense 2500 / 6 = 416.7 TFLOP/s fp32-equivalent): the instruction "
+                                      "mix the kernel executes; frac_vs_fp32_mfma prices the same work against "
+                                      "the fp32 MFMA's 157.3 TFLOP/s dense peak"} if split6_on(dtype) else {})},
         "job_roofline": {"flop_per_frame": fpf, "achieved_tflops_per_gpu": round(value * fpf / world / 1e12, 2),
-                         "frac": round(value * fpf / world / 1e12 / peak, 4)},
+                         "frac": round(value * fpf / world / 1e12 / peak, 4),
+                         **({"frac_vs_fp32_mfma": round(value * fpf / world / 1e12 / PEAK_TFLOPS["fp32"], 4)}
+                            if split6_on(dtype) else {})},
         "kernels": kernels,
         "kernel_coverage": coverage,
         "hbm_kernels": attention_hbm(ka),

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 7
+#define AAA_ABI_VERSION 8
 
 enum aaa_status {
   AAA_OK = 0,
@@ -85,6 +85,10 @@ typedef struct aaa_cfg {
  * observation (main_mp.py:49-53 casts it to float on the host); the cast is
  * fused into the kernel that lays the frames out for conv1. */
 #define AAA_FLAG_FRAMES_U8 2
+/* Do not consume / fail on partner-timeout reports of earlier launches at
+ * entry (see aaa_pair_status): the caller checks them itself after the
+ * iteration, e.g. through aaa_pair_flag and the guarded optimizer. */
+#define AAA_FLAG_DEFER_STRANDED 4
 
 typedef struct aaa_io {
   /* inputs */
@@ -198,21 +202,24 @@ int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t s
  * workgroup's first wait); a wait that expires is counted in a word of
  * pinned, device-mapped host memory and the kernel proceeds on a stale
  * partner slice (later waits of that workgroup return at once, so a kernel
- * whose partner never runs ends within about one budget).  aaa_forward /
- * aaa_backward consume pending counts at entry and return AAA_E_STRANDED;
- * aaa_pair_status synchronises ``stream`` (NULL: the device) and returns the
- * count (>= 0; clear != 0 resets it).
- * aaa_pair_flag enqueues on ``stream`` a copy of the pending count (as seen
- * by the device at that point of the stream, not consumed) into dst[0] as a
- * float: a learner puts it beside its gradients so the gradient all-reduce
- * carries it to every rank and aaa_adam_step_guarded skips the update of a
- * step whose gradients came from a stranded launch, with no host sync.
- * aaa_debug_pair_spin is a TEST HOOK, not part of a production call
- * sequence: it sets the wait budget to ``ticks`` 100-MHz ticks (0 = the
- * default above) so the report path can be exercised. */
+ * whose partner never runs ends within about one budget).  The count is
+ * monotonic; its two readers keep their own snapshots of it:
+ *  - the host: aaa_forward / aaa_backward consume the counts reported since
+ *    the host last did and return AAA_E_STRANDED -- unless the cfg carries
+ *    AAA_FLAG_DEFER_STRANDED, for a caller that must not fail mid-iteration
+ *    (a data-parallel learner whose peers would wait in a collective) and
+ *    checks with aaa_pair_status after it; aaa_pair_status synchronises
+ *    ``stream`` (NULL: the device) and returns that count (>= 0; clear != 0
+ *    consumes it);
+ *  - the device: aaa_pair_flag enqueues on ``stream`` a kernel that writes
+ *    into dst[0], as a float, the counts reported since the previous
+ *    aaa_pair_flag on this device, in stream order.  A learner puts it beside
+ *    its gradients so the gradient all-reduce carries it to every rank and
+ *    aaa_adam_step_counted / _guarded skips the update of a step whose
+ *    gradients came from a stranded launch, with no host sync; host-side
+ *    consumption never resets what the device-side reader sees. */
 int aaa_pair_status(hipStream_t stream, int clear);
 int aaa_pair_flag(float* dst, hipStream_t stream);
-int aaa_debug_pair_spin(long ticks);
 
 /* ---- optional kernel timing (benchmarks) ----
  * While enabled, the runtime records a hipEvent pair on the launch stream
@@ -273,6 +280,16 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
  * device float, e.g. the all-reduced aaa_pair_flag slot of the gradients):
  * no parameter or moment is written and no host sync is needed. */
 int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* guard, int ntensors,
+                          float* const* params, const float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                          hipStream_t stream);
+/* The guarded update with the step count kept on the device: *step_dev (one
+ * device int, 0 before the first update) is the number of updates applied so
+ * far; this one runs as update *step_dev + 1 (torch's bias corrections of
+ * that step, in double) and, in stream order after it, *step_dev advances
+ * only if the guard let the update through -- so a skipped step leaves the
+ * moments AND the bias corrections exactly where they were. */
+int aaa_adam_step_counted(const aaa_adam_hparams* hp, int* step_dev, const float* guard, int ntensors,
                           float* const* params, const float* const* grads, float* const* exp_avg,
                           float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
                           hipStream_t stream);

@@ -57,29 +57,26 @@ def _filler():
 
 
 class strand_next_launch:
-    """Test hook: make the next multi-workgroup launch strand deterministically.
-    A filler holds half the CUs for 5 ms on a side stream while the partner-wait
-    budget is 100 us (aaa_debug_pair_spin), so the workgroups placed first give
-    up on partners that cannot be placed yet.  Restores the default budget."""
+    """Make the next multi-workgroup launch strand deterministically: a filler
+    holds half the CUs on a side stream for longer than the default partner-
+    wait budget (1 s + 20 ms per step, common.h pair_wait: 1.4 s at T = 20),
+    so the workgroups placed first give up on partners that cannot be placed
+    until the filler drains.  No test hook in libaaa.so is involved."""
 
-    def __init__(self, cuda, cus=128, usec=5000, budget_ticks=10000):
-        self.cuda, self.cus, self.usec, self.budget = cuda, cus, usec, budget_ticks
+    def __init__(self, cuda, cus=128, usec=1_900_000):
+        self.cuda, self.cus, self.usec = cuda, cus, usec
 
     def __enter__(self):
         lib = _filler()
         self.side = torch.cuda.Stream(self.cuda)
         self.sink = torch.zeros(4096, device=self.cuda)
         torch.cuda.synchronize()
-        N.debug_pair_spin(self.budget)
         assert lib.aaa_test_filler(self.cus, self.usec, self.sink.data_ptr(), self.side.cuda_stream) == 0
-        time.sleep(0.002)
+        time.sleep(0.005)
         return self
 
     def __exit__(self, *exc):
-        try:
-            torch.cuda.synchronize()
-        finally:
-            N.debug_pair_spin(0)
+        torch.cuda.synchronize()
         return False
 
 
@@ -153,9 +150,13 @@ def test_resident_launch_beside_filler(cuda, shape):
 
 
 def test_guarded_adam_skips_stranded_step(cuda):
-    """A launch whose partner wait expired leaves its count in the report word;
-    aaa_pair_flag copies it (stream order, no sync) into the guard slot and
-    the guarded Adam then writes nothing.  A zero guard updates as usual."""
+    """A launch whose partner wait expired raises the monotonic report word;
+    aaa_pair_flag writes, in stream order, the reports since its own previous
+    snapshot into the guard slot, and the guarded Adam then writes nothing --
+    even when a host-side call consumed the report between the stranded launch
+    and the flag (the device-side reader has its own snapshot).
+    The counted Adam leaves its device step counter at 0; a zero guard updates
+    and counts as usual."""
     B, T, H, nq, dtype, _ = SHAPES["pairs_c4"]
     args = _setup(cuda, B, T, H, nq, dtype)
     n = args[0].n_params
@@ -164,29 +165,39 @@ def test_guarded_adam_skips_stranded_step(cuda):
     p = torch.randn(n, device=cuda)
     g = torch.randn(n, device=cuda)
     m, v = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
     from aaa_amd.optim import adam_flat_
     N.pair_status(clear=True)
+    N.pair_flag(guard)                 # this reader's snapshot: up to date
     runner, flat, packed, basis, frames, ws, dl, dv = args
     before = p.clone()
     with strand_next_launch(cuda):
         runner.forward(flat, packed, basis, frames, ws, want_attn=False)
-        N.pair_flag(guard)         # before any API call consumes the report
-        adam_flat_(p, g, m, v, 1, guard=guard)
-    assert float(guard.item()) > 0, "no partner wait expired beside the filler"
+    consumed = N.pair_status(clear=True)   # the host consumes the report first ...
+    assert consumed > 0, "no partner wait expired beside the filler"
+    N.pair_flag(guard)                 # ... and the device-side reader still sees it
+    adam_flat_(p, g, m, v, 0, guard=guard, step_dev=step)
+    assert float(guard.item()) == consumed
     assert torch.equal(p, before) and float(m.abs().max()) == 0.0, "the guarded Adam updated a stranded step"
-    assert N.pair_status(clear=True) > 0
-    guard.zero_()
-    adam_flat_(p, g, m, v, 1, guard=guard)
+    assert int(step.item()) == 0, "a skipped update advanced the step counter"
+    N.pair_flag(guard)                 # nothing new since the last flag
+    assert float(guard.item()) == 0.0
+    adam_flat_(p, g, m, v, 0, guard=guard, step_dev=step)
     torch.cuda.synchronize()
-    assert not torch.equal(p, before)
+    assert not torch.equal(p, before) and int(step.item()) == 1
+    # the counted update is torch's step-1 update
+    p2, m2, v2 = before.clone(), torch.zeros_like(p), torch.zeros_like(p)
+    adam_flat_(p2, g, m2, v2, 1)
+    assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2)
 
 
 def test_learner_stranded_step_leaves_params(cuda):
     """Learner.train_step with stranded partners (a filler holds half the CUs
-    and the wait budget is 100 us): either the backward's entry
-    check raises AAA_E_STRANDED (the forward's report was already visible) or
-    the guard slot skips the update -- the parameters never change; a clean
-    step afterwards updates them and check_health() is quiet."""
+    past the wait budget): the step completes without raising mid-iteration
+    (AAA_FLAG_DEFER_STRANDED -- a rank that raised between its collectives
+    would leave its peers in an unmatched all-reduce), the guard slot skips the
+    update and its count, and check_health() raises afterwards; a clean step
+    then updates the parameters as Adam step 1."""
     from aaa_amd.learner import Learner
     B, T, H, nq, dtype, _ = SHAPES["pairs_c4"]
     lr = Learner(B, T, H, H, nq, 18, dtype, cuda, frames_u8=True)
@@ -195,14 +206,16 @@ def test_learner_stranded_step_leaves_params(cuda):
     dv = torch.from_numpy(detinit.cotangent(3, (T, B, 18))).to(cuda)
     before = lr.flat.clone()
     N.pair_status(clear=True)
-    with strand_next_launch(cuda):
-        try:
-            lr.train_step(frames, dl, dv)
-        except RuntimeError as e:
-            assert "status -5" in str(e), e
-    assert torch.equal(lr.flat, before), "a stranded step reached the parameters"
-    N.pair_status(clear=True)
-    lr.train_step(frames, dl, dv)
+    lr.step(frames, dl, dv)            # settle the guard's snapshot on a clean step
     torch.cuda.synchronize()
     lr.check_health()
-    assert not torch.equal(lr.flat, before)
+    with strand_next_launch(cuda):
+        lr.train_step(frames, dl, dv)  # must not raise
+    assert torch.equal(lr.flat, before), "a stranded step reached the parameters"
+    assert lr.opt_steps == 0
+    lr.train_step(frames, dl, dv)      # the report is still pending on the host: no raise, and a clean update
+    torch.cuda.synchronize()
+    assert not torch.equal(lr.flat, before) and lr.opt_steps == 1
+    with pytest.raises(RuntimeError, match="timed out"):
+        lr.check_health()
+    lr.check_health()                  # reported once

@@ -49,3 +49,19 @@ def test_dp_learner_sums_to_full_batch(world, dtype, b, H, nq, want):
     assert res["ok"] and res["world"] == world, res
     if want:   # the per-rank kernels are the multi-workgroup ones this case is meant to cover
         assert all(want in v for v in res["variants_per_rank"].values()), res
+
+
+def test_dp_stranded_step_skipped_on_every_rank():
+    """a rank whose frame-resident launch strands must not raise
+    between its collectives (its peers would hang in an unmatched all-reduce);
+    the guard slot skips the update -- and the device-side Adam step count --
+    on every rank, check_health() raises afterwards, and the next clean step
+    updates every rank identically (tools/dp_check.py AAA_DP_STRAND=1)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tools", "dp_check.py")]
+    env = dict(os.environ, AAA_DP_BACKEND="gloo", OMP_NUM_THREADS="2", AAA_DP_STRAND="1", AAA_DP_B="32")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
+    res = json.loads(lines[-1])
+    assert res["ok"] and res["raised_mid_step"] is None, res

@@ -57,8 +57,8 @@ def test_paired_kernels_run_and_report_clean(cuda):
 
 
 def test_stranded_pair_is_reported(cuda):
-    """With half the CUs held by a filler kernel and a 100-us partner-wait
-    budget, some wait expires: the report word counts it, and the next API
+    """With half the CUs held by a filler kernel past the partner-wait budget,
+    some wait expires: the report word counts it, and the next API
     call fails with AAA_E_STRANDED (once) instead of silently continuing."""
     from test_gpu_coresidency import strand_next_launch
     args = _setup(cuda)

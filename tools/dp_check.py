@@ -19,6 +19,15 @@ selects the paired frame-resident kernels, >= 160 the one-workgroup ones on a
 256-CU part; fp32 at 16..32 the frame-group kernels), AAA_DP_T unroll length,
 AAA_DP_H frame side (168: the band-mode kernels for bf16), AAA_DP_NQ heads.  Prints one JSON line on rank 0; exit
 status 1 on a mismatch.
+
+AAA_DP_STRAND=1 instead checks the stranded-launch path across ranks (ADVICE
+r04): the LAST rank holds most CUs with a filler past the partner-wait budget
+while every rank runs Learner.train_step, so a frame-resident launch times
+out.  Every rank must finish the step (no rank raises between its
+collectives: the learner defers the API's stranded check), no rank's
+parameters or Adam step count may change (the guard slot rides in the
+HEAD+CORE all-reduce), check_health() must raise on a stranded rank, and a
+clean step afterwards must update every rank identically.
 """
 import json
 import os
@@ -51,11 +60,75 @@ def oracle_grads(X, Gl, Gv, dtype, A, nq):
     return {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}
 
 
+def strand_check(rank, world, dev):
+    import ctypes
+    import time
+    dtype, b, T, H, nq, A = "bf16", int(os.environ.get("AAA_DP_B", "32")), 20, 84, 4, 18
+    lr = Learner(b, T, H, H, nq, A, dtype, dev, frames_u8=True)
+    X = torch.from_numpy(detinit.frames_u8(1234 + rank, (T, b, H, H, 3))).to(dev)
+    Gl = torch.from_numpy(detinit.normal(2 + rank, (T, b, A))).to(dev)
+    Gv = torch.from_numpy(detinit.normal(3 + rank, (T, b, A))).to(dev)
+    lr.step(X, Gl, Gv)                 # clean step: settles the guard's snapshot
+    torch.cuda.synchronize()
+    N.pair_status(clear=True)
+    before = lr.flat.clone()
+    res = {"mode": "strand", "world": world, "B_per_rank": b}
+    dist.barrier()
+    stranded_rank = world - 1
+    if rank == stranded_rank:
+        lib = ctypes.CDLL(os.path.join(ROOT, "tests", "native", "libaaa_filler.so"))
+        lib.aaa_test_filler.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+        side = torch.cuda.Stream(dev)
+        sink = torch.zeros(4096, device=dev)
+        # 200 of 256 CUs: the ranks' two paired grids (2 * b workgroups each) cannot all be placed
+        assert lib.aaa_test_filler(200, 1_900_000, sink.data_ptr(), side.cuda_stream) == 0
+        time.sleep(0.005)
+    raised = None
+    try:
+        lr.train_step(X, Gl, Gv)
+    except RuntimeError as e:       # the property under test: this must not happen
+        raised = str(e)
+    torch.cuda.synchronize()
+    unchanged = bool(torch.equal(lr.flat, before))
+    steps = lr.opt_steps
+    try:
+        lr.check_health()
+        health = "quiet"
+    except RuntimeError:
+        health = "raised"
+    # ranks share one GPU here, so the filler may strand any rank's launch: at least one must report
+    anyh = torch.tensor([1.0 if health == "raised" else 0.0])
+    dist.all_reduce(anyh, op=dist.ReduceOp.MAX)
+    ok = raised is None and unchanged and steps == 0 and anyh.item() == 1.0
+    lr.train_step(X, Gl, Gv)           # clean: every rank updates, identically
+    torch.cuda.synchronize()
+    lr.check_health()
+    moved = not torch.equal(lr.flat, before)
+    digest = torch.tensor([float(lr.flat.double().sum()), float(lr.opt_steps)], dtype=torch.float64)
+    allv = [torch.zeros_like(digest) for _ in range(world)]
+    dist.all_gather(allv, digest)
+    same = all(torch.equal(allv[0], v) for v in allv)
+    ok = ok and moved and same and lr.opt_steps == 1
+    flags = torch.tensor([1.0 if ok else 0.0])
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    res.update({"raised_mid_step": raised, "params_unchanged_after_stranded_step": unchanged,
+                "adam_steps_after_stranded_step": steps, "health_rank": health, "clean_step_moved": moved,
+                "ranks_identical_after_clean_step": same, "ok": bool(flags.item() == 1.0)})
+    if rank == 0 or not ok:
+        print(json.dumps({"rank": rank, **res}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if not res["ok"]:
+        sys.exit(1)
+
+
 def main():
     dist.init_process_group(os.environ.get("AAA_DP_BACKEND", "gloo"))
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
+    if os.environ.get("AAA_DP_STRAND") == "1":
+        return strand_check(rank, world, dev)
     dtype = os.environ.get("AAA_DP_DTYPE", "fp32")
     b = int(os.environ.get("AAA_DP_B", "2"))
     T = int(os.environ.get("AAA_DP_T", "3"))

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 7   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 8   # include/aaa.h AAA_ABI_VERSION
 E_STRANDED = -5   # AAA_E_STRANDED
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 FWD_VISION, FWD_CORE, FWD_TAIL, FWD_ALL = 1, 2, 4, 7
@@ -29,8 +29,8 @@ EXPORTS = (
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
-    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag", "aaa_debug_pair_spin",
-    "aaa_adam_step_guarded", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
+    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag",
+    "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
 )
 # include/aaa.h enum aaa_timer
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
@@ -49,6 +49,7 @@ IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action"
              "core_h0", "core_c0", "core_hT", "core_cT", "dcore_hT", "dcore_cT", "dcore_h0", "dcore_c0")
 FLAG_STATEFUL_CORE = 1
 FLAG_FRAMES_U8 = 2
+FLAG_DEFER_STRANDED = 4
 
 
 class TimerStats(ctypes.Structure):
@@ -128,6 +129,7 @@ def load(path: str = LIB_PATH):
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
             "aaa_adam_step_guarded": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, P, I, P, P, P, P, P, P, P]),
             "aaa_pair_flag": (I, [P, P]),
+            "aaa_adam_step_counted": (I, [ctypes.POINTER(AdamHP), P, P, I, P, P, P, P, P, P, P]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
             "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
             "aaa_convlstm_packed_bytes": (S, [ctypes.POINTER(CellDesc)]),
@@ -147,7 +149,6 @@ def load(path: str = LIB_PATH):
             "aaa_actor_workspace_bytes": (S, [CP]),
             "aaa_actor_step": (I, [CP, ctypes.POINTER(ActorIO), P]),
             "aaa_pair_status": (I, [P, I]),
-            "aaa_debug_pair_spin": (I, [ctypes.c_long]),
         }
         ab_override = "AAA_LIB" in os.environ
         missing = [name for name in sig if not hasattr(lib, name)]
@@ -245,22 +246,20 @@ def pair_status(clear: bool = True, stream=None) -> int:
 
 
 def pair_flag(dst, stream=None) -> None:
-    """Enqueue a copy of the pending partner-timeout count into the one-element
-    fp32 device tensor ``dst`` (stream order, not consumed, no host sync)."""
+    """Enqueue a kernel writing into the one-element fp32 device tensor ``dst``
+    the partner timeouts reported since the previous pair_flag on this device
+    (stream order, no host sync; independent of host-side consumption)."""
     check(load().aaa_pair_flag(dst.data_ptr(), stream if stream is not None else stream_ptr(dst.device)), "pair_flag")
 
 
-def debug_pair_spin(ticks: int) -> None:
-    """TEST HOOK: bound the multi-workgroup kernels' partner wait to ``ticks``
-    100-MHz ticks after a workgroup's first wait (0 = the default budget)."""
-    check(load().aaa_debug_pair_spin(int(ticks)), "debug_pair_spin")
-
-
 def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None,
-              guard=None) -> None:
+              guard=None, step_dev=None) -> None:
     """One fused Adam launch over lists of same-length fp32 device tensors
     (aaa_adam_step; with ``guard``, a one-element fp32 device tensor,
-    aaa_adam_step_guarded: no update when guard != 0)."""
+    aaa_adam_step_guarded: no update when guard != 0; with ``step_dev``, a
+    one-element int32 device tensor, aaa_adam_step_counted: ``step`` is
+    ignored, the update is number step_dev + 1 and step_dev advances on the
+    device only when the update was applied)."""
     n = len(params)
     VP = ctypes.c_void_p * max(n, 1)
     def arr(ts):
@@ -270,7 +269,13 @@ def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp
         assert len(group) == n
     mx = arr(max_exp_avg_sq)
     st = stream if stream is not None else stream_ptr()
-    if guard is not None:
+    if step_dev is not None:
+        assert step_dev.numel() == 1 and step_dev.is_cuda and str(step_dev.dtype) == "torch.int32"
+        check(load().aaa_adam_step_counted(ctypes.byref(hp), step_dev.data_ptr(),
+                                           guard.data_ptr() if guard is not None else None, n, arr(params),
+                                           arr(grads), arr(exp_avg), arr(exp_avg_sq), mx, numel, st),
+              "adam_step_counted")
+    elif guard is not None:
         check(load().aaa_adam_step_guarded(ctypes.byref(hp), int(step), guard.data_ptr(), n, arr(params), arr(grads),
                                            arr(exp_avg), arr(exp_avg_sq), mx, numel, st), "adam_step_guarded")
     else:

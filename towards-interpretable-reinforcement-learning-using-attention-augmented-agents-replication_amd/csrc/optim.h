@@ -22,11 +22,14 @@ struct AdamHost {
   long step;
   int amsgrad, maximize;
   const float* guard = nullptr;   // device float: skip the update when != 0
+  int* step_dev = nullptr;        // device step counter (aaa_adam_step_counted): step = *step_dev + 1,
+                                  // advanced in stream order only when the update was applied
 };
 
 int adam_chunks(size_t numel);
-hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st);
-hipError_t pair_flag_launch(const int* report, float* dst, hipStream_t st);
+// advance: count this update on h.step_dev after the launch (the last table of a step)
+hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st, bool advance);
+hipError_t pair_flag_launch(const int* report, int* base, float* dst, hipStream_t st);
 
 // loss.hip: REINFORCE (finish_episode) loss + logits cotangent, one workgroup per episode
 hipError_t reinforce_launch(int T, int B, int A, const float* logits, const int* actions, const float* rewards,

@@ -10,8 +10,10 @@
 //   v  = v * beta2 + (1 - beta2) * g * g
 //   vm = max(vmax, v) when amsgrad (vmax <- vm), else v
 //   p  = p + (-lr / (1 - beta1^step)) * m / (sqrt(vm) / sqrt(1 - beta2^step) + eps)
-// The step-dependent scalars are computed on the host in double and rounded to
-// fp32 once, as torch does.  HBM traffic: 16 B read + 12 B written per element
+// The step-dependent scalars are computed in double and rounded to fp32 once,
+// as torch does: on the host from the caller's step, or -- with a device step
+// counter (aaa_adam_step_counted) -- by each workgroup from that counter, so a
+// step the guard skipped does not advance the bias corrections.  HBM traffic: 16 B read + 12 B written per element
 // (20 + 16 with amsgrad) -- the kernel is bound by HBM (or Infinity Cache)
 // bandwidth, so it streams 16-byte vectors, 4 per thread.
 #include <cmath>
@@ -25,7 +27,16 @@ struct AdamScalars {
   float wd, one_m_b1, b2, one_m_b2, step_size_neg, bc2_sqrt, eps;
   int amsgrad, maximize;
   const float* guard;   // skip the whole update when *guard != 0 (aaa_adam_step_guarded), or nullptr
+  const int* step_dev;  // device step counter (aaa_adam_step_counted), or nullptr: the scalars above hold
+  double lr, beta1, beta2;   // the host's doubles (torch's Python floats), read only with step_dev
 };
+
+// Bias-corrected scalars of update number *step_dev + 1, in double as on the host.
+__device__ __forceinline__ void adam_device_step(AdamScalars& s) {
+  const double step = (double)(*s.step_dev) + 1.0;
+  s.step_size_neg = (float)(-(s.lr / (1.0 - pow(s.beta1, step))));
+  s.bc2_sqrt = (float)sqrt(1.0 - pow(s.beta2, step));
+}
 
 __device__ __forceinline__ float adam_elem(float& p, float g, float& m, float& v, float* vmax, const AdamScalars& s) {
   if (s.maximize) g = -g;
@@ -49,6 +60,7 @@ constexpr int kAdamChunk = kAdamThreads * kAdamVec * 4;       // elements per wo
 // pointers are all 16-byte aligned use 16-byte vectors, the rest scalars.
 __global__ void __launch_bounds__(kAdamThreads) k_adam(AdamTable tab, AdamScalars s) {
   if (s.guard && *s.guard != 0.f) return;   // gradients of a stranded launch: no update on any rank
+  if (s.step_dev) adam_device_step(s);
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < tab.n && tab.chunk0[t + 1] <= b) ++t;
@@ -92,7 +104,12 @@ __global__ void __launch_bounds__(kAdamThreads) k_adam(AdamTable tab, AdamScalar
   }
 }
 
-hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st) {
+// After k_adam in stream order: count the update iff the guard let it through.
+__global__ void k_adam_advance(const float* __restrict__ guard, int* __restrict__ step_dev) {
+  if (threadIdx.x == 0 && !(guard && *guard != 0.f)) step_dev[0] = step_dev[0] + 1;
+}
+
+hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hipStream_t st, bool advance) {
   AdamScalars s;
   s.wd = (float)h.weight_decay;
   s.one_m_b1 = (float)(1.0 - h.beta1);
@@ -104,19 +121,29 @@ hipError_t adam_launch(const AdamTable& tab, int nchunks, const AdamHost& h, hip
   s.amsgrad = h.amsgrad;
   s.maximize = h.maximize;
   s.guard = h.guard;
-  if (nchunks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_adam, dim3(nchunks), dim3(kAdamThreads), 0, st, tab, s);
+  s.step_dev = h.step_dev;
+  s.lr = h.lr;
+  s.beta1 = h.beta1;
+  s.beta2 = h.beta2;
+  if (nchunks > 0) hipLaunchKernelGGL(k_adam, dim3(nchunks), dim3(kAdamThreads), 0, st, tab, s);
+  if (h.step_dev && advance) hipLaunchKernelGGL(k_adam_advance, dim3(1), dim3(64), 0, st, h.guard, h.step_dev);
   return hipGetLastError();
 }
 
-// The pending partner-timeout count of the frame-resident kernels (the pinned,
-// device-mapped report word) as one float, read in stream order.
-__global__ void k_pair_flag(const int* __restrict__ report, float* __restrict__ dst) {
-  if (threadIdx.x == 0) dst[0] = (float)__hip_atomic_load(report, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// The partner timeouts of the frame-resident kernels reported since the last
+// k_pair_flag on this device, as one float, in stream order: the report word
+// is monotonic (rt_core.hip), ``base`` is this reader's own snapshot of it.
+__global__ void k_pair_flag(const int* __restrict__ report, int* __restrict__ base, float* __restrict__ dst) {
+  if (threadIdx.x == 0) {
+    const int cur = __hip_atomic_load(report, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int b = __hip_atomic_load(base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    dst[0] = (float)(unsigned)(cur - b);
+    __hip_atomic_store(base, cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-hipError_t pair_flag_launch(const int* report, float* dst, hipStream_t st) {
-  hipLaunchKernelGGL(k_pair_flag, dim3(1), dim3(64), 0, st, report, dst);
+hipError_t pair_flag_launch(const int* report, int* base, float* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pair_flag, dim3(1), dim3(64), 0, st, report, base, dst);
   return hipGetLastError();
 }
 

@@ -98,9 +98,9 @@ inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // entry consumes pending reports and fails with AAA_E_STRANDED (the results of
 // the call that stranded are invalid); aaa_pair_status syncs a stream first.
 // Allocated once per process on first use, never freed (no HIP call at exit).
-extern long g_pair_spin;   // partner-wait budget override in ticks (aaa_debug_pair_spin; 0 = default)
 int pair_budget(int T);    // partner-wait budget of a T-step launch, 100-MHz ticks
 int* pair_report(int dev);  // this device's report word, device-mapped (nullptr: cannot map)
+int* pair_flag_base(int dev);  // aaa_pair_flag's own snapshot of it, device-mapped
 int pair_take();            // pending reports of the current device (consumed)
 int pair_peek();            // ... (left pending)
 int pair_check();           // AAA_E_STRANDED if any are pending

@@ -206,8 +206,9 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // profiles/r02/ab/wgrad_split.txt)
     const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, 512 / tiles)), rows / CW::BK));
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
-                   strf("register-staged %dx%d BK%d%s, %d-way split-K atomics [kernel: gemm_kernel+LdIm2colTB]", CW::BI,
-                        CW::BJ, CW::BK, split6_of<CW>::value ? " (fp32 as bf16x6 split products)" : "", ns));
+                   strf("register-staged %dx%d BK%d%s, %d-way split-K atomics [kernel: gemm_kernel+%d, %d, %d, +LdIm2colTB]",
+                        CW::BI, CW::BJ, CW::BK, split6_of<CW>::value ? " (fp32 as bf16x6 split products)" : "", ns,
+                        CW::BI, CW::BJ, CW::BK));
     HIPCHK((launch_gemm<CW, LA, LB>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
   };

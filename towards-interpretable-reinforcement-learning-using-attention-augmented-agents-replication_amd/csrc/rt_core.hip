@@ -26,7 +26,7 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   if (c->nq != 4 && c->nq != 8) return fail(AAA_E_ARG, "nq must be 4 or 8 (got %d)", c->nq);
   if (c->A < 1 || c->A > 256) return fail(AAA_E_ARG, "A out of range (%d)", c->A);
   if (c->dtype != AAA_F32 && c->dtype != AAA_BF16) return fail(AAA_E_ARG, "bad dtype %d", c->dtype);
-  if (c->flags & ~(AAA_FLAG_STATEFUL_CORE | AAA_FLAG_FRAMES_U8)) return fail(AAA_E_ARG, "unknown flags 0x%x", c->flags);
+  if (c->flags & ~(AAA_FLAG_STATEFUL_CORE | AAA_FLAG_FRAMES_U8 | AAA_FLAG_DEFER_STRANDED)) return fail(AAA_E_ARG, "unknown flags 0x%x", c->flags);
   L.sc = (c->flags & AAA_FLAG_STATEFUL_CORE) != 0;
   L.fu8 = (c->flags & AAA_FLAG_FRAMES_U8) != 0;
   L.B = c->B; L.T = c->T; L.F = c->B * c->T; L.H = c->H; L.W = c->W;
@@ -206,23 +206,29 @@ int check_device() {
 }
 
 // ------------------------------------------------- paired-kernel reports --
-// The paired frame-resident kernels (two cooperating workgroups per frame)
-// bound their partner waits (common.h pair_wait).  A timed-out wait adds 1 to
-// this device's report word: pinned host memory mapped into the device, so the
-// host reads it without a copy or a sync.  Every aaa_forward / aaa_backward
-// entry consumes pending reports and fails with AAA_E_STRANDED (the results of
-// the call that stranded are invalid); aaa_pair_status syncs a stream first.
+// The multi-workgroup frame-resident kernels bound their partner waits
+// (common.h pair_wait).  A timed-out wait adds 1 to this device's report word:
+// pinned host memory mapped into the device, so the host reads it without a
+// copy or a sync.  The word is MONOTONIC -- nothing resets it -- and it has two
+// independent readers, each holding its own snapshot:
+//   * the host (pair_take / pair_peek): reports past g_pair_seen[dev]; every
+//     aaa_forward / aaa_backward entry consumes them and fails with
+//     AAA_E_STRANDED unless the call defers them (AAA_FLAG_DEFER_STRANDED);
+//   * the device (aaa_pair_flag): k_pair_flag writes, in stream order, the
+//     reports past its own base word (words [64, 128) of the same page) and
+//     advances that base -- so a host-side consumption between the stranded
+//     launch and the guard can never hide the timeout from the guarded Adam
+//     (ADVICE r04).
 // Allocated once per process on first use, never freed (no HIP call at exit).
 static std::mutex g_pair_mu;
-static int* g_pair_host = nullptr;    // [64] words, one per device ordinal
+static int* g_pair_host = nullptr;    // [128] words: [0,64) reports, [64,128) device-side bases
 static int* g_pair_dev = nullptr;     // the same words, device-mapped
-long g_pair_spin = 0;   // partner-wait budget override, 100-MHz ticks (aaa_debug_pair_spin; 0 = pair_budget's)
+static unsigned g_pair_seen[64] = {};  // host-side snapshot per device ordinal
 
 // Partner-wait budget of one multi-workgroup launch of T steps: 1 s plus 20 ms
 // per step (the slowest legitimate launch, C5's band BPTT, takes ~80 us per
 // step), so only a partner that is not running at all exhausts it.
 int pair_budget(int T) {
-  if (g_pair_spin > 0) return (int)std::min<long>(g_pair_spin, 0x7fffffffL);
   return (int)std::min<long>(100000000L + 2000000L * (long)T, 0x7fffffffL);
 }
 
@@ -230,10 +236,10 @@ int* pair_report(int dev) {
   std::lock_guard<std::mutex> lk(g_pair_mu);
   if (!g_pair_host) {
     void* h = nullptr;
-    if (hipHostMalloc(&h, 64 * sizeof(int), hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+    if (hipHostMalloc(&h, 128 * sizeof(int), hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
         hipSuccess)
       return nullptr;
-    memset(h, 0, 64 * sizeof(int));
+    memset(h, 0, 128 * sizeof(int));
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) return nullptr;
     g_pair_host = (int*)h;
@@ -242,22 +248,24 @@ int* pair_report(int dev) {
   return g_pair_dev + dev;
 }
 
-// Pending reports of the current device (consumed).
-int pair_take() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  std::lock_guard<std::mutex> lk(g_pair_mu);
-  if (!g_pair_host) return 0;
-  return __atomic_exchange_n(g_pair_host + dev, 0, __ATOMIC_ACQ_REL);
+int* pair_flag_base(int dev) {
+  return pair_report(dev) ? g_pair_dev + 64 + dev : nullptr;
 }
 
-int pair_peek() {
+static int pair_pending(bool consume) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
   std::lock_guard<std::mutex> lk(g_pair_mu);
   if (!g_pair_host) return 0;
-  return __atomic_load_n(g_pair_host + dev, __ATOMIC_ACQUIRE);
+  const unsigned cur = (unsigned)__atomic_load_n(g_pair_host + dev, __ATOMIC_ACQUIRE);
+  const unsigned n = cur - g_pair_seen[dev];
+  if (consume) g_pair_seen[dev] = cur;
+  return (int)std::min<unsigned>(n, 0x7fffffffu);
 }
+
+// Pending reports of the current device since the host last consumed them.
+int pair_take() { return pair_pending(true); }
+int pair_peek() { return pair_pending(false); }
 
 int pair_check() {
   const int n = pair_take();

@@ -179,7 +179,7 @@ int aaa_forward(const aaa_cfg* cfg, const aaa_io* io, hipStream_t stream) {
   if (r) return r;
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, false))) return r;
-  if ((r = pair_check())) return r;
+  if (!(cfg->flags & AAA_FLAG_DEFER_STRANDED) && (r = pair_check())) return r;
   return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream, AAA_FWD_ALL)
                           : forward_impl<float>(L, io, stream, AAA_FWD_ALL);
 }
@@ -193,7 +193,7 @@ int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStre
   if (!(phases & AAA_FWD_CORE) && L.dt != AAA_F32) return fail(AAA_E_ARG, "skipping the core: fp32 configs only");
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, false))) return r;
-  if ((r = pair_check())) return r;
+  if (!(cfg->flags & AAA_FLAG_DEFER_STRANDED) && (r = pair_check())) return r;
   return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream, phases) : forward_impl<float>(L, io, stream, phases);
 }
 
@@ -243,7 +243,7 @@ int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t s
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, true))) return r;
   if (phases & ~AAA_BWD_ALL || !phases) return fail(AAA_E_ARG, "bad phase mask %d", phases);
-  if ((r = pair_check())) return r;
+  if (!(cfg->flags & AAA_FLAG_DEFER_STRANDED) && (r = pair_check())) return r;
   return L.dt == AAA_BF16 ? backward_impl<__bf16>(L, io, phases, stream)
                           : backward_impl<float>(L, io, phases, stream);
 }
@@ -263,14 +263,9 @@ int aaa_pair_flag(float* dst, hipStream_t stream) {
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   const int* rep = pair_report(dev);
-  if (!rep) return fail(AAA_E_LAUNCH, "cannot map the partner-timeout report word");
-  HIPCHK(pair_flag_launch(rep, dst, stream));
-  return AAA_OK;
-}
-
-int aaa_debug_pair_spin(long ticks) {
-  if (ticks < 0 || ticks > 0x7fffffffL) return fail(AAA_E_ARG, "pair wait budget must be in [0, 2^31) ticks (0 = default)");
-  g_pair_spin = ticks;
+  int* base = pair_flag_base(dev);
+  if (!rep || !base) return fail(AAA_E_LAUNCH, "cannot map the partner-timeout report word");
+  HIPCHK(pair_flag_launch(rep, base, dst, stream));
   return AAA_OK;
 }
 
@@ -281,21 +276,21 @@ int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* co
                                stream);
 }
 
-int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* guard, int ntensors,
-                          float* const* params, const float* const* grads, float* const* exp_avg,
-                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
-                          hipStream_t stream) {
+static int adam_impl(const aaa_adam_hparams* hp, long step, int* step_dev, const float* guard, int ntensors,
+                     float* const* params, const float* const* grads, float* const* exp_avg,
+                     float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                     hipStream_t stream) {
   if (!hp || ntensors < 0 || (ntensors > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel)))
     return fail(AAA_E_ARG, "adam: NULL argument");
-  if (step < 1) return fail(AAA_E_ARG, "adam: step must be >= 1 (got %ld)", step);
+  if (!step_dev && step < 1) return fail(AAA_E_ARG, "adam: step must be >= 1 (got %ld)", step);
   if (hp->amsgrad && !max_exp_avg_sq) return fail(AAA_E_ARG, "adam: amsgrad needs max_exp_avg_sq");
   if (!(hp->lr >= 0.0) || !(hp->eps >= 0.0) || !(hp->beta1 >= 0.0 && hp->beta1 < 1.0) ||
       !(hp->beta2 >= 0.0 && hp->beta2 < 1.0) || !(hp->weight_decay >= 0.0))
     return fail(AAA_E_ARG, "adam: invalid hyper-parameters");
   int r = check_device();
   if (r) return r;
-  AdamHost h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, step, hp->amsgrad ? 1 : 0, hp->maximize ? 1 : 0,
-             guard};
+  AdamHost h{hp->lr, hp->beta1, hp->beta2, hp->eps, hp->weight_decay, step_dev ? 1 : step, hp->amsgrad ? 1 : 0,
+             hp->maximize ? 1 : 0, guard, step_dev};
   for (int t0 = 0; t0 < ntensors; t0 += kAdamMaxTensors) {
     AdamTable tab;
     memset(&tab, 0, sizeof tab);
@@ -315,9 +310,27 @@ int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* gu
       if (nch + c > (1L << 30)) return fail(AAA_E_ARG, "adam: tensor %d too large", t);
       nch += (int)c;
     }
-    HIPCHK(adam_launch(tab, nch, h, stream));
+    HIPCHK(adam_launch(tab, nch, h, stream, t0 + kAdamMaxTensors >= ntensors));
   }
+  if (ntensors == 0 && step_dev) HIPCHK(adam_launch(AdamTable{}, 0, h, stream, true));
   return AAA_OK;
+}
+
+int aaa_adam_step_guarded(const aaa_adam_hparams* hp, long step, const float* guard, int ntensors,
+                          float* const* params, const float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                          hipStream_t stream) {
+  return adam_impl(hp, step, nullptr, guard, ntensors, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq, numel,
+                   stream);
+}
+
+int aaa_adam_step_counted(const aaa_adam_hparams* hp, int* step_dev, const float* guard, int ntensors,
+                          float* const* params, const float* const* grads, float* const* exp_avg,
+                          float* const* exp_avg_sq, float* const* max_exp_avg_sq, const size_t* numel,
+                          hipStream_t stream) {
+  if (!step_dev) return fail(AAA_E_ARG, "adam: NULL step counter");
+  return adam_impl(hp, 0, step_dev, guard, ntensors, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq, numel,
+                   stream);
 }
 
 int aaa_reinforce(int T, int B, int A, const float* logits, const int* actions, const float* rewards, double gamma,

@@ -16,11 +16,17 @@ together once CORE is enqueued (overlapping the VISION phase), VISION's at
 the end, and the next step's forward waits for the comm stream.
 
 Stranded-launch guard: one extra fp32 slot after the gradients receives the
-device's pending partner-timeout count (aaa_pair_flag) after the CORE phase;
-it rides in the HEAD+CORE all-reduce, so every rank sees any rank's timeout,
-and the fused Adam skips the update on the device when it is non-zero
-(aaa_adam_step_guarded) -- gradients of a stranded launch never reach the
-parameters, with no host sync.  ``check_health()`` raises on it.
+partner timeouts reported on this device since the previous step
+(aaa_pair_flag: a device-side snapshot of a monotonic word, so no host call
+can consume them first) after the CORE phase; it rides in the HEAD+CORE
+all-reduce, so every rank sees any rank's timeout, and the fused Adam skips
+the update on the device when it is non-zero -- gradients of a stranded
+launch never reach the parameters, with no host sync.  The Adam step count
+lives on the device too (aaa_adam_step_counted), advanced only by an applied
+update, so a skipped step leaves the bias corrections where they were.  The
+learner's runner defers the API's own stranded check (AAA_FLAG_DEFER_STRANDED):
+no rank can raise between its collectives and leave its peers waiting in an
+unmatched all-reduce; ``check_health()`` raises after the step instead.
 """
 from __future__ import annotations
 
@@ -40,7 +46,7 @@ class Learner:
     def __init__(self, B: int, T: int, H: int = 84, W: int = 84, nq: int = 4, A: int = 18,
                  dtype: str = "fp32", device=None, seed: int = 0, group=None, lr: float = 1e-3,
                  frames_u8: bool = False):
-        self.runner = r = UnrollRunner(B, T, H, W, nq, A, dtype, device, frames_u8=frames_u8)
+        self.runner = r = UnrollRunner(B, T, H, W, nq, A, dtype, device, frames_u8=frames_u8, defer_stranded=True)
         self.device = r.device
         params = detinit.deterministic_params(seed, A, nq)
         self.flat = torch.from_numpy(np.concatenate([v.reshape(-1) for v in params.values()])).to(self.device)
@@ -54,7 +60,7 @@ class Learner:
         self.lr = lr
         self.exp_avg = torch.zeros_like(self.grads)
         self.exp_avg_sq = torch.zeros_like(self.grads)
-        self.opt_steps = 0
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=self.device)   # Adam updates applied
         self.basis = SpatialBasis(r.h, r.w).S.to(self.device).contiguous()
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -131,6 +137,11 @@ class Learner:
         return {"buckets": buckets, "exposed_ms": round(exposed, 4),
                 "policy": "no collective beside a frame-resident launch: HEAD+CORE reduced after CORE, VISION last"}
 
+    @property
+    def opt_steps(self) -> int:
+        """Adam updates applied so far (reads the device counter: syncs)."""
+        return int(self.step_dev.item())
+
     def check_health(self):
         """Raise if a frame-resident launch of this rank timed out waiting for a
         partner since the last check (syncs the stream; the guarded Adam has
@@ -142,9 +153,10 @@ class Learner:
 
     def optimizer_step(self):
         """Adam (lr=1e-3, torch defaults; main_mp.py:92) on the flat params, one
-        launch, skipped on the device when the guard slot is non-zero."""
-        self.opt_steps += 1
-        adam_flat_(self.flat, self.grads, self.exp_avg, self.exp_avg_sq, self.opt_steps, lr=self.lr, guard=self.guard)
+        launch, skipped on the device when the guard slot is non-zero (and then
+        not counted: the device step counter advances only on an update)."""
+        adam_flat_(self.flat, self.grads, self.exp_avg, self.exp_avg_sq, 0, lr=self.lr, guard=self.guard,
+                   step_dev=self.step_dev)
 
     def train_step(self, frames, dlogits, dvalues, overlap: bool = True):
         out = self.step(frames, dlogits, dvalues, overlap=overlap)

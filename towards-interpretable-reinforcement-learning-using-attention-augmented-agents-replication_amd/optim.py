@@ -100,10 +100,12 @@ def _bump_versions(ps) -> None:
 
 def adam_flat_(params: torch.Tensor, grads: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor,
                step: int, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-               guard: torch.Tensor | None = None) -> None:
+               guard: torch.Tensor | None = None, step_dev: torch.Tensor | None = None) -> None:
     """Adam over one flat fp32 buffer (the Learner's state_dict-ordered params): one launch.
-    ``guard`` (one fp32 device element): skip the update on the device when it is non-zero."""
+    ``guard`` (one fp32 device element): skip the update on the device when it is non-zero.
+    ``step_dev`` (one int32 device element, updates applied so far): use it instead of
+    ``step`` and advance it on the device only when the update ran."""
     hp = N.AdamHP(float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), 0, 0)
     N.adam_step(hp, step, [params], [grads], [exp_avg], [exp_avg_sq], None, stream=N.stream_ptr(params.device),
-                guard=guard)
+                guard=guard, step_dev=step_dev)
     _bump_versions([params])

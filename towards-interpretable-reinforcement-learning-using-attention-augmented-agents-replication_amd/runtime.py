@@ -15,7 +15,8 @@ from . import _native as N
 
 class UnrollRunner:
     def __init__(self, B: int, T: int, H: int, W: int, nq: int = 4, A: int = 18,
-                 dtype: str = "fp32", device=None, stateful_core: bool = False, frames_u8: bool = False):
+                 dtype: str = "fp32", device=None, stateful_core: bool = False, frames_u8: bool = False,
+                 defer_stranded: bool = False):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(f"dtype must be 'fp32' or 'bf16', got {dtype!r}")
         self.lib = N.load()
@@ -25,7 +26,8 @@ class UnrollRunner:
         self.stateful_core = bool(stateful_core)
         self.frames_u8 = bool(frames_u8)
         self.cfg = N.Cfg(B, T, H, W, nq, A, N.BF16 if dtype == "bf16" else N.F32,
-                         (N.FLAG_STATEFUL_CORE if stateful_core else 0) | (N.FLAG_FRAMES_U8 if frames_u8 else 0))
+                         (N.FLAG_STATEFUL_CORE if stateful_core else 0) | (N.FLAG_FRAMES_U8 if frames_u8 else 0)
+                         | (N.FLAG_DEFER_STRANDED if defer_stranded else 0))
         self.B, self.T, self.H, self.W, self.nq, self.A, self.dtype = B, T, H, W, nq, A, dtype
         self.h, self.w = N.grid(H, W)
         self.P = self.h * self.w
