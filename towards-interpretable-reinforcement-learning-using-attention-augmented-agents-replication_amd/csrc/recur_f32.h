@@ -549,6 +549,394 @@ k_convlstm_fwd_f32(RecF32Params p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pre-split frame-group forward (S6, G = 8): the same recurrence, mapping and A
+// stream as k_convlstm_fwd_f32<8, 0, true, true, 4>, but the B operand -- the
+// LDS images of x_t and h_{t-1} -- is held ALREADY split into its three bf16
+// parts, so the K loop does no splitting at all (tools/ubench/f32rec: the
+// in-loop split of the B fragments was 19 % of the launch, "S6 no B split").
+// Each value is split once per step where it enters the image: x_{t+1} and the
+// partners' h slices as they are loaded from XH, the workgroup's own h_t in the
+// epilogue.  The split images are 1.5x the fp32 bytes, so they drop the zero
+// border: a lane whose 3x3 neighbour is off the grid (or whose column is a
+// padding column) reads the all-zero pixel P instead (per-lane tap mask).
+//
+// Image layout (both): pixel p at p * pitch; its 16-channel group g (the two
+// quads of one S6 k-step) holds, per part (hi, mid, lo) and lane half hh, the
+// 8 bf16 of channels 16g + {4hh..4hh+3, 8+4hh..8+4hh+3} -- exactly a lane's
+// bf16x8 operand -- at chunk (part * NG + g) * 2 + hh (16 B each; NG = 8 groups
+// for h, 4 for x).  Pitches 784 / 400 B are odd multiples of 16: the 16 lanes of
+// a ds_read_b128 group (consecutive columns = consecutive pixels under every
+// tap) hit 16 distinct bank groups, and a k-step's three parts are immediate
+// offsets from one per-tap lane address.  The epilogue's staging aliases the x
+// image (x_{t+1} is written after the epilogue).
+constexpr int kPsHP = 784, kPsXP = 400;                 // pixel pitches (B)
+constexpr int kPsNP = 129;                              // pixels (P <= 128) + the zero pixel
+constexpr int kPsHB = kPsNP * kPsHP, kPsXB = kPsNP * kPsXP;
+constexpr int kPsGT = 0, kPsCT = 32 * 144;               // per-wave staging: gate tile, c tile
+constexpr int kPsSTG = kPsCT + 32 * 48;                  // 6 KB per wave
+constexpr int kPsHT = 4 * kPsSTG;                        // the workgroup's h_t tile: 128 pixels x 16 channels, pitch 80 B
+static_assert(kPsHT + 128 * 80 <= kPsXB, "staging aliases the x image");
+
+// split 16 fp32 channels of one pixel (group order) into the image's 6 chunks
+__device__ __forceinline__ void ps_store_group(unsigned char* img, int pix_off, int NG, int g, const f32x4 (&v)[4]) {
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const float x8[8] = {v[hh][0], v[hh][1], v[hh][2], v[hh][3], v[2 + hh][0], v[2 + hh][1], v[2 + hh][2], v[2 + hh][3]};
+    bf16x8 hi, mid, lo;
+    split3_bf16(x8, hi, mid, lo);
+    *reinterpret_cast<bf16x8*>(img + pix_off + ((0 * NG + g) * 2 + hh) * 16) = hi;
+    *reinterpret_cast<bf16x8*>(img + pix_off + ((1 * NG + g) * 2 + hh) * 16) = mid;
+    *reinterpret_cast<bf16x8*>(img + pix_off + ((2 * NG + g) * 2 + hh) * 16) = lo;
+  }
+}
+
+// ABL (diagnostic builds only, tools/ubench/f32ps; production launches use 0): bit 0 = no
+// epilogue math / HBM stores, bit 2 = no partner exchange, bit 3 = no MFMAs, bit 5 = no
+// A-stream loads in the K loop.
+// MAP: wave -> tiles.  0: wave w takes both row blocks and column block w (each A quad is
+// streamed by all four waves); 1: wave w takes row block w & 1 and column blocks
+// 2 (w >> 1), +1 (each A quad streamed by two waves, each B part read by two).  The A stream
+// (L2 -> L1 -> VGPR, no LDS room left beside the split images) is the kernel's bound
+// (tools/ubench/f32ps: no A loads -29 %), so MAP 1 halves its L1 traffic.
+template <int ABL = 0, int MAP = 1, int PD = 8>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_convlstm_fwd_f32ps(RecF32Params p) {
+  static_assert(8 % PD == 0 && PD >= 4 && PD <= kF32PD, "PD");   // slot = quad % PD; a pair never wraps
+  constexpr int G = 8, NPU = (128 * 7 + 255) / 256, NXU = (128 * 4 + 255) / 256;
+  constexpr int RPW = MAP ? 1 : 2, NCB = MAP ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) unsigned char him[kPsHB];
+  __shared__ __attribute__((aligned(16))) unsigned char xim[kPsXB];
+
+  const int blk = (int)blockIdx.x, xcd = blk & 7, loc = blk >> 3;
+  const int b = xcd + 8 * (loc / G), kh = loc % G;
+  if (b >= p.B) return;   // padding group of the last XCD column (never a partner of a live frame)
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  uint64_t wdl = 0;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int P = p.P, W = p.w;
+  const size_t M = (size_t)p.B * P;
+  const int rw = MAP ? (wave & 1) : 0;
+  const int rbg0 = 2 * kh + rw;                 // the wave's first global row block
+  auto cbk = [&](int c) { return MAP ? 2 * (wave >> 1) + c : wave; };
+  unsigned char* stg = xim + wave * kPsSTG;
+
+  // per lane and column block: the column, its 3x3 validity mask (padding columns: none valid)
+  int colc[NCB], vmask[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    colc[c] = 32 * cbk(c) + r32;
+    vmask[c] = 0;
+    if (colc[c] < P) {
+      const int y = colc[c] / W, x = colc[c] % W;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        if ((unsigned)yy < (unsigned)p.h && (unsigned)xx < (unsigned)W) vmask[c] |= 1 << tap;
+      }
+    }
+  }
+  // lane byte address of tap ``tap``'s neighbour pixel (or the zero pixel) in an image of ``pitch``
+  auto tapbase = [&](int c, int tap, int pitch) -> uint32_t {
+    const int nb = colc[c] + (tap / 3 - 1) * W + (tap % 3 - 1);
+    return (uint32_t)((((vmask[c] >> tap) & 1) ? nb : P) * pitch + hh * 16);
+  };
+
+  // XH slot loads of 16-channel groups: unit u = (pixel, group) -> 4 x 16 B (sc1 for partner slices)
+  auto xh_rsrc = [&](int slot) {
+    return make_rsrc(p.XH + ((size_t)slot * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 4));
+  };
+  auto ld_group = [&](__amdgpu_buffer_rsrc_t rs, int px, int chan0, bool sc1, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t off = px < P ? (uint32_t)((px * 192 + chan0 + 4 * k) * 4) : kOOB;
+      v[k] = __builtin_bit_cast(f32x4, sc1 ? __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSC1)
+                                           : __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  f32x4 xv[NXU][4];
+  auto x_issue = [&](int slot) {   // x_slot: units (pixel, group 0..3)
+    const __amdgpu_buffer_rsrc_t rs = xh_rsrc(slot);
+#pragma unroll
+    for (int n = 0; n < NXU; ++n) {
+      const int u = tid + 256 * n;
+      ld_group(rs, u >> 2, 16 * (u & 3), false, xv[n]);
+    }
+  };
+  auto x_store = [&] {
+#pragma unroll
+    for (int n = 0; n < NXU; ++n) {
+      const int u = tid + 256 * n, px = u >> 2;
+      if (px < P) ps_store_group(xim, px * kPsXP, 4, u & 3, xv[n]);
+    }
+  };
+
+  {  // the zero pixel of both images
+    u32x4* z = reinterpret_cast<u32x4*>(him + P * kPsHP);
+    for (int i = tid; i < kPsHP / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    z = reinterpret_cast<u32x4*>(xim + P * kPsXP);
+    for (int i = tid; i < kPsXP / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  x_issue(0);
+  x_store();
+  if (!p.h0_zero) {   // h_{-1} (XH slot 0, all 8 groups) into the h image
+    const __amdgpu_buffer_rsrc_t rs = xh_rsrc(0);
+    for (int u = tid; u < P * 8; u += 256) {
+      f32x4 v[4];
+      ld_group(rs, u >> 3, 64 + 16 * (u & 7), false, v);
+      ps_store_group(him, (u >> 3) * kPsHP, 8, u & 7, v);
+    }
+  }
+
+  // per-lane state: bias of the lane's rows, c of its (pixel, channel) pairs -- tile (r, c)
+  // lane (r32, hh): element 4g + e = gate e of channel 8 (rbg0 + r) + 2g + hh at column colc[c]
+  f32x4 bz[RPW][4];
+  float cst[RPW][NCB][4];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 8 * (rbg0 + r) + 2 * g + hh;
+      bz[r][g] = *reinterpret_cast<const f32x4*>(p.bias + 4 * ch);
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) cst[r][c][g] = colc[c] < P ? p.Cst[((size_t)b * P + colc[c]) * 128 + ch] : 0.f;
+    }
+
+  // A stream (pre-split fragment-order weights, k_split_frag): quad q's part of row block rb
+  const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wf6, (uint32_t)(16 * kF32QP * 3 * 512));
+  auto lda6 = [&](int q, int r, int part) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         rsw6, lane * 8, (((rbg0 + r) * kF32QP + q) * 3 + part) * 512, 0));
+  };
+  u32x2 a6[PD][RPW][3];
+  auto preload = [&] {
+#pragma unroll
+    for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6(s, r, part);
+  };
+  preload();
+  __syncthreads();   // x_0 / h_{-1} images and the zero pixels written
+
+  for (int t = 0; t < p.T; ++t) {
+    f32x16 acc[RPW][NCB];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < NCB; ++c)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.f;
+    // B parts of group g at the lane addresses ``base``: three immediate offsets per column block
+    auto ldb = [&](const unsigned char* img, const uint32_t (&base)[NCB], int NG, int g, bf16x8 (&bv)[NCB][3]) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c)
+#pragma unroll
+        for (int part = 0; part < 3; ++part)
+          bv[c][part] = *reinterpret_cast<const bf16x8*>(img + base[c] + (part * NG + g) * 32);
+    };
+    // quads qn, qn + 1 (slot even): A parts pre-split in the stream, B parts pre-split in the image
+    auto pair = [&](int qn, int slot, const bf16x8 (&bv)[NCB][3], auto&& load_next_b) {
+      bf16x8 a3[RPW][3];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int part = 0; part < 3; ++part)
+          a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[slot][r][part].x, a6[slot][r][part].y,
+                                                         a6[slot + 1][r][part].x, a6[slot + 1][r][part].y});
+      if constexpr (!(ABL & 32)) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+          for (int part = 0; part < 3; ++part) {
+            a6[(slot + PD - 1) % PD][r][part] = lda6(qn + PD - 1, r, part);
+            a6[slot][r][part] = lda6(qn + PD, r, part);
+          }
+      }
+      load_next_b();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          if constexpr ((ABL & 8) != 0) {   // keep every operand alive, no MFMA
+            acc[r][c][0] += (float)ah[0] * (float)bv[c][0][0] + (float)am[1] * (float)bv[c][1][1] +
+                            (float)al[2] * (float)bv[c][2][2];
+          } else {
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bv[c][0], acc[r][c], 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bv[c][2], acc[r][c], 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bv[c][1], acc[r][c], 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bv[c][0], acc[r][c], 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bv[c][1], acc[r][c], 0, 0, 0);
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bv[c][0], acc[r][c], 0, 0, 0);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    bf16x8 bp[2][NCB][3];
+    // partners' groups of h_{t-1} (XH slot t): loaded into registers mid x-part
+    f32x4 pv[NPU][4];
+    const bool exch = t > 0 && !(ABL & 4);
+    AAA_F32_STAMP(t, 0);
+    auto partner_issue = [&] {
+      wave_wait_flags(p.flags + b * G, ((1ull << G) - 1) & ~(1ull << kh), t, p.report, p.spin, wdl);
+      const __amdgpu_buffer_rsrc_t rs = xh_rsrc(t);
+#pragma unroll
+      for (int n = 0; n < NPU; ++n) {
+        const int u = tid + 256 * n, px = u / 7, j = u % 7, g = j < kh ? j : j + 1;
+        ld_group(rs, px, 64 + 16 * g, true, pv[n]);
+      }
+    };
+    auto partner_store = [&] {
+#pragma unroll
+      for (int n = 0; n < NPU; ++n) {
+        const int u = tid + 256 * n, px = u / 7, j = u % 7, g = j < kh ? j : j + 1;
+        if (px < P) ps_store_group(him, px * kPsHP, 8, g, pv[n]);
+      }
+    };
+    auto bases = [&](int tap, int pitch, uint32_t (&o)[NCB]) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) o[c] = tapbase(c, tap, pitch);
+    };
+
+    // ---- x-part: 9 taps x 4 groups over the x image
+    {
+      uint32_t xb[NCB], xn[NCB];
+      bases(0, kPsXP, xb);
+      ldb(xim, xb, 4, 0, bp[0]);
+      for (int tap = 0; tap < 9; ++tap) {
+        bases(tap < 8 ? tap + 1 : 8, kPsXP, xn);
+        int qt = tap * 8;
+        asm volatile("" : "+s"(qt));
+        if (tap == 2 && exch) partner_issue();
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          pair(qt + 2 * g, (2 * g) % PD, bp[g & 1], [&] {
+            if (g < 3) ldb(xim, xb, 4, g + 1, bp[(g + 1) & 1]);
+            else if (tap < 8) ldb(xim, xn, 4, 0, bp[0]);
+          });
+        }
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) xb[c] = xn[c];
+      }
+    }
+    const bool hpart = t > 0 || !p.h0_zero;
+    if (exch) partner_store();
+    barrier_lds();   // every wave is done with x_t; the partners' h_{t-1} is in the image
+    AAA_F32_STAMP(t, 1);
+    if (hpart) {
+      // ---- h-part: 9 taps x 8 groups over the h image
+      uint32_t hb[NCB], hn[NCB];
+      bases(0, kPsHP, hb);
+      ldb(him, hb, 8, 0, bp[0]);
+      for (int tap = 0; tap < 9; ++tap) {
+        bases(tap < 8 ? tap + 1 : 8, kPsHP, hn);
+        int qt = kF32QX + tap * 16;
+        asm volatile("" : "+s"(qt));
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+          pair(qt + 2 * g, (2 * g) % PD, bp[g & 1], [&] {
+            if (g < 7) ldb(him, hb, 8, g + 1, bp[(g + 1) & 1]);
+            else if (tap < 8) ldb(him, hn, 8, 0, bp[0]);
+          });
+        }
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) hb[c] = hn[c];
+      }
+    } else {   // the prefetched A quads are the h-part's: restart the stream at quad 0
+      preload();
+    }
+    barrier_lds();   // every wave is done with both images: staging (aliasing x) and h_t may be written
+    AAA_F32_STAMP(t, 2);
+    if (t + 1 < p.T) x_issue(t + 1);   // x_{t+1} lands under the epilogue
+
+    // ---- epilogue: gate math + cell update lane-local; Gt / c_t staged per wave through its
+    // LDS tiles (whole pixel rows per store instruction); h_t into the workgroup's h tile
+    const size_t rowt = (size_t)t * M + (size_t)b * P;
+    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c)   // keep the accumulators alive: one value each into the h tile
+          *reinterpret_cast<float*>(xim + kPsHT + (colc[c] & 127) * 80 + 4 * r) = acc[r][c][0] + acc[r][c][15];
+    } else {
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int chl = 2 * g + hh, ch = 8 * (rbg0 + r) + chl;
+            float gi, gf, gc, go, cc, h;
+            GateFwd::run(acc[r][c][4 * g] + bz[r][g][0], acc[r][c][4 * g + 1] + bz[r][g][1],
+                         acc[r][c][4 * g + 2] + bz[r][g][2], acc[r][c][4 * g + 3] + bz[r][g][3], cst[r][c][g], gi, gf,
+                         gc, go, cc, h);
+            cst[r][c][g] = cc;
+            *reinterpret_cast<f32x4*>(stg + kPsGT + r32 * 144 + 16 * chl) = f32x4{gi, gf, gc, go};
+            *reinterpret_cast<float*>(stg + kPsCT + r32 * 48 + 4 * chl) = cc;
+            *reinterpret_cast<float*>(xim + kPsHT + colc[c] * 80 + 4 * (8 * (rbg0 + r - 2 * kh) + chl)) = h;
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const int col0 = 32 * cbk(c);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {   // Gt: 32 pixels x 8 chunks of 16 B (rows 32 rbg .. + 32)
+            const int q = k * 64 + lane, px = q >> 3, ch16 = q & 7, pix = col0 + px;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + kPsGT + px * 144 + 16 * ch16);
+            if (pix < P) *reinterpret_cast<u32x4*>(p.Gt + (rowt + pix) * 512 + 32 * (rbg0 + r) + 4 * ch16) = v;
+          }
+          {  // c_t: 32 pixels x 2 chunks of 16 B (channels 8 rbg .. + 8)
+            const int px = lane >> 1, half = lane & 1, pix = col0 + px;
+            const u32x4 vc = *reinterpret_cast<const u32x4*>(stg + kPsCT + px * 48 + 16 * half);
+            if (pix < P) *reinterpret_cast<u32x4*>(p.Cst + (rowt + M + pix) * 128 + 8 * (rbg0 + r) + 4 * half) = vc;
+          }
+          __builtin_amdgcn_wave_barrier();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+    barrier_lds();   // the workgroup's h_t tile is complete
+    if constexpr (!(ABL & 1)) {
+      // h_t, the workgroup's 16 channels: Hs, XH slot t+1 (sc1: the partners' and the weight
+      // gradient's operand) and the own group of the split h image; thread = (pixel, half)
+      const int px = tid >> 1, half = tid & 1;
+      if (px < P) {
+        const unsigned char* ht = xim + kPsHT + px * 80;
+        const u32x4 h0 = *reinterpret_cast<const u32x4*>(ht + 32 * half);
+        const u32x4 h1 = *reinterpret_cast<const u32x4*>(ht + 32 * half + 16);
+        float* hs = p.Hs + (rowt + px) * 128 + 16 * kh + 8 * half;
+        *reinterpret_cast<u32x4*>(hs) = h0;
+        *reinterpret_cast<u32x4*>(hs + 4) = h1;
+        const __amdgpu_buffer_rsrc_t rs = xh_rsrc(t + 1);
+        const uint32_t off = (uint32_t)((px * 192 + 64 + 16 * kh + 8 * half) * 4);
+        __builtin_amdgcn_raw_buffer_store_b128(h0, rs, off, 0, kSC1);
+        __builtin_amdgcn_raw_buffer_store_b128(h1, rs, off + 16, 0, kSC1);
+        // the split image's lane half ``half`` holds channels {4 half .. +3, 8 + 4 half .. +3}
+        const f32x4 va = *reinterpret_cast<const f32x4*>(ht + 16 * half);
+        const f32x4 vb = *reinterpret_cast<const f32x4*>(ht + 32 + 16 * half);
+        const float x8[8] = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+        bf16x8 hi, mid, lo;
+        split3_bf16(x8, hi, mid, lo);
+        unsigned char* dst = him + px * kPsHP + half * 16;
+        *reinterpret_cast<bf16x8*>(dst + (0 * 8 + kh) * 32) = hi;
+        *reinterpret_cast<bf16x8*>(dst + (1 * 8 + kh) * 32) = mid;
+        *reinterpret_cast<bf16x8*>(dst + (2 * 8 + kh) * 32) = lo;
+      }
+    }
+    barrier_lds();   // every wave is done with the staging and the h tile (they alias the x image)
+    AAA_F32_STAMP(t, 3);
+    if (t + 1 < p.T) x_store();
+    // publish h_t: every wave's stores retired, a barrier (also: x_{t+1} in the image), one flag store
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();
+    if (tid == 0) __hip_atomic_store(p.flags + b * G + kh, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    AAA_F32_STAMP(t, 4);
+  }
+}
+
 inline bool f32_rec_fits(int h, int w) { return rec_fits(h, w); }
 
 // Workgroups per frame for B frames on a device of ``cus`` CUs (0: does not fit one residency wave).
@@ -567,7 +955,10 @@ inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool 
   }
   // G = 8, S6: the WIDE mapping with 4 A quads in flight (tools/ubench/f32rec: 7-10% under
   // the two-column-block mapping with 8, most of it from the shallower prefetch)
-  const void* k = G == 8   ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true, true, 4>)
+  // G = 8, S6: the pre-split images (k_convlstm_fwd_f32ps); AAA_F32_PRESPLIT=0 (A/B) the in-loop split
+  const bool ps = s6 && G == 8 && p.P <= 128 && std::getenv("AAA_F32_PRESPLIT") == nullptr;
+  const void* k = ps       ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32ps<0, 1, 8>)
+                  : G == 8 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true, true, 4>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>))
                   : G == 4 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4, 0, true>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<4>))
