@@ -419,6 +419,16 @@ template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
 struct GemmCfgS6 : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, WK_> {
   static constexpr bool SPLIT3 = true, SPLIT6 = true;
 };
+// The same products with each operand split ONCE per workgroup, where its staged fp32
+// chunk is committed to LDS (lds_store_split3), instead of once per wave per fragment
+// read: the LDS stages hold the three bf16 part tiles of each operand and the K loop
+// reads bf16 fragments only (gemm_kernel_s6l; the register-staged TB loaders).
+template <class C, class = void> struct split6l_of : std::false_type {};
+template <class C> struct split6l_of<C, std::enable_if_t<C::SPLIT6L>> : std::true_type {};
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_>
+struct GemmCfgS6L : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, 1> {
+  static constexpr bool SPLIT3 = true, SPLIT6 = true, SPLIT6L = true;
+};
 __device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -427,6 +437,23 @@ __device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8& hi, bf1
     mid[e] = (__bf16)r;
     lo[e] = (__bf16)(r - (float)mid[e]);
   }
+}
+
+// Split-at-commit (GemmCfgS6L): 4 fp32 of a staged chunk -> their three bf16 parts, 8 B
+// each, into the three part tiles of one operand stage (``plane`` elements apart).
+__device__ __forceinline__ void lds_store_split3(__bf16* dst, int plane, const u32x4& raw) {
+  const f32x4 f = __builtin_bit_cast(f32x4, raw);
+  bf16x4 hi, mid, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = (__bf16)f[e];
+    const float r = f[e] - (float)hi[e];
+    mid[e] = (__bf16)r;
+    lo[e] = (__bf16)(r - (float)mid[e]);
+  }
+  *reinterpret_cast<bf16x4*>(dst) = hi;
+  *reinterpret_cast<bf16x4*>(dst + plane) = mid;
+  *reinterpret_cast<bf16x4*>(dst + 2 * plane) = lo;
 }
 
 __device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
@@ -604,6 +631,102 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
       }
 }
 
+// Split-at-commit split6 GEMM (GemmCfgS6L): the register-staged double buffer of
+// gemm_kernel, with each stage holding the hi / mid / lo bf16 tiles of both operands
+// (the loaders' commit3).  Per 16-k step a wave reads 3 (MI + MJ) bf16 fragments and
+// issues 6 MI MJ MFMAs; no VALU split in the loop.  Same products, same order, same
+// parts as the SPLIT6 path of gemm_kernel: bit-identical results.
+template <class C, class LA, class LB, class EP>
+__global__ void __launch_bounds__(C::NT)
+gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
+  constexpr int BI = C::BI, BJ = C::BJ, BK = C::BK, WI = C::WI, WJ = C::WJ;
+  constexpr int WTI = BI / WI, WTJ = BJ / WJ, MI = WTI / 32, MJ = WTJ / 32;
+  static_assert(C::WK == 1 && MI >= 1 && MJ >= 1 && BK % 16 == 0, "tile shape");
+  using TA = TileK<__bf16, BI, BK, LA::KC>;
+  using TB = TileK<__bf16, BJ, BK, LB::KC>;
+  constexpr int PA = TA::ELEMS, PB = TB::ELEMS, STG = 3 * (PA + PB);
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STG];
+
+  int ti, tj, tz;
+  tile_of(tm, ti, tj, tz);
+  const int i0 = ti * BI, j0 = tj * BJ;
+  const int kb = tz * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+
+  LA la(pa, i0);
+  LB lb(pb, j0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wi = wave / WJ, wj = wave - (wave / WJ) * WJ;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[MI][MJ];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int nk = (ke - kb + BK - 1) / BK;
+  typename LA::Regs ra;
+  typename LB::Regs rb;
+  la.fetch(kb, ke, ra);
+  lb.fetch(kb, ke, rb);
+  la.commit3(smem, PA, ra);
+  lb.commit3(smem + 3 * PA, PB, rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const __bf16* cur = smem + (kt & 1) * STG;
+    __bf16* nxt = smem + ((kt & 1) ^ 1) * STG;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.fetch(kb + (kt + 1) * BK, ke, ra);
+      lb.fetch(kb + (kt + 1) * BK, ke, rb);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < BK / 16; ++s2) {
+      const int kofs = 16 * s2 + 8 * h;
+      bf16x8 af[MI][3], bfr[MJ][3];
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) af[a][p] = frag_bf16<TA>(cur + p * PA, wi * WTI + a * 32 + r32, kofs);
+#pragma unroll
+      for (int b = 0; b < MJ; ++b)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bfr[b][p] = frag_bf16<TB>(cur + 3 * PA + p * PB, wj * WTJ + b * 32 + r32, kofs);
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) {   // smallest products first, as gemm_kernel's SPLIT6
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bfr[b][0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][2], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][0], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][1], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][0], acc[a][b], 0, 0, 0);
+        }
+    }
+    if (more) {
+      la.commit3(nxt, PA, ra);
+      lb.commit3(nxt + 3 * PA, PB, rb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < MJ; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i = i0 + wi * WTI + a * 32 + 8 * g + 4 * h;
+        const int j = j0 + wj * WTJ + b * 32 + r32;
+        ep(i, j, acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
+      }
+}
+
 // Host-side launcher.  Mi/Nj are the D extents, K the reduction length,
 // nsplit the number of K slices (epilogue must accumulate when nsplit > 1).
 template <class C, class LA, class LB, class EP>
@@ -615,8 +738,12 @@ inline hipError_t launch_gemm(const typename LA::Params& pa, const typename LB::
   kchunk = (kchunk + C::BK - 1) / C::BK * C::BK;
   nsplit = (K + kchunk - 1) / kchunk;
   dim3 grid((Nj + C::BJ - 1) / C::BJ, (Mi + C::BI - 1) / C::BI, nsplit);
-  hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
-                     tile_map(grid));
+  if constexpr (split6l_of<C>::value)
+    hipLaunchKernelGGL((gemm_kernel_s6l<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
+                       tile_map(grid));
+  else
+    hipLaunchKernelGGL((gemm_kernel<C, LA, LB, EP>), grid, dim3(C::NT), 0, st, pa, pb, ep, K, kchunk,
+                       tile_map(grid));
   return hipGetLastError();
 }
 

@@ -78,6 +78,8 @@ struct LdRowsTB {
   int ldo[PER];
   int rowbytes;
   bool act[PER];
+  // split-at-commit GEMMs (gemm.h GemmCfgS6L): the chunk's place in the bf16 part tiles
+  __device__ __forceinline__ static int off16(int ch) { return Tile<__bf16, R, BK, false>::off((ch % CPK) * VG, ch / CPK); }
   __device__ __forceinline__ LdRowsTB(const Params& p, int row0) {
     rs = make_rsrc(p.src, (uint32_t)((size_t)p.ktotal * p.ld * sizeof(G)));
     rowbytes = p.ld * (int)sizeof(G);
@@ -99,6 +101,11 @@ struct LdRowsTB {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+  __device__ __forceinline__ void commit3(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split3(lds + off16(threadIdx.x + c * NT), plane, buf[c]);
   }
 };
 
@@ -222,6 +229,7 @@ struct LdIm2colTB {
   int kr[PER], ky[PER], kx[PER], toff[PER];
   int ldo[PER];
   bool act[PER];
+  __device__ __forceinline__ static int off16(int ch) { return Tile<__bf16, R, BK, false>::off((ch % CPK) * VG, ch / CPK); }
   __device__ __forceinline__ LdIm2colTB(const Params& p, int row0) : g(p.g) {
     rs = make_rsrc(p.src, p.src_bytes);
 #pragma unroll
@@ -257,6 +265,11 @@ struct LdIm2colTB {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + ldo[c], buf[c]);
+  }
+  __device__ __forceinline__ void commit3(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split3(lds + off16(threadIdx.x + c * NT), plane, buf[c]);
   }
 };
 

@@ -303,10 +303,14 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
       using CS6 = std::conditional_t<std::is_same<T, float>::value, decltype(cfg), CfgWFor<T>>;
       return wgrad_lstm(CS6{});
     };
-    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 3);
+    // 4 = 256x256 with each operand split once where it is committed to LDS (GemmCfgS6L, BK16,
+    // two stages of bf16 part tiles); 5 = its 256x128 4-wave form
+    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 4);
     const int rc = tile6 == 1   ? s6(GemmCfgS6<128, 256, 32, 2, 2>{})
                    : tile6 == 2 ? s6(GemmCfgS6<256, 128, 32, 2, 2>{})
                    : tile6 == 3 ? s6(GemmCfgS6<256, 256, 32, 2, 4>{})
+                   : tile6 == 4 ? s6(GemmCfgS6L<256, 256, 16, 2, 4>{})
+                   : tile6 == 5 ? s6(GemmCfgS6L<256, 128, 16, 2, 2>{})
                                 : s6(GemmCfgS6<128, 128, 32, 2, 2>{});
     if (rc) return rc;
   } else {
