@@ -211,12 +211,13 @@ def test_dx_split6_tiles(cuda, monkeypatch, tile):
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"dx tile {tile}: ")
 
 
-@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4", "5", "6"])
 def test_wgrad_split6_tiles(cuda, monkeypatch, tile):
     """The fp32 ConvLSTM weight gradient (attention.py:117-122's eight gate convs,
     autograd at main_mp.py:77) on split products: register-staged 128x128,
     128x256, 256x128, 256x256 with the split per fragment read, and 256x256 /
-    256x128 with each operand split once as it is committed to LDS (GemmCfgS6L);
+    256x128 with each operand split once as it is committed to LDS (GemmCfgS6L),
+    and 256x256 split-at-commit with two K tiles of loads in flight;
     T*B*P = 605 pixel rows -> a ragged last K tile of every split-K slice."""
     monkeypatch.setenv("AAA_WGRAD_S6_TILE", tile)
     T, B = 5, 1

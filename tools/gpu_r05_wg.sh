@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method threa
   > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/tests.log | head -20; exit $rc; }
 BA="--no-cpu-baseline --no-dropin --no-episode"
 for i in 1 2; do
-  for t in 4 3 5; do
+  for t in 4 6; do
     AAA_WGRAD_S6_TILE=$t timeout -k 10 200 python bench.py $BA > $O/t${t}_$i.json 2> $O/t${t}_$i.err || { echo "t$t rc=$?"; tail $O/t${t}_$i.err; exit 1; }
   done
 done

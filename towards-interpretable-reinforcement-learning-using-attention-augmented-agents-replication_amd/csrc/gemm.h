@@ -425,9 +425,10 @@ struct GemmCfgS6 : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, WK_> {
 // reads bf16 fragments only (gemm_kernel_s6l; the register-staged TB loaders).
 template <class C, class = void> struct split6l_of : std::false_type {};
 template <class C> struct split6l_of<C, std::enable_if_t<C::SPLIT6L>> : std::true_type {};
-template <int BI_, int BJ_, int BK_, int WI_, int WJ_>
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int FD_ = 1>
 struct GemmCfgS6L : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, 1> {
   static constexpr bool SPLIT3 = true, SPLIT6 = true, SPLIT6L = true;
+  static constexpr int FD = FD_;   // K tiles of global loads in flight (register stages)
 };
 __device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
@@ -669,21 +670,37 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
   const int nk = (ke - kb + BK - 1) / BK;
-  typename LA::Regs ra;
-  typename LB::Regs rb;
-  la.fetch(kb, ke, ra);
-  lb.fetch(kb, ke, rb);
-  la.commit3(smem, PA, ra);
-  lb.commit3(smem + 3 * PA, PB, rb);
+  // FD = 2: the loads of tile k+2 are in flight while tile k+1 is committed and tile k
+  // multiplied (two register stages), so a load has two K steps of MFMAs to land
+  constexpr int FD = C::FD;
+  typename LA::Regs ra[FD];
+  typename LB::Regs rb[FD];
+  la.fetch(kb, ke, ra[0]);
+  lb.fetch(kb, ke, rb[0]);
+  if constexpr (FD == 2) {
+    if (nk > 1) {
+      la.fetch(kb + BK, ke, ra[1]);
+      lb.fetch(kb + BK, ke, rb[1]);
+    }
+  }
+  la.commit3(smem, PA, ra[0]);
+  lb.commit3(smem + 3 * PA, PB, rb[0]);
   __syncthreads();
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const __bf16* cur = smem + (kt & 1) * STG;
-    __bf16* nxt = smem + ((kt & 1) ^ 1) * STG;
+  // one K step; E = kt & 1 (compile-time, so the register stages stay in registers)
+  auto step = [&](int kt, auto E) {
+    constexpr int e = decltype(E)::value;
+    const __bf16* cur = smem + e * STG;
+    __bf16* nxt = smem + (e ^ 1) * STG;
     const bool more = kt + 1 < nk;
-    if (more) {
-      la.fetch(kb + (kt + 1) * BK, ke, ra);
-      lb.fetch(kb + (kt + 1) * BK, ke, rb);
+    if constexpr (FD == 2) {   // tile kt+2 into register stage e (tile kt's, committed a step ago)
+      if (kt + 2 < nk) {
+        la.fetch(kb + (kt + 2) * BK, ke, ra[e]);
+        lb.fetch(kb + (kt + 2) * BK, ke, rb[e]);
+      }
+    } else if (more) {
+      la.fetch(kb + (kt + 1) * BK, ke, ra[0]);
+      lb.fetch(kb + (kt + 1) * BK, ke, rb[0]);
     }
 #pragma unroll
     for (int s2 = 0; s2 < BK / 16; ++s2) {
@@ -709,11 +726,16 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][0], acc[a][b], 0, 0, 0);
         }
     }
-    if (more) {
-      la.commit3(nxt, PA, ra);
-      lb.commit3(nxt + 3 * PA, PB, rb);
+    if (more) {   // tile kt+1: register stage e ^ 1 (FD 2) or 0
+      constexpr int rs1 = FD == 2 ? (e ^ 1) : 0;
+      la.commit3(nxt, PA, ra[rs1]);
+      lb.commit3(nxt + 3 * PA, PB, rb[rs1]);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, std::integral_constant<int, 0>{});
+    if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{});
   }
 #pragma unroll
   for (int a = 0; a < MI; ++a)

@@ -204,7 +204,10 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // about two workgroups per CU of splits (both fit a CU; the 1024-WG rule of
     // the other weight gradients doubled the output atomics for the same time:
     // profiles/r02/ab/wgrad_split.txt)
-    const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, 512 / tiles)), rows / CW::BK));
+    // (split-at-commit tiles hold 110 KB of LDS: one workgroup per CU, so one split per CU:
+    // C2 655 us at 18-way against 679 at 36 and 845 at 27, profiles/r05/ab/wgrad_s6l/)
+    const int per_cu = split6l_of<CW>::value ? device_cus() : 512;
+    const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, per_cu / tiles)), rows / CW::BK));
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
                    strf("register-staged %dx%d BK%d%s, %d-way split-K atomics [kernel: gemm_kernel+%d, %d, %d, +LdIm2colTB]",
                         CW::BI, CW::BJ, CW::BK, split6_of<CW>::value ? " (fp32 as bf16x6 split products)" : "", ns,
@@ -304,13 +307,15 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
       return wgrad_lstm(CS6{});
     };
     // 4 = 256x256 with each operand split once where it is committed to LDS (GemmCfgS6L, BK16,
-    // two stages of bf16 part tiles); 5 = its 256x128 4-wave form
-    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 4);
+    // two stages of bf16 part tiles); 5 = its 256x128 4-wave form; 6 (default) = 4 with two K
+    // tiles of loads in flight: C2 633 vs 646 us (4) vs 776 (3) (profiles/r05/ab/wgrad_s6l/)
+    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 6);
     const int rc = tile6 == 1   ? s6(GemmCfgS6<128, 256, 32, 2, 2>{})
                    : tile6 == 2 ? s6(GemmCfgS6<256, 128, 32, 2, 2>{})
                    : tile6 == 3 ? s6(GemmCfgS6<256, 256, 32, 2, 4>{})
                    : tile6 == 4 ? s6(GemmCfgS6L<256, 256, 16, 2, 4>{})
                    : tile6 == 5 ? s6(GemmCfgS6L<256, 128, 16, 2, 2>{})
+                   : tile6 == 6 ? s6(GemmCfgS6L<256, 256, 16, 2, 4, 2>{})
                                 : s6(GemmCfgS6<128, 128, 32, 2, 2>{});
     if (rc) return rc;
   } else {
