@@ -97,11 +97,17 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 // S6: the MFMAs on the bf16 MFMA at fp32 accuracy, two quads per k-step with
 // three-way split operands (as recur_f32.h S6, gemm.h SPLIT6).
 // PDS: the S6 kernel's A quads in flight (4 or 8).
-template <int ABL = 0, bool S6 = false, int PDS = kB32PD>
+// PS (S6 only): the dZ image held pre-split (recur_f32.h k_convlstm_fwd_f32ps's layout:
+// borderless, the zero pixel P, pixel pitch 400 B, chunk (part * 4 + g) * 2 + hh for the
+// 16-row group g) -- the gate backward splits each dZ value once as it writes the image,
+// and the K loop reads bf16 parts only (no per-wave split of the B fragments).
+template <int ABL = 0, bool S6 = false, int PDS = kB32PD, bool PS = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_bwd_f32(RecBwdF32Params p) {
+  static_assert(!PS || S6, "PS: the split-product kernel");
   constexpr int G = 8, NG = 2;                   // NG: (pixel, 4-channel) groups per thread (484 <= 512)
-  __shared__ __attribute__((aligned(16))) unsigned char zim[kB32IB];   // own dZ rows of the current step
+  constexpr int IMB = PS ? kPsXB : kB32IB;
+  __shared__ __attribute__((aligned(16))) unsigned char zim[IMB];   // own dZ rows of the current step
   __shared__ __attribute__((aligned(16))) f32x4 own[128][4];           // own partial dh [px][channel quad]
   __shared__ __attribute__((aligned(16))) float bred[4][64];           // per-wave bias partials
 
@@ -123,9 +129,9 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     return p.xp + ((((size_t)buf * p.B + b) * 8 + dst) * 8 + src) * 128 * 16;
   };
 
-  {  // zero the image (borders stay zero)
+  {  // zero the image (borders / the zero pixel stay zero)
     u32x4* z = reinterpret_cast<u32x4*>(zim);
-    for (int i = tid; i < kB32IB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
+    for (int i = tid; i < IMB / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
 
@@ -166,13 +172,16 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       const int px = (tid + 256 * n) >> 2;
       if (px < P) {
         const int ip = hidx(px);
+        f32x4 zg[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const f32x4 z = *reinterpret_cast<const f32x4*>(p.dZ + ((size_t)(p.T - 1) * M + (size_t)b * P + px) * 512 +
                                                           64 * kh + 16 * cq + 4 * e);
           bs[e] += z;
-          *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(4 * cq + e, px)) = z;
+          zg[e] = z;
+          if constexpr (!PS) *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(4 * cq + e, px)) = z;
         }
+        if constexpr (PS) ps_store_group(zim, px * kPsXP, 4, cq, zg);
       }
     }
     bias_flush(p.T - 1, bs);   // (its barrier also completes the image)
@@ -185,6 +194,26 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     hb[c] = p.colhb[col];
     sb[c] = (col < P ? col : P - 1) - p.w - 1;
   }
+  // PS: per column block, the column and its valid-tap mask under the transposed gather
+  // (tap (ky, kx) reads pixel (y + 1 - ky, x + 1 - kx); padding columns: none valid)
+  int colc[2], vmk[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    colc[c] = 32 * (2 * cw + c) + r32;
+    vmk[c] = 0;
+    if (colc[c] < P) {
+      const int y = colc[c] / p.w, x = colc[c] % p.w;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int yy = y + 1 - tap / 3, xx = x + 1 - tap % 3;
+        if ((unsigned)yy < (unsigned)p.h && (unsigned)xx < (unsigned)p.w) vmk[c] |= 1 << tap;
+      }
+    }
+  }
+  auto psbase = [&](int c, int tap) -> uint32_t {
+    const int nb = colc[c] + (1 - tap / 3) * p.w + (1 - tap % 3);
+    return (uint32_t)((((vmk[c] >> tap) & 1) ? nb : P) * kPsXP + hh * 16);
+  };
   const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(8 * kB32QP * 4 * 1024));
   auto lda = [&](int q, int r) {
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -258,7 +287,59 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       }
     };
     f32x4 bfr[2][2];
-    if constexpr (S6) {
+    if constexpr (S6 && PS) {
+      bf16x8 bq[2][2][3];   // [pair parity][column block][part]
+      auto ldq = [&](int tap, int g, bf16x8 (&o)[2][3]) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const uint32_t base = psbase(c, tap);
+#pragma unroll
+          for (int part = 0; part < 3; ++part)
+            o[c][part] = *reinterpret_cast<const bf16x8*>(zim + base + (part * 4 + g) * 32);
+        }
+      };
+      ldq(0, 0, bq[0]);
+      for (int tap = 0; tap < 9; ++tap) {
+        int qt = tap * 8;
+        asm volatile("" : "+s"(qt));
+#pragma unroll
+        for (int q8 = 0; q8 < 8; q8 += 2) {
+          const int pb = (q8 >> 1) & 1, nb = pb ^ 1;
+          bf16x8 a3[2][3];
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+              a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8 % PD][r][part].x, a6[q8 % PD][r][part].y,
+                                                             a6[q8 % PD + 1][r][part].x, a6[q8 % PD + 1][r][part].y});
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int part = 0; part < 3; ++part) {
+              a6[(q8 + PD - 1) % PD][r][part] = lda6(qt + q8 + PD - 1, r, part);
+              a6[q8 % PD][r][part] = lda6(qt + q8 + PD, r, part);
+            }
+          if (q8 < 6) ldq(tap, (q8 >> 1) + 1, bq[nb]);
+          else if (tap < 8) ldq(tap + 1, 0, bq[nb]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const bf16x8 bh = bq[pb][c][0], bm = bq[pb][c][1], bl = bq[pb][c][2];
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[r][c], 0, 0, 0);
+              acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[r][c], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else if constexpr (S6) {
       f32x4 bp[4][2];   // B fragments of two pairs of quads
       ldb(0, 0, bp[0]);
       ldb(0, 1, bp[1]);
@@ -414,6 +495,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       if (px >= P) continue;
       const int ip = hidx(px);
       float* zo = p.dZ + ((size_t)(s - 1) * M + (size_t)b * P + px) * 512 + 64 * kh;
+      f32x4 zg[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float di, df, dcg, dout;
@@ -421,10 +503,12 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
                  dout);
         const f32x4 z{di, df, dcg, dout};
         bs[e] += z;
+        zg[e] = z;
         const int q = 4 * cq + e;   // 16-B chunk (4 rows) of the workgroup's 64 rows
-        *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(q, px)) = z;
+        if constexpr (!PS) *reinterpret_cast<f32x4*>(zim + ip * 256 + sw16(q, px)) = z;
         *reinterpret_cast<f32x4*>(zo + 4 * q) = z;
       }
+      if constexpr (PS) ps_store_group(zim, px * kPsXP, 4, cq, zg);
     }
     bias_flush(s - 1, bs);   // (its barrier also completes the image before the next dgrad)
     AAA_B32_STAMP(it, 3);
@@ -448,6 +532,10 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 =
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
   // S6: 4 A quads in flight (tools/ubench/f32rec: 3% under 8, fewer registers parked in AGPRs)
+  // S6: the dZ image pre-split (PS); AAA_F32_PRESPLIT=0 (A/B) keeps the in-loop split
+  const bool ps = s6 && std::getenv("AAA_F32_PRESPLIT") == nullptr;
+  if (ps) return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true>),
+                                 f32_grid(p.B, 8), 256, p, st);
   return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4>)
                             : reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>),
                          f32_grid(p.B, 8), 256, p, st);
