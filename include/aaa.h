@@ -221,6 +221,23 @@ int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t s
 int aaa_pair_status(hipStream_t stream, int clear);
 int aaa_pair_flag(float* dst, hipStream_t stream);
 
+/* ---- workspace inspection (checkers, diagnostics) ----
+ * Byte offset and size, inside an aaa_forward workspace laid out for ``cfg``,
+ * of a forward product a checker may read after the call (the workspace is
+ * caller-owned device memory; nothing here syncs or copies):
+ *   AAA_WS_ANSWER_HIDDEN  (T*B, 512) fp32: relu(answer_processor.0(answer)),
+ *                         attention.py:277-282 -- its > 0 pattern is the
+ *                         ReLU mask the hand-written backward applies;
+ *   AAA_WS_QUERY_HIDDEN0  (T*B, 128) fp32: relu(query.model.0(h_{t-1})),
+ *   AAA_WS_QUERY_HIDDEN1  (T*B, 72 nq) fp32: relu(query.model.2(.)), the
+ *                         stateful core's query MLP (attention.py:184-198);
+ *                         AAA_FLAG_STATEFUL_CORE only.
+ * Frame f = t*B + b.  AAA_E_ARG for an unknown region or one the cfg does not
+ * compute.  A test reads these masks to run the oracle's backward through the
+ * same ReLU on/off pattern (tests/helpers.py hip_relu_masks). */
+enum aaa_ws_region { AAA_WS_ANSWER_HIDDEN = 0, AAA_WS_QUERY_HIDDEN0 = 1, AAA_WS_QUERY_HIDDEN1 = 2 };
+int aaa_workspace_region(const aaa_cfg* cfg, int region, size_t* offset, size_t* bytes);
+
 /* ---- optional kernel timing (benchmarks) ----
  * While enabled, the runtime records a hipEvent pair on the launch stream
  * around every launch of the kernel classes below.  aaa_timing_read()

@@ -241,11 +241,22 @@ class KinkProbe:
     lets the backward flip one unit's mask (``flip = (call, flat index)``):
     ``near(eps)`` lists the units within eps of zero, so a test can bound the
     gradient over every on/off choice of those units (tests/helpers.py
-    kink_envelope)."""
+    kink_envelope).
 
-    def __init__(self):
+    ``masks`` (call index -> bool tensor of the pre-activation's shape): run
+    those ReLUs with the given on/off pattern instead of ``pre > 0``, forward
+    (x * mask) and backward (g * mask) -- the mask-matched oracle: the HIP
+    path's own masks (aaa_workspace_region, tests/helpers.py hip_relu_masks)
+    put the oracle's gradient on the same side of every kink as the kernels',
+    so a bf16 comparison needs no kink allowance.  ``mismatch`` counts, per
+    call, the units where the given mask disagrees with the oracle's own sign."""
+
+    def __init__(self, masks=None):
         self.pre = []
         self.flip = None
+        self.masks = masks
+        self.mismatch = {}
+        self.mismatch_pre = {}   # call -> largest |pre-activation| among the disagreeing units
 
     def near(self, eps, limit=8):
         """(t, flat index, |pre|) of the units with |pre| < eps, nearest first."""
@@ -260,15 +271,23 @@ class KinkProbe:
 class _ProbedReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, probe, t):
-        ctx.save_for_backward(x)
         ctx.probe, ctx.t = probe, t
         probe.pre.append(x.detach().clone())
-        return x.clamp_min(0)
+        given = probe.masks.get(t) if probe.masks is not None else None
+        if given is None:
+            ctx.save_for_backward(x > 0)
+            return x.clamp_min(0)
+        given = given.reshape(x.shape).to(torch.bool)
+        dis = given != (x > 0)
+        probe.mismatch[t] = int(dis.sum())
+        probe.mismatch_pre[t] = float(x.detach().abs()[dis].max()) if bool(dis.any()) else 0.0
+        ctx.save_for_backward(given)
+        return x * given.to(x.dtype)
 
     @staticmethod
     def backward(ctx, g):
-        (x,) = ctx.saved_tensors
-        m = (x > 0).to(g.dtype)
+        (mb,) = ctx.saved_tensors
+        m = mb.to(g.dtype)
         f = ctx.probe.flip
         if f is not None and f[0] == ctx.t:
             m.view(-1)[f[1]] = 1.0 - m.view(-1)[f[1]]

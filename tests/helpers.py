@@ -143,3 +143,59 @@ def kink_envelope(loss, params: dict, probe, eps: float = KINK_EPS, limit: int =
     for n, p in params.items():
         p.grad = base[n]
     return base, env, units
+
+
+def oracle_masks(trace, B: int, stateful: bool = False) -> dict:
+    """Agent.relu_trace -- per forward call {"answer": (T_c*B, 512) bool[, "q0", "q1"]},
+    UnrollRunner.relu_masks -- as KinkProbe masks keyed by the oracle's probe call
+    index: per step t, answer_processor.0 at t, or in the stateful core the query
+    MLP's ReLUs at 3t, 3t+1 and answer_processor.0 at 3t+2 (oracle/ref_cpu.py
+    _head / _query call order)."""
+    masks, t = {}, 0
+    for call in trace:
+        steps = call["answer"].shape[0] // B
+        for s in range(steps):
+            rows = slice(s * B, (s + 1) * B)
+            if stateful:
+                masks[3 * t], masks[3 * t + 1], masks[3 * t + 2] = (call[k][rows] for k in ("q0", "q1", "answer"))
+            else:
+                masks[t] = call["answer"][rows]
+            t += 1
+    return masks
+
+
+def kink_report(diag: dict, grads: dict, what: str, pre_scale: float = 1.0) -> dict:
+    """The mask-matched comparison's diagnostics: how many ReLU units the HIP path
+    switched differently from the oracle's own sign (and the largest |pre| among
+    them), and the kink envelope of the oracle's gradient at those masks (what a
+    flip of a near-zero unit would move), as ||envelope|| / ||grad|| per tensor.
+    Asserts the disagreeing units are all within rounding of zero -- the property
+    that makes running the oracle through the HIP path's masks legitimate.
+    Appends a JSON line to gpurun_out/kink_report.jsonl."""
+    import json
+    env = diag.get("env") or {}
+    ratios = {}
+    for n, e in env.items():
+        gn = float(grads[n].double().norm()) if n in grads else 0.0
+        if gn > 0:
+            ratios[n] = float(e.double().norm()) / gn
+    rep = {"what": what, "mismatched_units": int(sum(diag["mismatch"].values())),
+           "max_mismatched_abs_pre": max(diag["mismatch_pre"].values(), default=0.0),
+           "near_zero_units": len(diag.get("units") or []),
+           "envelope_norm_ratio_max": max(ratios.values(), default=0.0),
+           "envelope_norm_ratio_top": dict(sorted(ratios.items(), key=lambda kv: -kv[1])[:3])}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "kink_report.jsonl"), "a") as f:
+        f.write(json.dumps(rep) + "\n")
+    assert rep["max_mismatched_abs_pre"] <= MISMATCH_PRE_MAX * pre_scale, (
+        f"{what}: a ReLU unit the HIP path switched differently from the oracle has |pre| "
+        f"{rep['max_mismatched_abs_pre']:.3e} -- not a rounding-level kink", rep)
+    return rep
+
+
+# |pre-activation| bound for a unit whose ReLU on/off choice may legitimately differ
+# between the HIP bf16 path and the bf16-emulated oracle: their forwards differ by
+# bf16 rounding of the conv operands and fp32 summation order (the answer-MLP
+# pre-activations agree to ~1e-4 absolute at these weights); a disagreement at a
+# unit further from zero than this would be a real forward error.
+MISMATCH_PRE_MAX = 2e-3

@@ -11,7 +11,7 @@ Reference: attention.py:110-126 (ConvLSTMCell.forward) over the unroll.
 import pytest
 import torch
 
-from helpers import assert_close, rel_err
+from helpers import assert_close, oracle_masks, rel_err
 from test_gpu_parity import _agent, _compare, _cot, _frames, _grads, _oracle, _run_unroll
 
 import attention
@@ -20,11 +20,13 @@ pytestmark = pytest.mark.gpu
 N = attention._pkg._native
 
 
-def _run(cuda, monkeypatch, band, T, B, nq=8):
+def _run(cuda, monkeypatch, band, T, B, nq=8, trace=None):
     monkeypatch.setenv("AAA_FRAMES_BAND", band)
     N.timing_enable(True)
     try:
-        out = _run_unroll(_agent(cuda, nq=nq, grid=(21, 21), conv_dtype="bf16"), T, B, cuda, H=168, W=168)
+        ag = _agent(cuda, nq=nq, grid=(21, 21), conv_dtype="bf16")
+        ag.relu_trace = trace
+        out = _run_unroll(ag, T, B, cuda, H=168, W=168)
         var = N.timing_stats(N.TIMER_FWD_STEP)["variant"]
         sb = N.timing_stats(N.TIMER_BPTT_STEP)
     finally:
@@ -53,8 +55,10 @@ def test_band_forward_vs_per_step(cuda, monkeypatch, T, B, nq):
 
 def test_band_forward_vs_emulated_oracle(cuda, monkeypatch):
     T, B = 3, 5
-    out = _run(cuda, monkeypatch, "1", T, B)
-    _compare(out, _oracle(T, B, nq=8, conv_mode="bf16", H=168, W=168), 2e-2, "band T=3 B=5: ")
+    trace = []
+    out = _run(cuda, monkeypatch, "1", T, B, trace=trace)
+    _compare(out, _oracle(T, B, nq=8, conv_mode="bf16", H=168, W=168, masks=oracle_masks(trace, B)), 2e-2,
+             "band T=3 B=5: ")
 
 
 def test_band_carried_state(cuda, monkeypatch):

@@ -30,7 +30,7 @@ EXPORTS = (
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
     "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag",
-    "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
+    "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_workspace_region", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
 )
 # include/aaa.h enum aaa_timer
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
@@ -50,6 +50,8 @@ IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_action"
 FLAG_STATEFUL_CORE = 1
 FLAG_FRAMES_U8 = 2
 FLAG_DEFER_STRANDED = 4
+# include/aaa.h enum aaa_ws_region
+WS_ANSWER_HIDDEN, WS_QUERY_HIDDEN0, WS_QUERY_HIDDEN1 = 0, 1, 2
 
 
 class TimerStats(ctypes.Structure):
@@ -130,6 +132,8 @@ def load(path: str = LIB_PATH):
             "aaa_adam_step_guarded": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, P, I, P, P, P, P, P, P, P]),
             "aaa_pair_flag": (I, [P, P]),
             "aaa_adam_step_counted": (I, [ctypes.POINTER(AdamHP), P, P, I, P, P, P, P, P, P, P]),
+            "aaa_workspace_region": (I, [ctypes.POINTER(Cfg), I, ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_size_t)]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),
             "aaa_sample_actions": (I, [I, I, P, ctypes.c_ulonglong, P, P, P, P, P]),
             "aaa_convlstm_packed_bytes": (S, [ctypes.POINTER(CellDesc)]),

@@ -310,6 +310,8 @@ class _UnrollFn(torch.autograd.Function):
         ws = runner.new_workspace()
         out = runner.forward(flat, packed, S, X, ws, pr, pa, h0, c0, want_attn=True, want_state=True,
                              core=(ch0, cc0) if runner.stateful_core else None)
+        if getattr(runner, "relu_trace", None) is not None:   # inspection hook (Agent.relu_trace)
+            runner.relu_trace.append(runner.relu_masks(ws))
         logits, values, attn, hT, cT = out[:5]
         chT, ccT = out[5:] if runner.stateful_core else (None, None)
         ctx.runner, ctx.flat, ctx.packed, ctx.ws, ctx.S, ctx.X = runner, flat, packed, ws, S, X
@@ -384,6 +386,11 @@ class Agent(nn.Module):
     # backward runs as multi-step BPTT calls (episode.py); False: one T=1
     # autograd node with its own saved workspace per call.
     fuse_episode_backward = True
+    # Inspection hook for checkers (None: off): a list that every forward call of
+    # this agent appends its ReLU masks to (UnrollRunner.relu_masks), in call
+    # order -- what the mask-matched oracle runs its backward through
+    # (tests/helpers.py oracle_masks).  Costs a host copy per call.
+    relu_trace = None
 
     # -- reference API --------------------------------------------------------
     def reset(self):
@@ -447,6 +454,7 @@ class Agent(nn.Module):
                                    f"call agent.to({X.device})")
         u8 = X.dtype == torch.uint8
         runner = self._runner(B, 1, H, W, X.device, False, u8)
+        runner.relu_trace = self.relu_trace
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
         flat, packed = self._packed_params(runner, params)
         key = runner._pack_cache[0]
@@ -493,6 +501,7 @@ class Agent(nn.Module):
         stateful = self.stateful_core or self.prev_hidden is not None
         u8 = X.dtype == torch.uint8      # the environment's observation: cast in-kernel (AAA_FLAG_FRAMES_U8)
         runner = self._runner(B, T, H, W, X.device, stateful, u8)
+        runner.relu_trace = self.relu_trace
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
         cell = self.vision.vision_lstm
         # prev_hidden holds the reference's (B, 128, w, h) tensors (attention.py:125); the

@@ -118,6 +118,24 @@ int aaa_timing_stats(int kind, aaa_timer_stats* out) {
   return rc;
 }
 
+int aaa_workspace_region(const aaa_cfg* cfg, int region, size_t* offset, size_t* bytes) {
+  if (!offset || !bytes) return fail(AAA_E_ARG, "workspace_region: NULL output");
+  Layout L;
+  if (int r = build_layout(cfg, L)) return r;
+  const size_t F = L.F;
+  switch (region) {
+    case AAA_WS_ANSWER_HIDDEN: *offset = L.hid1; *bytes = F * 512 * 4; return AAA_OK;
+    case AAA_WS_QUERY_HIDDEN0:
+      if (!L.sc) break;
+      *offset = L.q1s; *bytes = F * 128 * 4; return AAA_OK;
+    case AAA_WS_QUERY_HIDDEN1:
+      if (!L.sc) break;
+      *offset = L.q2s; *bytes = F * (size_t)L.qd * 4; return AAA_OK;
+    default: break;
+  }
+  return fail(AAA_E_ARG, "workspace_region: region %d not computed by this cfg", region);
+}
+
 int aaa_grid(int H, int W, int* h, int* w) {
   if (!h || !w) return fail(AAA_E_ARG, "NULL output");
   *h = conv_out(conv_out(H, 8, 4, 1), 4, 2, 2);

@@ -153,6 +153,8 @@ class Episode:
         r = self.runner
         logits, values, attn, hT, cT = r.forward(self.flat, self.packed, self.basis, X, self.ws, pr, pa, h, c,
                                                  want_attn=True, want_state=True)
+        if getattr(r, "relu_trace", None) is not None:   # inspection hook (Agent.relu_trace)
+            r.relu_trace.append(r.relu_masks(self.ws))
         self.cur = (hT, cT)
         if (t + 1) % self.seg == 0:
             self.ckpt[t + 1] = (hT, cT)
@@ -201,6 +203,7 @@ class Episode:
                 continue
             L = t1 - t0
             ru = self.agent._runner(B, L, r.H, r.W, self.device, False, r.frames_u8)
+            ru.relu_trace = None             # the re-run is not a forward call of the caller's
             assert ru.pk_bytes == r.pk_bytes   # packed layouts do not depend on B or T
             frames = torch.cat([self.steps[t][0] for t in range(t0, t1)]) if L > 1 else self.steps[t0][0]
             pr = _stack([self.steps[t][2] for t in range(t0, t1)], (1, B), self.device)

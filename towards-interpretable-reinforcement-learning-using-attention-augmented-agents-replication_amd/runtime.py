@@ -47,6 +47,27 @@ class UnrollRunner:
     def state_shape(self):
         return (self.B, self.h, self.w, 128)
 
+    def workspace_region(self, workspace, region: int):
+        """A forward product inside ``workspace`` (aaa_workspace_region): an
+        (T*B, n) fp32 view, e.g. N.WS_ANSWER_HIDDEN = relu(answer_processor.0)."""
+        off, nb = ctypes.c_size_t(), ctypes.c_size_t()
+        N.check(self.lib.aaa_workspace_region(ctypes.byref(self.cfg), int(region), ctypes.byref(off),
+                                              ctypes.byref(nb)), "workspace_region")
+        F = self.T * self.B
+        return workspace[off.value:off.value + nb.value].view(torch.float32).view(F, nb.value // (4 * F))
+
+    def relu_masks(self, workspace):
+        """The on/off pattern of every ReLU the hand-written backward masks with,
+        after a forward into ``workspace`` (host bool tensors, (T*B, n)):
+        "answer" = answer_processor.0 (attention.py:277-282) and, in the stateful
+        core, "q0" / "q1" = the query MLP's two (attention.py:184-198).  For
+        checkers: the mask-matched oracle (oracle/ref_cpu.py KinkProbe.masks)."""
+        out = {"answer": self.workspace_region(workspace, N.WS_ANSWER_HIDDEN) > 0}
+        if self.stateful_core:
+            out["q0"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN0) > 0
+            out["q1"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN1) > 0
+        return {k: v.cpu() for k, v in out.items()}
+
     # -- calls ------------------------------------------------------------
     def pack(self, flat_params, packed):
         assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
@@ -292,6 +313,27 @@ class ActorRunner:
 
     def state_shape(self):
         return (self.B, self.h, self.w, 128)
+
+    def workspace_region(self, workspace, region: int):
+        """A forward product inside ``workspace`` (aaa_workspace_region): an
+        (T*B, n) fp32 view, e.g. N.WS_ANSWER_HIDDEN = relu(answer_processor.0)."""
+        off, nb = ctypes.c_size_t(), ctypes.c_size_t()
+        N.check(self.lib.aaa_workspace_region(ctypes.byref(self.cfg), int(region), ctypes.byref(off),
+                                              ctypes.byref(nb)), "workspace_region")
+        F = self.T * self.B
+        return workspace[off.value:off.value + nb.value].view(torch.float32).view(F, nb.value // (4 * F))
+
+    def relu_masks(self, workspace):
+        """The on/off pattern of every ReLU the hand-written backward masks with,
+        after a forward into ``workspace`` (host bool tensors, (T*B, n)):
+        "answer" = answer_processor.0 (attention.py:277-282) and, in the stateful
+        core, "q0" / "q1" = the query MLP's two (attention.py:184-198).  For
+        checkers: the mask-matched oracle (oracle/ref_cpu.py KinkProbe.masks)."""
+        out = {"answer": self.workspace_region(workspace, N.WS_ANSWER_HIDDEN) > 0}
+        if self.stateful_core:
+            out["q0"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN0) > 0
+            out["q1"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN1) > 0
+        return {k: v.cpu() for k, v in out.items()}
 
     def pack(self, flat_params, packed):
         assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
