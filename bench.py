@@ -475,6 +475,13 @@ def main():
         "kernel_coverage": coverage,
         "hbm_kernels": attention_hbm(ka),
     }
+    # The data-parallel overlap budget: Learner.step issues the
+    # HEAD+CORE gradient all-reduce once the CORE phase is enqueued, and only the VISION
+    # phase's kernels remain to hide it; the VISION bucket's all-reduce is exposed.
+    vb = allk[N.TIMER_VISION_BWD]
+    o_core, n_par = learner.bounds[1][0], learner.runner.n_params
+    out["overlap_window_ms"] = round(vb["ms"], 4) if vb["launches"] else None
+    out["allreduce_buckets_bytes"] = {"HEAD+CORE (+guard)": 4 * (n_par + 1 - o_core), "VISION": 4 * o_core}
     if world > 1:   # RCCL gradient all-reduce of the last timed step, per bucket
         out["comm"] = {**learner.comm_stats(), "backend": dist.get_backend(),
                        "note": "allreduce_ms: RCCL time per bucket on the comm stream; exposed_ms: comm still "

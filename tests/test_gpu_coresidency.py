@@ -58,12 +58,16 @@ def _filler():
 
 class strand_next_launch:
     """Make the next multi-workgroup launch strand deterministically: a filler
-    holds half the CUs on a side stream for longer than the default partner-
-    wait budget (1 s + 20 ms per step, common.h pair_wait: 1.4 s at T = 20),
-    so the workgroups placed first give up on partners that cannot be placed
-    until the filler drains.  No test hook in libaaa.so is involved."""
+    holds 17 CUs of every XCD (136 workgroups, one per CU, dispatched round-robin
+    over the 8 XCDs) on a side stream for longer than the default partner-wait
+    budget (1 s + 20 ms per step, common.h pair_wait: 1.4 s at T = 20).  The
+    launch's workgroups of one frame share an XCD at consecutive local slots
+    (recur*.h block mapping), so with an odd 15 CUs free per XCD the last frame
+    placed on each XCD has a partner that cannot be placed until the filler
+    drains -- a timeout, whatever the pairing (2, 4 or 8 workgroups per frame).
+    No test hook in libaaa.so is involved."""
 
-    def __init__(self, cuda, cus=128, usec=1_900_000):
+    def __init__(self, cuda, cus=136, usec=1_900_000):
         self.cuda, self.cus, self.usec = cuda, cus, usec
 
     def __enter__(self):
@@ -211,6 +215,8 @@ def test_learner_stranded_step_leaves_params(cuda):
     lr.check_health()
     with strand_next_launch(cuda):
         lr.train_step(frames, dl, dv)  # must not raise
+    assert N.pair_status(clear=False) > 0, "no partner wait expired beside the filler (test premise)"
+    assert float(lr.guard.item()) > 0, "the guard slot missed the stranded launch"
     assert torch.equal(lr.flat, before), "a stranded step reached the parameters"
     assert lr.opt_steps == 0
     lr.train_step(frames, dl, dv)      # the report is still pending on the host: no raise, and a clean update
