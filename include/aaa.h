@@ -172,21 +172,26 @@ enum aaa_fwd_phase {
   AAA_FWD_ALL = 7
 };
 /* aaa_forward with a phase mask: AAA_FWD_ALL, or AAA_FWD_VISION |
- * AAA_FWD_TAIL (fp32 configs).  Replaces the recomputation half of the
+ * AAA_FWD_TAIL (configs whose slices are row-major: not the frame-resident
+ * bf16 BPTT's channel-quad-major ones).  Replaces the recomputation half of the
  * reference's per-step graph (main_mp.py:54 -> attention.py:110-126). */
 int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t stream);
 
 /* The ConvLSTM products of steps [t0, t0+n) between an aaa_forward workspace
- * and flat fp32 buffers: gates (n, B*h*w, 512) post-activation (i, f, c~, o
- * interleaved per channel), c (n, B*h*w, 128) = c_t, h (n, B*h*w, 128) = h_t
- * (pixel-major, channel fastest).  Export reads a workspace aaa_forward
+ * and flat buffers: gates (n, B*h*w, 512) post-activation (i, f, c~, o
+ * interleaved per channel), c (n, B*h*w, 128) = c_t fp32, h (n, B*h*w, 128) =
+ * h_t (pixel-major, channel fastest).  Element types (aaa_core_elem_bytes):
+ * fp32 configs all fp32; bf16 configs gates in the workspace's gate storage
+ * (fp16, or fp32 with AAA_GATES_F16=0) and h bf16 (the operand the next step
+ * and the weight gradient read).  Export reads a workspace aaa_forward
  * filled; import writes one for aaa_forward_phases without CORE (and the h
- * half of the [x | h] operand slots).  fp32 configs only; device pointers,
- * stream-ordered, no host sync. */
-int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, float* gates, float* c, float* h,
+ * half of the [x | h] operand slots).  Not for channel-quad-major slices
+ * (large-batch bf16: AAA_E_ARG); device pointers, stream-ordered, no host sync. */
+int aaa_core_elem_bytes(const aaa_cfg* cfg, int* gate_bytes, int* h_bytes);
+int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, void* gates, float* c, void* h,
                     hipStream_t stream);
-int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const float* gates, const float* c,
-                    const float* h, hipStream_t stream);
+int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const void* gates, const float* c,
+                    const void* h, hipStream_t stream);
 
 /* Backward of the loss sum(logits*dlogits)+sum(values*dvalues) (+ state
  * cotangents) through the saved activations of the matching aaa_forward.
@@ -368,6 +373,13 @@ typedef struct aaa_actor_io {
   int* actions;              /* (B) or NULL (no draw)                          */
   float* logp;               /* (B) or NULL                                    */
   float* dlogp_dlogits;      /* (B, A) or NULL                                 */
+  float* gates;              /* (B, h, w, 512) or NULL: the ConvLSTM step's gate
+                                activations (i, f, c~, o), row 4*ch + gate -- the
+                                products a fused episode backward imports
+                                (aaa_core_import) instead of re-running the step */
+  float* h_out;              /* (B, h, w, 128) or NULL: h_t written here instead of
+                                over ``h`` (which is then only read)         */
+  float* c_out;              /* (B, h, w, 128) or NULL: likewise c_t           */
 } aaa_actor_io;
 size_t aaa_actor_workspace_bytes(const aaa_cfg* cfg);
 int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t stream);

@@ -68,16 +68,26 @@ def _cmp(a, b, tol, what):
             assert rel_err(a[n].numpy(), b[n].numpy()) <= tol, f"{what} {n}: {rel_err(a[n].numpy(), b[n].numpy()):.3e}"
 
 
-@pytest.mark.parametrize("T,B,seg,u8,extras,store", [(9, 2, 4, True, False, "1"), (7, 3, 64, False, True, "1"),
-                                                    (70, 1, 64, True, True, "1"), (9, 2, 4, True, False, "0"),
-                                                    (37, 1, 64, True, False, "1")])
-def test_episode_matches_per_step_path(cuda, monkeypatch, T, B, seg, u8, extras, store):
+@pytest.mark.parametrize("T,B,seg,u8,extras,store,actor", [(9, 2, 4, True, False, "1", "0"),
+                                                          (7, 3, 64, False, True, "1", "0"),
+                                                          (70, 1, 64, True, True, "1", "0"),
+                                                          (9, 2, 4, True, False, "0", "0"),
+                                                          (37, 1, 64, True, False, "1", "0"),
+                                                          (9, 2, 4, True, False, "1", "1"),
+                                                          (7, 3, 64, False, True, "1", "1"),
+                                                          (70, 1, 64, True, True, "1", "1")])
+def test_episode_matches_per_step_path(cuda, monkeypatch, T, B, seg, u8, extras, store, actor):
     """Segments of 4 (3 segments, ragged last), one segment, and 70 steps over
     the default 64-step segment; uint8 and fp32 frames; prev_reward/action;
     the kept ConvLSTM products (16-step blocks, a ragged last block at 37) or
-    the recomputed recurrence (AAA_EPISODE_STORE=0)."""
+    the recomputed recurrence (AAA_EPISODE_STORE=0).  Recorded on the learner's
+    T=1 forward (AAA_EPISODE_ACTOR=0: the per-step path's own kernels, so the
+    logits are bit-identical and the gradients agree to 1e-5) or on the actor
+    chain (its own fp32 kernels: logits within 1e-5, gradients within the fp32
+    criterion 1e-4)."""
     monkeypatch.setattr(E, "EPISODE_SEGMENT", seg)
     monkeypatch.setenv("AAA_EPISODE_STORE", store)
+    monkeypatch.setenv("AAA_EPISODE_ACTOR", actor)
     X = _frames(T, B)
     Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
     Gv = torch.from_numpy(detinit.normal(3, (T, B, A)))
@@ -88,15 +98,22 @@ def test_episode_matches_per_step_path(cuda, monkeypatch, T, B, seg, u8, extras,
     ag = _agent(cuda, True)
     lf, gf = _episode(ag, X, Gl, Gv, cuda, pr, pa, u8)
     assert isinstance(ag._episode, E.Episode) and len(ag._episode.steps) == T
+    assert (ag._episode.actor is not None) == (actor == "1" and store == "1")
     ref = _agent(cuda, False)
     lr_, gr = _episode(ref, X, Gl, Gv, cuda, pr, pa, u8)
     assert ref._episode is None
-    assert torch.equal(lf, lr_)            # the forward is the per-step forward either way
-    _cmp(gf, gr, 1e-5, "fused vs per-step")
+    if actor == "0":
+        assert torch.equal(lf, lr_)            # the forward is the per-step forward
+        _cmp(gf, gr, 1e-5, "fused vs per-step")
+    else:
+        assert_close(lf.numpy(), lr_.numpy(), 1e-5, "actor-chain logits vs per-step")
+        _cmp(gf, gr, 1e-4, "fused (actor chain) vs per-step")
 
 
-def test_episode_matches_oracle(cuda, monkeypatch):
+@pytest.mark.parametrize("actor", ["1", "0"])
+def test_episode_matches_oracle(cuda, monkeypatch, actor):
     monkeypatch.setattr(E, "EPISODE_SEGMENT", 3)
+    monkeypatch.setenv("AAA_EPISODE_ACTOR", actor)
     T, B = 7, 2
     X = _frames(T, B)
     Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
@@ -162,7 +179,7 @@ def test_parameter_change_starts_new_episode(cuda, monkeypatch):
     gf, n_eps = run(True)
     gr, _ = run(False)
     assert n_eps == 2
-    _cmp(gf, gr, 1e-5, "parameter change")
+    _cmp(gf, gr, 1e-4, "parameter change")   # recorded on the actor chain: the fp32 criterion
 
 
 @pytest.mark.parametrize("store", ["1", "0"])
@@ -233,17 +250,38 @@ def test_core_import_replaces_the_recurrence(cuda, u8):
     torch.cuda.synchronize()
     assert torch.equal(l1, l2) and torch.equal(v1, v2)
     assert rel_err(g2.cpu().numpy(), g1.cpu().numpy()) < 1e-6
-    with pytest.raises(ValueError, match="contiguous fp32"):
+    with pytest.raises(ValueError, match="contiguous"):
         r.core_import(ws2, 0, 2, core[0][:1], core[1][:2], core[2][:2])
 
 
-def test_core_transfer_refuses_bf16_and_bad_ranges(cuda):
+def test_core_transfer_bf16_types_and_bad_ranges(cuda):
+    """bf16 runners move their own element types (fp16 gates, bf16 h: the
+    workspace's storage, aaa_core_elem_bytes); fp32 buffers are refused, as are
+    steps outside [0, T)."""
+    from aaa_amd import _native as N
+    T, B = 5, 2
     ag = _agent(cuda, False, dtype="bf16")
-    r = ag._runner(2, 3, 84, 84, cuda, False, True)
+    r = ag._runner(B, T, 84, 84, cuda, False, True)
+    assert r.core_dtypes() == (torch.float16, torch.float32, torch.bfloat16)
     ws = r.new_workspace()
-    core = [torch.empty(s, device=cuda) for s in r.core_shapes(3)]
-    with pytest.raises(RuntimeError, match="fp32 configs only"):
-        r.core_export(ws, 0, 3, *core)
+    with pytest.raises(ValueError, match="contiguous"):
+        r.core_export(ws, 0, 3, *[torch.empty(s, device=cuda) for s in r.core_shapes(3)])
+    # round trip: export a forward's products, import them into a fresh workspace, VISION | TAIL only
+    S = ag._basis_for(r.h, r.w, 84, 84, cuda)
+    flat, packed = ag._packed_params(r, list(ag.parameters()))
+    X = _frames(T, B).to(cuda)
+    dl = torch.from_numpy(detinit.normal(2, (T, B, A))).to(cuda)
+    l1, v1, _, _, _ = r.forward(flat, packed, S, X, ws, want_attn=False)
+    core = [torch.empty(s, dtype=dt, device=cuda) for s, dt in zip(r.core_shapes(T), r.core_dtypes())]
+    r.core_export(ws, 0, T, *core)
+    g1, _, _ = r.backward(flat, packed, S, X, ws, dl)
+    ws2 = r.new_workspace()
+    r.core_import(ws2, 0, T, *core)
+    l2, v2, _, _, _ = r.forward(flat, packed, S, X, ws2, want_attn=False, phases=N.FWD_VISION | N.FWD_TAIL)
+    g2, _, _ = r.backward(flat, packed, S, X, ws2, dl)
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(v1, v2)
+    assert rel_err(g2.cpu().numpy(), g1.cpu().numpy()) < 1e-5
     agf = _agent(cuda, False)
     rf = agf._runner(2, 3, 84, 84, cuda, False, True)
     core = [torch.empty(s, device=cuda) for s in rf.core_shapes(2)]
@@ -251,18 +289,102 @@ def test_core_transfer_refuses_bf16_and_bad_ranges(cuda):
         rf.core_export(rf.new_workspace(), 2, 2, *core)
 
 
-def test_bf16_episode_recomputes_and_matches_per_step_path(cuda, monkeypatch):
-    """bf16 agents keep no ConvLSTM products (the store is fp32-only): the
-    fused backward re-runs the recurrence and must still give the per-step
+@pytest.mark.parametrize("store", ["1", "0"])
+def test_bf16_episode_matches_per_step_path(cuda, monkeypatch, store):
+    """bf16 agents keep their ConvLSTM products too (fp16 gates, fp32 c, bf16
+    h), so the fused backward imports them instead of re-running the
+    recurrence (AAA_EPISODE_STORE=0: the re-run); either way the per-step
     path's gradients (same bf16 kernels and rounding points)."""
     monkeypatch.setattr(E, "EPISODE_SEGMENT", 4)
+    monkeypatch.setenv("AAA_EPISODE_STORE", store)
     T, B = 6, 2
     X = _frames(T, B)
     Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
     Gv = torch.from_numpy(detinit.normal(3, (T, B, A)))
     ag = _agent(cuda, True, dtype="bf16")
     lf, gf = _episode(ag, X, Gl, Gv, cuda)
-    assert ag._episode.store is None
+    assert (ag._episode.store is None) == (store == "0") and ag._episode.actor is None
+    if store == "1":
+        assert len(ag._episode.store) == 2     # two 4-step blocks (STORE_BLOCK capped by the segment)
     lr_, gr = _episode(_agent(cuda, False, dtype="bf16"), X, Gl, Gv, cuda)
     assert torch.equal(lf, lr_)
-    _cmp(gf, gr, 2e-2, "bf16 fused vs per-step")
+    _cmp(gf, gr, 2e-3, "bf16 fused vs per-step")
+
+
+@pytest.mark.parametrize("actor,store", [("1", "1"), ("0", "1"), ("0", "0")])
+def test_state_cotangent_at_intermediate_steps(cuda, monkeypatch, actor, store):
+    """The reference keeps a live (h, c) in ``prev_hidden`` after every step
+    (attention.py:125), so a loss may use any step's state: here the logits of
+    every step plus the ConvLSTM state after steps 2, 5 (a segment boundary),
+    8 and the last -- h and c with different weights.  The fused episode cuts
+    its segments after each such step and adds the cotangent to the carry; it
+    must match the per-step path (one autograd node per call)."""
+    monkeypatch.setattr(E, "EPISODE_SEGMENT", 6)
+    monkeypatch.setenv("AAA_EPISODE_ACTOR", actor)
+    monkeypatch.setenv("AAA_EPISODE_STORE", store)
+    T, B = 11, 2
+    X = _frames(T, B)
+    G = torch.from_numpy(detinit.normal(2, (T, B, A)))
+    taps = {2: 0.7, 5: -0.4, 8: 1.3, T - 1: 0.5}
+
+    def run(fuse):
+        ag = _agent(cuda, fuse)
+        ag.reset()
+        ag.zero_grad(set_to_none=True)
+        loss = 0
+        for t in range(T):
+            lg, _ = ag(X[t].to(cuda))
+            loss = loss + (lg * G[t].to(cuda)).sum()
+            if t in taps:
+                h, c = ag.vision.vision_lstm.prev_hidden
+                wh = torch.from_numpy(detinit.normal(10 + t, tuple(h.shape))).to(cuda)
+                loss = loss + taps[t] * (h * wh).sum() + 0.3 * (c * c).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return _grads(ag)
+    _cmp(run(True), run(False), 1e-5 if actor == "0" else 1e-4, "state cotangents mid-episode")
+
+
+def test_policy_mixed_act_and_forward(cuda, monkeypatch):
+    """One episode whose steps come from Policy.act (the draw fused into the step
+    node) and from plain agent(x) calls: the log-prob cotangents fold in where a
+    draw was recorded and nowhere else (no missing-Jacobian error)."""
+    from aaa_amd.policy import Policy
+    monkeypatch.setattr(E, "EPISODE_SEGMENT", 4)
+    T = 9
+    X = _frames(T, 1)
+    G = torch.from_numpy(detinit.normal(2, (T, 1, A)))
+
+    def run(fuse):
+        ag = _agent(cuda, fuse)
+        pol = Policy(ag, seed=3)
+        ag.reset()
+        ag.zero_grad(set_to_none=True)
+        loss = 0
+        for t in range(T):
+            if t % 3 == 1:
+                lg, _ = ag(X[t].to(cuda))
+                loss = loss + (lg * G[t].to(cuda)).sum()
+            else:
+                _, logp = pol.act(X[t, 0].to(cuda))
+                loss = loss - (t + 1) * 0.1 * logp.sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return _grads(ag)
+    _cmp(run(True), run(False), 1e-4, "mixed act/forward episode")
+
+
+def test_episode_store_budget(cuda, monkeypatch):
+    """AAA_EPISODE_STORE_MB caps the kept ConvLSTM products: past
+    the budget the steps are recomputed from checkpoints, with the same result."""
+    monkeypatch.setattr(E, "EPISODE_SEGMENT", 8)
+    monkeypatch.setenv("AAA_EPISODE_STORE_MB", "1")   # one 16-step block at B = 2, 84x84: 2 x 16 x 242 x 768 x 4 B = 23.8 MB > 1 MB
+    T, B = 20, 2
+    X = _frames(T, B)
+    Gl = torch.from_numpy(detinit.normal(2, (T, B, A)))
+    Gv = torch.from_numpy(detinit.normal(3, (T, B, A)))
+    ag = _agent(cuda, True)
+    _, gf = _episode(ag, X, Gl, Gv, cuda)
+    assert ag._episode.store == {} and ag._episode.store_bytes == 0
+    _, gr = _episode(_agent(cuda, False), X, Gl, Gv, cuda)
+    _cmp(gf, gr, 1e-4, "store past its budget")

@@ -30,7 +30,8 @@ EXPORTS = (
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
     "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag",
-    "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_workspace_region", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
+    "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_workspace_region",
+    "aaa_core_elem_bytes", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
 )
 # include/aaa.h enum aaa_timer
 TIMER_FWD_STEP, TIMER_BPTT_STEP, TIMER_CORE_WGRAD, TIMER_ATTN_FWD, TIMER_ATTN_BWD = 0, 1, 2, 3, 4
@@ -70,7 +71,8 @@ ACTOR_IO_FIELDS = ("params", "packed", "basis", "frames", "prev_reward", "prev_a
 class ActorIO(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ACTOR_IO_FIELDS] + [
         ("seed", ctypes.c_ulonglong), ("counter", ctypes.c_void_p), ("actions", ctypes.c_void_p),
-        ("logp", ctypes.c_void_p), ("dlogp_dlogits", ctypes.c_void_p)]
+        ("logp", ctypes.c_void_p), ("dlogp_dlogits", ctypes.c_void_p), ("gates", ctypes.c_void_p),
+        ("h_out", ctypes.c_void_p), ("c_out", ctypes.c_void_p)]
 
 
 class AdamHP(ctypes.Structure):
@@ -132,6 +134,7 @@ def load(path: str = LIB_PATH):
             "aaa_adam_step_guarded": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, P, I, P, P, P, P, P, P, P]),
             "aaa_pair_flag": (I, [P, P]),
             "aaa_adam_step_counted": (I, [ctypes.POINTER(AdamHP), P, P, I, P, P, P, P, P, P, P]),
+            "aaa_core_elem_bytes": (I, [ctypes.POINTER(Cfg), ctypes.POINTER(I), ctypes.POINTER(I)]),
             "aaa_workspace_region": (I, [ctypes.POINTER(Cfg), I, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]),
             "aaa_reinforce": (I, [I, I, I, P, P, P, ctypes.c_double, P, P, P, P]),

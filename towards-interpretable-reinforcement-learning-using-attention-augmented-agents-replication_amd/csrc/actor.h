@@ -25,9 +25,11 @@ struct ActorParams {
   const float *Wihp, *blc;   // LSTMCell [1024][256] rows 4u+g, b_ih + b_hh
   const float *Whd, *bhd;    // heads [ldy][256], bias
   // state (in place) and outputs
-  float *hst, *cst;          // (B, P, 128)
+  float *hst, *cst;          // (B, P, 128) state in (and out, in place, unless hout / cout)
+  float *hout, *cout;        // (B, P, 128) the step's h_t / c_t, or NULL (written into hst / cst)
   float *logits, *values;    // (B, A)
   float* attn;               // (B, P, nq) or NULL
+  float* gates;              // (B, P, 512) gate activations, row 4ch+g, or NULL
   // workspace
   float *X, *Hs, *hid1, *AO, *LH;
   // action draw (actions == NULL: none)

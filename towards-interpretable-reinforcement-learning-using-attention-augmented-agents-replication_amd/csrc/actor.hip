@@ -203,8 +203,9 @@ __global__ void __launch_bounds__(512) k_act_convlstm(ActorParams p, int npg) {
     const size_t si = ((size_t)f * p.P + pix) * 128 + ch;
     float gi, gf, gc, go, c, h;
     GateFwd::run(z[0] + b[0], z[1] + b[1], z[2] + b[2], z[3] + b[3], p.cst[si], gi, gf, gc, go, c, h);
-    p.cst[si] = c;
+    (p.cout ? p.cout : p.cst)[si] = c;
     p.Hs[si] = h;
+    if (p.gates) *reinterpret_cast<f32x4*>(p.gates + ((size_t)f * p.P + pix) * 512 + 4 * ch) = f32x4{gi, gf, gc, go};
   }
 }
 
@@ -245,7 +246,7 @@ __global__ void __launch_bounds__(256) k_act_attn(ActorParams p) {
   {   // this workgroup's slice of h_t -> the carried state (read by the next step's ConvLSTM kernel)
     const int n4 = P * 32, per = (n4 + gridDim.x - 1) / gridDim.x;
     const f32x4* src = reinterpret_cast<const f32x4*>(O);
-    f32x4* dst = reinterpret_cast<f32x4*>(p.hst + (size_t)f * P * 128);
+    f32x4* dst = reinterpret_cast<f32x4*>((p.hout ? p.hout : p.hst) + (size_t)f * P * 128);
     for (int i = blockIdx.x * per + tid; i < min(n4, (int)(blockIdx.x + 1) * per); i += 256) dst[i] = src[i];
   }
   __syncthreads();

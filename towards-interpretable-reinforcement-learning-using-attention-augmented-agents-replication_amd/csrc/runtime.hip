@@ -208,49 +208,70 @@ int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStre
   if (r) return r;
   if (phases != AAA_FWD_ALL && phases != (AAA_FWD_VISION | AAA_FWD_TAIL))
     return fail(AAA_E_ARG, "forward phases %d: AAA_FWD_ALL or AAA_FWD_VISION | AAA_FWD_TAIL", phases);
-  if (!(phases & AAA_FWD_CORE) && L.dt != AAA_F32) return fail(AAA_E_ARG, "skipping the core: fp32 configs only");
+  if (!(phases & AAA_FWD_CORE) && cqm_layout(L))
+    return fail(AAA_E_ARG, "skipping the core: not with channel-quad-major slices (the frame-resident BPTT's)");
   if ((r = check_device())) return r;
   if ((r = check_io(L, io, false))) return r;
   if (!(cfg->flags & AAA_FLAG_DEFER_STRANDED) && (r = pair_check())) return r;
   return L.dt == AAA_BF16 ? forward_impl<__bf16>(L, io, stream, phases) : forward_impl<float>(L, io, stream, phases);
 }
 
-// The recurrence's per-step products in the fp32 workspace (rt_core.hip
-// build_layout): Gt [T][M][512], Cst [T+1][M][128] (slot t+1 = c_t), Hs
-// [T][M][128] (= h_t), XH [T+1][M][192] (channels 64.. of slot t+1 = h_t).
+// The recurrence's per-step products in the workspace (rt_core.hip
+// build_layout): Gt [T][M][512] (fp32, or fp16 on the bf16 path's gate
+// storage), Cst [T+1][M][128] fp32 (slot t+1 = c_t), Hs [T][M][128] fp32 (= h_t;
+// fp32 path only), XH [T+1][M][192] (channels 64.. of slot t+1 = h_t, in the
+// operand type: the bf16 path's only copy of h_t).
 static int core_xfer_check(const aaa_cfg* cfg, Layout& L, const void* ws, int t0, int n) {
   int r = build_layout(cfg, L);
   if (r) return r;
-  if (L.dt != AAA_F32) return fail(AAA_E_ARG, "core export/import: fp32 configs only");
   if (cqm_layout(L)) return fail(AAA_E_ARG, "core export/import: channel-quad-major slices unsupported");
   if (!ws || t0 < 0 || n < 1 || t0 + n > L.T) return fail(AAA_E_ARG, "core export/import: steps [%d, %d) of T=%d", t0, t0 + n, L.T);
   return check_device();
 }
+static int core_gate_bytes(const Layout& L) { return L.dt == AAA_BF16 && gates_f16(L.dt, L.B * L.P) ? 2 : 4; }
 
-int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, float* gates, float* c, float* h,
+int aaa_core_elem_bytes(const aaa_cfg* cfg, int* gate_bytes, int* h_bytes) {
+  if (!gate_bytes || !h_bytes) return fail(AAA_E_ARG, "core_elem_bytes: NULL output");
+  Layout L;
+  if (int r = build_layout(cfg, L)) return r;
+  *gate_bytes = core_gate_bytes(L);
+  *h_bytes = L.esz;
+  return AAA_OK;
+}
+
+int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, void* gates, float* c, void* h,
                     hipStream_t st) {
   Layout L;
   if (int r = core_xfer_check(cfg, L, workspace, t0, n)) return r;
   const char* ws = (const char*)workspace;
-  const size_t M = (size_t)L.B * L.P;
-  if (gates) HIPCHK(hipMemcpyAsync(gates, ws + L.Gt + (size_t)t0 * M * 512 * 4, (size_t)n * M * 512 * 4, hipMemcpyDeviceToDevice, st));
+  const size_t M = (size_t)L.B * L.P, ge = core_gate_bytes(L);
+  if (gates) HIPCHK(hipMemcpyAsync(gates, ws + L.Gt + (size_t)t0 * M * 512 * ge, (size_t)n * M * 512 * ge, hipMemcpyDeviceToDevice, st));
   if (c) HIPCHK(hipMemcpyAsync(c, ws + L.Cst + (size_t)(t0 + 1) * M * 128 * 4, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
-  if (h) HIPCHK(hipMemcpyAsync(h, ws + L.Hs + (size_t)t0 * M * 128 * 4, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  if (h && L.esz == 4)
+    HIPCHK(hipMemcpyAsync(h, ws + L.Hs + (size_t)t0 * M * 128 * 4, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+  else if (h)   // bf16: the h half of XH slots t0+1 .. t0+n (n*M consecutive 192-channel rows)
+    HIPCHK(hipMemcpy2DAsync(h, 128 * 2, ws + L.XH + ((size_t)(t0 + 1) * M * 192 + 64) * 2, 192 * 2, 128 * 2, n * M,
+                            hipMemcpyDeviceToDevice, st));
   return AAA_OK;
 }
 
-int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const float* gates, const float* c,
-                    const float* h, hipStream_t st) {
+int aaa_core_import(const aaa_cfg* cfg, void* workspace, int t0, int n, const void* gates, const float* c,
+                    const void* h, hipStream_t st) {
   Layout L;
   if (int r = core_xfer_check(cfg, L, workspace, t0, n)) return r;
   if (!gates || !c || !h) return fail(AAA_E_ARG, "core import: gates, c and h are required");
   char* ws = (char*)workspace;
-  const size_t M = (size_t)L.B * L.P;
-  HIPCHK(hipMemcpyAsync(ws + L.Gt + (size_t)t0 * M * 512 * 4, gates, (size_t)n * M * 512 * 4, hipMemcpyDeviceToDevice, st));
+  const size_t M = (size_t)L.B * L.P, ge = core_gate_bytes(L);
+  HIPCHK(hipMemcpyAsync(ws + L.Gt + (size_t)t0 * M * 512 * ge, gates, (size_t)n * M * 512 * ge, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipMemcpyAsync(ws + L.Cst + (size_t)(t0 + 1) * M * 128 * 4, c, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipMemcpyAsync(ws + L.Hs + (size_t)t0 * M * 128 * 4, h, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
-  // slots t0+1 .. t0+n of XH are n*M consecutive 192-channel rows: one launch
-  HIPCHK(state_to_xh<float>((int)(n * M), h, (float*)(ws + L.XH) + (size_t)(t0 + 1) * M * 192, st));
+  if (L.esz == 4) {
+    HIPCHK(hipMemcpyAsync(ws + L.Hs + (size_t)t0 * M * 128 * 4, h, (size_t)n * M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    // slots t0+1 .. t0+n of XH are n*M consecutive 192-channel rows: one launch
+    HIPCHK(state_to_xh<float>((int)(n * M), (const float*)h, (float*)(ws + L.XH) + (size_t)(t0 + 1) * M * 192, st));
+  } else {
+    HIPCHK(hipMemcpy2DAsync(ws + L.XH + ((size_t)(t0 + 1) * M * 192 + 64) * 2, 192 * 2, h, 128 * 2, 128 * 2, n * M,
+                            hipMemcpyDeviceToDevice, st));
+  }
   return AAA_OK;
 }
 
@@ -427,6 +448,8 @@ int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t strea
   p.Wihp = (const float*)(pk + L.k_Wihp); p.blc = (const float*)(pk + L.k_blc);
   p.Whd = (const float*)(pk + L.k_Whd); p.bhd = (const float*)(pk + L.k_bhd);
   p.hst = io->h; p.cst = io->c; p.logits = io->logits; p.values = io->values; p.attn = io->attn;
+  p.gates = io->gates;
+  p.hout = io->h_out; p.cout = io->c_out;
   p.X = (float*)(ws + off[0]); p.Hs = (float*)(ws + off[1]); p.hid1 = (float*)(ws + off[2]);
   p.AO = (float*)(ws + off[3]); p.LH = (float*)(ws + off[4]);
   p.seed = io->seed; p.counter = io->counter; p.actions = io->actions; p.logp = io->logp; p.jac = io->dlogp_dlogits;

@@ -11,33 +11,43 @@ latency-bound (0.5 ms per step) and a 10,000-step episode (:151) would hold
 Here the per-step ``Agent.forward`` calls of one episode record into an
 ``Episode``:
 
-* each step runs the T=1 forward (its logits drive the action draw at once)
-  on one reused workspace, and keeps only what the BPTT needs to redo it:
-  the step's frames (a reference to the caller's tensor, version-checked),
-  prev_reward / prev_action, and the ConvLSTM state at every ``seg``-th step;
+* each step runs the agent step (its logits drive the action draw at once)
+  and keeps only what the BPTT needs to redo it: the step's frames (a
+  reference to the caller's tensor, version-checked), prev_reward /
+  prev_action, the ConvLSTM state at every ``seg``-th step, and -- the
+  episode *store* -- the step's ConvLSTM products (gate activations, c_t, h_t:
+  ``B*h*w*768*4`` bytes, 1.66 MB at 210x160, up to a byte budget);
+* fp32 agents with the reference's zero-state policy core and B <= 16 record
+  on the actor chain (aaa_actor_step: six launches sized for small B, its
+  ConvLSTM step writing the gate activations straight into the store, the
+  action drawn in the same call); other agents on the learner's T=1 forward
+  (aaa_forward), whose products are exported into the store
+  (aaa_core_export; fp32 runners);
 * every step's autograd node takes the episode's *anchor* -- a scalar output
   of one node whose inputs are the 34 parameters and the episode's initial
   ConvLSTM state -- so autograd runs the anchor's backward only after every
   step node reached by the loss has delivered its cotangents;
-* the step nodes only stash (dlogits, dvalues) (and a state cotangent on the
-  last step, when a later call continued from it); the anchor's backward then
-  re-runs the episode as multi-step unrolls of ``seg`` steps from the
-  checkpointed states and back-propagates each with one hand-written BPTT
-  call (``aaa_forward`` / ``aaa_backward``, T = seg), last segment first,
-  carrying dh/dc between segments, and returns the summed parameter grads
-  (and the initial state's grads) in one go.
+* the step nodes only stash (dlogits, dvalues), a log-prob cotangent, and a
+  cotangent of the step's output state (h_t, c_t: the ``prev_hidden`` the
+  reference keeps live after every step, attention.py:125); the anchor's
+  backward then re-runs the episode as multi-step unrolls -- segments of at
+  most ``seg`` steps, additionally cut after every step whose state received a
+  cotangent -- from checkpointed or stored states, back-propagates each with one
+  hand-written BPTT call (T = its length), last segment first, carrying dh/dc
+  between segments and adding each cut's state cotangent to the carry, and
+  returns the summed parameter grads (and the initial state's grads) in one go.
+  Where the store holds a segment's products the re-run imports them
+  (aaa_core_import) and runs only the batched vision encoder and tail
+  (aaa_forward_phases without CORE); elsewhere it recomputes the recurrence.
 
 The result is the gradient of the same loss through the same op sequence
-(the recomputed forward runs the same kernels as the per-step one at this
-batch, up to summation order).  The memory kept per step is the frames plus
-``2 * B*h*w*128*4 / seg`` bytes of state.
+(the re-run uses the recorded products, or the same kernels as the per-step
+forward at this batch, up to summation order).
 
-fp32 agents also keep each step's ConvLSTM products (gate activations, c_t,
-h_t: ``B*h*w*768*4`` bytes, 1.66 MB at 210x160) exported from the per-step
-workspace (``aaa_core_export``); the segment's re-run then imports them and
-skips the recurrence (``aaa_forward_phases`` without CORE) -- the 64
-sequential step launches that dominated the recomputation -- and runs only
-the batched vision encoder and tail.  AAA_EPISODE_STORE=0 recomputes instead.
+Memory: the frames, ``2 * B*h*w*128*4 / seg`` bytes of checkpointed state per
+step, and the store: ``B*h*w*768*4`` bytes per step up to AAA_EPISODE_STORE_MB
+(default 4096 MB: 2,470 steps at 210x160, B = 1), past which the steps are
+recomputed.  AAA_EPISODE_STORE=0 keeps no store (and records on aaa_forward).
 """
 from __future__ import annotations
 
@@ -103,11 +113,9 @@ class _EpisodeActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, ep, t, anchor, sampler):
-        from .policy import _sample_raw
         ctx.set_materialize_grads(False)
         ctx.ep, ctx.t = ep, t
-        logits, values, attn, hT, cT = ep.forward_step(t)
-        action, logp, jac = _sample_raw(logits[0], sampler.seed, sampler.counter)
+        logits, values, attn, hT, cT, action, logp, jac = ep.forward_step(t, sampler)
         ep.jac[t] = jac
         ctx.mark_non_differentiable(attn, action)
         return logits, values, attn, hT, cT, action, logp
@@ -126,31 +134,102 @@ class Episode:
         self.agent, self.runner, self.flat, self.packed, self.key, self.basis = agent, runner, flat, packed, key, basis
         self.device = runner.device
         self.seg = max(1, int(EPISODE_SEGMENT if seg is None else seg))
-        self.ws = runner.new_workspace()          # per-step scratch, reused: nothing of it is kept
         self.steps = []                            # (frames (1,B,H,W,3), version, pr, pa)
         h = None if h0 is None else h0.detach().contiguous()
         c = None if c0 is None else c0.detach().contiguous()
-        self.ckpt = {0: (h, c)}                    # segment start -> ConvLSTM state entering it
+        self.ckpt = {0: (h, c)}                    # step -> ConvLSTM state entering it (segment starts)
         self.cur = (h, c)
         self.cot, self.ext = {}, {}
         self.cotp, self.jac = {}, {}               # log-prob cotangents / draw Jacobians (_EpisodeActFn)
-        # step block t // STORE_BLOCK -> (gates, c, h) of its steps (fp32: aaa_core_export), or None (recompute)
-        self.store = {} if (runner.cfg.dtype == N.F32 and os.environ.get("AAA_EPISODE_STORE", "1") != "0") else None
+        # step block t // STORE_BLOCK -> (gates, c, h) of its steps, up to the byte budget; bf16 runners
+        # keep their own element types (fp16 gates, bf16 h), not the channel-quad-major slices of
+        # the large-batch frame-resident BPTT (no episode runs at such batches)
+        store_on = os.environ.get("AAA_EPISODE_STORE", "1") != "0"
+        self.store = {} if store_on else None
+        self.store_budget = int(float(os.environ.get("AAA_EPISODE_STORE_MB", "4096")) * 2**20)
+        self.store_bytes = 0
         self.blk = max(1, min(self.seg, STORE_BLOCK))
-        while self.seg % self.blk:   # blocks never straddle a segment
-            self.blk -= 1
         self.state_ref = None                      # the prev_hidden tuple this episode last set
         self.anchor = None
+        # the recording step: the actor chain (aaa_actor_step) where it applies, else aaa_forward T=1
+        self.actor = None
+        if store_on and runner.cfg.dtype == N.F32 and runner.B <= 16 and os.environ.get("AAA_EPISODE_ACTOR", "1") != "0":
+            from .policy import _actor_chain_fits
+            if _actor_chain_fits(runner.B, runner.H, runner.W, runner.nq, runner.A):
+                from .runtime import ActorRunner
+                cache = agent.__dict__.setdefault("_episode_actors", {})   # one per geometry, kept across episodes
+                key = (runner.B, runner.H, runner.W, str(self.device), runner.frames_u8)
+                if key not in cache:
+                    ar = ActorRunner(runner.B, runner.H, runner.W, runner.nq, runner.A, self.device,
+                                     frames_u8=runner.frames_u8)
+                    cache[key] = (ar, ar.new_workspace())
+                self.actor, self.ws = cache[key]
+        if self.actor is not None and h is None:   # the actor chain reads a state tensor: zeros
+            shp = runner.state_shape()
+            self.hbuf, self.cbuf = torch.zeros(shp, device=self.device), torch.zeros(shp, device=self.device)
+        else:
+            self.ws = runner.new_workspace()      # per-step scratch, reused: nothing of it is kept
 
     # -- forward --------------------------------------------------------------
     def record(self, X, pr, pa):
         self.steps.append((X, X._version, pr, pa))
         return len(self.steps) - 1
 
-    def forward_step(self, t):
+    def _slot(self, t):
+        """(gates, c, h) store rows of step t ((1, M, 512), (1, M, 128) x 2), or None past the budget."""
+        if self.store is None:
+            return None
+        k, i = divmod(t, self.blk)
+        if k not in self.store:
+            shapes, dts = self.runner.core_shapes(self.blk), self.runner.core_dtypes()
+            nbytes = sum(a * b * c * torch.empty((), dtype=dt).element_size() for (a, b, c), dt in zip(shapes, dts))
+            if self.store_bytes + nbytes > self.store_budget:
+                return None
+            self.store[k] = tuple(torch.empty(s, dtype=dt, device=self.device) for s, dt in zip(shapes, dts))
+            self.store_bytes += nbytes
+        g, c, h = self.store[k]
+        return g[i:i + 1], c[i:i + 1], h[i:i + 1]
+
+    def forward_step(self, t, sampler=None):
+        """Run step t: (logits, values, attn, hT, cT) -- plus (action, logp, jac)
+        with a ``sampler`` (the draw of Policy.act)."""
         X, _, pr, pa = self.steps[t]
-        h, c = self.cur
         r = self.runner
+        slot = self._slot(t)
+        if self.actor is not None:
+            B, A = r.B, r.A
+            logits = torch.empty(1, B, A, device=self.device)
+            values = torch.empty(1, B, A, device=self.device)
+            attn = torch.empty(1, B, r.h, r.w, r.nq, device=self.device)
+            draw = ()
+            if sampler is not None:
+                draw = (torch.empty(B, dtype=torch.int32, device=self.device),
+                        torch.empty(B, device=self.device), torch.empty(B, A, device=self.device))
+            shp = r.state_shape()
+            h, c = self.cur
+            if h is None:   # zero state entering the episode
+                h, c = self.hbuf, self.cbuf
+            if slot is not None:   # h_t, c_t straight into the store rows (written by the kernels, so no
+                # in-place op on the store's blocks: these views are handed out as prev_hidden)
+                hT, cT = slot[2].view(shp), slot[1].view(shp)
+            else:
+                hT, cT = torch.empty(shp, device=self.device), torch.empty(shp, device=self.device)
+            self.actor.step(self.flat, self.packed, self.basis, X[0], self.ws, h, c, logits[0],
+                            values[0], attn[0], None if pr is None else pr.reshape(-1),
+                            None if pa is None else pa.reshape(-1),
+                            seed=sampler.seed if sampler is not None else 0,
+                            counter=sampler.counter if sampler is not None else None,
+                            actions=draw[0] if draw else None, logp=draw[1] if draw else None,
+                            dlogp=draw[2] if draw else None, gates=slot[0] if slot is not None else None,
+                            h_out=hT, c_out=cT)
+            if getattr(r, "relu_trace", None) is not None:
+                raise RuntimeError("Agent.relu_trace: the actor-chain recording keeps no learner workspace; "
+                                   "set AAA_EPISODE_ACTOR=0 to trace an episode")
+            self.cur = (hT, cT)
+            if (t + 1) % self.seg == 0:
+                self.ckpt[t + 1] = (hT, cT)
+            return (logits, values, attn, hT, cT) + draw
+        h, c = self.cur
         logits, values, attn, hT, cT = r.forward(self.flat, self.packed, self.basis, X, self.ws, pr, pa, h, c,
                                                  want_attn=True, want_state=True)
         if getattr(r, "relu_trace", None) is not None:   # inspection hook (Agent.relu_trace)
@@ -158,12 +237,11 @@ class Episode:
         self.cur = (hT, cT)
         if (t + 1) % self.seg == 0:
             self.ckpt[t + 1] = (hT, cT)
-        if self.store is not None:
-            k, i = divmod(t, self.blk)
-            if k not in self.store:
-                self.store[k] = tuple(torch.empty(s, device=self.device) for s in r.core_shapes(self.blk))
-            g, c, h = self.store[k]
-            r.core_export(self.ws, 0, 1, g[i:i + 1], c[i:i + 1], h[i:i + 1])
+        if slot is not None:
+            r.core_export(self.ws, 0, 1, *slot)
+        if sampler is not None:
+            from .policy import _sample_raw
+            return (logits, values, attn, hT, cT) + _sample_raw(logits[0], sampler.seed, sampler.counter)
         return logits, values, attn, hT, cT
 
     # -- backward -------------------------------------------------------------
@@ -177,6 +255,32 @@ class Episode:
             ph, pc = self.ext.get(t, (None, None))
             self.ext[t] = (_add(ph, dh), _add(pc, dc))
 
+    def _stored(self, t0, t1):
+        """Whether the store holds every step of [t0, t1)."""
+        return self.store is not None and all((t // self.blk) in self.store for t in range(t0, t1))
+
+    def _state_entering(self, b):
+        """(h, c) entering step b: a checkpoint, the store's h_{b-1} / c_{b-1}, or a
+        forward re-run of the steps since the last checkpoint before b."""
+        if b in self.ckpt:
+            return self.ckpt[b]
+        r = self.runner
+        shp = r.state_shape()
+        if self._stored(b - 1, b):
+            g, c, h = self.store[(b - 1) // self.blk]
+            i = (b - 1) % self.blk
+            return h[i].view(shp).float(), c[i].view(shp)
+        a = max(k for k in self.ckpt if k < b)
+        h0, c0 = self.ckpt[a]
+        ru = self.agent._runner(r.B, b - a, r.H, r.W, self.device, False, r.frames_u8)
+        ru.relu_trace = None
+        frames = torch.cat([self.steps[t][0] for t in range(a, b)])
+        pr = _stack([self.steps[t][2] for t in range(a, b)], (1, r.B), self.device)
+        pa = _stack([self.steps[t][3] for t in range(a, b)], (1, r.B), self.device)
+        _, _, _, hT, cT = ru.forward(self.flat, self.packed, self.basis, frames, ru.new_workspace(), pr, pa, h0, c0,
+                                     want_attn=False, want_state=True)
+        return hT, cT
+
     def backward_all(self, want_state: bool):
         """Every recorded step's cotangents -> (flat param grads, dh0, dc0)."""
         n = len(self.steps)
@@ -185,19 +289,18 @@ class Episode:
             if X._version != ver:
                 raise RuntimeError(f"aaa: the frames of episode step {t} were modified in place after the forward; "
                                    f"the fused episode backward needs them unchanged (as autograd would)")
-        bad = [t for t in self.ext if t != n - 1]
-        if bad:
-            raise NotImplementedError(f"aaa: a gradient reached the ConvLSTM state of episode step {bad[0]} (not the "
-                                      f"last); the fused episode backward takes state cotangents on the last step "
-                                      f"only -- set agent.fuse_episode_backward = False for this pattern")
         total = torch.zeros(r.n_params, device=self.device)
-        dh, dc = self.ext.get(n - 1, (None, None))
-        starts = list(range(0, n, self.seg))
+        # segments: every seg-th step, and a cut after each step whose output state has a cotangent
+        cuts = sorted(set(range(0, n, self.seg)) | {t + 1 for t in self.ext if t + 1 < n})
+        bounds = list(zip(cuts, cuts[1:] + [n]))
         A, B = r.A, r.B
-        for k, t0 in reversed(list(enumerate(starts))):
-            t1 = min(n, t0 + self.seg)
+        dh = dc = None
+        for t0, t1 in reversed(bounds):
+            if (t1 - 1) in self.ext:   # the cotangent of the state leaving this segment joins the carry
+                eh, ec = self.ext[t1 - 1]
+                dh, dc = _add(dh, eh), _add(dc, ec)
             live = any(t in self.cot or t in self.cotp for t in range(t0, t1)) or dh is not None or dc is not None
-            need_state = k > 0 or want_state
+            need_state = t0 > 0 or want_state
             if not live:                  # no cotangent reaches this segment or anything before it through it
                 dh = dc = None
                 continue
@@ -211,16 +314,20 @@ class Episode:
             dl = _stack([self.cot.get(t, (None, None))[0] for t in range(t0, t1)], (1, B, A), self.device, zero=True)
             dv = _stack([self.cot.get(t, (None, None))[1] for t in range(t0, t1)], (1, B, A), self.device, zero=True)
             if any(t in self.cotp for t in range(t0, t1)):   # dlogits += jac * dlogp, all steps at once
-                J = torch.stack([self.jac[t] for t in range(t0, t1)])
+                zj = torch.zeros(B, A, device=self.device)   # steps recorded by plain forward calls: no draw
+                J = torch.stack([self.jac.get(t, zj) for t in range(t0, t1)])
                 G = _stack([self.cotp.get(t) for t in range(t0, t1)], (1, B), self.device, zero=True)
                 dl = torch.addcmul(dl, J, G.unsqueeze(-1))
-            h0, c0 = self.ckpt[t0]
+            h0, c0 = self._state_entering(t0)
             ws = ru.new_workspace()
-            if self.store is not None:   # the recorded products: no recurrence re-run
-                for b0 in range(t0, t1, self.blk):
-                    nb = min(self.blk, t1 - b0)
-                    sg, sc, sh = self.store[b0 // self.blk]
-                    ru.core_import(ws, b0 - t0, nb, sg[:nb], sc[:nb], sh[:nb])
+            if self._stored(t0, t1):   # the recorded products: no recurrence re-run
+                t = t0
+                while t < t1:
+                    k, i = divmod(t, self.blk)
+                    nb = min(self.blk - i, t1 - t)
+                    sg, sc, sh = self.store[k]
+                    ru.core_import(ws, t - t0, nb, sg[i:i + nb], sc[i:i + nb], sh[i:i + nb])
+                    t += nb
                 ru.forward(self.flat, self.packed, self.basis, frames, ws, pr, pa, h0, c0, want_attn=False,
                            phases=N.FWD_VISION | N.FWD_TAIL)
             else:

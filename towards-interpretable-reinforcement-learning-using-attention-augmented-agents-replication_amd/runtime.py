@@ -119,17 +119,28 @@ class UnrollRunner:
         M = self.B * self.h * self.w
         return (n, M, 512), (n, M, 128), (n, M, 128)
 
+    def core_dtypes(self):
+        """Element types of (gates, c, h) in core_export / core_import: fp32 runners
+        all fp32; bf16 runners the workspace's gate storage (fp16) and bf16 h."""
+        if not hasattr(self, "_core_dt"):
+            ge, he = ctypes.c_int(), ctypes.c_int()
+            N.check(self.lib.aaa_core_elem_bytes(ctypes.byref(self.cfg), ctypes.byref(ge), ctypes.byref(he)),
+                    "core_elem_bytes")
+            self._core_dt = (torch.float16 if ge.value == 2 else torch.float32, torch.float32,
+                             torch.bfloat16 if he.value == 2 else torch.float32)
+        return self._core_dt
+
     def core_export(self, workspace, t0, n, gates, c, h):
-        """Steps [t0, t0+n) of the recurrence's products (fp32 runners) -> gates, c, h (core_shapes)."""
-        for x, shp in zip((gates, c, h), self.core_shapes(n)):
-            _check_out(x, shp)
+        """Steps [t0, t0+n) of the recurrence's products -> gates, c, h (core_shapes, core_dtypes)."""
+        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self.core_dtypes()):
+            _check_out(x, shp, dt)
         N.check(self.lib.aaa_core_export(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
                                          N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_export")
 
     def core_import(self, workspace, t0, n, gates, c, h):
         """The inverse of core_export, into a workspace for forward(phases=FWD_VISION | FWD_TAIL)."""
-        for x, shp in zip((gates, c, h), self.core_shapes(n)):
-            _check_out(x, shp)
+        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self.core_dtypes()):
+            _check_out(x, shp, dt)
         N.check(self.lib.aaa_core_import(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
                                          N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_import")
 
@@ -169,10 +180,10 @@ class UnrollRunner:
             raise RuntimeError("frames must be on the GPU")
 
 
-def _check_out(t, shape):
-    if (t is None or tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or not t.is_contiguous()
+def _check_out(t, shape, dtype=torch.float32):
+    if (t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or not t.is_contiguous()
             or t.device.type != "cuda"):
-        raise ValueError(f"expected a contiguous fp32 device tensor {tuple(shape)}, got "
+        raise ValueError(f"expected a contiguous {dtype} device tensor {tuple(shape)}, got "
                          f"{None if t is None else (tuple(t.shape), t.dtype, t.device)}")
 
 
@@ -314,27 +325,6 @@ class ActorRunner:
     def state_shape(self):
         return (self.B, self.h, self.w, 128)
 
-    def workspace_region(self, workspace, region: int):
-        """A forward product inside ``workspace`` (aaa_workspace_region): an
-        (T*B, n) fp32 view, e.g. N.WS_ANSWER_HIDDEN = relu(answer_processor.0)."""
-        off, nb = ctypes.c_size_t(), ctypes.c_size_t()
-        N.check(self.lib.aaa_workspace_region(ctypes.byref(self.cfg), int(region), ctypes.byref(off),
-                                              ctypes.byref(nb)), "workspace_region")
-        F = self.T * self.B
-        return workspace[off.value:off.value + nb.value].view(torch.float32).view(F, nb.value // (4 * F))
-
-    def relu_masks(self, workspace):
-        """The on/off pattern of every ReLU the hand-written backward masks with,
-        after a forward into ``workspace`` (host bool tensors, (T*B, n)):
-        "answer" = answer_processor.0 (attention.py:277-282) and, in the stateful
-        core, "q0" / "q1" = the query MLP's two (attention.py:184-198).  For
-        checkers: the mask-matched oracle (oracle/ref_cpu.py KinkProbe.masks)."""
-        out = {"answer": self.workspace_region(workspace, N.WS_ANSWER_HIDDEN) > 0}
-        if self.stateful_core:
-            out["q0"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN0) > 0
-            out["q1"] = self.workspace_region(workspace, N.WS_QUERY_HIDDEN1) > 0
-        return {k: v.cpu() for k, v in out.items()}
-
     def pack(self, flat_params, packed):
         assert flat_params.dtype == torch.float32 and flat_params.is_contiguous()
         assert flat_params.numel() == self.n_params, (flat_params.numel(), self.n_params)
@@ -343,7 +333,7 @@ class ActorRunner:
 
     def step(self, flat_params, packed, basis, frames, workspace, h, c, logits, values, attn=None,
              prev_reward=None, prev_action=None, seed: int = 0, counter=None, actions=None, logp=None,
-             dlogp=None):
+             dlogp=None, gates=None, h_out=None, c_out=None):
         """frames (B, H, W, 3) uint8 (or fp32 without frames_u8); h, c updated in
         place; logits/values (B, A), attn (B, h, w, nq) or None; actions (B,)
         int32 (None: no draw) with logp (B,) / dlogp (B, A) and the device draw
@@ -360,7 +350,7 @@ class ActorRunner:
         for k, v in dict(params=flat_params, packed=packed, basis=basis, frames=frames, prev_reward=prev_reward,
                          prev_action=prev_action, h=h, c=c, logits=logits, values=values, attn=attn,
                          workspace=workspace, counter=counter, actions=actions, logp=logp,
-                         dlogp_dlogits=dlogp).items():
+                         dlogp_dlogits=dlogp, gates=gates, h_out=h_out, c_out=c_out).items():
             setattr(io, k, None if v is None else v.data_ptr())
         io.seed = int(seed) & (2**64 - 1)
         N.check(self.lib.aaa_actor_step(ctypes.byref(self.cfg), ctypes.byref(io), N.stream_ptr(self.device)),
