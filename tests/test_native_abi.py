@@ -117,11 +117,11 @@ def test_reinforce_loss_has_no_cpu_fallback():
         reinforce_loss(torch.zeros(3, 1, 18), [0, 1, 2], [1.0, 0.0, 1.0])
 
 
-def test_actor_layout_refuses_readout_lds_overflow():
-    """The actor chain's readout kernel keeps a frame's P x nq logits in LDS
-    (csrc/actor.h actor_attn_lds): a grid whose readout exceeds the LDS is
-    refused by the layout query (GraphActor then takes the learner's T=1
-    forward) instead of failing at launch."""
+def test_actor_layout_refuses_readout_overflow():
+    """The actor chain's readout merges at most kActMaxChunks position chunks
+    per frame (csrc/actor.h; P <= 2048): a larger grid is refused by the layout
+    query (GraphActor then takes the learner's T=1 forward) instead of failing
+    at launch."""
     lib = N.load()
     small = N.Cfg(1, 1, 210, 160, 8, 18, N.F32, N.FLAG_FRAMES_U8)
     big = N.Cfg(1, 1, 506, 506, 8, 18, N.F32, N.FLAG_FRAMES_U8)   # 64x64 grid: 4096 x 8 logits

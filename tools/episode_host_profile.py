@@ -31,12 +31,70 @@ if __name__ == "__main__":
         for t in range(T_ep):
             policy(obs[t])
 
+    def episode_async():   # Policy.act: the same steps without the per-step .item() host sync
+        agent.reset()
+        agent.zero_grad(set_to_none=True)
+        policy.saved_log_probs = []
+        for t in range(T_ep):
+            policy.act(obs[t])
+
     episode()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     episode()
     torch.cuda.synchronize()
     print(f"ms per step (no profiler): {(time.perf_counter() - t0) / T_ep * 1e3:.3f}")
+    t0 = time.perf_counter()
+    episode_async()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"ms per step without the .item() sync: host enqueue {(t1 - t0) / T_ep * 1e3:.3f}, "
+          f"to device done {(t2 - t0) / T_ep * 1e3:.3f}")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    episode_async()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"device ms per step (events around the async episode): {e0.elapsed_time(e1) / T_ep:.3f}")
+    # one step at a time from an idle device: host time of Policy.act (returns after its launches)
+    # and the device time left after it returns
+    agent.reset()
+    policy.saved_log_probs = []
+    hs, ds = [], []
+    for t in range(T_ep):
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        act, _ = policy.act(obs[t])
+        a1 = time.perf_counter()
+        int(act.item())
+        a2 = time.perf_counter()
+        hs.append(a1 - a0)
+        ds.append(a2 - a1)
+    hs.sort(), ds.sort()
+    print(f"isolated step: Policy.act host median {hs[T_ep // 2] * 1e3:.3f} ms, then .item() wait median "
+          f"{ds[T_ep // 2] * 1e3:.3f} ms")
+    if "--backward" in sys.argv:   # the bench's whole episode: forward steps + finish_episode loss + backward
+        import numpy as np
+        rewards = (detinit.frames_u8(4322, (T_ep,)) % 3).astype(np.float32).tolist()
+        for _ in range(3):
+            episode()
+            R, returns = 0.0, []
+            for r in rewards[::-1]:
+                R = r + 0.99 * R
+                returns.insert(0, R)
+            returns = torch.tensor(returns, device=dev)
+            returns = (returns - returns.mean()) / (returns.std() + 1e-7)
+            loss = torch.cat([-lp * Rt for lp, Rt in zip(policy.saved_log_probs, returns)]).sum()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e0.record()
+            loss.backward()
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"backward: host {(time.perf_counter() - t0) * 1e3:.3f} ms, device {e0.elapsed_time(e1):.3f} ms")
+        sys.exit(0)
     pr = cProfile.Profile()
     pr.enable()
     episode()

@@ -41,6 +41,20 @@ __all__ = ["ConvLSTMCell", "VisionNetwork", "QueryNetwork", "SpatialBasis", "spa
            "apply_alpha", "Agent"]
 
 
+# Generation of the process's module structure: bumped whenever any module
+# registers a parameter or a submodule (torch's global registration hooks), so
+# a cached parameter list is re-made after such a change (Agent._param_list).
+_STRUCT_GEN = [0]
+
+
+def _bump_struct(*_):
+    _STRUCT_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_struct)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_struct)
+
+
 def _no_cpu(t, what):
     if not t.is_cuda:
         raise RuntimeError(f"aaa: {what} runs only on the MI355X HIP path; move it and its inputs to a ROCm GPU "
@@ -403,8 +417,9 @@ class Agent(nn.Module):
         """One step (attention.py:298-368): X (B, H, W, 3) -> logits, values (B, A)."""
         pr = None if prev_reward is None else prev_reward.reshape(1, -1)
         pa = None if prev_action is None else prev_action.reshape(1, -1)
-        if self._episode_eligible(X):
-            logits, values, attn = self._episode_step(X, pr, pa)
+        params = self._episode_params(X)
+        if params is not None:
+            logits, values, attn = self._episode_step(X, pr, pa, params)
         else:
             logits, values, attn = self._step(X.unsqueeze(0), pr, pa)
         self.last_attention = attn[0]
@@ -416,9 +431,10 @@ class Agent(nn.Module):
         """Policy.act's step (forward + action draw, policy.py) as one node of the
         open episode when the fused episode backward applies: (action, log_prob),
         else None (the caller then runs forward() and samples itself)."""
-        if not self._episode_eligible(X):
+        params = self._episode_params(X)
+        if params is None:
             return None
-        logits, values, attn, action, logp = self._episode_step(X, None, None, sampler)
+        logits, values, attn, action, logp = self._episode_step(X, None, None, params, sampler)
         self.last_attention = attn[0]
         return action, logp
 
@@ -434,12 +450,40 @@ class Agent(nn.Module):
         return logits, values, attn
 
     # -- internals ----------------------------------------------------------
-    def _episode_eligible(self, X):
-        return (self.fuse_episode_backward and torch.is_grad_enabled() and X.is_cuda and X.dim() == 4
-                and not (self.stateful_core or self.prev_hidden is not None)
-                and any(p.requires_grad for p in self.parameters()))
+    def _param_list(self):
+        """``list(self.parameters())`` without walking the module tree per call
+        (~60 us of Python per walk; an actor pays it every step).  The list is
+        re-made after any parameter or submodule registration (_STRUCT_GEN)
+        and whenever a module's parameter or child count changed (deletions
+        register nothing); in-place changes keep the same Parameter objects."""
+        c = self.__dict__.get("_plist")
+        if c is not None and c[0] == _STRUCT_GEN[0]:
+            n = 0
+            for m in c[1]:
+                n += len(m._parameters) + len(m._modules)
+            if n == c[2]:
+                return c[3]
+        mods = list(self.modules())
+        n = sum(len(m._parameters) + len(m._modules) for m in mods)
+        ps = list(self.parameters())
+        self.__dict__["_plist"] = (_STRUCT_GEN[0], mods, n, ps)
+        return ps
 
-    def _episode_step(self, X, pr, pa, sampler=None):
+    def _check_devices(self, params, device):
+        for p in params:
+            if p.device != device:
+                raise RuntimeError(f"agent parameters are on {p.device} but frames are on {device}; "
+                                   f"call agent.to({device})")
+
+    def _episode_params(self, X):
+        """The parameter list when this per-step call records into an episode, else None."""
+        if not (self.fuse_episode_backward and X.is_cuda and X.dim() == 4 and torch.is_grad_enabled()
+                and not (self.stateful_core or self.prev_hidden is not None)):
+            return None
+        params = self._param_list()
+        return params if any(p.requires_grad for p in params) else None
+
+    def _episode_step(self, X, pr, pa, params, sampler=None):
         """One per-step call recorded into the open episode (episode.py): a new
         episode after reset(), a parameter change, another geometry, or a
         prev_hidden the episode did not set itself."""
@@ -447,16 +491,11 @@ class Agent(nn.Module):
         B, H, W, C = X.shape
         if C != 3:
             raise ValueError(f"frames must be (..., H, W, 3), got {tuple(X.shape)}")
-        params = list(self.parameters())
-        for p in params:
-            if p.device != X.device:
-                raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
-                                   f"call agent.to({X.device})")
         u8 = X.dtype == torch.uint8
         runner = self._runner(B, 1, H, W, X.device, False, u8)
         runner.relu_trace = self.relu_trace
         S = self._basis_for(runner.h, runner.w, H, W, X.device)
-        flat, packed = self._packed_params(runner, params)
+        flat, packed = self._packed_params(runner, params, self)
         key = runner._pack_cache[0]
         cell = self.vision.vision_lstm
         ep = self._episode
@@ -493,11 +532,7 @@ class Agent(nn.Module):
         T, B, H, W, C = X.shape
         if C != 3:
             raise ValueError(f"frames must be (..., H, W, 3), got {tuple(X.shape)}")
-        params = list(self.parameters())
-        for p in params:
-            if p.device != X.device:
-                raise RuntimeError(f"agent parameters are on {p.device} but frames are on {X.device}; "
-                                   f"call agent.to({X.device})")
+        params = self._param_list()
         stateful = self.stateful_core or self.prev_hidden is not None
         u8 = X.dtype == torch.uint8      # the environment's observation: cast in-kernel (AAA_FLAG_FRAMES_U8)
         runner = self._runner(B, T, H, W, X.device, stateful, u8)
@@ -522,7 +557,7 @@ class Agent(nn.Module):
                 if v is not None and tuple(v.shape) != (B, self.hidden_size):
                     raise RuntimeError(f"{name} has shape {tuple(v.shape)}, expected {(B, self.hidden_size)}")
         Xf = X.contiguous() if u8 else X.float().contiguous()
-        flat, packed = self._packed_params(runner, params)
+        flat, packed = self._packed_params(runner, params, self)
         logits, values, attn, hT, cT, chT, ccT = _UnrollFn.apply(runner, flat, packed, S, Xf, pr, pa, h0, c0,
                                                                  ch0, cc0, *params)
         cell.prev_hidden = (hT.permute(0, 3, 2, 1), cT.permute(0, 3, 2, 1))
@@ -533,16 +568,20 @@ class Agent(nn.Module):
         return logits, values, attn
 
     @staticmethod
-    def _packed_params(runner, params):
+    def _packed_params(runner, params, agent=None):
         """Flat fp32 params + their packed operand layout, re-made only when a
         parameter changed (its storage or in-place version counter: optimizer
         steps, load_state_dict, .to()).  An actor stepping one frame at a time
         (main_mp.py:100, test_model.py:44) then pays no per-step re-pack.  The
-        cached tensors are never written again, so graphs that saved them stay valid."""
+        cached tensors are never written again, so graphs that saved them stay valid.
+        A re-pack first checks that every parameter is on the runner's device (a
+        cache hit means the same storages, so the same devices, as that check)."""
         key = tuple((p.data_ptr(), p._version) for p in params)
         cached = getattr(runner, "_pack_cache", None)
         if cached is not None and cached[0] == key:
             return cached[1], cached[2]
+        if agent is not None:
+            agent._check_devices(params, runner.device)
         with torch.no_grad():
             flat = torch.cat([p.detach().reshape(-1) for p in params])
             packed = runner.new_packed()

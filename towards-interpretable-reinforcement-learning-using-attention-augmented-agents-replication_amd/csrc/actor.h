@@ -32,6 +32,12 @@ struct ActorParams {
   float* gates;              // (B, P, 512) gate activations, row 4ch+g, or NULL
   // workspace
   float *X, *Hs, *hid1, *AO, *LH;
+  float* Zp;                 // ConvLSTM split-K partial tiles (B, 8 * npt, kActLstmKS, 4096)
+  int* zcnt;                 // (B, 8 * npt) arrival counters of those tiles, (B) of the readout
+                             // chunks, 1 of the LSTMCell; all zeroed by the vision launch
+  float* Lg;                 // (B, P, nq) attention logits (for the map)
+  float* Apart;              // (B, nch, nq, kAttnPart) readout partials of position chunks
+  float* arow;               // (B, ans_ld) answer_processor input row
   // action draw (actions == NULL: none)
   unsigned long long seed;
   unsigned long long* counter;
@@ -42,11 +48,19 @@ struct ActorParams {
 
 hipError_t actor_launch(const ActorParams& p, hipStream_t st);
 
-// Dynamic LDS of the attention-readout launch (k_act_attn): the logits of all P
-// positions x nq queries, the queries, the readout's partial sums, the answer
-// row.  Above 64 KB the launch raises the kernel's limit; above kActLdsMax the
-// chain does not apply (actor_layout refuses it: such grids use aaa_forward).
-constexpr size_t kActLdsMax = 160 * 1024;
+// Attention readout geometry: kAttnChunk positions per workgroup, each
+// chunk's (query) partial = 184 readout sums + its max + its sum (+2 pad); at
+// most kActMaxChunks chunks per frame (the combining workgroup's LDS), so the
+// chain applies to P <= kAttnChunk * kActMaxChunks (larger grids: aaa_forward).
+constexpr int kAttnChunk = 16;
+constexpr int kAttnPart = 188;
+constexpr int kActMaxChunks = 128;
+__host__ __device__ inline int actor_chunks(int P) { return (P + kAttnChunk - 1) / kAttnChunk; }
+
+// ConvLSTM launch geometry: 64 gate rows x 64 pixels per tile, 8 row tiles
+// (one per XCD), ceil(P / 64) pixel tiles, K (1728) cut into kActLstmKS slices.
+constexpr int kActLstmKS = 6;
+__host__ __device__ inline int actor_pix_tiles(int P) { return (P + 63) / 64; }
 size_t actor_attn_lds(int P, int nq, int ans_ld);
 
 }  // namespace aaa

@@ -7,11 +7,13 @@
 // The learner's kernels are whole-batch GEMMs; at B = 1 they run as ~25
 // latency-bound launches (188-226 us graph-replayed, profiles/r01).  Here each
 // stage is split across the chip by its OUTPUT (conv2 pixels, ConvLSTM
-// channel x pixel tiles, answer rows, LSTMCell units), so every stage is a
-// few microseconds, and the chain is six launches.  Six launches and not one
-// persistent kernel: a seam inside one launch costs a grid barrier (~4-5 us,
-// MI355X_MICROARCH.md 'barrier-xcd'), a kernel boundary ~1.2-1.5 us
-// ('boundary'); the answer MLP / LSTMCell / heads seams are all-to-all.
+// tile x K-slice, readout position chunks, answer rows, LSTMCell units), and
+// the chain is six launches.  Launches and not one persistent kernel: a
+// seam inside one launch costs a grid barrier (~4-5 us, MI355X_MICROARCH.md
+// 'barrier-xcd'), a kernel boundary ~1.2-1.5 us ('boundary'); the answer MLP /
+// LSTMCell / heads seams are all-to-all.  The two reductions that are not
+// (the ConvLSTM's K slices, the readout's position chunks) finish inside
+// their launch: the last workgroup to arrive at a counter merges the partials.
 //
 // Numerics: fp32 throughout (the ConvLSTM and conv1 on exact-fp32
 // v_mfma_f32_16x16x4_f32, the rest fp32 FMA); only the summation order
@@ -20,6 +22,7 @@
 // aaa_sample_actions on the same logits, seed and counter.
 #include "actor.h"
 #include "epilogues.h"
+#include "loaders_b.h"
 #include "sampling.h"
 
 namespace aaa {
@@ -65,6 +68,12 @@ __global__ void __launch_bounds__(256) k_act_vision(ActorParams p) {
   __shared__ float red2[4][16][65];
   const int pix = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int oy = pix / p.w, ox = pix - oy * p.w;
+  if (pix == 0) {   // this step's ConvLSTM tile, readout and LSTMCell counters, before those launches
+    const int nt = 8 * actor_pix_tiles(p.P);
+    for (int i = tid; i < nt; i += 256) p.zcnt[f * nt + i] = 0;
+    if (tid == 0) p.zcnt[p.B * nt + f] = 0;
+    if (tid == 0 && f == 0) p.zcnt[p.B * nt + p.B] = 0;   // the LSTMCell's (one launch-wide counter)
+  }
   // conv2 weights of this wave's 16 channels, lane's 8 K values: issued first
   f32x4 w2a[16], w2b[16];
 #pragma unroll
@@ -143,200 +152,301 @@ __global__ void __launch_bounds__(256) k_act_vision(ActorParams p) {
 
 // ---------------------------------------------------------- ConvLSTM ------
 // ConvLSTMCell step (attention.py:110-126, zero peepholes) as an implicit
-// GEMM D[512 gate rows][P pixels] = W[.][1728] * [x | h_{t-1}] (3x3 taps),
-// cut into 16-row x 16-pixel tiles (4 channels x 4 gates, gate-interleaved
-// rows) so that B = 1 still spreads over 32 x ceil(P/16) workgroups (256 at
-// 84x84).  Eight waves split K (108 blocks of 16; each lane prefetches its
-// weight and input float4 of every block before the first MFMA), the
-// partials meet in LDS, and wave 0 holds, per lane, the four gates of one
-// (channel, pixel): the cell update runs there (c in place; h to Hs, which
-// the attention kernel copies into the state after reading it).
-// blockIdx -> tile is XCD-aware: the ceil(P/16) pixel tiles of a channel group
-// share an XCD (blockIdx % 8), so its 110 KB weight slab is read into one L2.
-constexpr int kLstmWaves = 8;
-constexpr int kLstmBlocks = 1728 / 16;                                         // 108
-constexpr int kLstmPer = (kLstmBlocks + kLstmWaves - 1) / kLstmWaves;          // 14
+// GEMM D[512 gate rows][P pixels] = W[.][1728] * [x | h_{t-1}] (3x3 taps) on
+// exact-fp32 MFMA.  The chain's floor is the fp32 MFMA rate (1.27 GFLOP at
+// 210x160 = 8 us chip-wide), so the tiling keeps the operand traffic far
+// below what the chip can feed: 64 rows (16 channels x 4 gates,
+// gate-interleaved) x 64 pixels per tile, each operand element read once per
+// tile, and K cut into kActLstmKS slices so that B = 1 still fills the chip
+// (8 x 9 tiles x 6 slices = 432 workgroups at 210x160).  Per K block of 16,
+// half the workgroup stages the weight rows and half the pixels' im2col
+// values (one float4 each, all of the slice's loads issued before the first
+// MFMA) into a double-buffered LDS tile; each wave then runs a 16-row x
+// 32-pixel block (one A read, two B reads, eight MFMAs).  The slices write
+// their partial tiles to the workspace and the last to arrive (a per-tile
+// counter the vision launch zeroed) sums them in slice order -- the same
+// result whichever slice is last -- and runs the cell update.
+// blockIdx -> tile is XCD-aware: row tile = blockIdx % 8, so an XCD's L2
+// holds one 442 KB weight slab, and a tile's slices share that L2.
+constexpr int kSC1 = 16;                      // buffer cache policy: sc1 (cross-workgroup hand-off)
+constexpr int kLsPitch = 20;                  // floats per LDS row: 80 B puts 16 rows on disjoint banks
+constexpr int kLsSteps = 108 / kActLstmKS;    // K blocks of 16 per slice
 
-__global__ void __launch_bounds__(512) k_act_convlstm(ActorParams p, int npg) {
-  __shared__ __attribute__((aligned(16))) float red[kLstmWaves][64][4];
+__global__ void __launch_bounds__(512) k_act_convlstm(ActorParams p, int npt) {
+  __shared__ __attribute__((aligned(16))) float Wt[2][64 * kLsPitch];
+  __shared__ __attribute__((aligned(16))) float Bt[2][64 * kLsPitch];
+  __shared__ int is_last;
   const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int bid = blockIdx.x, xcd = bid & 7, slot = bid >> 3;
-  const int chg = xcd * 4 + slot / npg, pxg = slot - (slot / npg) * npg;
-  const int r = lane & 15, q = lane >> 4;
-  const int pix = pxg * 16 + r;
-  const bool pin = pix < p.P;
-  const int pc = pin ? pix : 0, y = pc / p.w, x = pc - y * p.w;
-  const float* wrow = p.WpXH + (size_t)(chg * 16 + r) * 1728 + 4 * q;
-  const float* Xf = p.X + (size_t)f * p.P * 64;
-  const float* Hf = p.hst + (size_t)f * p.P * 128;
-  f32x4 wk[kLstmPer], xk[kLstmPer];
-  bool ok[kLstmPer];
-#pragma unroll
-  for (int i = 0; i < kLstmPer; ++i) {
-    const int kb = wv + kLstmWaves * i;
-    const int kbc = kb < kLstmBlocks ? kb : kLstmBlocks - 1;
-    const int tap = kbc / 12, c0 = (kbc - tap * 12) * 16 + 4 * q;
-    const int ky = tap / 3, kx = tap - ky * 3, ny = y + ky - 1, nx = x + kx - 1;
-    ok[i] = pin && kb < kLstmBlocks && ny >= 0 && ny < p.h && nx >= 0 && nx < p.w;
-    const int np = ok[i] ? ny * p.w + nx : 0;
-    xk[i] = c0 < 64 ? ld4(Xf + (size_t)np * 64 + c0) : ld4(Hf + (size_t)np * 128 + (c0 - 64));
-    wk[i] = ld4(wrow + kbc * 16);
-  }
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int rt = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int pt = slot / kActLstmKS, ks = slot - pt * kActLstmKS;
+  const int tile = f * 8 * npt + pt * 8 + rt;
+  // loader role: threads 0..255 the weight rows, 256..511 the pixels; 4 threads per row
+  const bool isw = tid < 256;
+  const int lr = (tid & 255) >> 2, qd = tid & 3;
   const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  f32x4 g[kLsSteps];
+  if (isw) {
+    const float* src = p.WpXH + (size_t)(rt * 64 + lr) * 1728 + ks * kLsSteps * 16 + 4 * qd;
 #pragma unroll
-  for (int i = 0; i < kLstmPer; ++i) {
-    const f32x4 xv = ok[i] ? xk[i] : zero;   // padding taps, the ragged last pixel tile, K past 1728
-    acc0 = mfma4(wk[i][0], xv[0], acc0);
-    acc1 = mfma4(wk[i][1], xv[1], acc1);
-    acc0 = mfma4(wk[i][2], xv[2], acc0);
-    acc1 = mfma4(wk[i][3], xv[3], acc1);
+    for (int i = 0; i < kLsSteps; ++i) g[i] = ld4(src + 16 * i);
+  } else {
+    const int pix = pt * 64 + lr;
+    const bool pin = pix < p.P;
+    const int pc = pin ? pix : 0, y = pc / p.w, x = pc - y * p.w;
+    const float* Xf = p.X + (size_t)f * p.P * 64;
+    const float* Hf = p.hst + (size_t)f * p.P * 128;
+#pragma unroll
+    for (int i = 0; i < kLsSteps; ++i) {
+      const int kb = ks * kLsSteps + i, tap = kb / 12, c0 = (kb - tap * 12) * 16 + 4 * qd;
+      const int ky = tap / 3, kx = tap - ky * 3, ny = y + ky - 1, nx = x + kx - 1;
+      const bool ok = pin && ny >= 0 && ny < p.h && nx >= 0 && nx < p.w;
+      const int np = ok ? ny * p.w + nx : 0;
+      const f32x4 v = c0 < 64 ? ld4(Xf + (size_t)np * 64 + c0) : ld4(Hf + (size_t)np * 128 + (c0 - 64));
+      g[i] = ok ? v : zero;   // padding taps and the ragged last pixel tile
+    }
   }
-  *reinterpret_cast<f32x4*>(red[wv][lane]) = acc0 + acc1;
-  __syncthreads();
-  if (wv == 0 && pin) {
-    f32x4 z = *reinterpret_cast<const f32x4*>(red[0][lane]);
+  const int st = lr * kLsPitch + 4 * qd;
+  const int rb = wv >> 1, pb = (wv & 1) * 2, i16 = lane & 15, kq = lane >> 4;
+  const int ra = (rb * 16 + i16) * kLsPitch + 4 * kq, rb0 = (pb * 16 + i16) * kLsPitch + 4 * kq;
+  f32x4 acc0 = zero, acc1 = zero;
 #pragma unroll
-    for (int k = 1; k < kLstmWaves; ++k) z += *reinterpret_cast<const f32x4*>(red[k][lane]);
-    const int ch = chg * 4 + q;
-    const f32x4 b = ld4(p.bl + 4 * ch);
+  for (int s = 0; s < kLsSteps; ++s) {
+    *reinterpret_cast<f32x4*>((isw ? Wt[s & 1] : Bt[s & 1]) + st) = g[s];
+    __syncthreads();   // double buffer: the buffer written here was last read before the previous barrier
+    const f32x4 a = *reinterpret_cast<const f32x4*>(Wt[s & 1] + ra);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(Bt[s & 1] + rb0);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(Bt[s & 1] + rb0 + 16 * kLsPitch);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      acc0 = mfma4(a[v], b0[v], acc0);
+      acc1 = mfma4(a[v], b1[v], acc1);
+    }
+  }
+  // partial tile (lane-native layout: 8 waves x 2 blocks x 64 lanes x 4) -> workspace.  Hand-off
+  // without fences (an agent release writes back the whole L2): write-through (sc1) stores, every
+  // wave's vmcnt(0), a barrier, one lane's agent-scope add; the last slice takes one agent acquire
+  // (the partials are rewritten every step) and reads them with sc1 loads (glds.h EpiSliceFix)
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.Zp + (size_t)tile * kActLstmKS * 4096, kActLstmKS * 4096 * 4);
+  const uint32_t po = (uint32_t)((wv * 512 + 4 * lane) * 4);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc0), rs, po + ks * 16384, 0, kSC1);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc1), rs, po + ks * 16384 + 1024, 0, kSC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.zcnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == kActLstmKS - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    is_last = old == kActLstmKS - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  f32x4 z[2] = {zero, zero};
+#pragma unroll
+  for (int k = 0; k < kActLstmKS; ++k) {
+    z[0] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, po + k * 16384, 0, kSC1));
+    z[1] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, po + k * 16384 + 1024, 0, kSC1));
+  }
+  const int ch = rt * 16 + rb * 4 + kq;
+  const f32x4 bias = ld4(p.bl + 4 * ch);
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int pix = pt * 64 + (pb + e) * 16 + i16;
+    if (pix >= p.P) continue;
     const size_t si = ((size_t)f * p.P + pix) * 128 + ch;
     float gi, gf, gc, go, c, h;
-    GateFwd::run(z[0] + b[0], z[1] + b[1], z[2] + b[2], z[3] + b[3], p.cst[si], gi, gf, gc, go, c, h);
+    GateFwd::run(z[e][0] + bias[0], z[e][1] + bias[1], z[e][2] + bias[2], z[e][3] + bias[3], p.cst[si], gi, gf,
+                 gc, go, c, h);
     (p.cout ? p.cout : p.cst)[si] = c;
     p.Hs[si] = h;
     if (p.gates) *reinterpret_cast<f32x4*>(p.gates + ((size_t)f * p.P + pix) * 512 + 4 * ch) = f32x4{gi, gf, gc, go};
   }
 }
 
-// ------------------------------------------- attention + answer layer 0 ---
-// Every workgroup of a frame recomputes the frame's attention readout
-// (attention.py:319-348 with the constant query, Q1: logits K.Q with
-// K = [O[:8] | S], softmax over the P positions, readout of V = [O[8:] | S],
-// answer row [a | Q | r | a_prev]) -- 93 KB of L2 reads and ~0.1 MFLOP, cheaper
-// than a seam -- then computes 512 / gridDim.x rows of answer_processor.0 +
-// ReLU (attention.py:277-282, 350) from it, one wave per row.  Workgroup 0
-// also writes the attention map; each workgroup copies its slice of h_t into
-// the carried state.
-constexpr int kActAttnSlices = 5;   // 46 column groups x 5 position slices = 230 readout threads
-
+// ----------------------------------------------------- attention readout --
+// attention.py:319-348 with the constant query (Q1): logits K.Q with
+// K = [O[:8] | S], spatial_softmax over the P positions (attention.py:235-241),
+// readout of V = [O[8:] | S] (apply_alpha, :244-254).  One workgroup per chunk
+// of kAttnChunk positions (34 at 210x160) reads only its positions' O and S
+// rows: it stores its logits (for the map), its per-query max m_c and sum
+// s_c of exp(l - m_c), and the partial readout sum_j exp(l_j - m_c) V_j.  The
+// last chunk to arrive (the ConvLSTM's sc1 hand-off) merges them in chunk
+// order -- weights exp(m_c - m) / sum_c exp(m_c - m) s_c, the same result
+// whichever chunk is last -- into the answer row [a | Q | r | a_prev | 0-pad]
+// and writes the attention map.  Each chunk also copies its share of h_t
+// into the carried state (read by the next step's ConvLSTM launch).
 template <int NQ>
-__global__ void __launch_bounds__(256) k_act_attn(ActorParams p) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int P = p.P;
-  float* L = sm;                                   // P*NQ
-  float* Qs = L + P * NQ;                          // NQ*72
-  float* red = Qs + NQ * 72;                       // SL*NQ*184
-  float* ans = red + kActAttnSlices * NQ * 184;    // ans_ld
-  const int f = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+__global__ void __launch_bounds__(256) k_act_attn(ActorParams p, int nch) {
+  __shared__ float Qs[NQ * 72];
+  __shared__ float E[kAttnChunk][NQ];
+  __shared__ float Wc[kActMaxChunks][NQ];
+  __shared__ float Mq[NQ], Tq[NQ];
+  __shared__ int is_last;
+  const int P = p.P, f = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* O = p.Hs + (size_t)f * P * 128;
   const float* S = p.basis;
-  // this wave's row of answer_processor.0 (gridDim.x * 4 = 512 rows), requested first: its
-  // loads run under the attention readout instead of after it
-  constexpr int NIT = (NQ * 256 + 2 + 7) / 8 * 8 / 256 + 1;   // float4 slices per lane over ans_ld
-  const int row = blockIdx.x * 4 + wv;
-  f32x4 w1r[NIT];
-#pragma unroll
-  for (int i = 0; i < NIT; ++i) {
-    const int k = min(4 * lane + 256 * i, p.ans_ld - 4);
-    w1r[i] = ld4(p.W1p + (size_t)row * p.ans_ld + k);
-  }
-  const float a0 = p.a0b[row];
+  const int p0 = c * kAttnChunk, np = min(kAttnChunk, P - p0);
   for (int i = tid; i < NQ * 72; i += 256) Qs[i] = p.Q[i];
-  {   // this workgroup's slice of h_t -> the carried state (read by the next step's ConvLSTM kernel)
-    const int n4 = P * 32, per = (n4 + gridDim.x - 1) / gridDim.x;
+  {   // this chunk's share of h_t -> the carried state
+    const int n4 = P * 32, per = (n4 + nch - 1) / nch;
     const f32x4* src = reinterpret_cast<const f32x4*>(O);
     f32x4* dst = reinterpret_cast<f32x4*>((p.hout ? p.hout : p.hst) + (size_t)f * P * 128);
-    for (int i = blockIdx.x * per + tid; i < min(n4, (int)(blockIdx.x + 1) * per); i += 256) dst[i] = src[i];
+    for (int i = c * per + tid; i < min(n4, (c + 1) * per); i += 256) dst[i] = src[i];
   }
   __syncthreads();
-  for (int pp = tid; pp < P; pp += 256) {
-    const f32x4 k0 = ld4(O + pp * 128), k1 = ld4(O + pp * 128 + 4);
-    float acc[NQ];
+  const __amdgpu_buffer_rsrc_t rl = make_rsrc(p.Lg + (size_t)f * P * NQ, (uint32_t)(P * NQ * 4));
+  if (tid < kAttnChunk * NQ) {   // logits: one thread per (position, query)
+    const int j = tid / NQ, q = tid - j * NQ;
+    float l = -INFINITY;
+    if (j < np) {
+      const int pp = p0 + j;
+      const float* Qq = Qs + q * 72;
+      f32x4 kv[18];
+      kv[0] = ld4(O + (size_t)pp * 128);
+      kv[1] = ld4(O + (size_t)pp * 128 + 4);
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) {
-      const float* Qq = Qs + qq * 72;
-      acc[qq] = k0[0] * Qq[0] + k0[1] * Qq[1] + k0[2] * Qq[2] + k0[3] * Qq[3] + k1[0] * Qq[4] + k1[1] * Qq[5] +
-                k1[2] * Qq[6] + k1[3] * Qq[7];
+      for (int k = 0; k < 16; ++k) kv[2 + k] = ld4(S + (size_t)pp * 64 + 4 * k);
+      __builtin_amdgcn_sched_barrier(0);   // all 18 loads in flight before the sums
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 18; ++k)
+        acc += kv[k][0] * Qq[4 * k] + kv[k][1] * Qq[4 * k + 1] + kv[k][2] * Qq[4 * k + 2] + kv[k][3] * Qq[4 * k + 3];
+      l = acc;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, l), rl, (uint32_t)((pp * NQ + q) * 4), 0,
+                                            kSC1);
     }
-#pragma unroll 4
-    for (int c = 0; c < 16; ++c) {
-      const f32x4 v = ld4(S + pp * 64 + 4 * c);
-#pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) {
-        const float* Qq = Qs + qq * 72 + 8 + 4 * c;
-        acc[qq] += v[0] * Qq[0] + v[1] * Qq[1] + v[2] * Qq[2] + v[3] * Qq[3];
-      }
-    }
-#pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) L[pp * NQ + qq] = acc[qq];
+    E[j][q] = l;
   }
   __syncthreads();
-  for (int qq = wv; qq < NQ; qq += 4) {   // spatial_softmax over the P positions (attention.py:235-241)
-    float m = -INFINITY;
-    for (int pp = lane; pp < P; pp += 64) m = fmaxf(m, L[pp * NQ + qq]);
-    m = wmax(m);
-    float s = 0.f;
-    for (int pp = lane; pp < P; pp += 64) {
-      const float e = expf(L[pp * NQ + qq] - m);
-      L[pp * NQ + qq] = e;
-      s += e;
-    }
-    const float inv = 1.f / wsum(s);
-    for (int pp = lane; pp < P; pp += 64) {
-      const float a = L[pp * NQ + qq] * inv;
-      L[pp * NQ + qq] = a;
-      if (blockIdx.x == 0 && p.attn) p.attn[((size_t)f * P + pp) * NQ + qq] = a;
-    }
+  for (int q = wv; q < NQ; q += 4) {   // the chunk's max and sum per query (lanes over positions)
+    const float l = lane < kAttnChunk ? E[lane][q] : -INFINITY;
+    const float m = wmax(l);
+    const float e = lane < np ? expf(l - m) : 0.f;
+    const float sm = wsum(e);
+    if (lane < kAttnChunk) E[lane][q] = e;
+    if (lane == 0) { Mq[q] = m; Tq[q] = sm; }
   }
   __syncthreads();
-  if (tid < 46 * kActAttnSlices) {   // readout (apply_alpha, attention.py:244-254)
-    const int g = tid % 46, sl = tid / 46;
+  float* part = p.Apart + (size_t)f * nch * NQ * kAttnPart;
+  const __amdgpu_buffer_rsrc_t rp = make_rsrc(part, (uint32_t)(nch * NQ * kAttnPart * 4));
+  for (int u = tid; u < 46 * NQ; u += 256) {   // partial readout: (column float4 g, query q)
+    const int q = u / 46, g = u - q * 46;
     const float* src = g < 30 ? O + 8 + 4 * g : S + 4 * (g - 30);
     const int ld = g < 30 ? 128 : 64;
-    float acc[NQ][4];
+    f32x4 vv[kAttnChunk];
 #pragma unroll
-    for (int qq = 0; qq < NQ; ++qq) acc[qq][0] = acc[qq][1] = acc[qq][2] = acc[qq][3] = 0.f;
-#pragma unroll 4
-    for (int pp = sl; pp < P; pp += kActAttnSlices) {
-      const f32x4 v = ld4(src + (size_t)pp * ld);
+    for (int j = 0; j < kAttnChunk; ++j) vv[j] = ld4(src + (size_t)(p0 + min(j, np - 1)) * ld);   // clamped rows
+    __builtin_amdgcn_sched_barrier(0);   // every load issued before the sums
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int qq = 0; qq < NQ; ++qq) {
-        const float a = L[pp * NQ + qq];
-        acc[qq][0] += a * v[0]; acc[qq][1] += a * v[1]; acc[qq][2] += a * v[2]; acc[qq][3] += a * v[3];
+    for (int j = 0; j < kAttnChunk; ++j) acc += (j < np ? E[j][q] : 0.f) * vv[j];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rp,
+                                           (uint32_t)(((c * NQ + q) * kAttnPart + 4 * g) * 4), 0, kSC1);
+  }
+  if (tid < NQ) {
+    const f32x4 ms = {Mq[tid], Tq[tid], 0.f, 0.f};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, ms), rp,
+                                           (uint32_t)(((c * NQ + tid) * kAttnPart + 184) * 4), 0, kSC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.zcnt + p.B * 8 * actor_pix_tiles(P) + f, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nch - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    is_last = old == nch - 1;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  for (int q = wv; q < NQ; q += 4) {   // merge weights: exp(m_c - m) / sum_c exp(m_c - m) s_c
+    float mc[kActMaxChunks / 64], sc[kActMaxChunks / 64];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kActMaxChunks / 64; ++k) {
+      const int cc = lane + 64 * k;
+      mc[k] = -INFINITY;
+      sc[k] = 0.f;
+      if (cc < nch) {
+        const f32x4 v = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rp, (uint32_t)(((cc * NQ + q) * kAttnPart + 184) * 4), 0, kSC1));
+        mc[k] = v[0];
+        sc[k] = v[1];
+      }
+      m = fmaxf(m, mc[k]);
+    }
+    m = wmax(m);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kActMaxChunks / 64; ++k) {
+      mc[k] = lane + 64 * k < nch ? expf(mc[k] - m) : 0.f;
+      t += mc[k] * sc[k];
+    }
+    t = wsum(t);
+    const float inv = 1.f / t;
+#pragma unroll
+    for (int k = 0; k < kActMaxChunks / 64; ++k)
+      if (lane + 64 * k < nch) Wc[lane + 64 * k][q] = mc[k] * inv;
+    if (lane == 0) { Mq[q] = m; Tq[q] = inv; }
+  }
+  __syncthreads();
+  float* arow = p.arow + (size_t)f * p.ans_ld;
+  for (int u = tid; u < 46 * NQ; u += 256) {   // answer row: the merged readouts
+    const int q = u / 46, g = u - q * 46;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < nch; c0 += 8) {   // 8 chunks' loads in flight (clamped, zero weights past nch)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int cc = min(c0 + k, nch - 1);
+        const float w = c0 + k < nch ? Wc[cc][q] : 0.f;
+        acc += w * __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rp, (uint32_t)(((cc * NQ + q) * kAttnPart + 4 * g) * 4), 0, kSC1));
       }
     }
-#pragma unroll
-    for (int qq = 0; qq < NQ; ++qq)
-      *reinterpret_cast<f32x4*>(red + (sl * NQ + qq) * 184 + 4 * g) =
-          f32x4{acc[qq][0], acc[qq][1], acc[qq][2], acc[qq][3]};
+    *reinterpret_cast<f32x4*>(arow + q * 184 + 4 * g) = acc;
   }
-  __syncthreads();
-  for (int i = tid; i < p.ans_ld; i += 256) {   // [a_0..a_nq-1 | Q | r | a_prev | 0-pad]
+  for (int i = NQ * 184 + tid; i < p.ans_ld; i += 256) {   // [.. | Q | r | a_prev | 0-pad]
     float v = 0.f;
-    if (i < NQ * 184) {
-#pragma unroll
-      for (int s2 = 0; s2 < kActAttnSlices; ++s2) v += red[s2 * NQ * 184 + i];
-    } else if (i < NQ * 256) {
-      v = Qs[i - NQ * 184];
-    } else if (i == NQ * 256) {
-      v = p.prev_reward ? p.prev_reward[f] : 0.f;
-    } else if (i == NQ * 256 + 1) {
-      v = p.prev_action ? p.prev_action[f] : 0.f;
-    }
-    ans[i] = v;
+    if (i < NQ * 256) v = Qs[i - NQ * 184];
+    else if (i == NQ * 256) v = p.prev_reward ? p.prev_reward[f] : 0.f;
+    else if (i == NQ * 256 + 1) v = p.prev_action ? p.prev_action[f] : 0.f;
+    arow[i] = v;
   }
-  __syncthreads();
-  {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int k = 4 * lane + 256 * i;
-      if (k < p.ans_ld) s += dot4(w1r[i], *reinterpret_cast<const f32x4*>(ans + k));
+  if (p.attn) {
+    for (int i = tid; i < P * NQ; i += 256) {
+      const int q = i % NQ;
+      const float l = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, (uint32_t)(i * 4), 0, kSC1));
+      p.attn[(size_t)f * P * NQ + i] = expf(l - Mq[q]) * Tq[q];
     }
-    s = wsum(s) + a0;
-    if (lane == 0) p.hid1[(size_t)f * 512 + row] = fmaxf(s, 0.f);
   }
+}
+
+// ------------------------------------------------- answer layer 0 (ReLU) --
+// answer_processor.0 + ReLU (attention.py:277-282, 350): one wave per row of
+// the [512][ans_ld] weights, the answer row read from the readout's output.
+template <int NQ>
+__global__ void __launch_bounds__(256) k_act_ans0(ActorParams p) {
+  constexpr int NIT = NQ == 4 ? 5 : 9;   // float4 slices per lane: 256 * NIT >= ans_ld
+  const int f = blockIdx.y, lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const float* wr = p.W1p + (size_t)row * p.ans_ld;
+  const float* x = p.arow + (size_t)f * p.ans_ld;
+  f32x4 wv[NIT], xv[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {   // clamped offsets: every load unconditional and in flight at once
+    const int k = min(4 * lane + 256 * i, p.ans_ld - 4);
+    wv[i] = ld4(wr + k);
+    xv[i] = ld4(x + k);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NIT; ++i)
+    if (4 * lane + 256 * i < p.ans_ld) s += dot4(wv[i], xv[i]);
+  s = wsum(s) + p.a0b[row];
+  if (lane == 0) p.hid1[(size_t)f * 512 + row] = fmaxf(s, 0.f);
 }
 
 // ------------------------------------------- answer layer 2 (linear) -----
@@ -353,38 +463,15 @@ __global__ void __launch_bounds__(256) k_act_ans2(ActorParams p) {
   }
 }
 
-// ------------------------------------------------- LSTMCell (zero state) --
-// policy_core from zero state (attention.py:354-355, Q1): one wave per unit u,
-// its four gate rows 4u..4u+3 of the interleaved [1024][256] weights;
-// c = i*g~ (+ f*0), h = o*tanh(c) -- the learner's EpiLstmCellFwd.
-__global__ void __launch_bounds__(256) k_act_lstmcell(ActorParams p) {
-  const int lane = threadIdx.x & 63, u = blockIdx.x * 4 + (threadIdx.x >> 6);
-  f32x4 w[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) w[g] = ld4(p.Wihp + (size_t)(4 * u + g) * 256 + 4 * lane);
-  const f32x4 b = ld4(p.blc + 4 * u);
-  for (int f = 0; f < p.B; ++f) {
-    const f32x4 x = ld4(p.AO + (size_t)f * 256 + 4 * lane);
-    float z[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) z[g] = wsum(dot4(w[g], x));
-    if (lane == 0) {
-      const float gi = sigm_acc(z[0] + b[0]), gf = sigm_acc(z[1] + b[1]);
-      const float gc = tanhf(z[2] + b[2]), go = sigm_acc(z[3] + b[3]);
-      const float c = gf * 0.f + gi * gc;
-      p.LH[(size_t)f * 256 + u] = go * tanhf(c);
-    }
-  }
-}
-
 // --------------------------------------------------- heads + action draw --
 // policy_head / values_head (attention.py:365-367) and Policy.forward's draw
 // (main_mp.py:54-58) in one workgroup: rows o < A -> logits, A <= o < 2A ->
 // values, then one wave per frame runs draw_row on the logits it just wrote
 // (the device counter is read by every wave before the single increment).
-__global__ void __launch_bounds__(256) k_act_heads(ActorParams p) {
-  __shared__ float lg[16 * 256];
+// LH comes from the other LSTMCell workgroups' sc1 stores: sc1 loads.
+__device__ __forceinline__ void heads_draw(const ActorParams& p, float* lg) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, A = p.A, R = 2 * A;
+  const __amdgpu_buffer_rsrc_t rh = make_rsrc(p.LH, (uint32_t)(p.B * 256 * 4));
   // rows in chunks of 8 per wave, each chunk's weight and state loads issued before its math
   for (int o0 = wv * 8; o0 < R; o0 += 32) {
     f32x4 w[8];
@@ -396,7 +483,8 @@ __global__ void __launch_bounds__(256) k_act_heads(ActorParams p) {
       b[j] = p.bhd[o];
     }
     for (int f = 0; f < p.B; ++f) {
-      const f32x4 x = ld4(p.LH + (size_t)f * 256 + 4 * lane);
+      const f32x4 x =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, (uint32_t)((f * 256 + 4 * lane) * 4), 0, kSC1));
       float s[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] = dot4(w[j], x);
@@ -426,34 +514,72 @@ __global__ void __launch_bounds__(256) k_act_heads(ActorParams p) {
   if (p.counter && tid == 0) *p.counter = ctr + 1ull;
 }
 
-}  // namespace
-
-size_t actor_attn_lds(int P, int nq, int ans_ld) {
-  return sizeof(float) * ((size_t)P * nq + (size_t)nq * 72 + (size_t)kActAttnSlices * nq * 184 + ans_ld);
+// ------------------------------------------- LSTMCell (zero state) + heads --
+// policy_core from zero state (attention.py:354-355, Q1): one wave per unit u,
+// its four gate rows 4u..4u+3 of the interleaved [1024][256] weights;
+// c = i*g~ (+ f*0), h = o*tanh(c) -- the learner's EpiLstmCellFwd.  The last
+// workgroup to arrive (sc1 hand-off as the ConvLSTM's) runs the heads and the
+// draw: one launch fewer than a separate heads kernel.
+__global__ void __launch_bounds__(256) k_act_lstmcell(ActorParams p) {
+  __shared__ float lg[16 * 256];
+  __shared__ int is_last;
+  const int tid = threadIdx.x, lane = tid & 63, u = blockIdx.x * 4 + (tid >> 6);
+  f32x4 w[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) w[g] = ld4(p.Wihp + (size_t)(4 * u + g) * 256 + 4 * lane);
+  const f32x4 b = ld4(p.blc + 4 * u);
+  const __amdgpu_buffer_rsrc_t rh = make_rsrc(p.LH, (uint32_t)(p.B * 256 * 4));
+  for (int f = 0; f < p.B; ++f) {
+    const f32x4 x = ld4(p.AO + (size_t)f * 256 + 4 * lane);
+    float z[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) z[g] = wsum(dot4(w[g], x));
+    if (lane == 0) {
+      const float gi = sigm_acc(z[0] + b[0]), gf = sigm_acc(z[1] + b[1]);
+      const float gc = tanhf(z[2] + b[2]), go = sigm_acc(z[3] + b[3]);
+      const float c = gf * 0.f + gi * gc;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, go * tanhf(c)), rh,
+                                            (uint32_t)((f * 256 + u) * 4), 0, kSC1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.zcnt + p.B * 8 * actor_pix_tiles(p.P) + p.B, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    is_last = old == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (is_last) heads_draw(p, lg);
 }
 
+}  // namespace
+
 hipError_t actor_launch(const ActorParams& p, hipStream_t st) {
-  if (p.B < 1 || p.B > 16 || (p.nq != 4 && p.nq != 8) || p.A < 1 || p.A > 256) return hipErrorInvalidValue;
-  const size_t lds = actor_attn_lds(p.P, p.nq, p.ans_ld);
-  if (lds > kActLdsMax) return hipErrorInvalidValue;
-  if (lds > 64 * 1024) {   // beyond the default dynamic-LDS limit: raise it for this launch's kernel
-    const void* k = p.nq == 4 ? reinterpret_cast<const void*>(&k_act_attn<4>) : reinterpret_cast<const void*>(&k_act_attn<8>);
-    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  if (p.B < 1 || p.B > 16 || (p.nq != 4 && p.nq != 8) || p.A < 1 || p.A > 256 || p.ans_ld % 4 ||
+      p.ans_ld > 2304 || actor_chunks(p.P) > kActMaxChunks)
+    return hipErrorInvalidValue;
   if (p.u8)
     hipLaunchKernelGGL(k_act_vision<uint8_t>, dim3(p.P, p.B), dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(k_act_vision<float>, dim3(p.P, p.B), dim3(256), 0, st, p);
-  const int npg = (p.P + 15) / 16;
-  hipLaunchKernelGGL(k_act_convlstm, dim3(32 * npg, p.B), dim3(512), 0, st, p, npg);
+  const int npt = actor_pix_tiles(p.P);
+  hipLaunchKernelGGL(k_act_convlstm, dim3(8 * kActLstmKS * npt, p.B), dim3(512), 0, st, p, npt);
+  const int nch = actor_chunks(p.P);
   if (p.nq == 4)
-    hipLaunchKernelGGL(k_act_attn<4>, dim3(128, p.B), dim3(256), lds, st, p);
+    hipLaunchKernelGGL(k_act_attn<4>, dim3(nch, p.B), dim3(256), 0, st, p, nch);
   else
-    hipLaunchKernelGGL(k_act_attn<8>, dim3(128, p.B), dim3(256), lds, st, p);
+    hipLaunchKernelGGL(k_act_attn<8>, dim3(nch, p.B), dim3(256), 0, st, p, nch);
+  if (p.nq == 4)
+    hipLaunchKernelGGL(k_act_ans0<4>, dim3(128, p.B), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(k_act_ans0<8>, dim3(128, p.B), dim3(256), 0, st, p);
   hipLaunchKernelGGL(k_act_ans2, dim3(64), dim3(256), 0, st, p);
   hipLaunchKernelGGL(k_act_lstmcell, dim3(64), dim3(256), 0, st, p);
-  hipLaunchKernelGGL(k_act_heads, dim3(1), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 

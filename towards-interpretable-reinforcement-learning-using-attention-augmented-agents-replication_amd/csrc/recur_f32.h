@@ -870,7 +870,7 @@ k_convlstm_fwd_f32ps(RecF32Params p) {
         for (int c = 0; c < NCB; ++c) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int chl = 2 * g + hh, ch = 8 * (rbg0 + r) + chl;
+            const int chl = 2 * g + hh;
             float gi, gf, gc, go, cc, h;
             GateFwd::run(acc[r][c][4 * g] + bz[r][g][0], acc[r][c][4 * g + 1] + bz[r][g][1],
                          acc[r][c][4 * g + 2] + bz[r][g][2], acc[r][c][4 * g + 3] + bz[r][g][3], cst[r][c][g], gi, gf,

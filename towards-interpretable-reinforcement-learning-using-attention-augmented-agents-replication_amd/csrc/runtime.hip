@@ -395,34 +395,39 @@ int aaa_sample_actions(int B, int A, const float* logits, unsigned long long see
 }
 
 // ---- actor step (include/aaa.h; csrc/actor.hip) ----
-// Workspace: conv2 output X (B,P,64), h_t Hs (B,P,128), hid1 (B,512), AO (B,256), LH (B,256).
-static int actor_layout(const aaa_cfg* cfg, Layout& L, size_t off[5], size_t* total) {
+// Workspace: conv2 output X (B,P,64), h_t Hs (B,P,128), hid1 (B,512), AO (B,256), LH (B,256),
+// the ConvLSTM's split-K partial tiles, the tile and readout counters, the attention logits,
+// the readout's chunk partials and the answer row (actor.h).
+static int actor_layout(const aaa_cfg* cfg, Layout& L, size_t off[10], size_t* total) {
   int r = build_layout(cfg, L);
   if (r) return r;
   if (cfg->T != 1) return fail(AAA_E_ARG, "actor_step: T must be 1 (got %d)", cfg->T);
   if (cfg->dtype != AAA_F32) return fail(AAA_E_ARG, "actor_step: fp32 weights only (bf16 agents use aaa_forward)");
   if (L.sc) return fail(AAA_E_ARG, "actor_step: the stateful policy core uses aaa_forward");
   if (cfg->B > 16) return fail(AAA_E_ARG, "actor_step: B <= 16 (got %d); larger batches use aaa_forward", cfg->B);
-  if (actor_attn_lds(L.P, L.nq, L.ans_ld) > kActLdsMax)
-    return fail(AAA_E_ARG, "actor_step: a %dx%d grid with %d queries exceeds the readout kernel's LDS; use aaa_forward",
-                L.h, L.w, L.nq);
+  if (actor_chunks(L.P) > kActMaxChunks)
+    return fail(AAA_E_ARG, "actor_step: a %dx%d grid exceeds the readout's %d position chunks; use aaa_forward",
+                L.h, L.w, kActMaxChunks);
   const size_t B = cfg->B, P = L.P;
-  const size_t sz[5] = {B * P * 64 * 4, B * P * 128 * 4, B * 512 * 4, B * 256 * 4, B * 256 * 4};
+  const size_t nt = 8 * (size_t)actor_pix_tiles(L.P), nch = actor_chunks(L.P), nq = L.nq;
+  const size_t sz[10] = {B * P * 64 * 4, B * P * 128 * 4, B * 512 * 4, B * 256 * 4, B * 256 * 4,
+                         B * nt * kActLstmKS * 4096 * 4, (B * nt + B + 1) * 4, B * P * nq * 4,
+                         B * nch * nq * kAttnPart * 4, B * (size_t)L.ans_ld * 4};
   size_t o = 0;
-  for (int i = 0; i < 5; ++i) { off[i] = o; o = al256(o + sz[i]); }
+  for (int i = 0; i < 10; ++i) { off[i] = o; o = al256(o + sz[i]); }
   *total = o;
   return AAA_OK;
 }
 
 size_t aaa_actor_workspace_bytes(const aaa_cfg* cfg) {
   Layout L;
-  size_t off[5], tot = 0;
+  size_t off[10], tot = 0;
   return actor_layout(cfg, L, off, &tot) ? 0 : tot;
 }
 
 int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t stream) {
   Layout L;
-  size_t off[5], tot = 0;
+  size_t off[10], tot = 0;
   int r = actor_layout(cfg, L, off, &tot);
   if (r) return r;
   if (!io || !io->params || !io->packed || !io->basis || !io->frames || !io->h || !io->c || !io->logits ||
@@ -452,6 +457,8 @@ int aaa_actor_step(const aaa_cfg* cfg, const aaa_actor_io* io, hipStream_t strea
   p.hout = io->h_out; p.cout = io->c_out;
   p.X = (float*)(ws + off[0]); p.Hs = (float*)(ws + off[1]); p.hid1 = (float*)(ws + off[2]);
   p.AO = (float*)(ws + off[3]); p.LH = (float*)(ws + off[4]);
+  p.Zp = (float*)(ws + off[5]); p.zcnt = (int*)(ws + off[6]);
+  p.Lg = (float*)(ws + off[7]); p.Apart = (float*)(ws + off[8]); p.arow = (float*)(ws + off[9]);
   p.seed = io->seed; p.counter = io->counter; p.actions = io->actions; p.logp = io->logp; p.jac = io->dlogp_dlogits;
   HIPCHK(actor_launch(p, stream));
   return AAA_OK;

@@ -146,6 +146,7 @@ class Episode:
         # the large-batch frame-resident BPTT (no episode runs at such batches)
         store_on = os.environ.get("AAA_EPISODE_STORE", "1") != "0"
         self.store = {} if store_on else None
+        self._slots = {}
         self.store_budget = int(float(os.environ.get("AAA_EPISODE_STORE_MB", "4096")) * 2**20)
         self.store_bytes = 0
         self.blk = max(1, min(self.seg, STORE_BLOCK))
@@ -164,10 +165,17 @@ class Episode:
                                      frames_u8=runner.frames_u8)
                     cache[key] = (ar, ar.new_workspace())
                 self.actor, self.ws = cache[key]
+        if self.actor is not None:   # one aaa_actor_io for the episode: the fixed pointers set once
+            import ctypes
+            self._io = N.ActorIO()
+            self._io.params, self._io.packed = flat.data_ptr(), packed.data_ptr()
+            self._io.basis, self._io.workspace = basis.data_ptr(), self.ws.data_ptr()
+            self._io_ref, self._cfg_ref = ctypes.byref(self._io), ctypes.byref(self.actor.cfg)
+            self._lib = N.load()
         if self.actor is not None and h is None:   # the actor chain reads a state tensor: zeros
             shp = runner.state_shape()
             self.hbuf, self.cbuf = torch.zeros(shp, device=self.device), torch.zeros(shp, device=self.device)
-        else:
+        elif self.actor is None:
             self.ws = runner.new_workspace()      # per-step scratch, reused: nothing of it is kept
 
     # -- forward --------------------------------------------------------------
@@ -176,19 +184,23 @@ class Episode:
         return len(self.steps) - 1
 
     def _slot(self, t):
-        """(gates, c, h) store rows of step t ((1, M, 512), (1, M, 128) x 2), or None past the budget."""
+        """(gates, c, h) store rows of step t ((1, M, 512), (1, M, 128) x 2) and its c / h rows as
+        state-shaped views, or None past the budget.  A block's row views are made once, with the block."""
         if self.store is None:
             return None
         k, i = divmod(t, self.blk)
-        if k not in self.store:
+        views = self._slots.get(k)
+        if views is None:
             shapes, dts = self.runner.core_shapes(self.blk), self.runner.core_dtypes()
             nbytes = sum(a * b * c * torch.empty((), dtype=dt).element_size() for (a, b, c), dt in zip(shapes, dts))
             if self.store_bytes + nbytes > self.store_budget:
                 return None
-            self.store[k] = tuple(torch.empty(s, dtype=dt, device=self.device) for s, dt in zip(shapes, dts))
+            self.store[k] = g, c, h = tuple(torch.empty(s, dtype=dt, device=self.device) for s, dt in zip(shapes, dts))
             self.store_bytes += nbytes
-        g, c, h = self.store[k]
-        return g[i:i + 1], c[i:i + 1], h[i:i + 1]
+            shp = self.runner.state_shape()
+            self._slots[k] = views = [(g[j:j + 1], c[j:j + 1], h[j:j + 1], c[j].view(shp), h[j].view(shp))
+                                      for j in range(self.blk)]
+        return views[i]
 
     def forward_step(self, t, sampler=None):
         """Run step t: (logits, values, attn, hT, cT) -- plus (action, logp, jac)
@@ -197,34 +209,44 @@ class Episode:
         r = self.runner
         slot = self._slot(t)
         if self.actor is not None:
-            B, A = r.B, r.A
-            logits = torch.empty(1, B, A, device=self.device)
-            values = torch.empty(1, B, A, device=self.device)
-            attn = torch.empty(1, B, r.h, r.w, r.nq, device=self.device)
-            draw = ()
-            if sampler is not None:
-                draw = (torch.empty(B, dtype=torch.int32, device=self.device),
-                        torch.empty(B, device=self.device), torch.empty(B, A, device=self.device))
-            shp = r.state_shape()
+            if getattr(r, "relu_trace", None) is not None:
+                raise RuntimeError("Agent.relu_trace: the actor-chain recording keeps no learner workspace; "
+                                   "set AAA_EPISODE_ACTOR=0 to trace an episode")
+            B, A, dev = r.B, r.A, self.device
+            logits = torch.empty(1, B, A, device=dev)
+            values = torch.empty(1, B, A, device=dev)
+            attn = torch.empty(1, B, r.h, r.w, r.nq, device=dev)
             h, c = self.cur
             if h is None:   # zero state entering the episode
                 h, c = self.hbuf, self.cbuf
             if slot is not None:   # h_t, c_t straight into the store rows (written by the kernels, so no
                 # in-place op on the store's blocks: these views are handed out as prev_hidden)
-                hT, cT = slot[2].view(shp), slot[1].view(shp)
+                cT, hT = slot[3], slot[4]
             else:
-                hT, cT = torch.empty(shp, device=self.device), torch.empty(shp, device=self.device)
-            self.actor.step(self.flat, self.packed, self.basis, X[0], self.ws, h, c, logits[0],
-                            values[0], attn[0], None if pr is None else pr.reshape(-1),
-                            None if pa is None else pa.reshape(-1),
-                            seed=sampler.seed if sampler is not None else 0,
-                            counter=sampler.counter if sampler is not None else None,
-                            actions=draw[0] if draw else None, logp=draw[1] if draw else None,
-                            dlogp=draw[2] if draw else None, gates=slot[0] if slot is not None else None,
-                            h_out=hT, c_out=cT)
-            if getattr(r, "relu_trace", None) is not None:
-                raise RuntimeError("Agent.relu_trace: the actor-chain recording keeps no learner workspace; "
-                                   "set AAA_EPISODE_ACTOR=0 to trace an episode")
+                shp = r.state_shape()
+                hT, cT = torch.empty(shp, device=dev), torch.empty(shp, device=dev)
+            # aaa_actor_step with the episode's io (the recorded frames, states and store rows are
+            # contiguous tensors of the runner's geometry by construction: ActorRunner.step's checks
+            # are not repeated per step)
+            io = self._io
+            io.frames, io.h, io.c, io.h_out, io.c_out = X.data_ptr(), h.data_ptr(), c.data_ptr(), hT.data_ptr(), \
+                cT.data_ptr()
+            io.logits, io.values, io.attn = logits.data_ptr(), values.data_ptr(), attn.data_ptr()
+            io.gates = slot[0].data_ptr() if slot is not None else None
+            prf = None if pr is None else pr.reshape(-1).to(dev, torch.float32).contiguous()
+            paf = None if pa is None else pa.reshape(-1).to(dev, torch.float32).contiguous()
+            io.prev_reward = None if prf is None else prf.data_ptr()
+            io.prev_action = None if paf is None else paf.data_ptr()
+            draw = ()
+            if sampler is not None:
+                draw = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, device=dev),
+                        torch.empty(B, A, device=dev))
+                io.seed = sampler.seed & (2**64 - 1)
+                io.counter = sampler.counter.data_ptr()
+                io.actions, io.logp, io.dlogp_dlogits = draw[0].data_ptr(), draw[1].data_ptr(), draw[2].data_ptr()
+            else:
+                io.seed, io.counter, io.actions, io.logp, io.dlogp_dlogits = 0, None, None, None, None
+            N.check(self._lib.aaa_actor_step(self._cfg_ref, self._io_ref, N.stream_ptr(dev)), "actor_step")
             self.cur = (hT, cT)
             if (t + 1) % self.seg == 0:
                 self.ckpt[t + 1] = (hT, cT)
@@ -238,7 +260,7 @@ class Episode:
         if (t + 1) % self.seg == 0:
             self.ckpt[t + 1] = (hT, cT)
         if slot is not None:
-            r.core_export(self.ws, 0, 1, *slot)
+            r.core_export(self.ws, 0, 1, *slot[:3])
         if sampler is not None:
             from .policy import _sample_raw
             return (logits, values, attn, hT, cT) + _sample_raw(logits[0], sampler.seed, sampler.counter)

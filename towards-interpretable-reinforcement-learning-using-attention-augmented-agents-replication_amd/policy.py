@@ -107,7 +107,8 @@ class Policy(nn.Module):
         self._slot = 0
 
     def _device(self):
-        return next(self.agent.parameters()).device
+        pl = getattr(self.agent, "_param_list", None)
+        return pl()[0].device if pl is not None else next(self.agent.parameters()).device
 
     def _upload(self, observation):
         dev = self._device()
