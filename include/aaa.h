@@ -186,7 +186,8 @@ int aaa_forward_phases(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStre
  * and the weight gradient read).  Export reads a workspace aaa_forward
  * filled; import writes one for aaa_forward_phases without CORE (and the h
  * half of the [x | h] operand slots).  Not for channel-quad-major slices
- * (large-batch bf16: AAA_E_ARG); device pointers, stream-ordered, no host sync. */
+ * (large-batch bf16: AAA_E_ARG; aaa_core_elem_bytes reports 0 bytes for such
+ * a geometry); device pointers, stream-ordered, no host sync. */
 int aaa_core_elem_bytes(const aaa_cfg* cfg, int* gate_bytes, int* h_bytes);
 int aaa_core_export(const aaa_cfg* cfg, const void* workspace, int t0, int n, void* gates, float* c, void* h,
                     hipStream_t stream);

@@ -12,6 +12,7 @@ from helpers import ROOT, assert_close, check_fp, detinit, kink_envelope, kink_r
 from oracle import ref_cpu
 
 import attention
+from aaa_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-4
@@ -223,13 +224,16 @@ def test_fused_splitk_slices(cuda, monkeypatch, tile, ns):
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"fused split-K {tile} x{ns}: ")
 
 
-@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("tile", ["0", "1", "2", "3", "4", "5", "6"])
 def test_dx_split6_tiles(cuda, monkeypatch, tile):
     """The fp32 batched dx (conv2-output grad) ring tiles on split products:
     64x64, 64x128, 64x64 BK64, 64x128 with the channel-chunk-major K order
     (ConvGeo::cmaj, reorder_cmaj weights), 64x128 with the weights pre-split
     into bf16 planes (GRows3B), and the same with dZ pre-split too
-    (GIm2colB3 over split_planes); B=5 -> ragged column tiles."""
+    (GIm2colB3 over split_planes), and the halo-staged conv (6); B=5 -> ragged
+    column tiles.  Tile 4 is the product's; the others exist in the A/B build only."""
+    if tile != "4" and not N.ablation_build():
+        pytest.skip("measured-slower dx tile: ablation builds only (make ablation, AAA_LIB)")
     monkeypatch.setenv("AAA_DX_S6_TILE", tile)
     T, B = 3, 5
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"dx tile {tile}: ")
@@ -242,7 +246,10 @@ def test_wgrad_split6_tiles(cuda, monkeypatch, tile):
     128x256, 256x128, 256x256 with the split per fragment read, and 256x256 /
     256x128 with each operand split once as it is committed to LDS (GemmCfgS6L),
     and 256x256 split-at-commit with two K tiles of loads in flight;
-    T*B*P = 605 pixel rows -> a ragged last K tile of every split-K slice."""
+    T*B*P = 605 pixel rows -> a ragged last K tile of every split-K slice.
+    Tile 6 is the product's; the others exist in the A/B build only."""
+    if tile != "6" and not N.ablation_build():
+        pytest.skip("measured-slower wgrad tile: ablation builds only (make ablation, AAA_LIB)")
     monkeypatch.setenv("AAA_WGRAD_S6_TILE", tile)
     T, B = 5, 1
     _compare(_run_unroll(_agent(cuda), T, B, cuda), _oracle(T, B), RTOL, f"wgrad tile {tile}: ")
@@ -600,7 +607,10 @@ def test_xp_chunks_ragged(cuda, monkeypatch, conv_dtype):
     """conv1's bordered RGBx operand is rebuilt from the frames in chunks of
     AAA_XP_CHUNK frames (forward layered conv1 and the backward's conv1 weight
     gradient; csrc/rt_backward.hip conv1_wgrad_frames): 100 frames in chunks of
-    64 + 36 give the oracle's gradients, uint8 and fp32 frames."""
+    64 + 36 give the oracle's gradients, uint8 and fp32 frames.  Measured
+    slower than keeping every frame's operand: ablation builds only."""
+    if not N.ablation_build():
+        pytest.skip("AAA_XP_CHUNK: ablation builds only (make ablation, AAA_LIB)")
     monkeypatch.setenv("AAA_XP_CHUNK", "64")
     T, B = 20, 5
     tol = RTOL if conv_dtype == "fp32" else 2e-2

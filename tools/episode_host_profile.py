@@ -94,6 +94,48 @@ if __name__ == "__main__":
             e1.record()
             torch.cuda.synchronize()
             print(f"backward: host {(time.perf_counter() - t0) * 1e3:.3f} ms, device {e0.elapsed_time(e1):.3f} ms")
+        if "--phases" in sys.argv:   # wall-clock phases of the backward (the engine runs it on its own thread)
+            from aaa_amd import episode as E
+            marks = {}
+            st0, ba0 = E.Episode.stash, E.Episode.backward_all
+
+            def stash(self, *a, **k):
+                marks.setdefault("first_stash", time.perf_counter())
+                marks["last_stash"] = time.perf_counter()
+                return st0(self, *a, **k)
+
+            def backward_all(self, *a, **k):
+                marks["bwd_all_start"] = time.perf_counter()
+                out = ba0(self, *a, **k)
+                marks["bwd_all_end"] = time.perf_counter()
+                torch.cuda.synchronize()
+                marks["bwd_all_synced"] = time.perf_counter()
+                return out
+            E.Episode.stash, E.Episode.backward_all = stash, backward_all
+            for _ in range(3):
+                episode()
+                loss = torch.cat([-lp * Rt for lp, Rt in zip(policy.saved_log_probs, returns)]).sum()
+                torch.cuda.synchronize()
+                marks.clear()
+                t0 = time.perf_counter()
+                loss.backward()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                print("backward phases (ms from loss.backward()):",
+                      {k: round((v - t0) * 1e3, 3) for k, v in sorted(marks.items(), key=lambda kv: kv[1])},
+                      "end", round((t1 - t0) * 1e3, 3))
+            E.Episode.stash, E.Episode.backward_all = st0, ba0
+        if "--cprofile" in sys.argv:
+            episode()
+            loss = torch.cat([-lp * Rt for lp, Rt in zip(policy.saved_log_probs, returns)]).sum()
+            torch.cuda.synchronize()
+            pr = cProfile.Profile()
+            pr.enable()
+            loss.backward()
+            torch.cuda.synchronize()
+            pr.disable()
+            pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+            pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
         sys.exit(0)
     pr = cProfile.Profile()
     pr.enable()

@@ -98,6 +98,12 @@ _lib = None
 _lock = threading.Lock()
 
 
+def ablation_build() -> bool:
+    """Whether the loaded library is the A/B build (make ablation; AAA_LIB=.../libaaa_ablation.so):
+    the measured-slower variants and the A/B environment knobs exist only there."""
+    return hasattr(load(), "aaa_ablation_build")
+
+
 def load(path: str = LIB_PATH):
     """Load libaaa.so (raises if absent).  Safe to call without a GPU."""
     global _lib

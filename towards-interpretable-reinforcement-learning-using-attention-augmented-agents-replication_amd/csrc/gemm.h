@@ -366,9 +366,13 @@ __device__ __forceinline__ void tile_of(const TileMap& m, int& ti, int& tj, int&
   tj = (int)m.ny.div((uint32_t)u);
   ti = u - tj * ny;
 }
-inline int xcd_remap_enabled() {
+inline int xcd_remap_enabled() {   // A/B (AAA_XCD_REMAP) in ablation builds only
+#ifdef AAA_ABLATION
   const char* e = getenv("AAA_XCD_REMAP");
   return e ? atoi(e) != 0 : 1;
+#else
+  return 1;
+#endif
 }
 inline TileMap tile_map(dim3 grid) {
   TileMap m;

@@ -1043,8 +1043,12 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
   // register prefetch of the V slice only on large grids (many positions per
   // slice): at 84x84 (11 per slice) the registers cost more occupancy than the
   // early loads buy (C3: 118 vs 104 us; 168x168, C5: 217 vs 275 us)
-  static const int pre_env = getenv("AAA_ATTN_PRE") ? atoi(getenv("AAA_ATTN_PRE")) : -1;   // A/B override
+#ifdef AAA_ABLATION   // A/B overrides (ablation builds)
+  static const int pre_env = getenv("AAA_ATTN_PRE") ? atoi(getenv("AAA_ATTN_PRE")) : -1;
   static const int sl_env = getenv("AAA_ATTN_SLICES") ? atoi(getenv("AAA_ATTN_SLICES")) : -1;
+#else
+  constexpr int pre_env = -1, sl_env = -1;
+#endif
   const bool pre = pre_env >= 0 ? pre_env != 0 : P > 2 * kAttnSlices * 11;
   const int sl = O.bf16 ? kAttnSlicesBf : sl_env > 0 ? sl_env : kAttnSlices;
   const size_t sh = (size_t)(P * nq + nq * 72 + sl * nq * 184) * sizeof(float);
@@ -1071,9 +1075,11 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
   };
   if (nq != 4 && nq != 8) return hipErrorInvalidValue;
   if (O.bf16) go(std::integral_constant<int, 0>{});   // (SL unused: kAttnSlicesBf)
+  else if (sl == kAttnSlices) go(std::integral_constant<int, kAttnSlices>{});
+#ifdef AAA_ABLATION
   else if (sl == 8) go(std::integral_constant<int, 8>{});
   else if (sl == 5) go(std::integral_constant<int, 5>{});
-  else if (sl == kAttnSlices) go(std::integral_constant<int, kAttnSlices>{});
+#endif
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -144,6 +144,10 @@ inline void rec_columns(int h, int w, short* colpp, short* colhb) {
     }
   };
   raster();
+#ifndef AAA_ABLATION
+  (void)NPH;
+  return;
+#else
   const char* e = getenv("AAA_REC_PERM");
   if (!(e && atoi(e) == 1) || P > 128) return;
   int bucket[16][9], nb[16] = {0};
@@ -172,6 +176,7 @@ inline void rec_columns(int h, int w, short* colpp, short* colhb) {
         colhb[c] = (short)(spare[r] - W2 - 1);
       }
     }
+#endif
 }
 
 #ifdef AAA_STAMPS

@@ -532,11 +532,13 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 =
     p.colhb[c] = (short)((pp / p.w) * (p.w + 2) + pp % p.w);
   }
   // S6: 4 A quads in flight (tools/ubench/f32rec: 3% under 8, fewer registers parked in AGPRs)
-  // S6: the dZ image pre-split (PS); AAA_F32_PRESPLIT=0 (A/B) keeps the in-loop split
-  const bool ps = s6 && std::getenv("AAA_F32_PRESPLIT") == nullptr;
-  if (ps) return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true>),
-                                 f32_grid(p.B, 8), 256, p, st);
-  return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4>)
+  // S6: the dZ image pre-split (PS; the in-loop split of AAA_F32_PRESPLIT=0 in ablation builds only)
+#ifdef AAA_ABLATION
+  if (s6 && std::getenv("AAA_F32_PRESPLIT") != nullptr)
+    return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4>), f32_grid(p.B, 8), 256, p,
+                           st);
+#endif
+  return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true>)
                             : reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>),
                          f32_grid(p.B, 8), 256, p, st);
 }

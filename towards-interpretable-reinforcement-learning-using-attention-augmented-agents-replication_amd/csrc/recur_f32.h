@@ -955,8 +955,13 @@ inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool 
   }
   // G = 8, S6: the WIDE mapping with 4 A quads in flight (tools/ubench/f32rec: 7-10% under
   // the two-column-block mapping with 8, most of it from the shallower prefetch)
-  // G = 8, S6: the pre-split images (k_convlstm_fwd_f32ps); AAA_F32_PRESPLIT=0 (A/B) the in-loop split
+  // G = 8, S6, P <= 128: the pre-split images (k_convlstm_fwd_f32ps); larger grids the in-loop
+  // split (AAA_F32_PRESPLIT=0 selects it everywhere in ablation builds)
+#ifdef AAA_ABLATION
   const bool ps = s6 && G == 8 && p.P <= 128 && std::getenv("AAA_F32_PRESPLIT") == nullptr;
+#else
+  const bool ps = s6 && G == 8 && p.P <= 128;
+#endif
   const void* k = ps       ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32ps<0, 1, 8>)
                   : G == 8 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true, true, 4>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>))

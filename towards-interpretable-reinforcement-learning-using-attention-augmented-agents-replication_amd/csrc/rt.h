@@ -215,10 +215,22 @@ inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+// A/B-only knobs (the same-box comparisons of tools/gpu_ab*.sh): read from the
+// environment only in -DAAA_ABLATION builds (make ablation -> libaaa_ablation.so,
+// loaded through AAA_LIB); the product library takes the default.  env_int stays
+// for the path selectors the parity tests drive.
+inline int ab_int(const char* name, int dflt) {
+#ifdef AAA_ABLATION
+  return env_int(name, dflt);
+#else
+  (void)name;
+  return dflt;
+#endif
+}
 // Steps per off-chain chunk: the whole unroll unless overlapping, and never
 // more than the frames one launch may address (Layout::fchunk).
 static int chunk_steps(const Layout& L) {
-  const int c = env_int("AAA_CHUNK", env_int("AAA_OVERLAP", 0) ? 4 : L.T);
+  const int c = ab_int("AAA_CHUNK", ab_int("AAA_OVERLAP", 0) ? 4 : L.T);
   return std::max(1, std::min({c, L.T, L.fchunk / L.B}));
 }
 bool f32_split6();   // fp32 path: large GEMMs as bf16x6 split products (rt_core.hip)
@@ -276,7 +288,7 @@ inline int splitk_slices(int K, int BK, int nsplit) {
 int frames_fwd(const Layout& L);
 static bool fused_x(int dt, int M) { return env_int("AAA_FUSED_X", dt == AAA_BF16 || M <= 1024 ? 1 : 0) != 0; }
 static bool gates_f16(int dt, int M) {
-  if (dt != AAA_BF16 || !fused_x(dt, M) || !env_int("AAA_GATES_F16", 1)) return false;
+  if (dt != AAA_BF16 || !fused_x(dt, M) || !ab_int("AAA_GATES_F16", 1)) return false;
   const int bt = step_tile((long)(128 / 32) * ((M + 31) / 32), "AAA_BPTT_TILE", true, true);
   return bt == 7 || bt == 8 || bt >= 19;
 }
@@ -339,7 +351,7 @@ template <template <typename, typename, int, int, int> class LA_,
           template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
 static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, int nsplit,
                             hipStream_t st) {
-  const int mode = env_int("AAA_HEAD_TILE", 0);
+  const int mode = ab_int("AAA_HEAD_TILE", 0);
   const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
   auto splitk = [&](auto cfg0) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
     if (g_tail6) {
@@ -362,17 +374,21 @@ static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, in
     return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
                                 ep, Mi, Nj, K, nsplit, st);
   };
+  if (mode == 0 && tiles < 192) return splitk(CFK4{});
+  if (mode == 1 || (mode == 0 && tiles >= 192)) return splitk(CF{});
+#ifdef AAA_ABLATION   // the measured-slower tail tiles (AAA_HEAD_TILE 2-5)
   if (mode == 3) return splitk(CFK{});
   if (mode == 4) return splitk(CFK4{});
   if (mode == 5) return splitk(CFK4B{});
-  if (mode == 0 && tiles < 192) return splitk(CFK4{});
-  if (mode == 1 || (mode == 0 && tiles >= 192)) return splitk(CF{});
   if (g_tail3 || g_tail6) return splitk(CF32{});
   using C = CF32;
   using A = LA_<float, float, C::BI, C::BK, C::NT>;
   using B = LB_<float, float, C::BJ, C::BK, C::NT>;
   return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows}, ep,
                               Mi, Nj, K, nsplit, st);
+#else
+  return hipErrorInvalidValue;   // unreachable: mode is 0 outside ablation builds
+#endif
 }
 
 // Tail GEMMs with very few columns (the actor's B=1, T=1 step: F = 1):
@@ -423,7 +439,7 @@ k_skinny_gemm(const float* __restrict__ W, int ldw, int Mi, const float* __restr
 // skinny kernel for <= kSkinnyMaxCols columns (AAA_SKINNY=0 disables), else head_gemm.
 template <class PA, class PB, class EP>
 static hipError_t tail_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, hipStream_t st) {
-  if (Nj <= kSkinnyMaxCols && K % 4 == 0 && pa.ld % 4 == 0 && pb.ld % 4 == 0 && env_int("AAA_SKINNY", 1)) {
+  if (Nj <= kSkinnyMaxCols && K % 4 == 0 && pa.ld % 4 == 0 && pb.ld % 4 == 0 && ab_int("AAA_SKINNY", 1)) {
     const int blocks = cdiv(cdiv(Mi, 4), 4);
     if (Nj == 1)
       hipLaunchKernelGGL((k_skinny_gemm<EP, 1>), dim3(blocks), dim3(256), 0, st, pa.src, pa.ld, Mi, pb.src, pb.ld, Nj,
@@ -455,7 +471,7 @@ static int wgrad_splits(int tiles, int K, int BK) {
 static int fused_splitk() { return std::max(2, std::min(4, env_int("AAA_FUSED_SPLITK", 3))); }
 // Ring depth of the split-K launches (2-4 stages: tiles in flight per workgroup; their few
 // k-steps per slice are latency-bound, not MFMA-bound).  AAA_SPLITK_NBUF.
-static int splitk_nbuf() { return std::max(2, std::min(4, env_int("AAA_SPLITK_NBUF", 2))); }
+static int splitk_nbuf() { return std::max(2, std::min(4, ab_int("AAA_SPLITK_NBUF", 2))); }
 template <class CK, class EP, typename T>
 static hipError_t step_gemm_splitk(const T* W, int ldw, int wrows, const T* src, const ConvGeo& g, int M,
                                    uint32_t src_bytes, const EP& ep, int Mi, int K, hipStream_t st, int nsplit,

@@ -33,8 +33,8 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     // bf16: FR = 2 frames per tile -- the 64 KB weight tile streamed once per two frames and twice the
     // MFMA work per DMA round trip (C3 4.97 -> 4.94 ms); fp32 keeps FR = 1 (C2 4.306 vs 4.341 ms)
     // (profiles/r02/ab/dgrad_fr.txt; AAA_DGRAD2_FR overrides)
-    const int fr = env_int("AAA_DGRAD2_FR", std::is_same<T, float>::value ? 1 : 2);
-    if (env_int("AAA_DGRAD2_HALO", 1)) {
+    const int fr = ab_int("AAA_DGRAD2_FR", std::is_same<T, float>::value ? 1 : 2);
+    if (ab_int("AAA_DGRAD2_HALO", 1)) {
       if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{});
       if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
         if (f32_split6() && fits(1, 128, 192)) return halo4(HaloCfgS6<128, 128, CKd, 2, 2, 1, 192>{});
@@ -43,10 +43,10 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
       // bf16, grids up to 21x21 (168x168 frames, C5): one frame per 512-column tile of 8 waves,
       // 32-channel chunks (two LDS images of 23x23 pixels), the epilogue in two column chunks
       if constexpr (!std::is_same<T, float>::value)
-        if (fits(1, 512, 640) && env_int("AAA_DGRAD2_WIDE", 1)) return halo4(HaloCfg<T, 128, 512, 32, 2, 4, 1, 640>{});
+        if (fits(1, 512, 640) && ab_int("AAA_DGRAD2_WIDE", 1)) return halo4(HaloCfg<T, 128, 512, 32, 2, 4, 1, 640>{});
     }
   }
-  if (env_int("AAA_CONV2_DGRAD_RING", 1)) {
+  if (ab_int("AAA_CONV2_DGRAD_RING", 1)) {
     // the LDS-DMA ring (dY2 is already in T), dY1 stored in T, conv1's bias
     // gradient summed from the fp32 values in the epilogue (no column-sum pass)
     constexpr int BKd = std::is_same<T, float>::value ? 32 : 64;
@@ -70,7 +70,7 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     };
     // K = 256: four BK steps per tile, so 256 columns per workgroup (twice the MFMA work per DMA round
     // trip of 32x128): C5 14.945 -> 14.74 ms per iteration (profiles/r02/ab/vision_tiles.txt); AAA_DGRAD2_TILE=0 the old tile
-    return env_int("AAA_DGRAD2_TILE", 1) == 1 ? classes(GemmCfg<T, 32, 256, BKd, 1, 4>{})
+    return ab_int("AAA_DGRAD2_TILE", 1) == 1 ? classes(GemmCfg<T, 32, 256, BKd, 1, 4>{})
                                              : classes(GemmCfg<T, 32, 128, BKd, 1, 4>{});
   }
   // register-staged fallback (fp32 only: dY2's loader converts from fp32)
@@ -106,7 +106,7 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
     // tiles of 4 waves, split-K over about one wave of workgroups, atomics from the accumulators
     // default 1 (C3 1.063M -> 1.075M frames/s, C5 277.4k -> 279.0k vs the register-staged GEMM;
     // 2 = the read-ahead ring, slower here: profiles/r03/ab/convwgrad/); 0 = register-staged
-    const int pipe = env_int("AAA_CONV2_WGRAD_PIPE", 1);
+    const int pipe = ab_int("AAA_CONV2_WGRAD_PIPE", 1);
     if (rows % 32 == 0 && pipe) {
       using CW = GemmCfg<T, 64, 256, 32, 1, 4>;
       using PA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
@@ -115,7 +115,7 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
       typename PB::Params pb{y1, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
                              (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
       EpiAtomicD ep{{gW, 512, 64, 512}};
-      const int ns = std::max(1, std::min(env_int("AAA_CONV2_WGRAD_WGS", 256) / 2, rows / (8 * CW::BK)));
+      const int ns = std::max(1, std::min(ab_int("AAA_CONV2_WGRAD_WGS", 256) / 2, rows / (8 * CW::BK)));
       if (pipe == 2) HIPCHK((launch_pipe_ra<CW, PA, PB, EpiAtomicD, 4>(pa, pb, ep, 64, 512, rows, ns, s)));
       else HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 64, 512, rows, ns, s)));
       return AAA_OK;
@@ -164,7 +164,7 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
     // waves over all (tap, channel) columns, BK = 64 pixels; a 16-B piece = 2 taps x 4 channels,
     // contiguous in the bordered RGBx image (KW = 8 even, pad 0: every piece in bounds)
     // default 1 (C3 +0.5 %, C5 +0.8 % vs the register-staged GEMM: profiles/r03/ab/convwgrad/)
-    const int pipe = env_int("AAA_CONV1_WGRAD_PIPE", 1);
+    const int pipe = ab_int("AAA_CONV1_WGRAD_PIPE", 1);
     if (rows1 % 64 == 0 && pipe) {
       using CW = GemmCfg<T, 32, 256, 64, 1, 4>;
       using PA = GRowsT<T, CW::BI, CW::BK, CW::NT>;
@@ -173,7 +173,7 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
       typename PB::Params pb{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
                              (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
       EpiAtomicD ep{{gW, 256, 32, 256}};
-      const int ns = std::max(1, std::min(env_int("AAA_CONV1_WGRAD_WGS", 256), rows1 / (8 * CW::BK)));
+      const int ns = std::max(1, std::min(ab_int("AAA_CONV1_WGRAD_WGS", 256), rows1 / (8 * CW::BK)));
       if (pipe == 2) HIPCHK((launch_pipe_ra<CW, PA, PB, EpiAtomicD, 4>(pa, pb, ep, 32, 256, rows1, ns, s)));
       else HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 32, 256, rows1, ns, s)));
       return AAA_OK;
@@ -181,7 +181,7 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
   }
   // AAA_CONV1_WGRAD_TILE=1 (A/B): one 32x256 tile covering every (tap, channel) column, so each
   // pixel's 8x8 window is gathered once instead of by four 64-column tiles
-  if (env_int("AAA_CONV1_WGRAD_TILE", 0) == 1) return run(GemmCfg<T, 32, 256, Cfg32For<T>::BK, 1, 4>{});
+  if (ab_int("AAA_CONV1_WGRAD_TILE", 0) == 1) return run(GemmCfg<T, 32, 256, Cfg32For<T>::BK, 1, 4>{});
   return run(Cfg32For<T>{});
 }
 
@@ -207,7 +207,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // (split-at-commit tiles hold 110 KB of LDS: one workgroup per CU, so one split per CU:
     // C2 655 us at 18-way against 679 at 36 and 845 at 27, profiles/r05/ab/wgrad_s6l/)
     const int per_cu = split6l_of<CW>::value ? device_cus() : 512;
-    const int ns = std::max(1, std::min(env_int("AAA_WGRAD_SPLIT", std::max(1, per_cu / tiles)), rows / CW::BK));
+    const int ns = std::max(1, std::min(ab_int("AAA_WGRAD_SPLIT", std::max(1, per_cu / tiles)), rows / CW::BK));
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
                    strf("register-staged %dx%d BK%d%s, %d-way split-K atomics [kernel: gemm_kernel+%d, %d, %d, +LdIm2colTB]",
                         CW::BI, CW::BJ, CW::BK, split6_of<CW>::value ? " (fp32 as bf16x6 split products)" : "", ns,
@@ -230,7 +230,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows, strf("LDS-DMA ring %dx%d BK%d, %d-deep [kernel: gemm_pipe_kernel+GIm2colT]", CW::BI, CW::BJ, CW::BK, NB));
     // split-K over pixels: about one resident wave of workgroups (fewer
     // passes of the output's atomics than the register path's ~1024)
-    const int wgs = env_int("AAA_WGRAD_WGS", 256);
+    const int wgs = ab_int("AAA_WGRAD_WGS", 256);
     const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
     HIPCHK((launch_pipe<CW, LA, LB, EpiAtomicD, NB, IL>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
@@ -247,7 +247,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     const int tiles = cdiv(512, CW::BI) * cdiv(1728, CW::BJ);
     TimerScope tim(AAA_TIMER_CORE_WGRAD, s, 2.0 * 512 * 1728 * rows,
                    strf("LDS-DMA read-ahead ring %dx%d BK%d, %d-deep [kernel: gemm_pipe_ra_kernel+GIm2colT]", CW::BI, CW::BJ, CW::BK, NB));
-    const int wgs = env_int("AAA_WGRAD_WGS", 256);
+    const int wgs = ab_int("AAA_WGRAD_WGS", 256);
     const int ns = std::max(1, std::min(wgs / tiles, rows / (8 * CW::BK)));
     HIPCHK((launch_pipe_ra<CW, LA, LB, EpiAtomicD, NB>(pa, pb, ep, 512, 1728, rows, ns, s)));
     return AAA_OK;
@@ -309,7 +309,9 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
     // 4 = 256x256 with each operand split once where it is committed to LDS (GemmCfgS6L, BK16,
     // two stages of bf16 part tiles); 5 = its 256x128 4-wave form; 6 (default) = 4 with two K
     // tiles of loads in flight: C2 633 vs 646 us (4) vs 776 (3) (profiles/r05/ab/wgrad_s6l/)
-    const int tile6 = env_int("AAA_WGRAD_S6_TILE", 6);
+    // (tiles 0-5: ablation builds only)
+#ifdef AAA_ABLATION
+    const int tile6 = ab_int("AAA_WGRAD_S6_TILE", 6);
     const int rc = tile6 == 1   ? s6(GemmCfgS6<128, 256, 32, 2, 2>{})
                    : tile6 == 2 ? s6(GemmCfgS6<256, 128, 32, 2, 2>{})
                    : tile6 == 3 ? s6(GemmCfgS6<256, 256, 32, 2, 4>{})
@@ -317,14 +319,20 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
                    : tile6 == 5 ? s6(GemmCfgS6L<256, 128, 16, 2, 2>{})
                    : tile6 == 6 ? s6(GemmCfgS6L<256, 256, 16, 2, 4, 2>{})
                                 : s6(GemmCfgS6<128, 128, 32, 2, 2>{});
+#else
+    const int rc = s6(GemmCfgS6L<256, 256, 16, 2, 4, 2>{});
+#endif
     if (rc) return rc;
   } else {
     // on the aux stream a small-footprint tile lets the chain's step kernels co-reside on a CU
-    const int wide = env_int("AAA_AUX_WIDE", aux ? 0 : 1);
-    // AAA_WGRAD_TILE=1 (A/B): 128x192 tiles, 1728 = 9 x 192 columns without the half-empty last tile of 128
+    const int wide = ab_int("AAA_AUX_WIDE", aux ? 0 : 1);
+#ifdef AAA_ABLATION   // AAA_WGRAD_TILE=1: 128x192 tiles, 1728 = 9 x 192 columns without the half-empty last tile
     const int rc = !wide ? wgrad_lstm(CfgFor<T>{})
-                   : env_int("AAA_WGRAD_TILE", 0) == 1 ? wgrad_lstm(GemmCfg<T, 128, 192, 32, 2, 2>{})
+                   : ab_int("AAA_WGRAD_TILE", 0) == 1 ? wgrad_lstm(GemmCfg<T, 128, 192, 32, 2, 2>{})
                                                        : wgrad_lstm(CfgWFor<T>{});
+#else
+    const int rc = !wide ? wgrad_lstm(CfgFor<T>{}) : wgrad_lstm(CfgWFor<T>{});
+#endif
     if (rc) return rc;
   }
   return AAA_OK;
@@ -619,21 +627,37 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // gradient summed from the tile in the epilogue (no column-sum pass)
         EpiStoreBiasT<float> ep{Wf(L.dY2) + (size_t)lo * M * 64, 64, 64, rows, grads + L.poff[C1B]};
         using ED = EpiStoreBiasT<float>;
-        using HF6 = HaloCfgS6<64, 128, 32, 1, 2, 1, 176>;   // one 11x11 frame per tile, its dZ image in LDS
-        if (f32_split6() && halo_fits<HF6>(L.h, L.w, 512) && env_int("AAA_HALO_DX_F32", 0)) {
-          // A/B only: the halo-staged conv (every dZ element read once per channel chunk, not once
-          // per tap as the ring's gather does) on split operands -- C2 478 vs 370 us for the ring
-          // (profiles/r04/ab/halo_dx_f32_c2_*.json: 2 waves per 64x128 tile, one frame each)
-          const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
-          HIPCHK((launch_halo<HF6>(hp, ep, s)));
-        } else if (f32_split6()) {   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6)
-          // (one wave per 64 rows -- 64x128 of 2 waves, 64x256 of 2 / 4 -- measured slower: 380-395 vs 360 us)
-          // A/B: 0 = 64x64, 1 = 64x128 (C2 355 / 344 / 373 us), 2 = 64x64 BK64, 3 = 64x128 with the K
-          // order channel-chunk-major (ConvGeo::cmaj: a chunk's 9 taps adjacent, so the 3x3 re-reads of
-          // dZ rows hit in L2 -- tap-major, the launch fetched 1.2 GB for 158 MB of dZ, PMC)
-          // default 4: 1 with the weights pre-split (C2 340 vs 357 us, profiles/r04/ab/README.md)
-          switch (env_int("AAA_DX_S6_TILE", 4)) {
-            case 3: {   // (A/B only: measured no faster, 365 vs 353 us -- the ring is not fetch-bound)
+        const int dx6 = f32_split6() ? ab_int("AAA_DX_S6_TILE", 4) : -1;
+        if (dx6 == 4) {   // the ring tile on the bf16 MFMA with three-way split operands (gemm.h SPLIT6):
+          // 64x128 with the weights pre-split (k_WdT6 planes), only dZ split in the loop
+          // (C2 340 vs 357 us for the in-loop split of both, profiles/r04/ab/README.md)
+          using C6 = GemmCfgS6<64, 128, 32, 2, 2>;
+          using LA3 = GRows3B<64, 32, C6::NT>;
+          using LBx = GIm2colB<float, 128, 32, C6::NT>;
+          HIPCHK((launch_pipe<C6, LA3, LBx, ED, 2>(
+              typename LA3::Params{(const __bf16*)(pk + L.k_WdT6), 4608, 64, (size_t)64 * 4608},
+              typename LBx::Params{dz, g, rows, zb}, ep, 64, rows, 4608, 1, s)));
+        } else if (dx6 < 0) {   // exact fp32 MFMA (AAA_F32_SPLIT6=0)
+          if (pipe_batched())
+            HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+          else
+            HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
+        } else {
+#ifdef AAA_ABLATION
+          // the measured-slower variants (ablation builds): 0 = 64x64, 1 = 64x128 in-loop split
+          // (C2 355 / 344 us), 2 = 64x64 BK64, 3 = 64x128 channel-chunk-major K order (ConvGeo::cmaj;
+          // 365 vs 353 us), 5 = tile 4 with dZ pre-split too (GIm2colB3 over split_planes: 467-473 vs
+          // 337 us), 6 = the halo-staged conv on split operands (C2 478 vs 370 us,
+          // profiles/r04/ab/halo_dx_f32_c2_*.json)
+          using HF6 = HaloCfgS6<64, 128, 32, 1, 2, 1, 176>;   // one 11x11 frame per tile, its dZ image in LDS
+          switch (dx6) {
+            case 6: {
+              if (!halo_fits<HF6>(L.h, L.w, 512)) return fail(AAA_E_ARG, "AAA_DX_S6_TILE=6: grid too large");
+              const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
+              HIPCHK((launch_halo<HF6>(hp, ep, s)));
+              break;
+            }
+            case 3: {
               HIPCHK(reorder_cmaj(WdT, 64, 512, 9, 32, (float*)(pk + L.k_WdTc), s));   // its weights, re-laid here
               ConvGeo gc = g;
               gc.cmaj = 32;
@@ -644,16 +668,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
             case 1:
               HIPCHK((step_gemm<GemmCfgS6<64, 128, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
-            case 4: {   // 64x128 with the weights pre-split (k_WdT6 planes): only dZ is split in the loop
-              using C6 = GemmCfgS6<64, 128, 32, 2, 2>;
-              using LA3 = GRows3B<64, 32, C6::NT>;
-              using LBx = GIm2colB<float, 128, 32, C6::NT>;
-              HIPCHK((launch_pipe<C6, LA3, LBx, ED, 2>(
-                  typename LA3::Params{(const __bf16*)(pk + L.k_WdT6), 4608, 64, (size_t)64 * 4608},
-                  typename LBx::Params{dz, g, rows, zb}, ep, 64, rows, 4608, 1, s)));
-              break;
-            }
-            case 5: {   // (A/B) case 4 with dZ pre-split too (L.dZ6 planes, bit-identical to the in-loop split)
+            case 5: {
               if (!L.dZ6) return fail(AAA_E_ARG, "AAA_DX_S6_TILE=5 set after the workspace was laid out");
               using C6 = GemmCfgS6<64, 128, 32, 2, 2>;
               using LA3 = GRows3B<64, 32, C6::NT>;
@@ -665,23 +680,15 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                   typename LB3::Params{z6, g, rows, zb / 2, (size_t)rows * 512}, ep, 64, rows, 4608, 1, s)));
               break;
             }
-
             case 2:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 64, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
               break;
             default:
               HIPCHK((step_gemm<GemmCfgS6<64, 64, 32, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s)));
           }
-        } else switch (pipe_batched() ? env_int("AAA_DX_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
-          case -1: HIPCHK((step_gemm<CfgFor<T>, false, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
-          case 1: HIPCHK((step_gemm<Cfg64For<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
-          case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED, 3, true>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
-          case 3: HIPCHK((step_gemm<CfgJFor<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
-          case 4:   // 64x64, 2-way in-WG split-K (8 waves), BK64
-            HIPCHK((step_gemm<GemmCfg<T, 64, 64, 64, 2, 2, 2>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608,
-                                                                                s)));
-            break;
-          default: HIPCHK((step_gemm<CfgFor<T>, true, T, T, ED>(WdT, 4608, 64, dz, g, rows, zb, ep, 64, 4608, s))); break;
+#else
+          return fail(AAA_E_ARG, "AAA_DX_S6_TILE %d: ablation builds only", dx6);
+#endif
         }
       } else {
         // bf16: dY2 stored bf16 (its readers round it to bf16 anyway), conv2's
@@ -692,10 +699,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         using HD = HaloCfg<__bf16, 64, 128, 64, 1, 2, 1, 176>;
         // 21x21 grids (168x168 frames): one frame per 512-column tile of 4 waves, 32-channel chunks
         using HW = HaloCfg<__bf16, 64, 512, 32, 1, 4, 1, 576>;
-        if (halo_fits<HD>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+        if (halo_fits<HD>(L.h, L.w, 512) && ab_int("AAA_HALO_DX", 1)) {
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HD>(hp, ep, s)));
-        } else if (halo_fits<HW>(L.h, L.w, 512) && env_int("AAA_HALO_DX", 1)) {
+        } else if (halo_fits<HW>(L.h, L.w, 512) && ab_int("AAA_HALO_DX", 1)) {
           const HaloParams hp{WdT, 4608, 64, dz, 512, 0, 512, zb, L.h, L.w, (hi - lo) * L.B, 1};
           HIPCHK((launch_halo<HW>(hp, ep, s)));
         } else {
@@ -723,7 +730,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       else if (!rc)
         rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
       if (rc) return rc;
-      if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
+      if (f32 && !ab_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
     }
     return AAA_OK;
   };
@@ -797,7 +804,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                         cqm_layout(L)};
         // single-workgroup and paired kernels: row-padded images (recur_bwd.h kBwIBP) where they fit
         // (C3 LDS bank conflicts 52.8 -> 10.0 %: profiles/r04/ab/rowpad_c3/); AAA_BW_ROWPAD=0 (A/B): 272-B rows only
-        rp.rowpad = fb <= 2 && env_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
+        rp.rowpad = fb <= 2 && ab_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));
@@ -1031,7 +1038,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         const int rc = vision_bwd<T>(L, pk, Wt(L.dY2), Wt(L.Y1), Wt(L.Xp), Wt(L.dY1), F, Wf(L.gWp2), Wf(L.gWp1),
                                      grads + L.poff[C0B], st, L.xpc < L.F ? io->frames : nullptr);
         if (rc) return rc;
-        if (f32 && !env_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
+        if (f32 && !ab_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(Wt(L.dY1), 32, rows1, 32, grads + L.poff[C0B], st));
       }
     }
     HIPCHK(unpack_cv((phases & AAA_BWD_CORE) ? Wf(L.gWpl) : nullptr, Wf(L.gbl), core_unpack, Wf(L.gWp2),

@@ -186,7 +186,7 @@ static int cnn_bwd_impl(const CnnLayout& CL, const char* pk, const float* dy2, f
   const int rc = vision_bwd<T>(L, pk, dy2t, (const T*)(ws + CL.Y1), (T*)(ws + CL.Xp), dY1, N, gW2, gW1,
                                grads + L.poff[C0B], st);
   if (rc) return rc;
-  if (std::is_same<T, float>::value && !env_int("AAA_CONV2_DGRAD_RING", 1))
+  if (std::is_same<T, float>::value && !ab_int("AAA_CONV2_DGRAD_RING", 1))
     HIPCHK(colsum(dY1, 32, N * L.P1, 32, grads + L.poff[C0B], st));
   HIPCHK(unpack_conv(gW2, 64, 32, 4, grads + L.poff[C1W], st));
   HIPCHK(unpack_conv1_rgbx(gW1, grads + L.poff[C0W], st));

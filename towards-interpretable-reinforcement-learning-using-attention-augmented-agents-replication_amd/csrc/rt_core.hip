@@ -87,7 +87,7 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   // and read by conv1's weight gradient; AAA_XP_CHUNK=n (A/B) keeps a chunk of n frames instead, rebuilt
   // from the observation right before conv1 (layered forward) or its weight gradient reads it (measured
   // slower: C3 vision backward 0.368 -> 0.666 ms for -0.03 ms in the forward)
-  const int xc = env_int("AAA_XP_CHUNK", 0);
+  const int xc = ab_int("AAA_XP_CHUNK", 0);
   L.xpc = xc > 0 ? (int)std::min<size_t>(F, (size_t)std::max(64, xc)) : (int)F;
   L.Xp = take((size_t)L.xpc * (L.H + 2) * (L.W + 2) * 4 * e);
   L.Y1 = take(F * L.P1 * 32 * e);
@@ -113,7 +113,7 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.dC = take(M * 128 * 4);
   L.dZ = take(F * P * 512 * e);                          // gate pre-activation grads, GEMM operand type
   // (A/B, AAA_DX_S6_TILE=5) fp32 dZ as three bf16 planes for the batched dx (0 = none)
-  L.dZ6 = take(e == 4 && env_int("AAA_DX_S6_TILE", 4) == 5 ? F * P * 512 * 6 : 0);
+  L.dZ6 = take(e == 4 && ab_int("AAA_DX_S6_TILE", 4) == 5 ? F * P * 512 * 6 : 0);
   // gate-bias partials per (step, column tile | frame half); the fp32 split-K chain's tiles are kSplitBj pixels
   const size_t zp_rows = std::max({(M + 31) / 32, 2 * (size_t)L.B,
                                    L.esz == 4 && bptt_splitk_fits(M) ? (M + kSplitBj - 1) / kSplitBj : 0});
@@ -294,7 +294,7 @@ static std::mutex g_aux_mu;
 // chain's step kernels ~2x (stream priority does not keep CUs free for them),
 // 6.31-6.55 ms vs 6.15 ms serial; so overlap is opt-in (AAA_OVERLAP=1).
 hipStream_t aux_stream() {
-  if (env_int("AAA_OVERLAP", 0) == 0) return nullptr;
+  if (ab_int("AAA_OVERLAP", 0) == 0) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> lk(g_aux_mu);
@@ -401,7 +401,7 @@ int f32_frames(const Layout& L) {
 // workgroups per frame as the forward's (AAA_FRAMES_BWD = 0 / 1 / 2 forces it).
 // Start offset of half the frames of the bf16 frame-resident kernels (common.h
 // stagger_wait), in microseconds -> 100-MHz ticks.
-int rec_stagger(const char* env) { return 100 * env_int(env, 0); }
+int rec_stagger(const char* env) { return 100 * ab_int(env, 0); }
 // default on: C2 150.6k -> 175.6k frames/s (profiles/r04/ab_split6); AAA_F32_SPLIT6=0 restores the fp32 MFMA
 bool f32_split6() { return env_int("AAA_F32_SPLIT6", 1) != 0; }
 // Band mode (recur_bwd.h BAND) wherever the forward runs in band mode: kRecBands.
@@ -413,7 +413,7 @@ int frames_bwd(const Layout& L, bool g16) {
   return frames_fwd(L) ? frames_g(L, "AAA_FRAMES_BWD") : 0;
 }
 int cqm_layout(const Layout& L) {
-  static const int mask = env_int("AAA_CQM", kCqmC | kCqmG | kCqmDO) & 7;   // A/B: tools/gpu_ab.sh
+  static const int mask = ab_int("AAA_CQM", kCqmC | kCqmG | kCqmDO) & 7;   // A/B: tools/gpu_ab.sh
   return frames_bwd(L, gates_f16(L.dt, L.B * L.P)) != 0 ? mask : 0;
 }
 

@@ -59,7 +59,7 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
   const int P = L.P;
   bool banded = false;   // bf16 frames too large for the frame-resident encoder: the banded conv1 (vision.h)
   if constexpr (std::is_same<T, __bf16>::value) {
-    if (band_fits(L.H, L.W, L.H1, L.W1) && env_int("AAA_VIS_BAND", 1)) {
+    if (band_fits(L.H, L.W, L.H1, L.W1) && ab_int("AAA_VIS_BAND", 1)) {
       const VisBandParams bp{frames, (const __bf16*)(pk + L.k_Wp1), prm + L.poff[C0B], xp_full ? Xp : nullptr, Y1, F,
                              L.H, L.W, L.H1, L.W1};
       HIPCHK(L.fu8 ? vision_conv1_band<uint8_t>(bp, st) : vision_conv1_band<float>(bp, st));
@@ -92,7 +92,7 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
         return AAA_OK;
       };
       // K = 256 is four BK steps: a wider column tile does more MFMA work per DMA round trip (A/B: AAA_CONV1_TILE)
-      const int c1t = env_int("AAA_CONV1_TILE", 0);
+      const int c1t = ab_int("AAA_CONV1_TILE", 0);
       int rc;
       if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
         if (f32_split6()) rc = conv1(GemmCfgS6<32, 128, BKc, 1, 4>{});
@@ -105,7 +105,7 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
   }
   if constexpr (std::is_same<T, __bf16>::value && std::is_same<OT, __bf16>::value) {
     // after the banded conv1: the banded conv2 (vision.h), Y1 rows staged in LDS per band
-    if (banded && band2_fits(L.H1, L.W1, L.h, L.w) && env_int("AAA_VIS_BAND2", 1)) {
+    if (banded && band2_fits(L.H1, L.W1, L.h, L.w) && ab_int("AAA_VIS_BAND2", 1)) {
       const VisBand2Params bp{Y1, (const __bf16*)(pk + L.k_Wp2), prm + L.poff[C1B], out, out_ld, F, L.H1, L.W1, L.h, L.w};
       HIPCHK(vision_conv2_band(bp, st));
       return AAA_OK;
@@ -288,9 +288,10 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
     const T* WpX = (const T*)(pk + L.k_WpX);
     const T* xs0 = Wt(L.XH) + (size_t)lo * M * 192;
     const uint32_t xb = (uint32_t)((size_t)(hi - lo) * M * 192 * L.esz);
-    using EX = EpiStoreT<float>;
-    switch (pipe_batched() ? env_int("AAA_XPART_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
+    switch (pipe_batched() ? ab_int("AAA_XPART_TILE", 0) : -1) {   // A/B: tools/ab_batched.sh
       case -1: HIPCHK((step_gemm<CfgFor<T>, false>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
+#ifdef AAA_ABLATION   // the measured-slower x-part tiles
+      using EX = EpiStoreT<float>;
       case 1: HIPCHK((step_gemm<Cfg64For<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
       case 2: HIPCHK((step_gemm<CfgFor<T>, true, T, T, EX, 3, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
       case 3: HIPCHK((step_gemm<CfgJFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
@@ -298,6 +299,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
       case 5:
         HIPCHK((step_gemm<GemmCfg<T, 128, 128, 32, 2, 2>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs)));
         break;
+#endif
       default: HIPCHK((step_gemm<CfgFor<T>, true>(WpX, 576, 512, xs0, g, rows, xb, ep, 512, 576, xs))); break;
     }
     return AAA_OK;

@@ -24,6 +24,11 @@ extern "C" {
 
 int aaa_abi_version(void) { return AAA_ABI_VERSION; }
 
+#ifdef AAA_ABLATION
+// Present only in the A/B library (make ablation): tells the tests and tools which build is loaded.
+int aaa_ablation_build(void) { return 1; }
+#endif
+
 int aaa_fastdiv_check(unsigned d, unsigned lo, unsigned hi, unsigned long long* mismatches) {
   if (!mismatches || d == 0 || d >= (1u << 31) || hi > (1u << 31) || lo > hi)
     return fail(AAA_E_ARG, "fastdiv_check: need 1 <= d < 2^31 and lo <= hi <= 2^31");
@@ -234,8 +239,9 @@ int aaa_core_elem_bytes(const aaa_cfg* cfg, int* gate_bytes, int* h_bytes) {
   if (!gate_bytes || !h_bytes) return fail(AAA_E_ARG, "core_elem_bytes: NULL output");
   Layout L;
   if (int r = build_layout(cfg, L)) return r;
-  *gate_bytes = core_gate_bytes(L);
-  *h_bytes = L.esz;
+  const bool ok = !cqm_layout(L);   // channel-quad-major slices: no export / import (0 bytes)
+  *gate_bytes = ok ? core_gate_bytes(L) : 0;
+  *h_bytes = ok ? L.esz : 0;
   return AAA_OK;
 }
 

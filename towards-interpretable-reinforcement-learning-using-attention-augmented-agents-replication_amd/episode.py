@@ -144,7 +144,9 @@ class Episode:
         # step block t // STORE_BLOCK -> (gates, c, h) of its steps, up to the byte budget; bf16 runners
         # keep their own element types (fp16 gates, bf16 h), not the channel-quad-major slices of
         # the large-batch frame-resident BPTT (no episode runs at such batches)
-        store_on = os.environ.get("AAA_EPISODE_STORE", "1") != "0"
+        # (not for the channel-quad-major slices of large-batch bf16 geometries: their products
+        # stay in the frame-resident layout, core_dtypes() is None, and the backward recomputes)
+        store_on = os.environ.get("AAA_EPISODE_STORE", "1") != "0" and runner.core_dtypes() is not None
         self.store = {} if store_on else None
         self._slots = {}
         self.store_budget = int(float(os.environ.get("AAA_EPISODE_STORE_MB", "4096")) * 2**20)

@@ -121,25 +121,35 @@ class UnrollRunner:
 
     def core_dtypes(self):
         """Element types of (gates, c, h) in core_export / core_import: fp32 runners
-        all fp32; bf16 runners the workspace's gate storage (fp16) and bf16 h."""
+        all fp32; bf16 runners the workspace's gate storage (fp16) and bf16 h.  None
+        where the geometry's products cannot be transferred (the channel-quad-major
+        slices of large-batch bf16 runs)."""
         if not hasattr(self, "_core_dt"):
             ge, he = ctypes.c_int(), ctypes.c_int()
             N.check(self.lib.aaa_core_elem_bytes(ctypes.byref(self.cfg), ctypes.byref(ge), ctypes.byref(he)),
                     "core_elem_bytes")
-            self._core_dt = (torch.float16 if ge.value == 2 else torch.float32, torch.float32,
-                             torch.bfloat16 if he.value == 2 else torch.float32)
+            self._core_dt = None if ge.value == 0 else (torch.float16 if ge.value == 2 else torch.float32,
+                                                        torch.float32,
+                                                        torch.bfloat16 if he.value == 2 else torch.float32)
         return self._core_dt
+
+    def _core_dts(self):
+        dts = self.core_dtypes()
+        if dts is None:
+            raise RuntimeError("aaa: this geometry keeps the recurrence's products in channel-quad-major slices; "
+                               "core_export / core_import do not apply (core_dtypes() is None)")
+        return dts
 
     def core_export(self, workspace, t0, n, gates, c, h):
         """Steps [t0, t0+n) of the recurrence's products -> gates, c, h (core_shapes, core_dtypes)."""
-        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self.core_dtypes()):
+        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self._core_dts()):
             _check_out(x, shp, dt)
         N.check(self.lib.aaa_core_export(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
                                          N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_export")
 
     def core_import(self, workspace, t0, n, gates, c, h):
         """The inverse of core_export, into a workspace for forward(phases=FWD_VISION | FWD_TAIL)."""
-        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self.core_dtypes()):
+        for x, shp, dt in zip((gates, c, h), self.core_shapes(n), self._core_dts()):
             _check_out(x, shp, dt)
         N.check(self.lib.aaa_core_import(ctypes.byref(self.cfg), N.ptr(workspace), int(t0), int(n), N.ptr(gates),
                                          N.ptr(c), N.ptr(h), N.stream_ptr(self.device)), "core_import")
