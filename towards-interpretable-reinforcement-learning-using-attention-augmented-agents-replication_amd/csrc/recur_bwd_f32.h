@@ -26,8 +26,16 @@
 // K order: 72 quads (9 taps x 8 groups of 8 dZ rows);
 // lane (r32, hh) reads the 4 rows 8 q8 + 4 hh .. + 3 of its pixel with one
 // ds_read_b128 (4 k-steps) and the matching 16 B of the fragment-order weights
-// (k_pack_wb32).  The dx rows stay in the batched dgrad GEMM after this kernel
-// (runtime.hip), which runs at the MFMA rate already.
+// (k_pack_wb32).
+// DX (the production S6 + PS kernel): the 64 dx rows (conv2's output gradient,
+// rows 0..63 of W^T) ride in the same K loop on the same pre-split dZ image --
+// a third 32-row block per wave (dx row block rw, its two column blocks), so
+// dZ is split once, where the gate backward produces it, for both dgrads
+// (the batched dx GEMM it replaces split each dZ element once per tap it
+// gathered).  The dx partials travel with the dh partials: workgroup kh owns dx
+// channels [8 kh, 8 kh + 8), sums the eight partials of its channels and
+// writes them to dY2 (every step, s = T-1 .. 0), and keeps their pixel sums
+// for conv2's bias gradient (dxb).
 #pragma once
 #include "common.h"
 #include "epilogues.h"
@@ -59,8 +67,26 @@ inline hipError_t pack_wb32(const float* WdT, float* Wb, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Exchange buffer floats: [kB32NBUF][B][8 dst][8 src][128 px][16 ch]
-inline size_t b32_xpart_floats(int B) { return (size_t)kB32NBUF * B * 64 * 128 * 16; }
+// Exchange buffer floats: [kB32NBUF][B][8 dst][8 src][128 px][kB32XC ch]: 16 dh channels, then
+// (DX) the destination's 8 dx channels
+constexpr int kB32XC = 24;
+inline size_t b32_xpart_floats(int B) { return (size_t)kB32NBUF * B * 64 * 128 * kB32XC; }
+
+// Wx[(((kh * kB32QP + q) * 2 + rb) * 64 + lane) * 4 + j] =
+//   WdT[32 rb + lane % 32][tap * 512 + 64 kh + 8 q8 + 4 (lane / 32) + j]: the dx rows (DX), k_pack_wb32's order
+static __global__ void __launch_bounds__(256) k_pack_wx32(const float* __restrict__ WdT, float* __restrict__ Wx) {
+  const int i = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
+  if (i >= 8 * kB32QP * 2 * 64) return;
+  const int lane = i & 63, rb = (i >> 6) & 1, kq = i >> 7, q = kq % kB32QP, kh = kq / kB32QP;
+  const int qq = q % kB32Q, tap = qq >> 3, q8 = qq & 7;
+  const int row = 32 * rb + (lane & 31), k = tap * 512 + 64 * kh + 8 * q8 + 4 * (lane >> 5);
+  *reinterpret_cast<f32x4*>(Wx + (size_t)i * 4) = *reinterpret_cast<const f32x4*>(WdT + (size_t)row * 4608 + k);
+}
+
+inline hipError_t pack_wx32(const float* WdT, float* Wx, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack_wx32, dim3((8 * kB32QP * 2 * 64 + 255) / 256), dim3(256), 0, st, WdT, Wx);
+  return hipGetLastError();
+}
 
 struct RecBwdF32Params {
   const float* Wb;     // fragment-order W_h^T (k_pack_wb32)
@@ -78,6 +104,9 @@ struct RecBwdF32Params {
   int T, B, h, w, P;
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
   const u32x2* Wb6 = nullptr;   // S6: the three-way split of Wb (recur_f32.h k_split_frag)
+  const u32x2* Wx6 = nullptr;   // DX: the three-way split of Wx (k_pack_wx32)
+  float* dx = nullptr;          // DX: (T, B, P, 64) <- conv2's output gradient (dY2)
+  float* dxb = nullptr;         // DX: (B, 64) <- its pixel-and-step sums (conv2's bias gradient per frame)
 };
 
 #ifdef AAA_STAMPS
@@ -101,14 +130,16 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 // borderless, the zero pixel P, pixel pitch 400 B, chunk (part * 4 + g) * 2 + hh for the
 // 16-row group g) -- the gate backward splits each dZ value once as it writes the image,
 // and the K loop reads bf16 parts only (no per-wave split of the B fragments).
-template <int ABL = 0, bool S6 = false, int PDS = kB32PD, bool PS = false>
+template <int ABL = 0, bool S6 = false, int PDS = kB32PD, bool PS = false, bool DX = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_convlstm_bwd_f32(RecBwdF32Params p) {
   static_assert(!PS || S6, "PS: the split-product kernel");
+  static_assert(!DX || PS, "DX: the pre-split kernel");
+  constexpr int NR = DX ? 3 : 2;                 // 32-row blocks per wave: two of dh (+ one of dx)
   constexpr int G = 8, NG = 2;                   // NG: (pixel, 4-channel) groups per thread (484 <= 512)
   constexpr int IMB = PS ? kPsXB : kB32IB;
   __shared__ __attribute__((aligned(16))) unsigned char zim[IMB];   // own dZ rows of the current step
-  __shared__ __attribute__((aligned(16))) f32x4 own[128][4];           // own partial dh [px][channel quad]
+  __shared__ __attribute__((aligned(16))) f32x4 own[128][DX ? 6 : 4];  // own partial dh [px][quad] (+ dx: quads 4, 5)
   __shared__ __attribute__((aligned(16))) float bred[4][64];           // per-wave bias partials
 
   const int blk = (int)blockIdx.x, xcd = blk & 7, loc = blk >> 3;
@@ -126,7 +157,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   auto sw16 = [](int q, int key) { return (q ^ (key & 15)) << 4; };
   // exchange slot of (buffer, destination, source): [128 px][16 ch]
   auto xslot = [&](int buf, int dst, int src) {
-    return p.xp + ((((size_t)buf * p.B + b) * 8 + dst) * 8 + src) * 128 * 16;
+    return p.xp + ((((size_t)buf * p.B + b) * 8 + dst) * 8 + src) * 128 * kB32XC;
   };
 
   {  // zero the image (borders / the zero pixel stay zero)
@@ -228,14 +259,21 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                          rsw6, lane * 8, (((kh * kB32QP + q) * 4 + 2 * rw + r) * 3 + part) * 512, 0));
   };
-  u32x2 a6[S6 ? PD : 1][2][3];
+  // DX: the dx rows' stream (k_pack_wx32 + k_split_frag): row block rw of the two
+  const __amdgpu_buffer_rsrc_t rsx6 = make_rsrc(p.Wx6, DX ? (uint32_t)(8 * kB32QP * 2 * 3 * 512) : 0u);
+  auto ldx6 = [&](int q, int part) {
+    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         rsx6, lane * 8, (((kh * kB32QP + q) * 2 + rw) * 3 + part) * 512, 0));
+  };
+  auto lda6r = [&](int q, int r, int part) { return r < 2 ? lda6(q, r, part) : ldx6(q, part); };
+  u32x2 a6[S6 ? PD : 1][NR][3];
 #pragma unroll
   for (int s = 0; s < PD - 1; ++s)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < NR; ++r) {
       if constexpr (S6) {
 #pragma unroll
-        for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6(s, r, part);
+        for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6r(s, r, part);
       } else {
         af[s][r] = lda(s, r);
       }
@@ -245,14 +283,16 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
   // orientation) reads dZ at (y + 1 - ky, x + 1 - kx) (ConvGeo transposed gather)
   auto tapoff = [&](int tap) { return (2 - tap / 3) * W2 + 2 - tap % 3; };
   auto tapkey = [&](int tap) { return (2 - tap / 3) * p.w + 2 - tap % 3; };
-  const int nsteps = p.T - 1 + (p.dh0 ? 1 : 0);   // dgrads: dZ_{T-1} .. dZ_1 (+ dZ_0 for dh0)
+  // dgrads: dZ_{T-1} .. dZ_1 (+ dZ_0 for dh0, or, with DX, for dx_0)
+  const int nsteps = p.T - 1 + ((p.dh0 || DX) ? 1 : 0);
+  f32x4 dxs = {0.f, 0.f, 0.f, 0.f};   // DX: this thread's dx quad summed over its pixel and the steps
   for (int it = 0; it < nsteps; ++it) {
     const int s = p.T - 1 - it;   // this dgrad reads dZ_s and yields dh_{s-1}
     const int buf = it % kB32NBUF;
     AAA_B32_STAMP(it, 0);
-    f32x16 acc[2][2];
+    f32x16 acc[NR][2];
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -305,25 +345,25 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
 #pragma unroll
         for (int q8 = 0; q8 < 8; q8 += 2) {
           const int pb = (q8 >> 1) & 1, nb = pb ^ 1;
-          bf16x8 a3[2][3];
+          bf16x8 a3[NR][3];
 #pragma unroll
-          for (int r = 0; r < 2; ++r)
+          for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int part = 0; part < 3; ++part)
               a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8 % PD][r][part].x, a6[q8 % PD][r][part].y,
                                                              a6[q8 % PD + 1][r][part].x, a6[q8 % PD + 1][r][part].y});
 #pragma unroll
-          for (int r = 0; r < 2; ++r)
+          for (int r = 0; r < NR; ++r)
 #pragma unroll
             for (int part = 0; part < 3; ++part) {
-              a6[(q8 + PD - 1) % PD][r][part] = lda6(qt + q8 + PD - 1, r, part);
-              a6[q8 % PD][r][part] = lda6(qt + q8 + PD, r, part);
+              a6[(q8 + PD - 1) % PD][r][part] = lda6r(qt + q8 + PD - 1, r, part);
+              a6[q8 % PD][r][part] = lda6r(qt + q8 + PD, r, part);
             }
           if (q8 < 6) ldq(tap, (q8 >> 1) + 1, bq[nb]);
           else if (tap < 8) ldq(tap + 1, 0, bq[nb]);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {
+          for (int r = 0; r < NR; ++r) {
             const bf16x8 ah = a3[r][0], am = a3[r][1], al = a3[r][2];
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
@@ -446,11 +486,30 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
             own[px][cl >> 2] = v;
           } else if constexpr (!(ABL & 8)) {
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v),
-                                                   make_rsrc(xslot(buf, dst, kh), 128 * 16 * 4),
-                                                   (uint32_t)((px * 16 + cl) * 4), 0, kSC1);
+                                                   make_rsrc(xslot(buf, dst, kh), 128 * kB32XC * 4),
+                                                   (uint32_t)((px * kB32XC + cl) * 4), 0, kSC1);
           }
         }
       }
+    if constexpr (DX) {   // dx tile (row block rw): element 4g + e = dx channel 32 rw + 8 g + 4 hh + e,
+      // owned by workgroup 4 rw + g at its quad hh
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int px = 32 * (2 * cw + c) + r32;
+        if (px >= P) continue;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int dst = 4 * rw + g;
+          const f32x4 v{acc[2][c][4 * g], acc[2][c][4 * g + 1], acc[2][c][4 * g + 2], acc[2][c][4 * g + 3]};
+          if (dst == kh)
+            own[px][4 + hh] = v;
+          else
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v),
+                                                   make_rsrc(xslot(buf, dst, kh), 128 * kB32XC * 4),
+                                                   (uint32_t)((px * kB32XC + 16 + 4 * hh) * 4), 0, kSC1);
+        }
+      }
+    }
     // publish this step's partials: every wave's stores retired, a barrier, one flag store
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_lds();
@@ -469,18 +528,38 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
         for (int j = 0; j < G - 1; ++j) {
           const int src = j < kh ? j : j + 1;
           pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                make_rsrc(xslot(buf, kh, src), 128 * 16 * 4),
-                                                (uint32_t)((px * 16 + 4 * cq) * 4), 0, kSC1));
+                                                make_rsrc(xslot(buf, kh, src), 128 * kB32XC * 4),
+                                                (uint32_t)((px * kB32XC + 4 * cq) * 4), 0, kSC1));
         }
 #pragma unroll
         for (int j = 0; j < G - 1; ++j) dhv[n] += pv[j];
       }
     }
-    if (s == 0) {   // dh0 = dh_{-1}: no gate backward
+    if constexpr (DX) {   // dx_s of the workgroup's 8 channels: thread -> (pixel tid / 2, quad tid % 2)
+      const int px = tid >> 1, xq = tid & 1;
+      f32x4 v = own[px][4 + xq];
+      f32x4 pv[G - 1];
 #pragma unroll
-      for (int n = 0; n < NG; ++n) {
-        const int px = (tid + 256 * n) >> 2;
-        if (px < P) *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + px) * 128 + 16 * kh + 4 * cq) = dhv[n];
+      for (int j = 0; j < G - 1; ++j) {
+        const int src = j < kh ? j : j + 1;
+        pv[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              make_rsrc(xslot(buf, kh, src), 128 * kB32XC * 4),
+                                              (uint32_t)((px * kB32XC + 16 + 4 * xq) * 4), 0, kSC1));
+      }
+#pragma unroll
+      for (int j = 0; j < G - 1; ++j) v += pv[j];   // summed in source order: the same whoever is last
+      if (px < P) {
+        *reinterpret_cast<f32x4*>(p.dx + ((size_t)s * M + (size_t)b * P + px) * 64 + 8 * kh + 4 * xq) = v;
+        dxs += v;
+      }
+    }
+    if (s == 0) {   // dh0 = dh_{-1}: no gate backward
+      if (p.dh0) {
+#pragma unroll
+        for (int n = 0; n < NG; ++n) {
+          const int px = (tid + 256 * n) >> 2;
+          if (px < P) *reinterpret_cast<f32x4*>(p.dh0 + ((size_t)b * P + px) * 128 + 16 * kh + 4 * cq) = dhv[n];
+        }
       }
       break;
     }
@@ -521,6 +600,24 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + px) * 128 + 16 * kh + 4 * cq) =
           f32x4{dcr[n][0], dcr[n][1], dcr[n][2], dcr[n][3]};
   }
+  if constexpr (DX) {   // conv2's bias gradient of this frame's 8 channels: sum the pixels (lanes of equal parity)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = dxs[e];
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      dxs[e] = v;
+    }
+    __syncthreads();   // (bred's last readers: bias_flush)
+    if (lane < 2)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bred[wave][4 * lane + e] = dxs[e];
+    __syncthreads();
+    if (tid < 8) p.dxb[(size_t)b * 64 + 8 * kh + tid] = bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid];
+  }
 }
 
 inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 = false) {
@@ -538,6 +635,11 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 =
     return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4>), f32_grid(p.B, 8), 256, p,
                            st);
 #endif
+  if (s6 && p.dx) {   // the production kernel: dx fused (DX)
+    if (!p.Wx6 || !p.dxb) return hipErrorInvalidValue;
+    return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true, true>),
+                           f32_grid(p.B, 8), 256, p, st);
+  }
   return launch_resident(s6 ? reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true>)
                             : reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0>),
                          f32_grid(p.B, 8), 256, p, st);

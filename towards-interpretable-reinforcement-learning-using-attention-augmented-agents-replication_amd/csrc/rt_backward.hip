@@ -838,10 +838,26 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                            L.T, L.B, L.h, L.w, L.P, {}};
         const bool s6 = f32_split6();
         rp.Wb6 = (const u32x2*)(pk + L.k_Wb6);
-        TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 128 * 4608 * (L.T - 1 + (io->dh0 ? 1 : 0)),
-                       strf("fp32 frame-group BPTT (dh rows)%s, %d steps per launch, 8 WG per frame [kernel: k_convlstm_bwd_f32]",
-                            s6 ? " (bf16x6 split products)" : "", L.T));
-        HIPCHK(convlstm_bwd_f32(rp, st, s6));
+        if (s6) {   // dx fused (DX): conv2's output gradient and its bias partials from the same K loop
+          rp.Wx6 = (const u32x2*)(pk + L.k_Wx6);
+          rp.dx = Wf(L.dY2);
+          rp.dxb = Wf(L.dxb);
+        }
+        {
+          // work: the dh rows over T-1 steps (+ dh0), and with dx fused the dx rows over all T steps (the
+          // batched dx it replaces) plus the dh rows of step 0 that the extra iteration computes
+          const double dh_steps = L.T - 1 + ((io->dh0 || s6) ? 1 : 0);
+          TimerScope tim(AAA_TIMER_BPTT_STEP, st, 2.0 * M * 4608 * (128.0 * dh_steps + (s6 ? 64.0 * L.T : 0.0)),
+                         s6 ? strf("fp32 frame-group BPTT + dx (bf16x6 split products), %d steps per launch, 8 WG "
+                                   "per frame [kernel: k_convlstm_bwd_f32]", L.T)
+                            : strf("fp32 frame-group BPTT (dh rows), %d steps per launch, 8 WG per frame "
+                                   "[kernel: k_convlstm_bwd_f32]", L.T));
+          HIPCHK(convlstm_bwd_f32(rp, st, s6));
+        }
+        if (s6) {
+          HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
+          dx_fused = true;
+        }
       }
     }
     for (int t = (fb || fb32) ? -1 : t1; t >= 0; --t) {

@@ -38,6 +38,8 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
     HIPCHK(pack_wb32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wb32), st));
     HIPCHK(split_frag((const float*)(pk + L.k_Wf32), pk + L.k_Wf6, 16 * kF32QP * 64, st));
     HIPCHK(split_frag((const float*)(pk + L.k_Wb32), pk + L.k_Wb6, 8 * kB32QP * 4 * 64, st));
+    HIPCHK(pack_wx32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wx32), st));
+    HIPCHK(split_frag((const float*)(pk + L.k_Wx32), pk + L.k_Wx6, 8 * kB32QP * 2 * 64, st));
     HIPCHK(split_planes((const float*)(pk + L.k_WdTl), 64L * 4608, (__bf16*)(pk + L.k_WdT6), st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
