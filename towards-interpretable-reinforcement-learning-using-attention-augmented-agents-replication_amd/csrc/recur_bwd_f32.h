@@ -72,19 +72,86 @@ inline hipError_t pack_wb32(const float* WdT, float* Wb, hipStream_t st) {
 constexpr int kB32XC = 24;
 inline size_t b32_xpart_floats(int B) { return (size_t)kB32NBUF * B * 64 * 128 * kB32XC; }
 
-// Wx[(((kh * kB32QP + q) * 2 + rb) * 64 + lane) * 4 + j] =
-//   WdT[32 rb + lane % 32][tap * 512 + 64 kh + 8 q8 + 4 (lane / 32) + j]: the dx rows (DX), k_pack_wb32's order
-static __global__ void __launch_bounds__(256) k_pack_wx32(const float* __restrict__ WdT, float* __restrict__ Wx) {
-  const int i = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk
-  if (i >= 8 * kB32QP * 2 * 64) return;
-  const int lane = i & 63, rb = (i >> 6) & 1, kq = i >> 7, q = kq % kB32QP, kh = kq / kB32QP;
-  const int qq = q % kB32Q, tap = qq >> 3, q8 = qq & 7;
-  const int row = 32 * rb + (lane & 31), k = tap * 512 + 64 * kh + 8 * q8 + 4 * (lane >> 5);
-  *reinterpret_cast<f32x4*>(Wx + (size_t)i * 4) = *reinterpret_cast<const f32x4*>(WdT + (size_t)row * 4608 + k);
+// Every fragment-order operand stream of the fp32 recurrences in ONE launch, straight from the
+// packed matrices (was nine launches per weight update): the forward's Wf (k_pack_wf32's order)
+// and the BPTT's Wb (k_pack_wb32's) as fp32 copies and three-way bf16 splits (k_split_frag's
+// layout), the dx rows' Wx split (DX: k_pack_wb32's order over W^T rows 0..63: chunk
+// (((kh * kB32QP + q) * 2 + rb) * 64 + lane)) and the batched dx's WdT planes
+// (split_planes over W^T rows 0..63).
+struct FragPack {
+  const float* WpXH;   // [512][1728]
+  const float* WdT;    // [192][4608]
+  float* Wf;           // fp32 fragment order (16 * kF32QP * 64 chunks)
+  u32x2* Wf6;
+  float* Wb;           // (8 * kB32QP * 4 * 64 chunks)
+  u32x2* Wb6;
+  u32x2* Wx6;          // (8 * kB32QP * 2 * 64 chunks)
+  __bf16* WdT6;        // 3 planes of 64 * 4608
+};
+__device__ __forceinline__ void split_chunk(const f32x4& x, u32x2 (&part)[3]) {
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    uint32_t h2[2], m2[2], l2[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float v = x[2 * e + k];
+      const __bf16 hi = (__bf16)v;
+      const float r = v - (float)hi;
+      const __bf16 mid = (__bf16)r;
+      const __bf16 lo = (__bf16)(r - (float)mid);
+      h2[k] = __builtin_bit_cast(uint16_t, hi);
+      m2[k] = __builtin_bit_cast(uint16_t, mid);
+      l2[k] = __builtin_bit_cast(uint16_t, lo);
+    }
+    part[0][e] = h2[0] | (h2[1] << 16);
+    part[1][e] = m2[0] | (m2[1] << 16);
+    part[2][e] = l2[0] | (l2[1] << 16);
+  }
+}
+constexpr int kFragNf = 16 * kF32QP * 64, kFragNb = 8 * kB32QP * 4 * 64, kFragNx = 8 * kB32QP * 2 * 64;
+constexpr int kFragNd = 64 * 4608 / 4;
+static __global__ void __launch_bounds__(256) k_pack_frag_f32(FragPack a) {
+  int c = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk of one stream
+  const int lane = c & 63;
+  const float* src;
+  float* f32dst = nullptr;
+  u32x2* dst6;
+  if (c < kFragNf) {
+    const int rq = c >> 6, q = rq % kF32QP, rb = rq / kF32QP;
+    src = a.WpXH + (size_t)(rb * 32 + (lane & 31)) * 1728 + f32_k(q % kF32Q) + (lane >> 5) * 4;
+    f32dst = a.Wf;
+    dst6 = a.Wf6;
+  } else if ((c -= kFragNf) < kFragNb) {
+    const int rb = (c >> 6) & 3, kq = c >> 8, q = kq % kB32QP, kh = kq / kB32QP, qq = q % kB32Q;
+    src = a.WdT + (size_t)(64 + 32 * rb + (lane & 31)) * 4608 + (qq >> 3) * 512 + 64 * kh + 8 * (qq & 7) +
+          4 * (lane >> 5);
+    f32dst = a.Wb;
+    dst6 = a.Wb6;
+  } else if ((c -= kFragNb) < kFragNx) {
+    const int rb = (c >> 6) & 1, kq = c >> 7, q = kq % kB32QP, kh = kq / kB32QP, qq = q % kB32Q;
+    src = a.WdT + (size_t)(32 * rb + (lane & 31)) * 4608 + (qq >> 3) * 512 + 64 * kh + 8 * (qq & 7) + 4 * (lane >> 5);
+    dst6 = a.Wx6;
+  } else if ((c -= kFragNx) < kFragNd) {   // planes: hi, mid, lo of W^T rows 0..63
+    const f32x4 x = *reinterpret_cast<const f32x4*>(a.WdT + (size_t)c * 4);
+    u32x2 part[3];
+    split_chunk(x, part);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x2*>(a.WdT6 + (size_t)p * 64 * 4608 + (size_t)c * 4) = part[p];
+    return;
+  } else {
+    return;
+  }
+  const f32x4 x = *reinterpret_cast<const f32x4*>(src);
+  if (f32dst) *reinterpret_cast<f32x4*>(f32dst + (size_t)c * 4) = x;
+  u32x2 part[3];
+  split_chunk(x, part);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) dst6[((c >> 6) * 3 + p) * 64 + lane] = part[p];
 }
 
-inline hipError_t pack_wx32(const float* WdT, float* Wx, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_wx32, dim3((8 * kB32QP * 2 * 64 + 255) / 256), dim3(256), 0, st, WdT, Wx);
+inline hipError_t pack_frag_f32(const FragPack& a, hipStream_t st) {
+  constexpr int n = kFragNf + kFragNb + kFragNx + kFragNd;
+  hipLaunchKernelGGL(k_pack_frag_f32, dim3((n + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -104,7 +171,7 @@ struct RecBwdF32Params {
   int T, B, h, w, P;
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
   const u32x2* Wb6 = nullptr;   // S6: the three-way split of Wb (recur_f32.h k_split_frag)
-  const u32x2* Wx6 = nullptr;   // DX: the three-way split of Wx (k_pack_wx32)
+  const u32x2* Wx6 = nullptr;   // DX: the three-way split of the dx rows (k_pack_frag_f32)
   float* dx = nullptr;          // DX: (T, B, P, 64) <- conv2's output gradient (dY2)
   float* dxb = nullptr;         // DX: (B, 64) <- its pixel-and-step sums (conv2's bias gradient per frame)
 };
@@ -259,7 +326,7 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
     return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
                                          rsw6, lane * 8, (((kh * kB32QP + q) * 4 + 2 * rw + r) * 3 + part) * 512, 0));
   };
-  // DX: the dx rows' stream (k_pack_wx32 + k_split_frag): row block rw of the two
+  // DX: the dx rows' stream (k_pack_frag_f32): row block rw of the two
   const __amdgpu_buffer_rsrc_t rsx6 = make_rsrc(p.Wx6, DX ? (uint32_t)(8 * kB32QP * 2 * 3 * 512) : 0u);
   auto ldx6 = [&](int q, int part) {
     return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(

@@ -34,13 +34,11 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
     HIPCHK(pack_wfrag((const __bf16*)(pk + L.k_WpXH), (__bf16*)(pk + L.k_Wfr), st));
     HIPCHK(pack_wbfrag((const __bf16*)(pk + L.k_WdTl), (__bf16*)(pk + L.k_Wbf), st));
   } else {   // the fp32 frame-group recurrence's fragment order (recur_f32.h)
-    HIPCHK(pack_wf32((const float*)(pk + L.k_WpXH), (float*)(pk + L.k_Wf32), st));
-    HIPCHK(pack_wb32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wb32), st));
-    HIPCHK(split_frag((const float*)(pk + L.k_Wf32), pk + L.k_Wf6, 16 * kF32QP * 64, st));
-    HIPCHK(split_frag((const float*)(pk + L.k_Wb32), pk + L.k_Wb6, 8 * kB32QP * 4 * 64, st));
-    HIPCHK(pack_wx32((const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wx32), st));
-    HIPCHK(split_frag((const float*)(pk + L.k_Wx32), pk + L.k_Wx6, 8 * kB32QP * 2 * 64, st));
-    HIPCHK(split_planes((const float*)(pk + L.k_WdTl), 64L * 4608, (__bf16*)(pk + L.k_WdT6), st));
+    // (pack_all wrote WpXH / WdT first: same stream)
+    HIPCHK(pack_frag_f32(FragPack{(const float*)(pk + L.k_WpXH), (const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wf32),
+                                  (u32x2*)(pk + L.k_Wf6), (float*)(pk + L.k_Wb32), (u32x2*)(pk + L.k_Wb6),
+                                  (u32x2*)(pk + L.k_Wx6), (__bf16*)(pk + L.k_WdT6)},
+                         st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
                     (float*)(pk + L.k_q1), (float*)(pk + L.k_q2), (float*)(pk + L.k_Q), st));
