@@ -48,6 +48,7 @@ namespace aaa {
 constexpr int kB32Q = 72;                     // quads per step (9 taps x 8)
 constexpr int kB32PD = 8;                     // A quads in flight (register slots): slot = q8
 constexpr int kB32QP = kB32Q + kB32PD - 1;    // packed quads per workgroup slice (first PD-1 repeated)
+constexpr int kB32PP = (kB32Q + kB32PD) / 2;   // packed quad PAIRS per workgroup slice (DX's paired streams)
 constexpr int kB32IB = 44 * 1024;             // own dZ image: 169 pixels x 64 rows fp32 (256 B)
 constexpr int kB32NBUF = 3;                   // partial-dh exchange buffers (step mod 3)
 
@@ -83,9 +84,12 @@ struct FragPack {
   const float* WdT;    // [192][4608]
   float* Wf;           // fp32 fragment order (16 * kF32QP * 64 chunks)
   u32x2* Wf6;
+  u32x4* Wf6p;         // the pre-split forward's paired stream (16 * kF32PP * 3 * 64 x 16 B)
   float* Wb;           // (8 * kB32QP * 4 * 64 chunks)
   u32x2* Wb6;
   u32x2* Wx6;          // (8 * kB32QP * 2 * 64 chunks)
+  u32x4* Wb6p;         // DX's paired streams: [kh][pair][rb][part][lane] x 16 B
+  u32x4* Wx6p;
   __bf16* WdT6;        // 3 planes of 64 * 4608
 };
 __device__ __forceinline__ void split_chunk(const f32x4& x, u32x2 (&part)[3]) {
@@ -109,7 +113,8 @@ __device__ __forceinline__ void split_chunk(const f32x4& x, u32x2 (&part)[3]) {
   }
 }
 constexpr int kFragNf = 16 * kF32QP * 64, kFragNb = 8 * kB32QP * 4 * 64, kFragNx = 8 * kB32QP * 2 * 64;
-constexpr int kFragNd = 64 * 4608 / 4;
+constexpr int kFragNd = 64 * 4608 / 4, kFragNp = 16 * kF32PP * 64;
+constexpr int kFragNbp = 8 * kB32PP * 4 * 64, kFragNxp = 8 * kB32PP * 2 * 64;
 static __global__ void __launch_bounds__(256) k_pack_frag_f32(FragPack a) {
   int c = blockIdx.x * 256 + (int)threadIdx.x;   // one 16-B chunk of one stream
   const int lane = c & 63;
@@ -131,7 +136,39 @@ static __global__ void __launch_bounds__(256) k_pack_frag_f32(FragPack a) {
     const int rb = (c >> 6) & 1, kq = c >> 7, q = kq % kB32QP, kh = kq / kB32QP, qq = q % kB32Q;
     src = a.WdT + (size_t)(32 * rb + (lane & 31)) * 4608 + (qq >> 3) * 512 + 64 * kh + 8 * (qq & 7) + 4 * (lane >> 5);
     dst6 = a.Wx6;
-  } else if ((c -= kFragNx) < kFragNd) {   // planes: hi, mid, lo of W^T rows 0..63
+  } else if ((c -= kFragNx) < kFragNp) {   // Wf6p: (row block, pair, lane) -> parts of quads 2 pj, 2 pj + 1
+    const int rp = c >> 6, pj = rp % kF32PP, rb = rp / kF32PP;
+    u32x2 part[2][3];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = (2 * pj + k) % kF32Q;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(a.WpXH + (size_t)(rb * 32 + (lane & 31)) * 1728 + f32_k(q) +
+                                                      (lane >> 5) * 4);
+      split_chunk(x, part[k]);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      a.Wf6p[(rp * 3 + p) * 64 + lane] = u32x4{part[0][p].x, part[0][p].y, part[1][p].x, part[1][p].y};
+    return;
+  } else if ((c -= kFragNp) < kFragNbp + kFragNxp) {   // DX's paired BPTT streams
+    const bool x = c >= kFragNbp;
+    if (x) c -= kFragNbp;
+    const int nrb = x ? 2 : 4, rb = (c >> 6) % nrb, kp = (c >> 6) / nrb, pj = kp % kB32PP, kh = kp / kB32PP;
+    u32x2 part[2][3];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int qq = (2 * pj + k) % kB32Q;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(
+          a.WdT + (size_t)((x ? 0 : 64) + 32 * rb + (lane & 31)) * 4608 + (qq >> 3) * 512 + 64 * kh + 8 * (qq & 7) +
+          4 * (lane >> 5));
+      split_chunk(v, part[k]);
+    }
+    u32x4* d = x ? a.Wx6p : a.Wb6p;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      d[((c >> 6) * 3 + p) * 64 + lane] = u32x4{part[0][p].x, part[0][p].y, part[1][p].x, part[1][p].y};
+    return;
+  } else if ((c -= kFragNbp + kFragNxp) < kFragNd) {   // planes: hi, mid, lo of W^T rows 0..63
     const f32x4 x = *reinterpret_cast<const f32x4*>(a.WdT + (size_t)c * 4);
     u32x2 part[3];
     split_chunk(x, part);
@@ -150,7 +187,7 @@ static __global__ void __launch_bounds__(256) k_pack_frag_f32(FragPack a) {
 }
 
 inline hipError_t pack_frag_f32(const FragPack& a, hipStream_t st) {
-  constexpr int n = kFragNf + kFragNb + kFragNx + kFragNd;
+  constexpr int n = kFragNf + kFragNb + kFragNx + kFragNp + kFragNbp + kFragNxp + kFragNd;
   hipLaunchKernelGGL(k_pack_frag_f32, dim3((n + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -172,6 +209,8 @@ struct RecBwdF32Params {
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
   const u32x2* Wb6 = nullptr;   // S6: the three-way split of Wb (recur_f32.h k_split_frag)
   const u32x2* Wx6 = nullptr;   // DX: the three-way split of the dx rows (k_pack_frag_f32)
+  const u32x4* Wb6p = nullptr;  // DX: Wb6 with quads 2j, 2j+1 of a part side by side per lane (one 16-B load)
+  const u32x4* Wx6p = nullptr;  // DX: the dx rows, paired the same way
   float* dx = nullptr;          // DX: (T, B, P, 64) <- conv2's output gradient (dY2)
   float* dxb = nullptr;         // DX: (B, 64) <- its pixel-and-step sums (conv2's bias gradient per frame)
 };
@@ -333,18 +372,38 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
                                          rsx6, lane * 8, (((kh * kB32QP + q) * 2 + rw) * 3 + part) * 512, 0));
   };
   auto lda6r = [&](int q, int r, int part) { return r < 2 ? lda6(q, r, part) : ldx6(q, part); };
-  u32x2 a6[S6 ? PD : 1][NR][3];
+  // DX: the paired streams -- one 16-B load per lane brings a part of both quads of a pair (half the
+  // load instructions of two 8-B loads); PD / 2 pairs in flight
+  const __amdgpu_buffer_rsrc_t rsbp = make_rsrc(p.Wb6p, DX ? (uint32_t)(8 * kB32PP * 4 * 3 * 1024) : 0u);
+  const __amdgpu_buffer_rsrc_t rsxp = make_rsrc(p.Wx6p, DX ? (uint32_t)(8 * kB32PP * 2 * 3 * 1024) : 0u);
+  auto ldp = [&](int pj, int r, int part) {
+    return r < 2 ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rsbp, lane * 16, (((kh * kB32PP + pj) * 4 + 2 * rw + r) * 3 + part) * 1024, 0))
+                 : __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rsxp, lane * 16, (((kh * kB32PP + pj) * 2 + rw) * 3 + part) * 1024, 0));
+  };
+  u32x2 a6[S6 && !DX ? PD : 1][NR][3];
+  u32x4 a6p[DX ? PD / 2 : 1][NR][3];
+  if constexpr (DX) {
 #pragma unroll
-  for (int s = 0; s < PD - 1; ++s)
+    for (int s = 0; s < PD / 2; ++s)
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if constexpr (S6) {
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6r(s, r, part);
-      } else {
-        af[s][r] = lda(s, r);
+        for (int part = 0; part < 3; ++part) a6p[s][r][part] = ldp(s, r, part);
+  } else {
+#pragma unroll
+    for (int s = 0; s < PD - 1; ++s)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        if constexpr (S6) {
+#pragma unroll
+          for (int part = 0; part < 3; ++part) a6[s][r][part] = lda6r(s, r, part);
+        } else {
+          af[s][r] = lda(s, r);
+        }
       }
-    }
+  }
 
   // the dgrad is the transposed conv: tap (ky, kx) of W^T (packed in the forward's
   // orientation) reads dZ at (y + 1 - ky, x + 1 - kx) (ConvGeo transposed gather)
@@ -413,19 +472,29 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
         for (int q8 = 0; q8 < 8; q8 += 2) {
           const int pb = (q8 >> 1) & 1, nb = pb ^ 1;
           bf16x8 a3[NR][3];
+          if constexpr (DX) {   // slot pair (q8 % PD) / 2, refilled with pair (qt + q8) / 2 + PD / 2 (wraps)
 #pragma unroll
-          for (int r = 0; r < NR; ++r)
+            for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int part = 0; part < 3; ++part)
-              a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8 % PD][r][part].x, a6[q8 % PD][r][part].y,
-                                                             a6[q8 % PD + 1][r][part].x, a6[q8 % PD + 1][r][part].y});
+              for (int part = 0; part < 3; ++part) {
+                a3[r][part] = __builtin_bit_cast(bf16x8, a6p[(q8 % PD) / 2][r][part]);
+                a6p[(q8 % PD) / 2][r][part] = ldp((qt + q8) / 2 + PD / 2, r, part);
+              }
+          } else {
 #pragma unroll
-          for (int r = 0; r < NR; ++r)
+            for (int r = 0; r < NR; ++r)
 #pragma unroll
-            for (int part = 0; part < 3; ++part) {
-              a6[(q8 + PD - 1) % PD][r][part] = lda6r(qt + q8 + PD - 1, r, part);
-              a6[q8 % PD][r][part] = lda6r(qt + q8 + PD, r, part);
-            }
+              for (int part = 0; part < 3; ++part)
+                a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[q8 % PD][r][part].x, a6[q8 % PD][r][part].y,
+                                                               a6[q8 % PD + 1][r][part].x, a6[q8 % PD + 1][r][part].y});
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+              for (int part = 0; part < 3; ++part) {
+                a6[(q8 + PD - 1) % PD][r][part] = lda6r(qt + q8 + PD - 1, r, part);
+                a6[q8 % PD][r][part] = lda6r(qt + q8 + PD, r, part);
+              }
+          }
           if (q8 < 6) ldq(tap, (q8 >> 1) + 1, bq[nb]);
           else if (tap < 8) ldq(tap + 1, 0, bq[nb]);
           __builtin_amdgcn_sched_barrier(0);
@@ -703,7 +772,7 @@ inline hipError_t convlstm_bwd_f32(RecBwdF32Params& p, hipStream_t st, bool s6 =
                            st);
 #endif
   if (s6 && p.dx) {   // the production kernel: dx fused (DX)
-    if (!p.Wx6 || !p.dxb) return hipErrorInvalidValue;
+    if (!p.Wb6p || !p.Wx6p || !p.dxb) return hipErrorInvalidValue;
     return launch_resident(reinterpret_cast<const void*>(&k_convlstm_bwd_f32<0, true, 4, true, true>),
                            f32_grid(p.B, 8), 256, p, st);
   }

@@ -47,6 +47,7 @@ constexpr int kF32QX = 72;                 // x-part quads (9 taps x 8)
 constexpr int kF32Q = 216;                 // quads per step
 constexpr int kF32PD = 8;                  // A quads in flight (register slots); divides 8, 16 and kF32Q
 constexpr int kF32QP = kF32Q + kF32PD - 1;  // packed quads per row block: the first PD-1 repeated at the end
+constexpr int kF32PP = (kF32Q + kF32PD) / 2;  // packed quad PAIRS per row block (the pre-split kernel's stream)
 constexpr int kF32XB = 44 * 1024;          // x image bytes: 169 x 256 B rounded up to whole 1-KB DMA pieces
 constexpr int kF32HB = 169 * 512;          // h image bytes
 constexpr int kF32GP = 144;                // epilogue staging: gate tile pixel pitch (128 B + 16)
@@ -125,6 +126,7 @@ struct RecF32Params {
   int h0_zero;         // slot 0's h part is zero (reset()): the t = 0 h-part is skipped
   short colhb[128];    // column -> top-left image pixel of its 3x3 window (padding columns: pixel P-1's)
   const u32x2* Wf6 = nullptr;   // S6: the three-way split of Wf (k_split_frag)
+  const u32x4* Wf6p = nullptr;  // the pre-split kernel's stream: quads 2j, 2j+1 of a part side by side per lane
 };
 
 // Blocks of the launch: 8 * G * ceil(B / 8) (XCD-local frame groups).
@@ -703,16 +705,18 @@ k_convlstm_fwd_f32ps(RecF32Params p) {
       for (int c = 0; c < NCB; ++c) cst[r][c][g] = colc[c] < P ? p.Cst[((size_t)b * P + colc[c]) * 128 + ch] : 0.f;
     }
 
-  // A stream (pre-split fragment-order weights, k_split_frag): quad q's part of row block rb
-  const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wf6, (uint32_t)(16 * kF32QP * 3 * 512));
-  auto lda6 = [&](int q, int r, int part) {
-    return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(
-                                         rsw6, lane * 8, (((rbg0 + r) * kF32QP + q) * 3 + part) * 512, 0));
+  // A stream (pre-split fragment-order weights, k_pack_frag_f32's paired stream): per lane one 16-B
+  // load brings a part of both quads of a pair (half the load instructions of two 8-B loads);
+  // PD / 2 pairs in flight
+  const __amdgpu_buffer_rsrc_t rsw6 = make_rsrc(p.Wf6p, (uint32_t)(16 * kF32PP * 3 * 1024));
+  auto lda6 = [&](int pj, int r, int part) {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rsw6, lane * 16, (((rbg0 + r) * kF32PP + pj) * 3 + part) * 1024, 0));
   };
-  u32x2 a6[PD][RPW][3];
+  u32x4 a6[PD / 2][RPW][3];
   auto preload = [&] {
 #pragma unroll
-    for (int s = 0; s < PD - 1; ++s)
+    for (int s = 0; s < PD / 2; ++s)
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
 #pragma unroll
@@ -743,17 +747,12 @@ k_convlstm_fwd_f32ps(RecF32Params p) {
 #pragma unroll
       for (int r = 0; r < RPW; ++r)
 #pragma unroll
-        for (int part = 0; part < 3; ++part)
-          a3[r][part] = __builtin_bit_cast(bf16x8, u32x4{a6[slot][r][part].x, a6[slot][r][part].y,
-                                                         a6[slot + 1][r][part].x, a6[slot + 1][r][part].y});
-      if constexpr (!(ABL & 32)) {
+        for (int part = 0; part < 3; ++part) a3[r][part] = __builtin_bit_cast(bf16x8, a6[slot / 2][r][part]);
+      if constexpr (!(ABL & 32)) {   // refill the slot pair with pair qn / 2 + PD / 2 (the stream wraps)
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
 #pragma unroll
-          for (int part = 0; part < 3; ++part) {
-            a6[(slot + PD - 1) % PD][r][part] = lda6(qn + PD - 1, r, part);
-            a6[slot][r][part] = lda6(qn + PD, r, part);
-          }
+          for (int part = 0; part < 3; ++part) a6[slot / 2][r][part] = lda6(qn / 2 + PD / 2, r, part);
       }
       load_next_b();
       __builtin_amdgcn_sched_barrier(0);

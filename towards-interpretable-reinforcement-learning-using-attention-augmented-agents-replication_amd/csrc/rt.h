@@ -65,7 +65,7 @@ struct Layout {
   int xpc;      // frames of the Xp chunk buffer (conv1's bordered RGBx operand, rebuilt per chunk)
   int qd, da, ans_in, ans_ld, ldy;
   size_t poff[NPARAM], psz[NPARAM], ptotal;
-  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_Wf6, k_Wb6, k_Wx6, k_WdTl, k_WdTc, k_WdT6, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
+  size_t k_Wp1, k_Wp2, k_WdT2, k_WpX, k_WpH, k_WpXH, k_Wfr, k_Wbf, k_Wf32, k_Wb32, k_Wf6, k_Wf6p, k_Wb6, k_Wx6, k_Wb6p, k_Wx6p, k_WdTl, k_WdTc, k_WdT6, k_bl, k_Wihhp, k_q1, k_q2, k_Q, k_W1p, k_Wihp, k_blc, k_Whd, k_bhd, packed;
   size_t Xp, Y1, XH, Hs, Cst, Gt, SQ, Am, ans, hid1, AO, LG, LC, LH;
   size_t dY, dLG, dAO, dH1, dAns, dO, dQp, dQs, dC, dZ, dZp, dY2, dY1, dxb, rflags, xpart, dhs, dZ6;
   size_t gWp1, gWp2, gWpl, gbl, gW1p, gWihp, gblc, gWhd, gbhd, ws;

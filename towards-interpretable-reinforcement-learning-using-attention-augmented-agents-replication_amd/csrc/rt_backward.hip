@@ -840,6 +840,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         rp.Wb6 = (const u32x2*)(pk + L.k_Wb6);
         if (s6) {   // dx fused (DX): conv2's output gradient and its bias partials from the same K loop
           rp.Wx6 = (const u32x2*)(pk + L.k_Wx6);
+          rp.Wb6p = (const u32x4*)(pk + L.k_Wb6p);
+          rp.Wx6p = (const u32x4*)(pk + L.k_Wx6p);
           rp.dx = Wf(L.dY2);
           rp.dxb = Wf(L.dxb);
         }

@@ -68,8 +68,11 @@ int build_layout(const aaa_cfg* c, Layout& L, int min_frames) {
   L.k_Wf32 = take(e == 4 ? (size_t)16 * kF32QP * 64 * 16 : 0);   // fp32 fragment-order [x|h] (frame-group recurrence, recur_f32.h)
   L.k_Wb32 = take(e == 4 ? (size_t)8 * kB32QP * 4 * 64 * 16 : 0);   // fp32 fragment-order W_h^T (frame-group BPTT, recur_bwd_f32.h)
   L.k_Wf6 = take(e == 4 ? (size_t)16 * kF32QP * 64 * 24 : 0);    // their three-way bf16 splits (S6, k_split_frag)
+  L.k_Wf6p = take(e == 4 ? (size_t)16 * kF32PP * 3 * 64 * 16 : 0);   // ... paired for the pre-split forward
   L.k_Wb6 = take(e == 4 ? (size_t)8 * kB32QP * 4 * 64 * 24 : 0);
   L.k_Wx6 = take(e == 4 ? (size_t)8 * kB32QP * 2 * 64 * 24 : 0);   // the dx rows of W^T, split (DX)
+  L.k_Wb6p = take(e == 4 ? (size_t)8 * kB32PP * 4 * 3 * 64 * 16 : 0);   // DX's paired streams
+  L.k_Wx6p = take(e == 4 ? (size_t)8 * kB32PP * 2 * 3 * 64 * 16 : 0);
   L.k_bl = take(512 * 4);
   L.k_W1p = take(512 * (size_t)L.ans_ld * 4);
   L.k_Wihp = take(1024 * 256 * 4);

@@ -36,8 +36,9 @@ int pack_impl(const Layout& L, const float* prm, char* pk, hipStream_t st) {
   } else {   // the fp32 frame-group recurrence's fragment order (recur_f32.h)
     // (pack_all wrote WpXH / WdT first: same stream)
     HIPCHK(pack_frag_f32(FragPack{(const float*)(pk + L.k_WpXH), (const float*)(pk + L.k_WdTl), (float*)(pk + L.k_Wf32),
-                                  (u32x2*)(pk + L.k_Wf6), (float*)(pk + L.k_Wb32), (u32x2*)(pk + L.k_Wb6),
-                                  (u32x2*)(pk + L.k_Wx6), (__bf16*)(pk + L.k_WdT6)},
+                                  (u32x2*)(pk + L.k_Wf6), (u32x4*)(pk + L.k_Wf6p), (float*)(pk + L.k_Wb32),
+                                  (u32x2*)(pk + L.k_Wb6), (u32x2*)(pk + L.k_Wx6), (u32x4*)(pk + L.k_Wb6p),
+                                  (u32x4*)(pk + L.k_Wx6p), (__bf16*)(pk + L.k_WdT6)},
                          st));
   }
   HIPCHK(query_pack(prm + L.poff[Q0B], prm + L.poff[Q2W], prm + L.poff[Q2B], prm + L.poff[Q4W], prm + L.poff[Q4B], L.nq,
@@ -205,6 +206,7 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
       {
         const bool s6 = f32_split6();
         rp.Wf6 = (const u32x2*)(pk + L.k_Wf6);
+        rp.Wf6p = (const u32x4*)(pk + L.k_Wf6p);
         TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
                        strf("fp32 frame-group [x|h] recurrence%s, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]",
                             s6 ? " (bf16x6 split products)" : "", L.T, G));
