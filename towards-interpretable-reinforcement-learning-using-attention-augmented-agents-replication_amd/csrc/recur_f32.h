@@ -945,6 +945,14 @@ inline int f32_rec_g(int B, int cus) {
   return 0;
 }
 
+// Whether convlstm_fwd_f32 runs the pre-split kernel (k_convlstm_fwd_f32ps) for this launch.
+inline bool f32_fwd_presplit(bool s6, int G, int P) {
+#ifdef AAA_ABLATION
+  if (std::getenv("AAA_F32_PRESPLIT") != nullptr) return false;
+#endif
+  return s6 && G == 8 && P <= 128;
+}
+
 inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool s6 = false) {
   if (!f32_rec_fits(p.h, p.w) || p.P != p.h * p.w || p.B < 1 || p.T < 1 || !p.flags || !p.report || p.spin < 0)
     return hipErrorInvalidValue;
@@ -956,11 +964,7 @@ inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool 
   // the two-column-block mapping with 8, most of it from the shallower prefetch)
   // G = 8, S6, P <= 128: the pre-split images (k_convlstm_fwd_f32ps); larger grids the in-loop
   // split (AAA_F32_PRESPLIT=0 selects it everywhere in ablation builds)
-#ifdef AAA_ABLATION
-  const bool ps = s6 && G == 8 && p.P <= 128 && std::getenv("AAA_F32_PRESPLIT") == nullptr;
-#else
-  const bool ps = s6 && G == 8 && p.P <= 128;
-#endif
+  const bool ps = f32_fwd_presplit(s6, G, p.P);
   const void* k = ps       ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32ps<0, 1, 8>)
                   : G == 8 ? (s6 ? reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8, 0, true, true, 4>)
                                  : reinterpret_cast<const void*>(&k_convlstm_fwd_f32<8>))

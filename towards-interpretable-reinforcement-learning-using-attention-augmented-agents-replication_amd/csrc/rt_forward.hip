@@ -208,8 +208,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
         rp.Wf6 = (const u32x2*)(pk + L.k_Wf6);
         rp.Wf6p = (const u32x4*)(pk + L.k_Wf6p);
         TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * (576.0 * L.T + 1152.0 * (L.T - (io->h0 ? 0 : 1))),
-                       strf("fp32 frame-group [x|h] recurrence%s, %d steps per launch, %d WG per frame [kernel: k_convlstm_fwd_f32]",
-                            s6 ? " (bf16x6 split products)" : "", L.T, G));
+                       strf("fp32 frame-group [x|h] recurrence%s, %d steps per launch, %d WG per frame [kernel: %s]",
+                            s6 ? " (bf16x6 split products)" : "", L.T, G,
+                            f32_fwd_presplit(s6, G, L.P) ? "k_convlstm_fwd_f32ps" : "k_convlstm_fwd_f32<"));
         HIPCHK(convlstm_fwd_f32(rp, G, st, s6));
       }
       return forward_tail<T>(L, io, st);
