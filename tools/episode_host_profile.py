@@ -58,6 +58,20 @@ if __name__ == "__main__":
     e1.record()
     torch.cuda.synchronize()
     print(f"device ms per step (events around the async episode): {e0.elapsed_time(e1) / T_ep:.3f}")
+    import gc
+    for label in ("gc on", "gc off", "gc on"):
+        if label == "gc off":
+            gc.disable()
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            episode()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) / T_ep * 1e3)
+        gc.enable()
+        ts.sort()
+        print(f"{label}: ms per step over 5 episodes: median {ts[2]:.3f} min {ts[0]:.3f} max {ts[-1]:.3f}")
     # one step at a time from an idle device: host time of Policy.act (returns after its launches)
     # and the device time left after it returns
     agent.reset()

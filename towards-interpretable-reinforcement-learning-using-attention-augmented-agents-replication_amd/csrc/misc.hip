@@ -313,7 +313,7 @@ __device__ uint64_t aaa_attn_stamps[16384 * 8];
 //     groups reduced through LDS.
 // Pieces of a V row: O = 30 fp32 quads or 15 bf16 octets (one padding piece
 // pads them to a multiple of 8 lanes), then S = 16 fp32 quads.
-template <int NQ, typename TO>
+template <int NQ, typename TO, int PPL>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))   // two frames per CU
 k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q, int qs,
            const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
@@ -334,7 +334,11 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const TO* O = Hs + (size_t)f * P * old;
   AAA_AT_STAMP(0);
-  const int part = tid & 7, pl = tid >> 3;   // phase 1: 64 positions per pass, 8 lanes each
+  // phase 1: 64 * PPL positions per pass, 8 lanes each; a lane takes PPL positions
+  // (64 apart) with the same channel pieces, so each da read from LDS (the phase's
+  // bound: NQ 16-B reads per piece) serves PPL positions
+  const int part = tid & 7, pl = tid >> 3;
+  constexpr int PPS = 64 * PPL;
   // the V pieces and key piece of position p: unconditional loads from valid
   // (clamped) addresses; a padding piece is zeroed at its use
   auto vload = [&](int p, u32x4 (&raw)[NK], u32x4& kraw) {
@@ -348,93 +352,116 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
     }
     kraw = *reinterpret_cast<const u32x4*>(O + (size_t)p * old + (BF ? 0 : 4 * (part & 1)));
   };
-  u32x4 raw[NK], kraw;
-  vload(min(pl, P - 1), raw, kraw);
+  u32x4 raw[PPL][NK], kraw[PPL];
+#pragma unroll
+  for (int u = 0; u < PPL; ++u) vload(min(pl + 64 * u, P - 1), raw[u], kraw[u]);
   for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
   for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
   for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
   __syncthreads();
   AAA_AT_STAMP(1);
-  for (int p0 = 0; p0 < P; p0 += 64) {
-    const int p = p0 + pl;
+  for (int p0 = 0; p0 < P; p0 += PPS) {
     // da's LDS reads stay inside the pass: hoisted out of the loop they would
     // hold NQ x 184 / 8 floats per lane in registers (spills)
     int opq = 0;
     asm volatile("" : "+v"(opq));
     const float* dap = da + opq;
-    float acc[NQ];
+    float acc[PPL][NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    for (int u = 0; u < PPL; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[u][q] = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int j = part + 8 * k;
       if (k < NKO && BF) {   // 8 bf16 channels of O
         const float m = j < NOP ? 1.f : 0.f;
-        const f32x4 v0 = bf4_f32(u32x2{raw[k].x, raw[k].y}) * m, v1 = bf4_f32(u32x2{raw[k].z, raw[k].w}) * m;
+        f32x4 v0[PPL], v1[PPL];
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) {
+          v0[u] = bf4_f32(u32x2{raw[u][k].x, raw[u][k].y}) * m;
+          v1[u] = bf4_f32(u32x2{raw[u][k].z, raw[u][k].w}) * m;
+        }
         const int c0 = 8 * min(j, NOP - 1);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
           const f32x4 d0 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
           const f32x4 d1 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0 + 4);
-          acc[q] += v0[0] * d0[0] + v0[1] * d0[1] + v0[2] * d0[2] + v0[3] * d0[3] +
-                    v1[0] * d1[0] + v1[1] * d1[1] + v1[2] * d1[2] + v1[3] * d1[3];
+#pragma unroll
+          for (int u = 0; u < PPL; ++u)
+            acc[u][q] += v0[u][0] * d0[0] + v0[u][1] * d0[1] + v0[u][2] * d0[2] + v0[u][3] * d0[3] +
+                         v1[u][0] * d1[0] + v1[u][1] * d1[1] + v1[u][2] * d1[2] + v1[u][3] * d1[3];
         }
       } else {               // 4 fp32 channels (O quads of the fp32 path, or S)
         const float m = k < NKO ? (j < NOP ? 1.f : 0.f) : 1.f;
-        const f32x4 v = __builtin_bit_cast(f32x4, raw[k]) * m;
+        f32x4 v[PPL];
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) v[u] = __builtin_bit_cast(f32x4, raw[u][k]) * m;
         const int c0 = k < NKO ? 4 * min(j, NOP - 1) : 120 + 4 * (j - NOPP);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
           const f32x4 d = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
-          acc[q] += v[0] * d[0] + v[1] * d[1] + v[2] * d[2] + v[3] * d[3];
+#pragma unroll
+          for (int u = 0; u < PPL; ++u) acc[u][q] += v[u][0] * d[0] + v[u][1] * d[1] + v[u][2] * d[2] + v[u][3] * d[3];
         }
       }
       // one piece's da reads at a time: the next piece's addresses depend on
       // this piece's sums (scheduled all up front the reads need NK * NQ * 4
       // registers and spill)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[q]));
+      for (int u = 0; u < PPL; ++u)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[u][q]));
       asm volatile("" : "+v"(opq));
       dap = da + opq;
     }
-    const u32x4 kr = kraw;
-    if (p0 + 64 < P) vload(min(p + 64, P - 1), raw, kraw);   // the next pass's pieces in flight
-    // 3-step transpose reduction over the 8 lanes of the position: lane part
-    // ends with the total of q = part (NQ = 8) or part & 3 (NQ = 4)
-    float v[NQ];
+    u32x4 kr[PPL];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) v[q] = acc[q];
-    if constexpr (NQ == 4) {
+    for (int u = 0; u < PPL; ++u) kr[u] = kraw[u];
+    if (p0 + PPS < P) {   // the next pass's pieces in flight
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], 4, 64);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool up = part & 4;
-        const float keep = up ? v[i + 4] : v[i], send = up ? v[i] : v[i + 4];
-        v[i] = keep + __shfl_xor(send, 4, 64);
-      }
+      for (int u = 0; u < PPL; ++u) vload(min(p0 + PPS + pl + 64 * u, P - 1), raw[u], kraw[u]);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool up = part & 2;
-      const float keep = up ? v[i + 2] : v[i], send = up ? v[i] : v[i + 2];
-      v[i] = keep + __shfl_xor(send, 2, 64);
-    }
-    {
-      const bool up = part & 1;
-      const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
-      v[0] = keep + __shfl_xor(send, 1, 64);
-    }
-    if (p < P) {
-      if (part < NQ) dA[p * NQ + part] = v[0];
-      if constexpr (BF) {
-        if (part == 0) {
-          *reinterpret_cast<f32x4*>(Kc + p * 8) = bf4_f32(u32x2{kr.x, kr.y});
-          *reinterpret_cast<f32x4*>(Kc + p * 8 + 4) = bf4_f32(u32x2{kr.z, kr.w});
-        }
+    for (int u = 0; u < PPL; ++u) {
+      const int p = p0 + pl + 64 * u;
+      // 3-step transpose reduction over the 8 lanes of the position: lane part
+      // ends with the total of q = part (NQ = 8) or part & 3 (NQ = 4)
+      float v[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[q] = acc[u][q];
+      if constexpr (NQ == 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], 4, 64);
       } else {
-        if (part < 2) *reinterpret_cast<u32x4*>(Kc + p * 8 + 4 * part) = kr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool up = part & 4;
+          const float keep = up ? v[i + 4] : v[i], send = up ? v[i] : v[i + 4];
+          v[i] = keep + __shfl_xor(send, 4, 64);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool up = part & 2;
+        const float keep = up ? v[i + 2] : v[i], send = up ? v[i] : v[i + 2];
+        v[i] = keep + __shfl_xor(send, 2, 64);
+      }
+      {
+        const bool up = part & 1;
+        const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
+        v[0] = keep + __shfl_xor(send, 1, 64);
+      }
+      if (p < P) {
+        if (part < NQ) dA[p * NQ + part] = v[0];
+        if constexpr (BF) {
+          if (part == 0) {
+            *reinterpret_cast<f32x4*>(Kc + p * 8) = bf4_f32(u32x2{kr[u].x, kr[u].y});
+            *reinterpret_cast<f32x4*>(Kc + p * 8 + 4) = bf4_f32(u32x2{kr[u].z, kr[u].w});
+          }
+        } else {
+          if (part < 2) *reinterpret_cast<u32x4*>(Kc + p * 8 + 4 * part) = kr[u];
+        }
       }
     }
   }
@@ -1103,12 +1130,25 @@ hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, con
     hipLaunchKernelGGL(kern, dim3(F), dim3(512), sh, st, o, O.ld, S, Q, qs, Am, dAns, da_ld, addq, P, dO, dQp, cqm);
   };
   if (nq != 4 && nq != 8) return hipErrorInvalidValue;
+  // positions per lane in the dA pass: 2 on large grids halves its LDS reads of da (C5,
+  // P = 441: 322 -> 296-311 us); at 84x84 (P = 121, two passes of 64 or one of 128) the
+  // doubled per-lane chain costs more than the shared reads save (C3 113 vs 119-122 us)
+  // (profiles/r05/ab/attn_bwd_ppl/)
+#ifdef AAA_ABLATION
+  static const int ppl_env = getenv("AAA_ATTN_BWD_PPL") ? atoi(getenv("AAA_ATTN_BWD_PPL")) : 0;
+#else
+  constexpr int ppl_env = 0;
+#endif
+  const int ppl = ppl_env ? ppl_env : P > 256 ? 2 : 1;
+  if (ppl != 1 && ppl != 2) return hipErrorInvalidValue;
   if (O.bf16) {
     const __bf16* o = (const __bf16*)O.p;
-    nq == 4 ? launch(k_attn_bwd<4, __bf16>, o) : launch(k_attn_bwd<8, __bf16>, o);
+    if (ppl == 2) nq == 4 ? launch(k_attn_bwd<4, __bf16, 2>, o) : launch(k_attn_bwd<8, __bf16, 2>, o);
+    else nq == 4 ? launch(k_attn_bwd<4, __bf16, 1>, o) : launch(k_attn_bwd<8, __bf16, 1>, o);
   } else {
     const float* o = (const float*)O.p;
-    nq == 4 ? launch(k_attn_bwd<4, float>, o) : launch(k_attn_bwd<8, float>, o);
+    if (ppl == 2) nq == 4 ? launch(k_attn_bwd<4, float, 2>, o) : launch(k_attn_bwd<8, float, 2>, o);
+    else nq == 4 ? launch(k_attn_bwd<4, float, 1>, o) : launch(k_attn_bwd<8, float, 1>, o);
   }
   return hipGetLastError();
 }

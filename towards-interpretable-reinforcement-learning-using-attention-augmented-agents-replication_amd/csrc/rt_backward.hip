@@ -318,6 +318,7 @@ int lstm_wgrad(const T* dz, const T* xh, int rows, int h, int w, float* gW, hipS
                    : tile6 == 4 ? s6(GemmCfgS6L<256, 256, 16, 2, 4>{})
                    : tile6 == 5 ? s6(GemmCfgS6L<256, 128, 16, 2, 2>{})
                    : tile6 == 6 ? s6(GemmCfgS6L<256, 256, 16, 2, 4, 2>{})
+                   : tile6 == 7 ? s6(GemmCfgS6L<256, 192, 16, 4, 2, 2>{})
                                 : s6(GemmCfgS6<128, 128, 32, 2, 2>{});
 #else
     const int rc = s6(GemmCfgS6L<256, 256, 16, 2, 4, 2>{});
