@@ -249,6 +249,8 @@ k_attn_fwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
       const int p = sl + i * NSL;
       if (p < P) fma_pos(p, cvt(pre[i]));
     }
+    // (a ring refilling each prefetch slot as it is consumed -- kAttnPre loads in flight
+    // through the whole slice -- measured slower: C5 203 vs 190 us, profiles/r05/ab/attn_fwd_ring/)
 #pragma unroll 4
     for (int p = sl + kAttnPre * NSL; p < P; p += NSL)
       fma_pos(p, cvt(*reinterpret_cast<const VR*>(src + (size_t)p * ldb)));
