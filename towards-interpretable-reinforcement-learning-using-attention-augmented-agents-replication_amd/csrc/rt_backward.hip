@@ -806,6 +806,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // single-workgroup and paired kernels: row-padded images (recur_bwd.h kBwIBP) where they fit
         // (C3 LDS bank conflicts 52.8 -> 10.0 %: profiles/r04/ab/rowpad_c3/); AAA_BW_ROWPAD=0 (A/B): 272-B rows only
         rp.rowpad = fb <= 2 && ab_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
+        rp.sc1_all = ab_int("AAA_BW_SC1_ALL", 0);   // band kernel (A/B): sc1 for every dZ row, as in round 4
         HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));
