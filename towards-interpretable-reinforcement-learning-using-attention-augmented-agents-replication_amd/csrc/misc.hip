@@ -368,11 +368,13 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
     int opq = 0;
     asm volatile("" : "+v"(opq));
     const float* dap = da + opq;
-    float acc[PPL][NQ];
+    // packed accumulators: each pair of channels on one v_pk_fma_f32 (the pass is VALU-bound
+    // once PPL positions share the da reads); the halves are summed after the last piece
+    f32x2 acc2[PPL][NQ];
 #pragma unroll
     for (int u = 0; u < PPL; ++u)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) acc[u][q] = 0.f;
+      for (int q = 0; q < NQ; ++q) acc2[u][q] = f32x2{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int j = part + 8 * k;
@@ -390,9 +392,14 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
           const f32x4 d0 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
           const f32x4 d1 = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0 + 4);
 #pragma unroll
-          for (int u = 0; u < PPL; ++u)
-            acc[u][q] += v0[u][0] * d0[0] + v0[u][1] * d0[1] + v0[u][2] * d0[2] + v0[u][3] * d0[3] +
-                         v1[u][0] * d1[0] + v1[u][1] * d1[1] + v1[u][2] * d1[2] + v1[u][3] * d1[3];
+          for (int u = 0; u < PPL; ++u) {
+            f32x2 a = acc2[u][q];
+            a = __builtin_elementwise_fma(f32x2{v0[u][0], v0[u][1]}, f32x2{d0[0], d0[1]}, a);
+            a = __builtin_elementwise_fma(f32x2{v0[u][2], v0[u][3]}, f32x2{d0[2], d0[3]}, a);
+            a = __builtin_elementwise_fma(f32x2{v1[u][0], v1[u][1]}, f32x2{d1[0], d1[1]}, a);
+            a = __builtin_elementwise_fma(f32x2{v1[u][2], v1[u][3]}, f32x2{d1[2], d1[3]}, a);
+            acc2[u][q] = a;
+          }
         }
       } else {               // 4 fp32 channels (O quads of the fp32 path, or S)
         const float m = k < NKO ? (j < NOP ? 1.f : 0.f) : 1.f;
@@ -404,7 +411,12 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
         for (int q = 0; q < NQ; ++q) {
           const f32x4 d = *reinterpret_cast<const f32x4*>(dap + q * 184 + c0);
 #pragma unroll
-          for (int u = 0; u < PPL; ++u) acc[u][q] += v[u][0] * d[0] + v[u][1] * d[1] + v[u][2] * d[2] + v[u][3] * d[3];
+          for (int u = 0; u < PPL; ++u) {
+            f32x2 a = acc2[u][q];
+            a = __builtin_elementwise_fma(f32x2{v[u][0], v[u][1]}, f32x2{d[0], d[1]}, a);
+            a = __builtin_elementwise_fma(f32x2{v[u][2], v[u][3]}, f32x2{d[2], d[3]}, a);
+            acc2[u][q] = a;
+          }
         }
       }
       // one piece's da reads at a time: the next piece's addresses depend on
@@ -413,10 +425,15 @@ k_attn_bwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
 #pragma unroll
       for (int u = 0; u < PPL; ++u)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc[u][q]));
+        for (int q = 0; q < NQ; ++q) asm volatile("" : "+v"(acc2[u][q]));
       asm volatile("" : "+v"(opq));
       dap = da + opq;
     }
+    float acc[PPL][NQ];
+#pragma unroll
+    for (int u = 0; u < PPL; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[u][q] = acc2[u][q][0] + acc2[u][q][1];
     u32x4 kr[PPL];
 #pragma unroll
     for (int u = 0; u < PPL; ++u) kr[u] = kraw[u];
