@@ -107,6 +107,12 @@ class Policy(nn.Module):
         self._slot = 0
 
     def _device(self):
+        # the agent's cached parameter list as last validated (the device of its first
+        # parameter: .to() moves parameters in place), without re-validating it -- the
+        # step's _episode_params does that once per step
+        c = getattr(self.agent, "__dict__", {}).get("_plist")
+        if c is not None and c[3]:
+            return c[3][0].device
         pl = getattr(self.agent, "_param_list", None)
         return pl()[0].device if pl is not None else next(self.agent.parameters()).device
 
