@@ -65,3 +65,6 @@ def test_dp_stranded_step_skipped_on_every_rank():
     assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
     res = json.loads(lines[-1])
     assert res["ok"] and res["raised_mid_step"] is None, res
+    if not res.get("stranded", True):
+        pytest.skip("the filler stranded no rank's launch on this box (premise unmet; both steps ordinary and "
+                    "identical on every rank)")

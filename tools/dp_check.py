@@ -99,7 +99,10 @@ def strand_check(rank, world, dev):
     # ranks share one GPU here, so the filler may strand any rank's launch: at least one must report
     anyh = torch.tensor([1.0 if health == "raised" else 0.0])
     dist.all_reduce(anyh, op=dist.ReduceOp.MAX)
-    ok = raised is None and unchanged and steps == 0 and anyh.item() == 1.0
+    # the premise: the filler stranded some rank's launch (it need not: placement on an idle box
+    # can leave every partner co-resident) -- otherwise the step was an ordinary one everywhere
+    stranded = anyh.item() == 1.0
+    ok = raised is None and unchanged and steps == 0 and stranded
     lr.train_step(X, Gl, Gv)           # clean: every rank updates, identically
     torch.cuda.synchronize()
     lr.check_health()
@@ -108,7 +111,11 @@ def strand_check(rank, world, dev):
     allv = [torch.zeros_like(digest) for _ in range(world)]
     dist.all_gather(allv, digest)
     same = all(torch.equal(allv[0], v) for v in allv)
-    ok = ok and moved and same and lr.opt_steps == 1
+    if stranded:
+        ok = ok and moved and same and lr.opt_steps == 1
+    else:   # nothing stranded: both steps ordinary, still identical on every rank
+        ok = raised is None and moved and same and lr.opt_steps == 2
+    res["stranded"] = stranded
     flags = torch.tensor([1.0 if ok else 0.0])
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     res.update({"raised_mid_step": raised, "params_unchanged_after_stranded_step": unchanged,
