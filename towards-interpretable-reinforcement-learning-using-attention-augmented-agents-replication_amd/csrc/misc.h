@@ -90,6 +90,20 @@ hipError_t gate_bwd_last(int M, int bj, const float* dO, const float* dhT, const
                          const float* ccur, float* dC, TZ* dz, float* part, hipStream_t st, int nsl = 1,
                          size_t sls = 0);
 hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, float* dY, hipStream_t st);
+// The tiny fills of a phase's start in ONE launch (each launch costs ~5 us on the stream however
+// little it does): up to 4 zeroed fp32 ranges, then optionally XH slot 0's h channels <- h0 (or 0)
+// (xh != nullptr) and the cotangent concat dY <- [dlogits | dvalues | 0] (dY != nullptr)
+struct ZeroRanges {
+  float* p[4];
+  long n[4];   // floats
+  int cnt;
+  void add(float* q, long m) {
+    if (q && m > 0) { p[cnt] = q; n[cnt] = m; ++cnt; }
+  }
+};
+template <typename T>
+hipError_t prologue(const ZeroRanges& z, int M, const float* h0, T* xh, int F, int A, int ldy, const float* dl,
+                    const float* dv, float* dY, hipStream_t st);
 template <typename T> hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st);
 template <typename T> hipError_t xh_to_state(int M, const T* xh, float* h, hipStream_t st);
 template <typename T> hipError_t cell_xh(int M, const float* x, const float* h, T* xh, hipStream_t st);

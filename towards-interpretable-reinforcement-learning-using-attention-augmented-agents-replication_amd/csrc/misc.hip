@@ -595,6 +595,38 @@ k_query_colgemv(const float* __restrict__ W, int N, int K, const float* __restri
   }
 }
 
+// k_query_colgemv (blocks [0, cgb)) and k_query_outer (the rest, 1024 threads each) in one
+// launch: the two products of a query layer's backward that need the same input gradient
+__global__ void __launch_bounds__(1024)
+k_query_colgemv_outer(const float* __restrict__ W, int N, int K, const float* __restrict__ x,
+                      const float* __restrict__ mask, float* __restrict__ y, int cgb, const float* __restrict__ a,
+                      int Na, const float* __restrict__ bv, int Kb, float* __restrict__ out, float* acopy) {
+  if ((int)blockIdx.x < cgb) {
+    __shared__ float red[16][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6, k = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (k < K) {
+#pragma unroll 4
+      for (int o = g; o < N; o += 16) s += W[(size_t)o * K + k] * x[o];
+    }
+    red[g][lane] = s;
+    __syncthreads();
+    if (g == 0 && k < K) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) t += red[w][lane];
+      y[k] = mask[k] > 0.f ? t : 0.f;
+    }
+    return;
+  }
+  const int n = Na * Kb, ob = (int)gridDim.x - cgb;
+  for (int i = ((int)blockIdx.x - cgb) * 1024 + (int)threadIdx.x; i < n; i += ob * 1024) {
+    const int o = i / Kb;
+    out[i] = a[o] * bv[i - o * Kb];
+    if (acopy && i < Na) acopy[i] = a[i];
+  }
+}
+
 // out[o][k] = a[o] * b[k] (weight grad of a rank-1 layer), acopy <- a (bias grad).
 __global__ void k_query_outer(const float* __restrict__ a, int N, const float* __restrict__ b, int K,
                               float* __restrict__ out, float* acopy) {
@@ -700,6 +732,40 @@ __global__ void k_state_to_xh(int M, const float* h0, T* xh) {
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += gridDim.x * blockDim.x) {
     const int m = idx >> 7, ch = idx & 127;
     xh[(size_t)m * 192 + 64 + ch] = (T)(h0 ? h0[idx] : 0.f);
+  }
+}
+
+// Block roles: [0, zb) zero the ranges (16-B stores where a range is 16-B aligned), [zb, zb + xb)
+// state_to_xh, the rest concat_dy -- each role grid-strides over its own blocks.
+template <typename T>
+__global__ void __launch_bounds__(256) k_prologue(ZeroRanges z, int zb, int M, const float* h0, T* xh, int xb, int F,
+                                                  int A, int ldy, const float* dl, const float* dv, float* dY) {
+  const int b = (int)blockIdx.x, tid = (int)threadIdx.x;
+  if (b < zb) {
+    const long st = (long)zb * 256, i0 = (long)b * 256 + tid;
+    for (int r = 0; r < z.cnt; ++r) {
+      float* p = z.p[r];
+      const long n = z.n[r], n4 = ((uintptr_t)p & 15) == 0 ? n / 4 : 0;
+      for (long i = i0; i < n4; i += st) reinterpret_cast<f32x4*>(p)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (long i = 4 * n4 + i0; i < n; i += st) p[i] = 0.f;
+    }
+    return;
+  }
+  if (b < zb + xb) {
+    const int n = M * 128;
+    for (int idx = (b - zb) * 256 + tid; idx < n; idx += xb * 256) {
+      const int m = idx >> 7, ch = idx & 127;
+      xh[(size_t)m * 192 + 64 + ch] = (T)(h0 ? h0[idx] : 0.f);
+    }
+    return;
+  }
+  const int cb = (int)gridDim.x - zb - xb, n = F * ldy;
+  for (int idx = (b - zb - xb) * 256 + tid; idx < n; idx += cb * 256) {
+    const int m = idx / ldy, o = idx - m * ldy;
+    float v = 0.f;
+    if (o < A) v = dl[(size_t)m * A + o];
+    else if (o < 2 * A) v = dv ? dv[(size_t)m * A + o - A] : 0.f;
+    dY[idx] = v;
   }
 }
 
@@ -1183,11 +1249,12 @@ hipError_t query_bwd(const float* dQs, const float* gb1, const float* W1, int an
   // straight into the grad buffer (gb2 doubles as dq2 for the next layer).
   const int qd = 72 * nq;
   (void)W1; (void)ans_in;
-  hipLaunchKernelGGL(k_query_colgemv, dim3((qd + 63) / 64), dim3(1024), 0, st, W4, qd, qd, dQs, q2, gb2);
-  hipLaunchKernelGGL(k_query_outer, dim3(nblk((long)qd * qd)), dim3(256), 0, st, dQs, qd, q2, qd, gW4, gb4);
-  hipLaunchKernelGGL(k_query_colgemv, dim3(2), dim3(1024), 0, st, W2, qd, 128, gb2, q1, gb0);
-  hipLaunchKernelGGL(k_query_outer, dim3(nblk((long)qd * 128)), dim3(256), 0, st, gb2, qd, q1, 128, gW2,
-                     (float*)nullptr);
+  // each layer's two products from the same input gradient in one launch (colgemv blocks, then outer)
+  const int cg4 = (qd + 63) / 64, ob4 = nblk((long)qd * qd, 1024), ob2 = nblk((long)qd * 128, 1024);
+  hipLaunchKernelGGL(k_query_colgemv_outer, dim3(cg4 + ob4), dim3(1024), 0, st, W4, qd, qd, dQs, q2, gb2, cg4, dQs,
+                     qd, q2, qd, gW4, gb4);
+  hipLaunchKernelGGL(k_query_colgemv_outer, dim3(2 + ob2), dim3(1024), 0, st, W2, qd, 128, gb2, q1, gb0, 2, gb2, qd,
+                     q1, 128, gW2, (float*)nullptr);
   return hipGetLastError();
 }
 
@@ -1219,6 +1286,20 @@ hipError_t concat_dy(int F, int A, int ldy, const float* dl, const float* dv, fl
 template <typename T>
 hipError_t state_to_xh(int M, const float* h0, T* xh, hipStream_t st) {
   hipLaunchKernelGGL(k_state_to_xh<T>, dim3(nblk((long)M * 128)), dim3(256), 0, st, M, h0, xh);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t prologue(const ZeroRanges& z, int M, const float* h0, T* xh, int F, int A, int ldy, const float* dl,
+                    const float* dv, float* dY, hipStream_t st) {
+  if (z.cnt < 0 || z.cnt > 4) return hipErrorInvalidValue;
+  long zn = 0;
+  for (int r = 0; r < z.cnt; ++r) zn += z.n[r];
+  const int zb = z.cnt ? std::min(nblk(zn / 4 + 1), 1024) : 0;
+  const int xb = xh ? std::min(nblk((long)M * 128), 1024) : 0;
+  const int cb = dY ? std::min(nblk((long)F * ldy), 1024) : 0;
+  if (zb + xb + cb == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_prologue<T>, dim3(zb + xb + cb), dim3(256), 0, st, z, zb, M, h0, xh, xb, F, A, ldy, dl, dv, dY);
   return hipGetLastError();
 }
 
@@ -1367,6 +1448,10 @@ template hipError_t cast<__bf16, float>(long, const __bf16*, float*, hipStream_t
 template hipError_t cast<float, float>(long, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<float>(int, const float*, float*, hipStream_t);
 template hipError_t state_to_xh<__bf16>(int, const float*, __bf16*, hipStream_t);
+template hipError_t prologue<float>(const ZeroRanges&, int, const float*, float*, int, int, int, const float*,
+                                    const float*, float*, hipStream_t);
+template hipError_t prologue<__bf16>(const ZeroRanges&, int, const float*, __bf16*, int, int, int, const float*,
+                                     const float*, float*, hipStream_t);
 template hipError_t xh_to_state<__bf16>(int, const __bf16*, float*, hipStream_t);
 template hipError_t pack_conv<float>(const float*, int, int, int, float*, hipStream_t);
 template hipError_t pack_conv<__bf16>(const float*, int, int, int, __bf16*, hipStream_t);

@@ -514,9 +514,10 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
   if (phases & AAA_BWD_HEAD) {
     {
       TimerScope tim(AAA_TIMER_MISC, st, 0.0, "grad/accumulator memsets, cotangent concat");
-      HIPCHK(hipMemsetAsync(grads, 0, L.ptotal * 4, st));
-      HIPCHK(hipMemsetAsync(ws + L.dQs, 0, L.ws - L.dQs, st));
-      HIPCHK(concat_dy(F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
+      ZeroRanges z{};   // the grads, the atomic accumulators and the cotangent concat: one launch
+      z.add(grads, (long)L.ptotal);
+      z.add(Wf(L.dQs), (long)((L.ws - L.dQs) / 4));
+      HIPCHK(prologue<T>(z, 0, nullptr, (T*)nullptr, F, L.A, L.ldy, io->dlogits, io->dvalues, Wf(L.dY), st));
     }
     if (L.sc) {
       const int rc = head_backward_stateful(L, io, st);
@@ -742,8 +743,14 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     const int cs = chunk_steps(L);
     std::unique_ptr<TimerScope> misc(new TimerScope(AAA_TIMER_MISC, st, 0.0, "BPTT state in, last-step gate backward"));
     // ConvLSTM BPTT, t = T-1 .. 0
-    if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
-    else HIPCHK(hipMemsetAsync(Wf(L.dC), 0, (size_t)M * 128 * 4, st));
+    {   // dc_T = 0 (or the carried grad), and the frame kernels' hand-off flags and dx bias partials: one launch
+      ZeroRanges z{};
+      if (!io->dcT) z.add(Wf(L.dC), (long)M * 128);
+      z.add(Wf(L.rflags), (long)8 * L.B);
+      z.add(Wf(L.dxb), (long)L.B * 64);
+      HIPCHK(prologue<T>(z, 0, nullptr, (T*)nullptr, 0, 0, 1, nullptr, nullptr, nullptr, st));
+      if (io->dcT) HIPCHK(hipMemcpyAsync(Wf(L.dC), io->dcT, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
+    }
     const int t1 = L.T - 1;
     // Sequential part: only the h rows (dh_{t-1}, fused with the gate backward
     // of step t-1); everything else runs in chunks off the chain.
@@ -807,9 +814,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // (C3 LDS bank conflicts 52.8 -> 10.0 %: profiles/r04/ab/rowpad_c3/); AAA_BW_ROWPAD=0 (A/B): 272-B rows only
         rp.rowpad = fb <= 2 && ab_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
         rp.sc1_all = ab_int("AAA_BW_SC1_ALL", 0);   // band kernel (A/B): sc1 for every dZ row, as in round 4
-        HIPCHK(hipMemsetAsync(Wf(L.dxb), 0, (size_t)L.B * 64 * 4, st));
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
-          HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)fb * L.B * 4, st));
           int dev = 0;
           HIPCHK(hipGetDevice(&dev));
           if (!(rp.report = pair_report(dev))) return fail(AAA_E_LAUNCH, "cannot map the paired-kernel report word");
@@ -830,7 +835,6 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     }
     if (fb32) {
       if constexpr (std::is_same<T, float>::value) {
-        HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)8 * L.B * 4, st));
         int dev = 0;
         HIPCHK(hipGetDevice(&dev));
         int* rep = pair_report(dev);

@@ -185,17 +185,20 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
   }
   {  // initial state (reset(): zeros, attention.py:142-149) or carried state
     TimerScope tim(AAA_TIMER_MISC, st, 0.0, "state in/out copies, memsets, bias column sums");
-    HIPCHK(state_to_xh<T>(M, io->h0, Wt(L.XH), st));
+    // one launch: h_0 into XH slot 0, c_0 = 0 (reset) and the hand-off flags of this forward's
+    // multi-workgroup recurrence launch (zeroed here for every kernel choice)
+    ZeroRanges z{};
+    if (!io->c0) z.add(Wf(L.Cst), (long)M * 128);
+    if (phases & AAA_FWD_CORE) z.add(Wf(L.rflags), (long)8 * L.B);
+    HIPCHK(prologue<T>(z, M, io->h0, Wt(L.XH), 0, 0, 1, nullptr, nullptr, nullptr, st));
     if (io->c0 && (cqm_layout(L) & kCqmC)) HIPCHK(cqm_convert(io->c0, Wf(L.Cst), L.B, L.P, 1, st));
     else if (io->c0) HIPCHK(hipMemcpyAsync(Wf(L.Cst), io->c0, (size_t)M * 128 * 4, hipMemcpyDeviceToDevice, st));
-    else HIPCHK(hipMemsetAsync(Wf(L.Cst), 0, (size_t)M * 128 * 4, st));
   }
   // no CORE (aaa_forward_phases, fp32): the recurrence's products are already in
   // Gt / Cst / Hs / XH (aaa_core_import)
   if (!(phases & AAA_FWD_CORE)) return forward_tail<T>(L, io, st);
   if constexpr (std::is_same<T, float>::value) {
     if (const int G = f32_frames(L)) {   // one frame-group launch for all T steps, x-part included (recur_f32.h)
-      HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)G * L.B * 4, st));
       int dev = 0;
       HIPCHK(hipGetDevice(&dev));
       int* rep = pair_report(dev);
@@ -230,7 +233,6 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
       using GT = decltype(gtag);
       if constexpr (!std::is_same<T, float>::value) {
         if (const int NBd = frames_band(L)) {   // one band-mode launch for all T steps (recur.h BAND)
-          HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)NBd * L.B * 4, st));
           int dev = 0;
           HIPCHK(hipGetDevice(&dev));
           int* rep = pair_report(dev);
@@ -248,7 +250,6 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
         if (const int G = frames_fwd(L)) {   // one frame-resident launch for all T steps (recur.h)
           int* rep = nullptr;
           if (G == 2) {
-            HIPCHK(hipMemsetAsync(ws + L.rflags, 0, (size_t)2 * L.B * 4, st));
             int dev = 0;
             HIPCHK(hipGetDevice(&dev));
             if (!(rep = pair_report(dev))) return fail(AAA_E_LAUNCH, "cannot map the paired-kernel report word");
