@@ -128,6 +128,26 @@ static int conv2_wgrad(const Layout& L, const T* dy2, const T* y1, int frames, f
   const int tiles = cdiv(64, C::BI) * cdiv(512, C::BJ);
   if constexpr (std::is_same<T, float>::value) {
     if (f32_split6()) {   // the same tile at fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
+      // A/B (AAA_CONV2_WGRAD_S6L, ablation builds): split-at-commit tiles -- slower here (C2 59.4 ->
+      // 67.9 us for 64x256, profiles/r05/ab/conv_wgrad_s6l/)
+      auto s6l = [&](auto cfg, int ns) -> int {
+        using CW = decltype(cfg);
+        using LA6 = LdRowsTB<T, T, CW::BI, CW::BK, CW::NT>;
+        using LB6 = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
+        typename LA6::Params pa6{dy2, 64, 64, rows};
+        typename LB6::Params pb6{y1, ConvGeo{32, 32, 0, L.H1, L.W1, L.h, L.w, 4, 2, 2, 0}.prep(), 512,
+                                 (uint32_t)((size_t)frames * L.P1 * 32 * L.esz)};
+        HIPCHK((launch_gemm<CW, LA6, LB6>(pa6, pb6, ep, 64, 512, rows, std::max(1, std::min(ns, rows / 128)), s)));
+        return AAA_OK;
+      };
+#ifdef AAA_ABLATION
+      const int c2s = ab_int("AAA_CONV2_WGRAD_S6L", 0);
+      if (c2s == 1) return s6l(GemmCfgS6L<64, 256, 16, 1, 4, 2>{}, 256);
+      if (c2s == 2) return s6l(GemmCfgS6L<64, 256, 16, 2, 4, 2>{}, 128);
+      if (c2s == 3) return s6l(GemmCfgS6L<64, 128, 16, 1, 2, 2>{}, 256);
+#else
+      (void)s6l;
+#endif
       HIPCHK((launch_gemm<typename S6Of<C>::type, LA, LB>(pa, pb, ep, 64, 512, rows, wgrad_splits(tiles, rows, C::BK), s)));
       return AAA_OK;
     }
@@ -178,6 +198,29 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
       else HIPCHK((launch_pipe<CW, PA, PB, EpiAtomicD, 4, 2>(pa, pb, ep, 32, 256, rows1, ns, s)));
       return AAA_OK;
     }
+  }
+  if constexpr (std::is_same<T, float>::value) {
+    // split-at-commit tile over all 256 (tap, channel) columns (GemmCfgS6L: each operand split once
+    // at its LDS commit, two K tiles of loads in flight), 512-way split-K: C2 76.9 -> 66.9 us against
+    // the 32x64 split6 tile (AAA_CONV1_WGRAD_S6L=0 in ablation builds; 2, 3: other tiles / splits,
+    // slower: profiles/r05/ab/conv_wgrad_s6l/)
+    const int c1s = f32_split6() ? ab_int("AAA_CONV1_WGRAD_S6L", 1) : 0;
+    auto s6l = [&](auto cfg, int ns) -> int {
+      using CW = decltype(cfg);
+      using LA6 = LdRowsTB<T, T, CW::BI, CW::BK, CW::NT>;
+      using LB6 = LdIm2colTB<T, T, CW::BJ, CW::BK, CW::NT>;
+      typename LA6::Params pa6{dy1, 32, 32, rows1};
+      typename LB6::Params pb6{xp, ConvGeo{4, 4, 0, L.H + 2, L.W + 2, L.H1, L.W1, 8, 4, 0, 0}.prep(), 256,
+                               (uint32_t)((size_t)frames * (L.H + 2) * (L.W + 2) * 4 * L.esz)};
+      EpiStore<true> ep6{gW, 256, 32, 256};
+      HIPCHK((launch_gemm<CW, LA6, LB6>(pa6, pb6, ep6, 32, 256, rows1, std::max(1, std::min(ns, rows1 / 128)), s)));
+      return AAA_OK;
+    };
+    if (c1s == 1) return s6l(GemmCfgS6L<32, 256, 16, 1, 4, 2>{}, 512);
+#ifdef AAA_ABLATION
+    if (c1s == 2) return s6l(GemmCfgS6L<32, 256, 16, 1, 4, 2>{}, 256);
+    if (c1s == 3) return s6l(GemmCfgS6L<32, 128, 16, 1, 2, 2>{}, 512);
+#endif
   }
   // AAA_CONV1_WGRAD_TILE=1 (A/B): one 32x256 tile covering every (tap, channel) column, so each
   // pixel's 8x8 window is gathered once instead of by four 64-column tiles
