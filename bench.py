@@ -337,8 +337,20 @@ def main():
     ap.add_argument("--timed-steps", type=int, default=1,
                     help="how many of the last timed steps carry the library's per-kernel HIP events "
                          "(1: the last step only, ~0.4 %% of the run's time; K: every timed step)")
+    ap.add_argument("--backend", default=os.environ.get("AAA_BENCH_BACKEND", "nccl"), choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL, the measured path; gloo only for the "
+                         "one-GPU rehearsal of the N > 1 branch in tests/test_gpu_bench_dp.py)")
+    ap.add_argument("--same-device", action="store_true",
+                    default=os.environ.get("AAA_BENCH_SAME_DEVICE") == "1",
+                    help="every rank on cuda:0 (the one-GPU rehearsal; RCCL refuses two ranks on one device)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="rows per rank instead of the config's (rehearsal only: two ranks sharing one GPU must "
+                         "keep their frame-resident grids within half the CUs each)")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["B"] = args.batch
+        cfg["desc"] = cfg["desc"] + f" [--batch {args.batch} per rank: rehearsal override]"
 
     import numpy as np
     import torch
@@ -348,10 +360,10 @@ def main():
     from aaa_amd.learner import Learner
     from aaa_amd.parallel import init_from_env
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)            # before the process group: RCCL binds this rank to its GPU
     dev = torch.device("cuda", local)
-    rank, world, local = init_from_env("nccl", device=dev)
+    rank, world, _ = init_from_env(args.backend, device=dev)
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     B, T, H, W, nq, dtype = cfg["B"], cfg["T"], cfg["H"], cfg["W"], cfg["nq"], cfg["dtype"]

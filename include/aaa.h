@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define AAA_ABI_VERSION 8
+#define AAA_ABI_VERSION 9
 
 enum aaa_status {
   AAA_OK = 0,
@@ -226,6 +226,13 @@ int aaa_backward(const aaa_cfg* cfg, const aaa_io* io, int phases, hipStream_t s
  *    consumption never resets what the device-side reader sees. */
 int aaa_pair_status(hipStream_t stream, int clear);
 int aaa_pair_flag(float* dst, hipStream_t stream);
+/* aaa_pair_flag_at (ABI 9): as aaa_pair_flag, but against the caller's own
+ * snapshot ``base`` (one int of device memory the caller owns; the kernel
+ * reads it, writes the count past it into dst[0] and advances it), so several
+ * readers on one device -- two learners, a learner and a diagnostic -- never
+ * take each other's timeouts.  A new reader syncs its base to the current
+ * report word with one call whose dst it discards. */
+int aaa_pair_flag_at(float* dst, int* base, hipStream_t stream);
 
 /* ---- workspace inspection (checkers, diagnostics) ----
  * Byte offset and size, inside an aaa_forward workspace laid out for ``cfg``,

@@ -257,6 +257,7 @@ class KinkProbe:
         self.masks = masks
         self.mismatch = {}
         self.mismatch_pre = {}   # call -> largest |pre-activation| among the disagreeing units
+        self.units = {}          # call -> units compared (the denominator of mismatch)
 
     def near(self, eps, limit=8):
         """(t, flat index, |pre|) of the units with |pre| < eps, nearest first."""
@@ -280,6 +281,7 @@ class _ProbedReLU(torch.autograd.Function):
         given = given.reshape(x.shape).to(torch.bool)
         dis = given != (x > 0)
         probe.mismatch[t] = int(dis.sum())
+        probe.units[t] = int(dis.numel())
         probe.mismatch_pre[t] = float(x.detach().abs()[dis].max()) if bool(dis.any()) else 0.0
         ctx.save_for_backward(given)
         return x * given.to(x.dtype)

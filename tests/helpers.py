@@ -179,7 +179,8 @@ def kink_report(diag: dict, grads: dict, what: str, pre_scale: float = 1.0) -> d
         gn = float(grads[n].double().norm()) if n in grads else 0.0
         if gn > 0:
             ratios[n] = float(e.double().norm()) / gn
-    rep = {"what": what, "mismatched_units": int(sum(diag["mismatch"].values())),
+    compared = int(sum((diag.get("compared") or {}).values()))
+    rep = {"what": what, "mismatched_units": int(sum(diag["mismatch"].values())), "compared_units": compared,
            "max_mismatched_abs_pre": max(diag["mismatch_pre"].values(), default=0.0),
            "near_zero_units": len(diag.get("units") or []),
            "envelope_norm_ratio_max": max(ratios.values(), default=0.0),
@@ -190,6 +191,11 @@ def kink_report(diag: dict, grads: dict, what: str, pre_scale: float = 1.0) -> d
     assert rep["max_mismatched_abs_pre"] <= MISMATCH_PRE_MAX * pre_scale, (
         f"{what}: a ReLU unit the HIP path switched differently from the oracle has |pre| "
         f"{rep['max_mismatched_abs_pre']:.3e} -- not a rounding-level kink", rep)
+    if diag.get("masked", True) and compared:
+        allowed = max(MISMATCH_UNITS_MIN, MISMATCH_FRAC_MAX * compared)
+        assert rep["mismatched_units"] <= allowed, (
+            f"{what}: {rep['mismatched_units']} of {compared} ReLU units switched differently from the oracle "
+            f"(allowed {allowed:.0f}) -- more than rounding-level kinks", rep)
     return rep
 
 
@@ -198,4 +204,10 @@ def kink_report(diag: dict, grads: dict, what: str, pre_scale: float = 1.0) -> d
 # bf16 rounding of the conv operands and fp32 summation order (the answer-MLP
 # pre-activations agree to ~1e-4 absolute at these weights); a disagreement at a
 # unit further from zero than this would be a real forward error.
-MISMATCH_PRE_MAX = 2e-3
+# Round 6: 1e-4, about 5x the largest disagreeing |pre| measured over the whole GPU suite
+# (1.98e-5 at the C3 shape, profiles/r05/parity/kink_report.jsonl; round 5 allowed 2e-3).
+MISMATCH_PRE_MAX = 1e-4
+# ... and how many units may disagree: at most this fraction of the units compared (round 5's
+# suite: at most 1.1e-5 of them -- 28 of 2.6M at B=256, T=20), or a couple in a small comparison
+MISMATCH_FRAC_MAX = 5e-5
+MISMATCH_UNITS_MIN = 2

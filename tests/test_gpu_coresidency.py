@@ -173,6 +173,9 @@ def test_guarded_adam_skips_stranded_step(cuda):
     from aaa_amd.optim import adam_flat_
     N.pair_status(clear=True)
     N.pair_flag(guard)                 # this reader's snapshot: up to date
+    own = torch.zeros(1, dtype=torch.int32, device=cuda)   # a second reader with its own snapshot (aaa_pair_flag_at)
+    own_guard = torch.zeros(1, device=cuda)
+    N.pair_flag(own_guard, base=own)   # synced to the current word
     runner, flat, packed, basis, frames, ws, dl, dv = args
     before = p.clone()
     with strand_next_launch(cuda):
@@ -186,6 +189,11 @@ def test_guarded_adam_skips_stranded_step(cuda):
     assert int(step.item()) == 0, "a skipped update advanced the step counter"
     N.pair_flag(guard)                 # nothing new since the last flag
     assert float(guard.item()) == 0.0
+    # the library's shared snapshot took the count twice over; the caller-owned one still sees it once
+    N.pair_flag(own_guard, base=own)
+    assert float(own_guard.item()) == consumed, "another reader's pair_flag took this reader's timeouts"
+    N.pair_flag(own_guard, base=own)
+    assert float(own_guard.item()) == 0.0
     adam_flat_(p, g, m, v, 0, guard=guard, step_dev=step)
     torch.cuda.synchronize()
     assert not torch.equal(p, before) and int(step.item()) == 1
@@ -230,3 +238,33 @@ def test_learner_stranded_step_leaves_params(cuda):
     with pytest.raises(RuntimeError, match="timed out"):
         lr.check_health()
     lr.check_health()                  # reported once
+
+
+def test_learner_guard_skips_injected_timeout(cuda):
+    """Deterministic Learner-level guard path (the filler-driven test
+    above depends on dispatch placement and may skip): a non-zero count in the
+    guard slot after the backward -- what the HEAD+CORE all-reduce delivers when
+    any rank's launch timed out -- makes the fused Adam skip the update and its
+    count, and check_health() raise on this rank, as on every rank that received
+    the same sum; the next clean step updates as Adam step 1 and stays quiet."""
+    from aaa_amd.learner import Learner
+    B, T, H, nq, dtype, _ = SHAPES["pairs_c4"]
+    lr = Learner(B, T, H, H, nq, 18, dtype, cuda, frames_u8=True)
+    frames = torch.from_numpy(detinit.frames_u8(1234, (T, B, H, H, 3))).to(cuda)
+    dl = torch.from_numpy(detinit.cotangent(2, (T, B, 18))).to(cuda)
+    dv = torch.from_numpy(detinit.cotangent(3, (T, B, 18))).to(cuda)
+    N.pair_status(clear=True)
+    before = lr.flat.clone()
+    lr.step(frames, dl, dv)
+    lr.guard.fill_(1.0)                # a peer rank's timeout, summed in by the all-reduce
+    lr.optimizer_step()
+    torch.cuda.synchronize()
+    assert torch.equal(lr.flat, before), "the guarded Adam applied a step whose guard was set"
+    assert lr.opt_steps == 0
+    with pytest.raises(RuntimeError, match="timed out"):
+        lr.check_health()
+    lr.train_step(frames, dl, dv)      # clean: the guard is rewritten by this step's own snapshot
+    torch.cuda.synchronize()
+    assert float(lr.guard.item()) == 0.0
+    assert not torch.equal(lr.flat, before) and lr.opt_steps == 1
+    lr.check_health()

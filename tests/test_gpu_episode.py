@@ -127,6 +127,31 @@ def test_episode_matches_oracle(cuda, monkeypatch, actor):
          "fused vs oracle")
 
 
+def test_long_actor_chain_episode_matches_oracle(cuda, monkeypatch):
+    """an episode recorded on the actor chain (its own fp32 kernels'
+    gates, c and h imported into the backward) while the backward recomputes the
+    vision encoder and the tail with the learner's kernels -- two summation
+    orders mixed in one BPTT.  Over 400 steps (7 segments of 64, the ConvLSTM
+    state carried through all of them) the mix must still meet the fp32
+    criterion against the CPU oracle: logits and every gradient at 1e-4."""
+    monkeypatch.setenv("AAA_EPISODE_STORE", "1")
+    monkeypatch.setenv("AAA_EPISODE_ACTOR", "1")
+    T, B = 400, 1
+    X = _frames(T, B, seed=4321)
+    Gl = torch.from_numpy(detinit.normal(12, (T, B, A)))
+    Gv = torch.from_numpy(detinit.normal(13, (T, B, A)))
+    ag = _agent(cuda, True)
+    lf, gf = _episode(ag, X, Gl, Gv, cuda)
+    assert ag._episode.actor is not None and len(ag._episode.steps) == T
+    torch.set_num_threads(16)
+    P = ref_cpu.tensor_params(detinit.deterministic_params(0, A))
+    rl, rv, _ = ref_cpu.unroll(P, X.float())
+    ((rl * Gl).sum() + (rv * Gv).sum()).backward()
+    assert_close(lf.numpy(), rl.detach().numpy(), 1e-4, "400-step actor-chain logits")
+    _cmp(gf, {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}, 1e-4,
+         "400-step actor-chain episode vs oracle")
+
+
 def test_episode_then_unroll_from_its_state(cuda, monkeypatch):
     """A later Agent.unroll continuing from the episode's state sends a state
     cotangent into the episode's last step (the BPTT's dhT / dcT)."""

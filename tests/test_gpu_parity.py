@@ -62,7 +62,7 @@ def _oracle(T, B, nq=4, scale=1.0, conv_mode="fp32", A=18, H=84, W=84, dtype=tor
         loss.backward()
         g = {n: (p.grad if p.grad is not None else torch.zeros_like(p)) for n, p in P.items()}
         env, units = {}, []
-    diag = {"env": env, "units": units, "mismatch": dict(probe.mismatch), "mismatch_pre": dict(probe.mismatch_pre),
+    diag = {"env": env, "units": units, "mismatch": dict(probe.mismatch), "mismatch_pre": dict(probe.mismatch_pre), "compared": dict(probe.units),
             "masked": masks is not None}
     return lg.detach(), vl.detach(), at.detach(), g, diag
 
@@ -567,6 +567,11 @@ def test_c5_full_size_bf16_vs_emulated_oracle(cuda):
         json.dump({"norm_relative_error": raw, "mismatch": diag["mismatch"]}, f, indent=1)
     bad = {n: e for n, e in raw.items() if e > 2e-2}
     assert not bad, f"C5 raw-frame gradients beyond 2e-2 norm-relative: {bad}"
+    for n in rgraw:   # and elementwise (round 6), as the /255 frames below
+        if float(rgraw[n].norm()) == 0.0:
+            assert float(graw[n].abs().max()) == 0.0, n
+        else:
+            assert_close(graw[n].numpy(), rgraw[n].float().numpy(), 2e-2, f"C5 bf16 raw-frame grad {n}")
     # /255 frames
     ag.zero_grad(set_to_none=True)
     ag.relu_trace = []

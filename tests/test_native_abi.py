@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.load().aaa_abi_version() == N.ABI_VERSION == 8
+    assert N.load().aaa_abi_version() == N.ABI_VERSION == 9
 
 
 @pytest.mark.parametrize("H,W,hw", [(84, 84, (11, 11)), (168, 168, (21, 21)), (210, 160, (27, 20))])
@@ -175,3 +175,28 @@ def test_package_modules_import():
     import importlib
     for m in ("learner", "policy", "optim", "parallel", "reinforce", "runtime", "attention"):
         importlib.import_module(f"aaa_amd.{m}")
+
+
+def test_param_cache_follows_replaced_parameters():
+    """Agent._param_list (the per-step parameter list the actor / episode paths
+    use) is re-made when a Parameter object is replaced without a registration
+    hook or a count change: a direct ``_parameters[k] = ...`` and ``.to()``
+    under the overwrite-on-conversion future flag."""
+    import torch
+    import attention
+    a = attention.Agent(num_actions=18)
+    ps = a._param_list()
+    assert ps == list(a.parameters()) and a._param_list() is ps
+    w = a.policy_head[0].weight
+    a.policy_head[0]._parameters["weight"] = torch.nn.Parameter(w.detach().clone())
+    ps2 = a._param_list()
+    assert ps2 is not ps and ps2 == list(a.parameters())
+    assert any(p is a.policy_head[0].weight for p in ps2) and not any(p is w for p in ps2)
+    prev = torch.__future__.get_overwrite_module_params_on_conversion()
+    torch.__future__.set_overwrite_module_params_on_conversion(True)
+    try:
+        a.double()
+        ps3 = a._param_list()
+        assert ps3 == list(a.parameters()) and all(p.dtype == torch.float64 for p in ps3)
+    finally:
+        torch.__future__.set_overwrite_module_params_on_conversion(prev)

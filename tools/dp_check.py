@@ -96,13 +96,18 @@ def strand_check(rank, world, dev):
         health = "quiet"
     except RuntimeError:
         health = "raised"
-    # ranks share one GPU here, so the filler may strand any rank's launch: at least one must report
-    anyh = torch.tensor([1.0 if health == "raised" else 0.0])
+    # ranks share one GPU here, so the filler may strand any rank's launch; check_health() decides
+    # from the all-reduced guard slot, so when one rank raises EVERY rank must (a rank
+    # that stays quiet would wait forever in the next step's all-reduce for the one that left)
+    hv = torch.tensor([1.0 if health == "raised" else 0.0])
+    anyh, allh = hv.clone(), hv.clone()
     dist.all_reduce(anyh, op=dist.ReduceOp.MAX)
+    dist.all_reduce(allh, op=dist.ReduceOp.MIN)
     # the premise: the filler stranded some rank's launch (it need not: placement on an idle box
     # can leave every partner co-resident) -- otherwise the step was an ordinary one everywhere
     stranded = anyh.item() == 1.0
-    ok = raised is None and unchanged and steps == 0 and stranded
+    res["health_all_ranks_agree"] = anyh.item() == allh.item()
+    ok = raised is None and unchanged and steps == 0 and stranded and res["health_all_ranks_agree"]
     lr.train_step(X, Gl, Gv)           # clean: every rank updates, identically
     torch.cuda.synchronize()
     lr.check_health()

@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("AAA_LIB") or os.path.join(_HERE, "libaaa.so")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 8   # include/aaa.h AAA_ABI_VERSION
+ABI_VERSION = 9   # include/aaa.h AAA_ABI_VERSION
 E_STRANDED = -5   # AAA_E_STRANDED
 BWD_HEAD, BWD_CORE, BWD_VISION, BWD_ALL = 1, 2, 4, 7
 FWD_VISION, FWD_CORE, FWD_TAIL, FWD_ALL = 1, 2, 4, 7
@@ -29,7 +29,7 @@ EXPORTS = (
     "aaa_convlstm_packed_bytes", "aaa_convlstm_workspace_bytes", "aaa_convlstm_pack", "aaa_convlstm_cell_fwd",
     "aaa_convlstm_cell_bwd", "aaa_vision_cnn_packed_bytes", "aaa_vision_cnn_workspace_bytes", "aaa_vision_cnn_pack",
     "aaa_vision_cnn_fwd", "aaa_vision_cnn_bwd", "aaa_attn_fwd", "aaa_attn_bwd",
-    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag",
+    "aaa_actor_workspace_bytes", "aaa_actor_step", "aaa_pair_status", "aaa_pair_flag", "aaa_pair_flag_at",
     "aaa_adam_step_guarded", "aaa_adam_step_counted", "aaa_workspace_region",
     "aaa_core_elem_bytes", "aaa_forward_phases", "aaa_core_export", "aaa_core_import",
 )
@@ -139,6 +139,7 @@ def load(path: str = LIB_PATH):
             "aaa_adam_step": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, I, P, P, P, P, P, P, P]),
             "aaa_adam_step_guarded": (I, [ctypes.POINTER(AdamHP), ctypes.c_long, P, I, P, P, P, P, P, P, P]),
             "aaa_pair_flag": (I, [P, P]),
+            "aaa_pair_flag_at": (I, [P, P, P]),
             "aaa_adam_step_counted": (I, [ctypes.POINTER(AdamHP), P, P, I, P, P, P, P, P, P, P]),
             "aaa_core_elem_bytes": (I, [ctypes.POINTER(Cfg), ctypes.POINTER(I), ctypes.POINTER(I)]),
             "aaa_workspace_region": (I, [ctypes.POINTER(Cfg), I, ctypes.POINTER(ctypes.c_size_t),
@@ -258,11 +259,21 @@ def pair_status(clear: bool = True, stream=None) -> int:
     return n
 
 
-def pair_flag(dst, stream=None) -> None:
+def pair_flag(dst, stream=None, base=None) -> None:
     """Enqueue a kernel writing into the one-element fp32 device tensor ``dst``
     the partner timeouts reported since the previous pair_flag on this device
-    (stream order, no host sync; independent of host-side consumption)."""
-    check(load().aaa_pair_flag(dst.data_ptr(), stream if stream is not None else stream_ptr(dst.device)), "pair_flag")
+    (stream order, no host sync; independent of host-side consumption).  With
+    ``base`` (a one-element int32 device tensor the caller owns) the count is
+    taken against that snapshot instead of the library's per-device one, so
+    other readers on the device cannot consume it (aaa_pair_flag_at)."""
+    st = stream if stream is not None else stream_ptr(dst.device)
+    if base is None:
+        check(load().aaa_pair_flag(dst.data_ptr(), st), "pair_flag")
+    else:
+        import torch
+        if base.dtype != torch.int32 or base.device != dst.device:
+            raise ValueError("pair_flag: base must be an int32 tensor on dst's device")
+        check(load().aaa_pair_flag_at(dst.data_ptr(), base.data_ptr(), st), "pair_flag_at")
 
 
 def adam_step(hp: AdamHP, step: int, params, grads, exp_avg, exp_avg_sq, max_exp_avg_sq=None, stream=None,

@@ -455,18 +455,34 @@ class Agent(nn.Module):
         (~60 us of Python per walk; an actor pays it every step).  The list is
         re-made after any parameter or submodule registration (_STRUCT_GEN)
         and whenever a module's parameter or child count changed (deletions
-        register nothing); in-place changes keep the same Parameter objects."""
+        register nothing), and whenever a cached entry is no longer the object its
+        module holds: a Parameter replaced without a registration hook or a count
+        change -- ``.to()`` under torch.__future__'s overwrite-on-conversion flag,
+        or a direct ``_parameters[k] = ...`` -- so gradients never
+        land on tensors the optimizer no longer holds.  In-place changes keep the
+        same Parameter objects."""
         c = self.__dict__.get("_plist")
         if c is not None and c[0] == _STRUCT_GEN[0]:
             n = 0
             for m in c[1]:
                 n += len(m._parameters) + len(m._modules)
             if n == c[2]:
-                return c[3]
+                ps = c[3]
+                for (d, k), p in zip(c[4], ps):
+                    if d.get(k) is not p:
+                        break
+                else:
+                    return ps
         mods = list(self.modules())
         n = sum(len(m._parameters) + len(m._modules) for m in mods)
-        ps = list(self.parameters())
-        self.__dict__["_plist"] = (_STRUCT_GEN[0], mods, n, ps)
+        slots, ps, seen = [], [], set()
+        for m in mods:   # the order of self.parameters(): modules in order, each one's own parameters
+            for k, p in m._parameters.items():
+                if p is not None and id(p) not in seen:
+                    seen.add(id(p))
+                    slots.append((m._parameters, k))
+                    ps.append(p)
+        self.__dict__["_plist"] = (_STRUCT_GEN[0], mods, n, ps, slots)
         return ps
 
     def _check_devices(self, params, device):

@@ -314,6 +314,18 @@ int aaa_pair_flag(float* dst, hipStream_t stream) {
   return AAA_OK;
 }
 
+int aaa_pair_flag_at(float* dst, int* base, hipStream_t stream) {
+  if (!dst || !base) return fail(AAA_E_ARG, "pair_flag_at: NULL dst or base");
+  int r = check_device();
+  if (r) return r;
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  const int* rep = pair_report(dev);
+  if (!rep) return fail(AAA_E_LAUNCH, "cannot map the partner-timeout report word");
+  HIPCHK(pair_flag_launch(rep, base, dst, stream));
+  return AAA_OK;
+}
+
 int aaa_adam_step(const aaa_adam_hparams* hp, long step, int ntensors, float* const* params,
                   const float* const* grads, float* const* exp_avg, float* const* exp_avg_sq,
                   float* const* max_exp_avg_sq, const size_t* numel, hipStream_t stream) {

@@ -57,6 +57,12 @@ class Learner:
         self._gbuf = torch.zeros(r.n_params + 4, device=self.device)
         self.grads = self._gbuf[:r.n_params]
         self.guard = self._gbuf[r.n_params:r.n_params + 1]
+        # this learner's own snapshot of the device's partner-timeout word (aaa_pair_flag_at): no
+        # other reader on the device (another learner, a bench, a diagnostic) can take its timeouts;
+        # synced to the current word now, so timeouts from before this learner existed are not its own
+        self._pair_base = torch.zeros(1, dtype=torch.int32, device=self.device)
+        N.pair_flag(self.guard, base=self._pair_base)
+        self._gbuf.zero_()
         self.lr = lr
         self.exp_avg = torch.zeros_like(self.grads)
         self.exp_avg_sq = torch.zeros_like(self.grads)
@@ -87,7 +93,7 @@ class Learner:
         logits, values, _, _, _ = r.forward(self.flat, self.packed, self.basis, frames, self.ws, want_attn=False)
         if self.world == 1:
             r.backward(self.flat, self.packed, self.basis, frames, self.ws, dlogits, dvalues, grads=self.grads)
-            N.pair_flag(self.guard)
+            N.pair_flag(self.guard, base=self._pair_base)
             return logits, values
         main = torch.cuda.current_stream(self.device)
         self._events = [] if comm_timing else None
@@ -96,7 +102,7 @@ class Learner:
             r.backward(self.flat, self.packed, self.basis, frames, self.ws, dlogits, dvalues, grads=self.grads,
                        phases=phase)
             if phase == N.BWD_CORE:   # every resident launch of this step is enqueued by now
-                N.pair_flag(self.guard)
+                N.pair_flag(self.guard, base=self._pair_base)
             if phase in issue:
                 self._allreduce(main, issue[phase], comm_timing)
         if comm_timing:
@@ -143,13 +149,18 @@ class Learner:
         return int(self.step_dev.item())
 
     def check_health(self):
-        """Raise if a frame-resident launch of this rank timed out waiting for a
-        partner since the last check (syncs the stream; the guarded Adam has
-        already refused such a step's update on every rank)."""
+        """Raise if a frame-resident launch of ANY rank timed out waiting for a
+        partner in the last step (syncs the stream).  The decision is the guard
+        slot, which the HEAD+CORE all-reduce summed over the ranks, so every rank
+        sees the same value and all ranks raise together -- none goes on into the
+        next step's collective while a peer has left.  The host-side
+        count is consumed too (it would otherwise fail the next API call of this
+        process); the guarded Adam has already refused the step's update."""
+        g = float(self.guard.item())
         n = N.pair_status(clear=True)
-        if n:
-            raise RuntimeError(f"aaa: {n} partner wait(s) of a frame-resident launch timed out; the affected "
-                               f"step's optimizer update was skipped on every rank")
+        if g != 0.0 or n:
+            raise RuntimeError(f"aaa: {int(g)} partner wait(s) of a frame-resident launch timed out on the "
+                               f"ranks ({n} on this one); the step's optimizer update was skipped on every rank")
 
     def optimizer_step(self):
         """Adam (lr=1e-3, torch defaults; main_mp.py:92) on the flat params, one
