@@ -48,6 +48,26 @@ def test_f32_frames_vs_oracle(cuda, monkeypatch, T, B, G):
             assert rel_err(out[3][n].numpy(), step[3][n].numpy()) <= 1e-5, f"f32 frames vs per-step grad {n}"
 
 
+def test_f32_frames_small_grid_vs_oracle(cuda, monkeypatch):
+    """P = 64 (64x64 frames: an 8x8 grid) on the pre-split frame-group kernels.
+    The forward's epilogue staging aliases the front of its x image; the images'
+    off-grid zero pixels must lie beyond it (round 6: the two slot-matched zero
+    pixels at the image end; the single zero pixel at P of round 5 sat inside
+    the staging for P < 88)."""
+    monkeypatch.setenv("AAA_F32_FRAMES", "8")
+    T, B = 4, 3
+    N.timing_enable(True)
+    try:
+        out = _run_unroll(_agent(cuda, grid=(8, 8)), T, B, cuda, H=64, W=64)
+        var = N.timing_stats(N.TIMER_FWD_STEP)["variant"]
+        bvar = N.timing_stats(N.TIMER_BPTT_STEP)["variant"]
+    finally:
+        N.timing_enable(False)
+    assert "8 WG per frame" in var and "frame-group BPTT" in bvar, (var, bvar)
+    _compare(out, _oracle(T, B, H=64, W=64), RTOL, "f32 frames 8x8 grid: ")
+    assert N.pair_status(clear=True) == 0
+
+
 @pytest.mark.parametrize("G", ["8", "4"])
 def test_f32_frames_carried_state(cuda, monkeypatch, G):
     """T per-step agent(X_t) calls (main_mp.py:54) -- every call after the first

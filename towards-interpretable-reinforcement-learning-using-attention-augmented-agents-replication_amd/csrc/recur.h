@@ -91,6 +91,14 @@ inline hipError_t pack_wfrag(const __bf16* W, __bf16* Wf, hipStream_t st) {
 
 // Whether a grid runs on the frame-resident kernels.
 inline bool rec_fits(int h, int w) { return h * w <= 128 && (h + 2) * (w + 2) <= kRecNPH; }
+// Row-padded h image of the single-workgroup and paired forward (round 6; the BPTT's
+// bw_rowpad layout, recur_bwd.h): image pixel ip at byte 272 ip + 16 rowpad (ip / W2).  With
+// rowpad = 14 the 16-B slot of (pixel, chunk j) is (ip - 2 (ip / W2) + j) mod 16, so a B-fragment
+// read of 16 consecutive GEMM columns covers 16 consecutive slots across grid-row ends (272-B
+// rows alone skip two slots at every row end: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.49 at
+// C3); a tap still moves every lane's address by one wave-uniform amount.  0 if the padded image
+// does not fit the h-image buffer.
+inline int rec_rowpad(int h, int w) { return (h + 2) * (17 * (w + 2) + 14) * 16 <= kRecNPHB * kRecHS * 2 ? 14 : 0; }
 // Band mode: the grid split into kRecBands bands of whole rows, each band's
 // pixels (<= 128 columns) plus one halo row above and below in the LDS images.
 inline int rec_band_rows(int h, int k) { return (k + 1) * h / kRecBands - k * h / kRecBands; }
@@ -113,6 +121,7 @@ struct RecFwdParams {
   int spin;            // G = 2 / band: partner-wait budget, 100-MHz ticks (pair_wait)
   int stagger;         // start offset (100-MHz ticks) of the frames with (b / 8) odd (stagger_wait)
   int cqm;             // kCqmC / kCqmG: Cst / Gt slices channel-quad-major (cqm4 / cqmg) instead of row-major
+  int rowpad;          // G = 1 / 2 (not band): 16-B slots after each h-image row (0 or 14: rec_rowpad)
   // GEMM column c -> pixel (colpp, -1 = padding column) and the top-left image
   // index of its 3x3 window (colhb); filled by convlstm_fwd_frames (rec_columns)
   short colpp[128], colhb[128];
@@ -243,6 +252,9 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   const int Pb = (r1 - r0) * p.w, pix0 = r0 * p.w;   // the band's pixels (the whole frame without BAND)
   const size_t M = (size_t)p.B * P;
   auto hidx = [&](int pp) { return (pp / p.w - r0 + 1) * W2 + pp % p.w + 1; };   // interior pixel -> image index
+  const int rp = BAND ? 0 : p.rowpad;
+  auto pixb = [&](int ip) { return 272 * ip + 16 * rp * (ip / W2); };   // h image pixel -> byte (rec_rowpad)
+  unsigned char* const himb = reinterpret_cast<unsigned char*>(him);
   const int rb0 = kh * (16 / G) + wave * NRB;   // the wave's first global row block (32 rows = 8 channels)
   const int cbase = 8 * rb0;                     // its first channel
   float* cw = cstl + wave * NRB * 16 * 64 + lane;   // + (rb*16 + cb*4 + g) * 64
@@ -287,7 +299,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     const __bf16* src = p.XH + (size_t)b * P * 192 + 64;
     const int hr0 = BAND ? max(r0 - 1, 0) : 0, hr1 = BAND ? min(r1 + 1, p.h) : p.h;
     for (int i = hr0 * p.w * 16 + tid; i < hr1 * p.w * 16; i += 256)
-      *reinterpret_cast<u32x4*>(him + hidx(i >> 4) * kRecHS + (i & 15) * 8) =
+      *reinterpret_cast<u32x4*>(himb + pixb(hidx(i >> 4)) + (i & 15) * 16) =
           *reinterpret_cast<const u32x4*>(src + (size_t)(i >> 4) * 192 + (i & 15) * 8);
   }
 
@@ -331,13 +343,21 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][cb][e] = 0.f;
-    const __bf16* hbp = him + hh * 8;
-    int hbs[4];   // laundered per step: no per-tap address tables hoisted out of the step loop
+    int hbs[4], hbb[4];   // laundered per step: no per-tap address tables hoisted out of the step loop
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       hbs[cb] = hb[cb];
       asm volatile("" : "+v"(hbs[cb]));
     }
+    // the h image's lane bases (the window's top-left pixel as a byte offset), made where the
+    // h-part starts so they never live beside the x-part's bases
+    auto h_bases = [&] {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        hbb[cb] = pixb(hb[cb]) + hh * 16;
+        asm volatile("" : "+v"(hbb[cb]));
+      }
+    };
     // B fragments of a k step: x image (chunk c4 of 4 at tap offset toff) or h image (chunk c8 of 8)
     auto ldx = [&](int toff, int c4, bf16x8 (&bf)[4]) {
 #pragma unroll
@@ -346,11 +366,13 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         bf[cb] = *reinterpret_cast<const bf16x8*>(xim + ip * 128 + (((2 * c4 + hh) ^ ((ip >> 1) & 7)) << 4));
       }
     };
-    auto ldh = [&](int toff, int c8, bf16x8 (&bf)[4]) {
+    // (the window's columns never cross an image row, so a tap adds 272 toff + 16 rowpad ky: wave-uniform)
+    auto ldh = [&](int toffb, int c8, bf16x8 (&bf)[4]) {
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(hbp + (hbs[cb] + toff) * kRecHS + c8 * 16);
+      for (int cb = 0; cb < 4; ++cb) bf[cb] = *reinterpret_cast<const bf16x8*>(himb + hbb[cb] + toffb + c8 * 32);
     };
     auto tapoff = [&](int tap) { return (tap / 3) * W2 + tap % 3; };
+    auto tapoffb = [&](int tap) { return 272 * tapoff(tap) + 16 * rp * (tap / 3); };
     // one k step: A prefetch PD-1 ahead, next B fragments, 16 MFMAs
     auto kstep = [&](int ks, int slot, bf16x8 (&bc)[4], auto&& load_next_b) {
       if constexpr (!(ABL & 1)) {
@@ -382,7 +404,10 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         kstep(kt + c4, c4 % PD, bfr[c4 & 1], [&] {
           if (c4 < 3) ldx(toff, c4 + 1, bfr[(c4 + 1) & 1]);
           else if (tap < 8) ldx(tn, 0, bfr[0]);
-          else if (G == 1 && !BAND) ldh(0, 0, bfr[0]);
+          else if (G == 1 && !BAND) {
+            h_bases();
+            ldh(0, 0, bfr[0]);
+          }
         });
     }
     barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
@@ -401,12 +426,13 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
           const int gy = i < nh ? r0 - 1 : r1, j = i < nh ? i : i - nh;
           if ((unsigned)gy < (unsigned)p.h) {
             const int pp = gy * p.w + (j >> 4);
-            *reinterpret_cast<u32x4*>(him + hidx(pp) * kRecHS + (j & 15) * 8) =
+            *reinterpret_cast<u32x4*>(himb + pixb(hidx(pp)) + (j & 15) * 16) =
                 __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)((pp * 192 + 64 + (j & 15) * 8) * 2), 0, kSC1);
           }
         }
         barrier_lds();
       }
+      h_bases();
       ldh(0, 0, bfr[0]);
     }
     if constexpr (G == 2) {
@@ -424,17 +450,18 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
         // visibility, hand-off table row 1)
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
         for (int i = tid; i < P * 8; i += 256)
-          *reinterpret_cast<u32x4*>(him + hidx(i >> 3) * kRecHS + 64 * (1 - kh) + (i & 7) * 8) =
+          *reinterpret_cast<u32x4*>(himb + pixb(hidx(i >> 3)) + 128 * (1 - kh) + (i & 7) * 16) =
               __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((i >> 3) * 192 + 64 + 64 * (1 - kh) + (i & 7) * 8) * 2),
                                                     0, (ABL & 16) ? 0 : kSC1);
         barrier_lds();
       }
+      h_bases();
       ldh(0, 0, bfr[0]);
     }
     AAA_FW_STAMP(t, 2);
     // h-part: 9 taps x 8 chunks (k steps 36..107)
     for (int tap = 0; tap < 9; ++tap) {
-      const int toff = tapoff(tap), tn = tap < 8 ? tapoff(tap + 1) : 0;
+      const int toff = tapoffb(tap), tn = tap < 8 ? tapoffb(tap + 1) : 0;
       int kt = kRecKX + tap * 8;
       asm volatile("" : "+s"(kt));
 #pragma unroll
@@ -462,7 +489,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       const int pp = scol[cb * 32 + pl];   // -1: padding column
-      __bf16* hl = him + hidx(max(pp, 0)) * kRecHS + c0;
+      __bf16* hl = reinterpret_cast<__bf16*>(himb + pixb(hidx(max(pp, 0)))) + c0;
       uint32_t gq[NRB][4][2];   // fp16 gate quads (i, f, c~, o), packed
       float hv[NRB][4], cv[NRB][4];
 #pragma unroll
@@ -558,7 +585,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
       for (int i = tid; i < Pb * HC; i += 256) {
         const int px = pix0 + i / HC, q = i % HC;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(himb + pixb(hidx(px)) + q * 16), rs,
                                                (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, kSC1);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -569,13 +596,13 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
       for (int i = tid; i < ((ABL & 2) ? 0 : P * HC); i += 256) {
         const int px = i / HC, q = i % HC;
         *reinterpret_cast<u32x4*>(p.XH + (rown + px) * 192 + 64 + q * 8) =
-            *reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8);
+            *reinterpret_cast<const u32x4*>(himb + pixb(hidx(px)) + q * 16);
       }
     } else {   // the partner reads these: sc1 stores (write through to the coherent level)
       const __amdgpu_buffer_rsrc_t rs = make_rsrc(p.XH + rown * 192, (uint32_t)(P * 192 * 2));
       for (int i = tid; i < P * HC; i += 256) {
         const int px = i / HC, q = i % HC + HC * kh;
-        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(him + hidx(px) * kRecHS + q * 8), rs,
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(himb + pixb(hidx(px)) + q * 16), rs,
                                                (uint32_t)((px * 192 + 64 + q * 8) * 2), 0, (ABL & 16) ? 0 : kSC1);
       }
       // publish h_t's half: every wave's stores retired, a barrier, then one

@@ -233,7 +233,7 @@ __device__ uint64_t aaa_b32_stamps[512 * 64 * 4];
 // three-way split operands (as recur_f32.h S6, gemm.h SPLIT6).
 // PDS: the S6 kernel's A quads in flight (4 or 8).
 // PS (S6 only): the dZ image held pre-split (recur_f32.h k_convlstm_fwd_f32ps's layout:
-// borderless, the zero pixel P, pixel pitch 400 B, chunk (part * 4 + g) * 2 + hh for the
+// borderless, the zero pixel kPsZP (the image's last), pixel pitch 400 B, chunk (part * 4 + g) * 2 + hh for the
 // 16-row group g) -- the gate backward splits each dZ value once as it writes the image,
 // and the K loop reads bf16 parts only (no per-wave split of the B fragments).
 template <int ABL = 0, bool S6 = false, int PDS = kB32PD, bool PS = false, bool DX = false>
@@ -347,9 +347,9 @@ k_convlstm_bwd_f32(RecBwdF32Params p) {
       }
     }
   }
-  auto psbase = [&](int c, int tap) -> uint32_t {
+  auto psbase = [&](int c, int tap) -> uint32_t {   // off-grid taps: the zero pixel kPsZP (recur_f32.h)
     const int nb = colc[c] + (1 - tap / 3) * p.w + (1 - tap % 3);
-    return (uint32_t)((((vmk[c] >> tap) & 1) ? nb : P) * kPsXP + hh * 16);
+    return ps_tap_base((vmk[c] >> tap) & 1, nb, kPsXP, hh);
   };
   const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(8 * kB32QP * 4 * 1024));
   auto lda = [&](int q, int r) {

@@ -572,13 +572,31 @@ k_convlstm_fwd_f32(RecF32Params p) {
 // tap) hit 16 distinct bank groups, and a k-step's three parts are immediate
 // offsets from one per-tap lane address.  The epilogue's staging aliases the x
 // image (x_{t+1} is written after the epilogue).
+//
+// The zero pixel (round 6: at the END of the image, index kPsZP): an off-grid
+// tap reads it.  At P (round 5) it sat inside the x image's aliased epilogue
+// staging for grids with P < 88 (e.g. 64x64 frames: an 8x8 grid), which
+// overwrote it after the first step -- logits 6.8e-2 off the oracle
+// (test_f32_frames_small_grid_vs_oracle).  Off-grid lanes all read that one
+// pixel, so a ds_read_b128 group with such lanes takes a second pass where
+// their slot meets an on-grid lane's (LDS conflict rate 0.34 forward, 0.26
+// BPTT at C2); a slot-matched pair of zero pixels (each off-grid lane at the
+// slot its on-grid address would have had) removed the conflicts and measured
+// SLOWER (C2 forward 745 -> 770 us, BPTT 836 -> 845: the per-tap slot
+// arithmetic costs more than the second pass; profiles/r06/ab/zero_slot/).
 constexpr int kPsHP = 784, kPsXP = 400;                 // pixel pitches (B)
-constexpr int kPsNP = 129;                              // pixels (P <= 128) + the zero pixel
+constexpr int kPsNP = 129;                              // pixels (P <= kPsZP) + the zero pixel
+constexpr int kPsZP = kPsNP - 1;                        // the zero pixel
+__device__ __forceinline__ uint32_t ps_tap_base(bool valid, int nb, int pitch, int hh) {
+  return (uint32_t)((valid ? nb : kPsZP) * pitch + hh * 16);
+}
 constexpr int kPsHB = kPsNP * kPsHP, kPsXB = kPsNP * kPsXP;
 constexpr int kPsGT = 0, kPsCT = 32 * 144;               // per-wave staging: gate tile, c tile
 constexpr int kPsSTG = kPsCT + 32 * 48;                  // 6 KB per wave
 constexpr int kPsHT = 4 * kPsSTG;                        // the workgroup's h_t tile: 128 pixels x 16 channels, pitch 80 B
 static_assert(kPsHT + 128 * 80 <= kPsXB, "staging aliases the x image");
+static_assert(kPsHT + 128 * 80 <= kPsZP * kPsXP, "the staging must not reach the zero pixel");
+
 
 // split 16 fp32 channels of one pixel (group order) into the image's 6 chunks
 __device__ __forceinline__ void ps_store_group(unsigned char* img, int pix_off, int NG, int g, const f32x4 (&v)[4]) {
@@ -642,7 +660,7 @@ k_convlstm_fwd_f32ps(RecF32Params p) {
   // lane byte address of tap ``tap``'s neighbour pixel (or the zero pixel) in an image of ``pitch``
   auto tapbase = [&](int c, int tap, int pitch) -> uint32_t {
     const int nb = colc[c] + (tap / 3 - 1) * W + (tap % 3 - 1);
-    return (uint32_t)((((vmask[c] >> tap) & 1) ? nb : P) * pitch + hh * 16);
+    return ps_tap_base((vmask[c] >> tap) & 1, nb, pitch, hh);
   };
 
   // XH slot loads of 16-channel groups: unit u = (pixel, group) -> 4 x 16 B (sc1 for partner slices)
@@ -675,9 +693,9 @@ k_convlstm_fwd_f32ps(RecF32Params p) {
   };
 
   {  // the zero pixel of both images
-    u32x4* z = reinterpret_cast<u32x4*>(him + P * kPsHP);
+    u32x4* z = reinterpret_cast<u32x4*>(him + kPsZP * kPsHP);
     for (int i = tid; i < kPsHP / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
-    z = reinterpret_cast<u32x4*>(xim + P * kPsXP);
+    z = reinterpret_cast<u32x4*>(xim + kPsZP * kPsXP);
     for (int i = tid; i < kPsXP / 16; i += 256) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
   x_issue(0);
@@ -950,7 +968,7 @@ inline bool f32_fwd_presplit(bool s6, int G, int P) {
 #ifdef AAA_ABLATION
   if (std::getenv("AAA_F32_PRESPLIT") != nullptr) return false;
 #endif
-  return s6 && G == 8 && P <= 128;
+  return s6 && G == 8 && P <= kPsZP;
 }
 
 inline hipError_t convlstm_fwd_f32(RecF32Params& p, int G, hipStream_t st, bool s6 = false) {
