@@ -247,7 +247,7 @@ inline bool halo_fits(int h, int w, int Cin) {
 
 // Host launcher: Mi output rows, nframes frames of h x w pixels.  Returns
 // hipErrorInvalidValue when the geometry does not fit the compile-time tile.
-template <class C, class EP, int KS = 3>
+template <class C, class EP, int KS = 3, int NBUF = 3>
 inline hipError_t launch_halo(const HaloParams& p, const EP& ep, hipStream_t st) {
   const int Hp = p.h + 2, Wp = p.w + 2;
   const int PO = KS == 2 && p.oh ? p.oh * p.ow : p.h * p.w;
@@ -257,7 +257,7 @@ inline hipError_t launch_halo(const HaloParams& p, const EP& ep, hipStream_t st)
   if (KS == 2 && p.oh && (p.oh > p.h || p.ow > p.w)) return hipErrorInvalidValue;
   if ((size_t)p.nframes * p.h * p.w * p.cs * sizeof(typename C::type) > 0x7fffffffu) return hipErrorInvalidValue;
   dim3 grid((p.nframes + C::FR - 1) / C::FR, (p.Mi + C::BI - 1) / C::BI, 1);
-  hipLaunchKernelGGL((conv3_halo_kernel<C, EP, 3, KS>), grid, dim3(C::NT), 0, st, p, ep, tile_map(grid));
+  hipLaunchKernelGGL((conv3_halo_kernel<C, EP, NBUF, KS>), grid, dim3(C::NT), 0, st, p, ep, tile_map(grid));
   return hipGetLastError();
 }
 

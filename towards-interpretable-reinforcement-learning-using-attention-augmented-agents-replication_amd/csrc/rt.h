@@ -28,6 +28,7 @@
 #include "recur_f32.h"
 #include "recur_bwd_f32.h"
 #include "vision.h"
+#include "vision_bwd.h"
 #include "misc.h"
 #include "optim.h"
 #include "actor.h"

@@ -19,14 +19,15 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     // K = 256 loops were pure latency (4 x 65 us at C3, 0.06 of bf16 peak)
     constexpr int CKd = std::is_same<T, float>::value ? 32 : 64;
     const int Ha = (L.H1 + 1) / 2, Wa = (L.W1 + 1) / 2;
-    auto halo4 = [&](auto cfg) -> int {
+    auto halo4 = [&](auto cfg, auto nbuf) -> int {
       using HC = decltype(cfg);
       EpiStoreParity4<T> ep(dy1, frames * Ha * Wa, Ha, Wa, L.H1, L.W1, gbias);
       const HaloParams hp{pk + L.k_WdT2, 256, 128, dy2, 64, 0, 64, (uint32_t)((size_t)frames * L.P * 64 * L.esz),
                           L.h, L.w, frames, 0, Ha, Wa};
-      HIPCHK((launch_halo<HC, EpiStoreParity4<T>, 2>(hp, ep, s)));
+      HIPCHK((launch_halo<HC, EpiStoreParity4<T>, 2, decltype(nbuf)::value>(hp, ep, s)));
       return AAA_OK;
     };
+    using NB3 = std::integral_constant<int, 3>;
     auto fits = [&](int fr, int bj, int hmax) {
       return fr * Ha * Wa <= bj && fr * (L.h + 2) * (L.w + 2) + 1 <= hmax && Ha <= L.h && Wa <= L.w;
     };
@@ -35,15 +36,20 @@ static int conv2_dgrad(const Layout& L, const char* pk, const T* dy2, T* dy1, in
     // (profiles/r02/ab/dgrad_fr.txt; AAA_DGRAD2_FR overrides)
     const int fr = ab_int("AAA_DGRAD2_FR", std::is_same<T, float>::value ? 1 : 2);
     if (ab_int("AAA_DGRAD2_HALO", 1)) {
-      if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{});
+      if (fr == 2 && fits(2, 256, 352)) return halo4(HaloCfg<T, 128, 256, CKd, 2, 2, 2, 352>{}, NB3{});
       if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
-        if (f32_split6() && fits(1, 128, 192)) return halo4(HaloCfgS6<128, 128, CKd, 2, 2, 1, 192>{});
+        // AAA_DGRAD2_NBUF=2 (A/B): a 2-stage weight ring, 80 KB of LDS -> two workgroups per CU
+        if (f32_split6() && fits(1, 128, 192)) {
+          if (ab_int("AAA_DGRAD2_NBUF", 3) == 2)
+            return halo4(HaloCfgS6<128, 128, CKd, 2, 2, 1, 192>{}, std::integral_constant<int, 2>{});
+          return halo4(HaloCfgS6<128, 128, CKd, 2, 2, 1, 192>{}, NB3{});
+        }
       }
-      if (fits(1, 128, 192)) return halo4(HaloCfg<T, 128, 128, CKd, 2, 2, 1, 192>{});
+      if (fits(1, 128, 192)) return halo4(HaloCfg<T, 128, 128, CKd, 2, 2, 1, 192>{}, NB3{});
       // bf16, grids up to 21x21 (168x168 frames, C5): one frame per 512-column tile of 8 waves,
       // 32-channel chunks (two LDS images of 23x23 pixels), the epilogue in two column chunks
       if constexpr (!std::is_same<T, float>::value)
-        if (fits(1, 512, 640) && ab_int("AAA_DGRAD2_WIDE", 1)) return halo4(HaloCfg<T, 128, 512, 32, 2, 4, 1, 640>{});
+        if (fits(1, 512, 640) && ab_int("AAA_DGRAD2_WIDE", 1)) return halo4(HaloCfg<T, 128, 512, 32, 2, 4, 1, 640>{}, NB3{});
     }
   }
   if (ab_int("AAA_CONV2_DGRAD_RING", 1)) {
@@ -424,6 +430,38 @@ int vision_bwd(const Layout& L, const char* pk, const T* dy2, const T* y1, T* xp
   return AAA_OK;
 }
 
+// The frame-resident vision backward (vision_bwd.h): bf16, uint8 observations (the environment's
+// dtype: fp32 frames keep the layered launches), the frame-resident encoder's geometry, and F
+// frames' dY1 buffer large enough for the workgroups' partials (AAA_VIS_BWD_FRAMES=0: the three
+// layered launches above; AAA_VBWD_MINF: a frames-per-CU floor, 0 by default -- with the partial
+// sums reduced 4 waves per 64 columns the fused kernel's fixed cost is ~30 us, below the layered
+// launches' own: C3 (20 frames per CU) 281 vs 358 us, C4 (10) 155 vs 199 us).
+template <typename T>
+static bool vbwd_on(const Layout& L, int F) {
+  if constexpr (!std::is_same<T, __bf16>::value) {
+    (void)L; (void)F;
+    return false;
+  } else {
+    return L.fu8 && vbwd_fits(L.H, L.W, L.H1, L.W1, L.h, L.w) && env_int("AAA_VIS_FRAMES", 1) &&
+           env_int("AAA_VIS_BWD_FRAMES", 1) && F >= env_int("AAA_VBWD_MINF", 0) * device_cus() &&
+           (size_t)vbwd_groups(F, device_cus()) * kVbPart * 4 <= (size_t)F * L.P1 * 32 * L.esz;
+  }
+}
+// F frames from ``f0``: conv2 wgrad (gW2 +=), conv2 dgrad + conv1 wgrad (gW1 +=, conv1 bias gb1 +=),
+// the partials in the frames' dY1 region (unused on this path)
+template <typename T>
+static int vbwd_run(const Layout& L, const char* pk, const void* frames, int f0, int F, const T* dy2, const T* y1,
+                    T* dy1, float* gW2, float* gW1, float* gb1, hipStream_t s) {
+  if constexpr (!std::is_same<T, __bf16>::value) {
+    return fail(AAA_E_ARG, "the frame-resident vision backward is bf16 only");
+  } else {
+    VisBwdParams vp{(const char*)frames + (size_t)f0 * L.H * L.W * 3 * (L.fu8 ? 1 : 4), dy2, y1,
+                    (const __bf16*)(pk + L.k_WdT2), (float*)dy1, F, L.H, L.W, L.H1, L.W1, L.h, L.w};
+    HIPCHK(vision_bwd_frames(vp, device_cus(), gW2, gW1, gb1, s));
+    return AAA_OK;
+  }
+}
+
 // ------------------------------------------------------------ backward ----
 // Stateful policy core, backward of the tail (phase HEAD): the dgrad chain runs
 // step by step from t = T-1 (the carries dh, dc of the core state flow through
@@ -758,9 +796,15 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       }
     }
     if (!vision_here) return AAA_OK;
-    TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L), "conv2 wgrad + dgrad, conv1 wgrad");
     const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
     T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
+    if (vbwd_on<T>(L, F1)) {   // one frame-resident launch (+ its partials' sum)
+      TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L),
+                     "frame-resident conv2 wgrad + dgrad + conv1 wgrad [kernel: k_vision_bwd_frames]");
+      return vbwd_run<T>(L, pk, io->frames, lo * L.B, F1, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, dy1,
+                         Wf(L.gWp2), Wf(L.gWp1), grads + L.poff[C0B], s);
+    }
+    TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L), "conv2 wgrad + dgrad, conv1 wgrad");
     const int rows1 = F1 * L.P1;
     constexpr bool f32 = std::is_same<T, float>::value;   // fp32 with AAA_CONV2_DGRAD_RING=0: conv1 bias by a column sum
     {  // conv2 wgrad
@@ -1097,8 +1141,14 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
 
   if (phases & AAA_BWD_VISION) {
     TimerScope tim(AAA_TIMER_VISION_BWD, st, vision_here ? 0.0 : (double)F * vision_bwd_flop(L),
-                   "conv2 wgrad + dgrad, conv1 wgrad, grad unpack");
-    if (!vision_here) {   // VISION alone: its chunk work over all frames, here
+                   vbwd_on<T>(L, F) ? "frame-resident conv2 wgrad + dgrad + conv1 wgrad [kernel: k_vision_bwd_frames], "
+                                      "grad unpack"
+                                    : "conv2 wgrad + dgrad, conv1 wgrad, grad unpack");
+    if (!vision_here && vbwd_on<T>(L, F)) {   // VISION alone, frame-resident
+      const int rc = vbwd_run<T>(L, pk, io->frames, 0, F, Wt(L.dY2), Wt(L.Y1), Wt(L.dY1), Wf(L.gWp2), Wf(L.gWp1),
+                                 grads + L.poff[C0B], st);
+      if (rc) return rc;
+    } else if (!vision_here) {   // VISION alone: its chunk work over all frames, here
       const int rows1 = F * L.P1;
       constexpr bool f32 = std::is_same<T, float>::value;
       {

@@ -258,8 +258,9 @@ int forward_impl(const Layout& L, const aaa_io* io, hipStream_t st, int phases) 
                               nullptr, (GT*)(ws + L.Gt), (int*)(ws + L.rflags), L.T, L.B, L.h, L.w, L.P,
                               rep, pair_budget(L.T), rec_stagger("AAA_REC_STAGGER_FWD")};
           rp.cqm = cqm_layout(L);
-          // row-padded h image (recur.h rec_rowpad; AAA_REC_ROWPAD=0 in ablation builds: 272-B rows only)
-          rp.rowpad = ab_int("AAA_REC_ROWPAD", 1) ? rec_rowpad(L.h, L.w) : 0;
+          // row-padded h image (recur.h rec_rowpad): measured neutral to 1 % slower (C3 forward 1234-1242 vs
+          // 1247-1269 us, profiles/r06/ab/rowpad_fwd/), so an A/B option (AAA_REC_ROWPAD=1, ablation builds)
+          rp.rowpad = ab_int("AAA_REC_ROWPAD", 0) ? rec_rowpad(L.h, L.w) : 0;
           TimerScope tim(AAA_TIMER_FWD_STEP, st, 2.0 * M * 512 * 1728 * L.T,
                          strf("bf16 frame-resident [x|h] recurrence, %d steps per launch, %d WG per frame%s [kernel: k_convlstm_fwd_frames+Lb0E]",
                               L.T, G, rp.rowpad ? ", row-padded h image" : ""));
