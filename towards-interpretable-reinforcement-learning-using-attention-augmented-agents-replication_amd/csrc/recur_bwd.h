@@ -89,6 +89,7 @@ struct RecBwdParams {   // dO, Gt, Cst: per-(frame, step) slices, channel-quad-m
   int cqm = kCqmC | kCqmG | kCqmDO;   // which slices are channel-quad-major (recur.h kCqm*)
   int rowpad = 0;         // single-workgroup kernel: 16-B slots after each image row (0 or 14: bw_rowpad)
   int sc1_all = 0;        // band kernel: every dZ store / chunk piece sc1 (A/B), not only the exchanged rows
+  int ring = 0;           // single-workgroup kernel: the LDS-DMA epilogue ring (k_convlstm_bwd_frames RING)
 };
 
 // Chunk images of the band kernel: image pixel ip (a (rows+2) x (w+2)
@@ -126,7 +127,8 @@ __device__ uint64_t aaa_bw_stamps[1024 * 64 * 8];
 
 // ABL (diagnostic A/B only: AAA_RECB_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
 // bit 1 = no epilogue HBM loads / stores, bit 2 = no MFMAs, bit 3 = no chunk-3 DMA, bit 4 = no halo exchange (band),
-// bit 5 = no dZ stores (epilogue loads kept), bit 6 = no epilogue loads (dZ stores kept).
+// bit 5 = no dZ stores (epilogue loads kept), bit 6 = no epilogue loads (dZ stores kept), bit 7 = no c_{s-1}
+// loads, bit 8 = no gate loads, bit 9 = no dO loads (single-workgroup kernel).
 //
 // BAND: 21x21 grids (168x168 frames) do not fit one workgroup's images, so
 // kRecBands workgroups split a frame by whole grid rows (recur.h band mode:
@@ -138,13 +140,24 @@ __device__ uint64_t aaa_bw_stamps[1024 * 64 * 8];
 // sc1 loads into the halo rows; chunks 2 and 3 come whole, halo rows included,
 // by LDS-DMA with the sc1 policy.  The bands of a frame get block indices of
 // equal residue mod 8 (one XCD under round-robin placement).
-template <int ABL = 0, bool BAND = false, bool DOACC = !BAND>
+//
+// RING (single-workgroup kernel only): the epilogue's inputs -- c_{s-1}, the 16 fp16 gates and the dc
+// carry of a unit -- arrive by LDS-DMA (inline asm, dma16a) into a wave-private ring of kBwEpD unit
+// slots that replaces the LDS dc carry (the carry lives in p.dC in HBM: read with the unit's inputs,
+// written back with its dZ), and the epilogue waits for a unit with its own counted vmcnt.  The
+// register ring's loads are compiler-visible: with the unit's dZ stores pending (gfx9 counts stores in
+// vmcnt) the compiler treats the counter as out of order and waits vmcnt(0) before every unit, so the
+// register ring never had more than one unit in flight; the DMA'd ring keeps kBwEpD units in flight.
+constexpr int kBwEpD = 4;   // RING: unit slots per wave (4 pieces of 1 KB each: c_{s-1}, gates 0-7, gates 8-15, dc)
+template <int ABL = 0, bool BAND = false, bool DOACC = !BAND, bool RING = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_convlstm_bwd_frames(RecBwdParams p) {
+  static_assert(!RING || (!BAND && DOACC), "the DMA'd epilogue ring is the single-workgroup DOACC kernel's");
   constexpr bool SWZ = BAND;             // swizzled 256-B pixel rows (band) or 272-B rows
   constexpr int PIT = SWZ ? 256 : 272;   // image pixel pitch (bytes)
   constexpr int IMG = SWZ ? kBwIBS : kBwIBP;   // bytes per chunk image
   __shared__ __attribute__((aligned(16))) unsigned char zim[2 * IMG];   // chunk images (0: chunks 0, 2; 1: 1, 3)
-  __shared__ __attribute__((aligned(16))) f32x4 dcl[4 * 16 * 64];          // dc carry, lane-native [wave][g*4+cb][lane]
+  __shared__ __attribute__((aligned(16))) f32x4 dcl[RING ? 1 : 4 * 16 * 64];   // dc carry, lane-native [wave][g*4+cb][lane]
+  __shared__ __attribute__((aligned(16))) unsigned char ering[RING ? 4 * kBwEpD * 4096 : 16];   // [wave][slot][piece][lane]
   int b = (int)blockIdx.x, band = 0, r0 = 0, r1 = p.h;   // band mode: this workgroup's grid rows [r0, r1)
   if constexpr (BAND) {
     const int blk = (int)blockIdx.x, loc = blk >> 3;
@@ -212,16 +225,66 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     fb[cb] = col;
   }
   // dc carry of the lane's 64 (channel, pixel) pairs: channels 32w + 8g + 4hh + e at pixel 32cb + r32
-  f32x4* dcw = dcl + wave * 16 * 64 + lane;   // + (g*4 + cb) * 64
+  f32x4* dcw = dcl + (RING ? 0 : wave * 16 * 64 + lane);   // + (g*4 + cb) * 64
+  if constexpr (!RING) {
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int col = cb * 32 + r32;
-      dcw[(g * 4 + cb) * 64] =
-          col < Pb ? *reinterpret_cast<const f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int cb = 0; cb < 4; ++cb) {
+        const int col = cb * 32 + r32;
+        dcw[(g * 4 + cb) * 64] =
+            col < Pb ? *reinterpret_cast<const f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+  // RING: unit u = (g, cb) of step s into the wave's slot u % kBwEpD -- four 1-KB DMA pieces, lane-native
+  // (lane i's 16 B at 16 i); columns past the band read out of range and land as zeros, whose gate
+  // backward is exactly zero (every gate 0)
+  unsigned char* const eslots = ering + wave * kBwEpD * 4096;
+  auto ring_issue = [&](int s, int u) {
+    int ln = lane;   // laundered: the unit's offsets are recomputed per step (hoisted, they spill)
+    asm volatile("" : "+v"(ln));
+    const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
+    const bool v = col < Pb && !(ABL & 66);
+    const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g, pp = pix0 + col;
+    const size_t fr = (size_t)s * M + (size_t)b * P;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(p.Cst + fr * 128, (uint32_t)(P * 128 * 4));
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.Gt + fr * 512, (uint32_t)(P * 512 * 2));
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(p.dC + (size_t)b * P * 128, (uint32_t)(P * 128 * 4));
+    unsigned char* slot = eslots + (u % kBwEpD) * 4096;
+    const uint32_t go = v ? (uint32_t)(slcg(pp, ch, P, p.cqm & kCqmG) * 2) : kOOB;
+    dma16a(rc, slot, v ? (uint32_t)(slc4(pp, ch, P, p.cqm & kCqmC) * 4) : kOOB);
+    dma16a(rg, slot + 1024, go);
+    dma16a(rg, slot + 2048, go, 16);
+    dma16a(rd, slot + 3072, v ? (uint32_t)((pp * 128 + ch) * 4) : kOOB);
+  };
+  // Wait until unit u's pieces have landed.  vmcnt(N) waits for all but the wave's N youngest
+  // vector-memory operations, loads, stores and LDS-DMA alike, in issue order (MI355X_MICROARCH), so N
+  // counts every operation issued after the unit's four pieces: per epilogue iteration v its two dZ
+  // stores, its dc store, the pieces of unit v + kBwEpD (v + kBwEpD < 16) and its dO load -- all
+  // unconditional (out-of-range columns use out-of-range offsets), so the count is exact; the
+  // operations it leaves out (dx stores between the pre-issue and the epilogue, gate-bias partial
+  // stores) only make the wait longer.
+  auto ring_wait = [&](int u) {
+    auto ops = [](int v) { return 3 + (v + kBwEpD < 16 ? 4 : 0) + 1; };
+    int n = 0;
+    if (u < kBwEpD) {   // pre-issued in unit order before iteration 0
+      n = 4 * (kBwEpD - 1 - u);
+      for (int v = 0; v < u; ++v) n += ops(v);
+    } else {            // issued in iteration u - kBwEpD, before that iteration's dO load
+      n = 1;
+      for (int v = u - kBwEpD + 1; v < u; ++v) n += ops(v);
     }
+    switch (n) {   // (u is a constant of the unrolled epilogue: the switch folds)
+#define AAA_RW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+      AAA_RW(0) AAA_RW(1) AAA_RW(2) AAA_RW(3) AAA_RW(4) AAA_RW(5) AAA_RW(6) AAA_RW(7) AAA_RW(8) AAA_RW(9)
+      AAA_RW(10) AAA_RW(11) AAA_RW(12) AAA_RW(13) AAA_RW(14) AAA_RW(15) AAA_RW(16) AAA_RW(17) AAA_RW(18)
+      AAA_RW(19) AAA_RW(20) AAA_RW(21) AAA_RW(22) AAA_RW(23) AAA_RW(24) AAA_RW(25) AAA_RW(26) AAA_RW(27)
+      AAA_RW(28) AAA_RW(29) AAA_RW(30) AAA_RW(31) AAA_RW(32)
+#undef AAA_RW
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
 
   // A stream: per k step the wave's h row block (wave) and its dx row block (4 + wave % 2)
   const __amdgpu_buffer_rsrc_t rsw = make_rsrc(p.Wb, (uint32_t)(6 * kBwKSP * 1024));
@@ -261,10 +324,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       const size_t fr = (size_t)s * M + (size_t)b * P;
       const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g, pp = pix0 + col;
       if constexpr (!DOACC) in.dO = *reinterpret_cast<const f32x4*>(p.dO + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmDO));
-      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));   // c_{s-1}
+      // (ABL 128 / 256: without the c / the gate loads -- which of the epilogue's inputs costs what)
+      if constexpr (!(ABL & 128)) in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));
+      else in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
       const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + fr * 512 + slcg(pp, ch, P, p.cqm & kCqmG));
-      in.gt[0] = gp[0];
-      in.gt[1] = gp[1];
+      if constexpr (!(ABL & 256)) {
+        in.gt[0] = gp[0];
+        in.gt[1] = gp[1];
+      } else {
+        in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
+      }
     } else {
       in.dO = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
       in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
@@ -275,9 +344,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto load_dO = [&](f32x16 (&acc)[4], int s, int u, int ln) {
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
     f32x4 v{0.f, 0.f, 0.f, 0.f};
-    if (s >= 0 && col < Pb && !(ABL & 66))
+    if constexpr (RING) {   // always one load (ring_wait counts it): out of range for s < 0 / past the band
+      const bool ok = s >= 0 && col < Pb && !(ABL & 66);
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.dO + ((size_t)max(s, 0) * M + (size_t)b * P) * 128,
+                                                  (uint32_t)(P * 128 * 4));
+      v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                        ro, ok ? (uint32_t)(slc4(pix0 + col, 32 * wave + 4 * (ln >> 5) + 8 * g, P,
+                                                                 p.cqm & kCqmDO) * 4)
+                                           : kOOB, 0, 0));
+    } else if (s >= 0 && col < Pb && !(ABL & (66 | 512))) {   // (ABL 512: without the dO loads)
       v = *reinterpret_cast<const f32x4*>(p.dO + ((size_t)s * M + (size_t)b * P) * 128 +
                                           slc4(pix0 + col, 32 * wave + 4 * (ln >> 5) + 8 * g, P, p.cqm & kCqmDO));
+    }
     acc[cb][4 * g] = v[0]; acc[cb][4 * g + 1] = v[1]; acc[cb][4 * g + 2] = v[2]; acc[cb][4 * g + 3] = v[3];
   };
 
@@ -293,6 +371,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     const int c0 = 32 * wave + 4 * hq;   // + 8g + e
     const size_t rows = (size_t)s * M + (size_t)b * P;
     const __amdgpu_buffer_rsrc_t rz = make_rsrc(p.dZ + rows * 512, (uint32_t)(P * 512 * 2));
+    const __amdgpu_buffer_rsrc_t rdc = make_rsrc(p.dC + (size_t)b * P * 128, (uint32_t)(P * 128 * 4));   // RING
+    (void)rdc;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       float bs[16];   // [e][gate] sums over the lane's pixels (this channel group)
@@ -302,6 +382,49 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int u = g * 4 + cb;
+        if constexpr (RING) {   // branch-free: out-of-range columns read zeros and store out of range
+          ring_wait(u);
+          const unsigned char* sl = eslots + (u % kBwEpD) * 4096 + ln * 16;
+          const f32x4 cp = *reinterpret_cast<const f32x4*>(sl);
+          const u32x4 gt[2] = {*reinterpret_cast<const u32x4*>(sl + 1024), *reinterpret_cast<const u32x4*>(sl + 2048)};
+          f32x4 dc = *reinterpret_cast<const f32x4*>(sl + 3072);
+          const int col = cb * 32 + pl, pp = pix0 + col;
+          const bool v = col < Pb;
+          const f32x4 dh{acc[cb][4 * g], acc[cb][4 * g + 1], acc[cb][4 * g + 2], acc[cb][4 * g + 3]};
+          float dz[16];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t w01 = gt[e >> 1][2 * (e & 1)], w23 = gt[e >> 1][2 * (e & 1) + 1];
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            const h2 a = __builtin_bit_cast(h2, w01), c2 = __builtin_bit_cast(h2, w23);
+            const f32x4 gv{(float)a[0], (float)a[1], (float)c2[0], (float)c2[1]};
+            float d = dc[e], di, df, dcg, dout;
+            gate_bwd_fast(dh[e], gv, cp[e], gv[1] * cp[e] + gv[0] * gv[2], d, di, df, dcg, dout);
+            dc[e] = d;
+            dz[4 * e] = di; dz[4 * e + 1] = df; dz[4 * e + 2] = dcg; dz[4 * e + 3] = dout;
+            bs[4 * e] += di; bs[4 * e + 1] += df; bs[4 * e + 2] += dcg; bs[4 * e + 3] += dout;
+          }
+          bf16x8 z0, z1;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { z0[i] = (__bf16)dz[i]; z1[i] = (__bf16)dz[8 + i]; }
+          if constexpr (!(ABL & 34)) {
+            const uint32_t zo = v ? (uint32_t)((pp * 512 + 4 * ch) * 2) : kOOB;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z0), rz, zo, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, z1), rz, zo, 16, 0);
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dc), rdc,
+                                                 v ? (uint32_t)((pp * 128 + ch) * 4) : kOOB, 0, 0);
+          if (wave < 2 && v) {   // chunk w of the next step's B operand: rows 4(ch - 32w) + gate = slots 4g + 2hq, +1
+            unsigned char* zi = zim + wave * IMG + pixb(hidx(pp));
+            const int s0 = 4 * g + 2 * hq;
+            *reinterpret_cast<bf16x8*>(zi + (s0 << 4)) = z0;
+            *reinterpret_cast<bf16x8*>(zi + ((s0 + 1) << 4)) = z1;
+          }
+          if (u + kBwEpD < 16) ring_issue(s, u + kBwEpD);   // the slot just read: unit u + kBwEpD
+          load_dO(acc, s - 1, u, ln);   // the slot's next value: dO_{s-1}
+          __builtin_amdgcn_sched_barrier(0);
+          continue;
+        }
         if (u + kRing - 1 < 16) ring[(u + kRing - 1) % kRing] = load_in(s, u + kRing - 1, ln);
         const EpIn& in = ring[u % kRing];
         const int col = cb * 32 + pl;
@@ -397,8 +520,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   {  // step T-1: no GEMM (dh = dO_{T-1} + dhT)
     f32x16 (&acc)[4] = acc_carry;
     EpIn ring[kRing];
+    if constexpr (RING) {
 #pragma unroll
-    for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(p.T - 1, u, lane);
+      for (int u = 0; u < kBwEpD; ++u) ring_issue(p.T - 1, u);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kRing - 1; ++u) ring[u] = load_in(p.T - 1, u, lane);
+    }
     if constexpr (DOACC) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -507,7 +635,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
                                     // retired (its later A loads did): refill it with chunk ck+1 from HBM
           if constexpr (!(ABL & 8)) dma_chunk(t, ck + 1);
         }
-        if (ck == 3 && t > 0) {   // the epilogue's first inputs, under chunk 3
+        if (!RING && ck == 3 && t > 0) {   // the epilogue's first inputs, under chunk 3
           int ln = lane;
           asm volatile("" : "+v"(ln));
   #pragma unroll
@@ -555,6 +683,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     };
     if (wave >> 1) kloop(std::integral_constant<int, 2>{});
     else kloop(std::integral_constant<int, 0>{});
+    if constexpr (RING) {
+      if (t > 0) {   // the next epilogue's first kBwEpD units, under the dx stores; the dc carries
+                     // they read were stored by the last epilogue (retired: vmcnt(0) first)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < kBwEpD; ++u) ring_issue(t - 1, u);
+      }
+    }
     {  // dx_t (conv2 output grad) to HBM in bf16; its fp32 sums into the conv2 bias partials
       const size_t rows = (size_t)t * M + (size_t)b * P;
 #pragma unroll
@@ -614,16 +750,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
       atomicAdd(p.dxb + (size_t)b * 64 + 32 * (wave & 1) + 8 * g + 4 * hh + e, v[0]);
     }
   }
-  // dc carry out (dc_0)
+  // dc carry out (dc_0; RING: already in p.dC, written by the last epilogue)
+  if constexpr (!RING) {
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int col = cb * 32 + r32;
-      if (col < Pb)
-        *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh) =
-            dcw[(g * 4 + cb) * 64];
-    }
+      for (int cb = 0; cb < 4; ++cb) {
+        const int col = cb * 32 + r32;
+        if (col < Pb)
+          *reinterpret_cast<f32x4*>(p.dC + ((size_t)b * P + pix0 + col) * 128 + 32 * wave + 8 * g + 4 * hh) =
+              dcw[(g * 4 + cb) * 64];
+      }
+  }
 }
 
 // Paired variant, for batches below the CU count: two workgroups per frame.
@@ -981,9 +1119,15 @@ inline hipError_t convlstm_bwd_frames(const RecBwdParams& p, hipStream_t st) {
 #define AAA_RECB_CASE(a) \
   case a: hipLaunchKernelGGL((k_convlstm_bwd_frames<a>), dim3(p.B), dim3(256), 0, st, p); return hipGetLastError();
     AAA_RECB_CASE(1) AAA_RECB_CASE(2) AAA_RECB_CASE(3) AAA_RECB_CASE(4) AAA_RECB_CASE(8) AAA_RECB_CASE(6)
-    AAA_RECB_CASE(32) AAA_RECB_CASE(64)
+    AAA_RECB_CASE(32) AAA_RECB_CASE(64) AAA_RECB_CASE(128) AAA_RECB_CASE(256) AAA_RECB_CASE(512)
 #undef AAA_RECB_CASE
     default: break;
+  }
+#endif
+#ifdef AAA_ABLATION   // the LDS-DMA epilogue ring (RING): measured slower, profiles/r06/ab/bw_ring/
+  if (p.ring) {
+    hipLaunchKernelGGL((k_convlstm_bwd_frames<0, false, true, true>), dim3(p.B), dim3(256), 0, st, p);
+    return hipGetLastError();
   }
 #endif
   hipLaunchKernelGGL((k_convlstm_bwd_frames<0>), dim3(p.B), dim3(256), 0, st, p);

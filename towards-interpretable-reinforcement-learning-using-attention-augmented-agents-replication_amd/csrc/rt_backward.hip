@@ -901,6 +901,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
         // (C3 LDS bank conflicts 52.8 -> 10.0 %: profiles/r04/ab/rowpad_c3/); AAA_BW_ROWPAD=0 (A/B): 272-B rows only
         rp.rowpad = fb <= 2 && ab_int("AAA_BW_ROWPAD", 1) ? bw_rowpad(L.h, L.w) : 0;
         rp.sc1_all = ab_int("AAA_BW_SC1_ALL", 0);   // band kernel (A/B): sc1 for every dZ row, as in round 4
+        // single-workgroup kernel: the epilogue's inputs by LDS-DMA into a counted ring (recur_bwd.h RING)
+        rp.ring = fb == 1 && ab_int("AAA_BW_RING", 0);   // measured slower: ablation builds only
         if (fb >= 2) {   // paired or band mode: hand-off flags [B][fb]
           int dev = 0;
           HIPCHK(hipGetDevice(&dev));
@@ -913,7 +915,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                              ? strf("bf16 band-mode frame-resident BPTT + dx, %d steps per launch, %d bands per frame, "
                                     "fp16 gates [kernel: k_convlstm_bwd_frames<0, true]", L.T, fb)
                              : strf("bf16 frame-resident BPTT + dx, %d steps per launch, %d WG per frame, fp16 gates "
-                                    "[kernel: %s]", L.T, fb, fb == 2 ? "k_convlstm_bwd_pairs" : "k_convlstm_bwd_frames<0, false"));
+                                    "[kernel: %s]", L.T, fb, fb == 2 ? "k_convlstm_bwd_pairs" : (rp.ring ? "k_convlstm_bwd_frames<ring>" : "k_convlstm_bwd_frames<0, false")));
           HIPCHK(fb == 2 ? convlstm_bwd_pairs(rp, st) : (fb == 1 ? convlstm_bwd_frames(rp, st) : convlstm_bwd_band(rp, st)));
         }
         HIPCHK(colsum<float>(Wf(L.dxb), 64, L.B, 64, grads + L.poff[C1B], st));
