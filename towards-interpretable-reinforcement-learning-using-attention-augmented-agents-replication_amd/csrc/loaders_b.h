@@ -21,6 +21,16 @@ constexpr uint32_t kOOB = 0x80000000u;  // >= num_records of every buffer we bui
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
+// The same from a base address and size the compiler cannot prove wave-uniform although they are
+// (e.g. derived through a lambda's captures): readfirstlane'd, so the descriptor sits in SGPRs -- an
+// inline-asm "s" operand (dma16a) otherwise receives VGPRs and does not assemble.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(size_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)bytes);
+  return make_rsrc(reinterpret_cast<const void*>((size_t)lo | ((size_t)hi << 32)), n);
+}
 __device__ __forceinline__ u32x4 bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0);
 }

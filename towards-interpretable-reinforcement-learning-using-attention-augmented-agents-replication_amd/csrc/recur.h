@@ -202,7 +202,8 @@ __device__ uint64_t aaa_fw_stamps[1024 * 64 * 8];
 #endif
 
 // ABL (diagnostic A/B only: AAA_REC_ABL, honoured only in a -DAAA_ABLATION build): bit 0 = no A loads in the K loop,
-// bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads.
+// bit 1 = no epilogue HBM stores, bit 2 = no MFMAs, bit 3 = no B fragment reads, bit 6 = the in-loop x-image
+// LDS-DMA compiler-visible (the pre-round-6 form).
 //
 // G = 2 (batches too small to give every CU a frame): two workgroups per frame,
 // half kh owning gate rows [256kh, 256kh+256) (its 64 channels); each step it
@@ -271,17 +272,26 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
   // fragment reads of 16 consecutive pixels then hit 16 distinct bank groups);
   // border pixels read outside the descriptor and land as zeros.  Wave w issues
   // the 1-KB pieces w, w+4, ... of the 22 (8 pixels each).
-  auto dma_x = [&](int t) {
+  // In the step loop (asm = true) the pieces are issued from inline asm (dma16a): a compiler-visible
+  // LDS-DMA in flight makes the compiler wait vmcnt(0) before every LDS read that might alias it -- the
+  // epilogue's staging, c and bias reads, each then also waiting for the gate / c / h stores issued just
+  // before it (~40 drains per step).  Nothing reads the x image before the h-part's A-stream waits, which
+  // retire these older pieces (vmcnt retires in issue order) ahead of the barrier that ends the step.
+  auto dma_x = [&](int t, bool asm_issue) {
     const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
+        make_rsrc_u(p.XH + ((size_t)t * M + (size_t)b * P) * 192, (uint32_t)(P * 192 * 2));
+    int ln = lane;   // laundered: the pieces' offsets are recomputed per step (hoisted, they spill)
+    asm volatile("" : "+v"(ln));
     for (int i = wave; i < kRecXB / 1024; i += 4) {
-      const int sl = i * 64 + lane, ip = sl >> 3, q = (sl & 7) ^ ((ip >> 1) & 7);
+      const int sl = i * 64 + ln, ip = sl >> 3, q = (sl & 7) ^ ((ip >> 1) & 7);
       const int py = r0 + ip / W2 - 1, px = ip % W2 - 1;
       const bool v = ip < NPH && (unsigned)py < (unsigned)p.h && (unsigned)px < (unsigned)p.w;
-      dma16(rs, xim + i * 1024, v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB);
+      const uint32_t vo = v ? (uint32_t)(((py * p.w + px) * 192 + q * 8) * 2) : kOOB;
+      if (asm_issue) dma16a(rs, xim + i * 1024, vo);
+      else dma16(rs, xim + i * 1024, vo);
     }
   };
-  dma_x(0);
+  dma_x(0, false);
   // cell state c_0 (Cst slot 0) into the lane-native LDS copy
 #pragma unroll
   for (int rb = 0; rb < NRB; ++rb)
@@ -412,7 +422,7 @@ __global__ void __launch_bounds__(256) k_convlstm_fwd_frames(RecFwdParams<GT> p)
     }
     barrier_lds();   // every wave is done with x_t: refill the image with x_{t+1} under the h-part
     AAA_FW_STAMP(t, 1);
-    if (t + 1 < p.T) dma_x(t + 1);
+    if (t + 1 < p.T) dma_x(t + 1, !(ABL & 64));   // (ABL 64, A/B: the compiler-visible form)
     if constexpr (BAND) {
       if (t > 0) {   // the neighbour bands' boundary rows of h_{t-1} (XH slot t) into the halo rows
         if (wave == 0)   // the neighbour bands' flags, both in one poll
@@ -651,7 +661,7 @@ inline hipError_t convlstm_fwd_frames(const RecFwdParams<GT>& p, int G, hipStrea
   switch (e ? atoi(e) : 0) {
 #define AAA_REC_CASE(a) \
   case a: hipLaunchKernelGGL((k_convlstm_fwd_frames<GT, 1, a>), dim3(p.B), dim3(256), 0, st, q); return hipGetLastError();
-    AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12)
+    AAA_REC_CASE(1) AAA_REC_CASE(2) AAA_REC_CASE(3) AAA_REC_CASE(4) AAA_REC_CASE(8) AAA_REC_CASE(12) AAA_REC_CASE(64)
 #undef AAA_REC_CASE
     default: break;
   }

@@ -320,32 +320,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
   auto load_in = [&](int s, int u, int ln) {
     EpIn in;
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
-    if (col < Pb && !(ABL & 66)) {   // the slices are channel-quad-major (recur.h cqm4 / cqmg)
-      const size_t fr = (size_t)s * M + (size_t)b * P;
-      const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g, pp = pix0 + col;
-      if constexpr (!DOACC) in.dO = *reinterpret_cast<const f32x4*>(p.dO + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmDO));
-      // (ABL 128 / 256: without the c / the gate loads -- which of the epilogue's inputs costs what)
-      if constexpr (!(ABL & 128)) in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));
-      else in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
-      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + fr * 512 + slcg(pp, ch, P, p.cqm & kCqmG));
-      if constexpr (!(ABL & 256)) {
-        in.gt[0] = gp[0];
-        in.gt[1] = gp[1];
-      } else {
-        in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
-      }
-    } else {
-      in.dO = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
-      in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
+    // buffer loads, out-of-range offsets past the band (the hardware returns zeros): no branch, and no
+    // zero-fill of the destinations on the other path -- a write to a register with a load in flight
+    // made the compiler wait vmcnt(0) right after issuing the ring's loads, so the ring held nothing
+    const bool v = col < Pb && !(ABL & 66);
+    const size_t fr = (size_t)s * M + (size_t)b * P;
+    const int ch = 32 * wave + 4 * (ln >> 5) + 8 * g, pp = pix0 + col;
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(p.Cst + fr * 128, (uint32_t)(P * 128 * 4));
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.Gt + fr * 512, (uint32_t)(P * 512 * 2));
+    if constexpr (!DOACC) {
+      const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.dO + fr * 128, (uint32_t)(P * 128 * 4));
+      in.dO = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            ro, v ? (uint32_t)(slc4(pp, ch, P, p.cqm & kCqmDO) * 4) : kOOB, 0, 0));
     }
+    in.cp = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rc, v && !(ABL & 128) ? (uint32_t)(slc4(pp, ch, P, p.cqm & kCqmC) * 4) : kOOB,
+                                          0, 0));
+    const uint32_t go = v && !(ABL & 256) ? (uint32_t)(slcg(pp, ch, P, p.cqm & kCqmG) * 2) : kOOB;
+    in.gt[0] = __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0);
+    in.gt[1] = __builtin_amdgcn_raw_buffer_load_b128(rg, go, 16, 0);
     return in;
   };
   // dO_s of unit u into its accumulator slot (zero past the band's columns, or for s < 0: dh_{-1} has no dO)
   auto load_dO = [&](f32x16 (&acc)[4], int s, int u, int ln) {
     const int g = u >> 2, cb = u & 3, col = cb * 32 + (ln & 31);
     f32x4 v{0.f, 0.f, 0.f, 0.f};
-    if constexpr (RING) {   // always one load (ring_wait counts it): out of range for s < 0 / past the band
-      const bool ok = s >= 0 && col < Pb && !(ABL & 66);
+    if constexpr (RING || !BAND) {   // always one load (RING: ring_wait counts it; no branch): out of range for s < 0 / past the band
+      const bool ok = s >= 0 && col < Pb && !(ABL & (66 | 512));
       const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.dO + ((size_t)max(s, 0) * M + (size_t)b * P) * 128,
                                                   (uint32_t)(P * 128 * 4));
       v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -858,21 +859,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 
   struct EpIn { f32x4 dO, cp; u32x4 gt[2]; };
   constexpr int kRing = 4, kU = 8;   // units u = (g, j), g-major
-  auto load_in = [&](int s, int u, int ln) {
+  auto load_in = [&](int s, int u, int ln) {   // channel-quad-major slices (recur.h cqm4 / cqmg)
+    // buffer loads with out-of-range offsets past P (zeros), no branch: k_convlstm_bwd_frames' load_in
     EpIn in;
     const int g = u >> 1, j = u & 1, pp = (cbA + j) * 32 + (ln & 31);
-    if (pp < P) {   // channel-quad-major slices (recur.h cqm4 / cqmg)
-      const size_t fr = (size_t)s * M + (size_t)b * P;
-      const int ch = 32 * hrb + 4 * (ln >> 5) + 8 * g;
-      in.dO = *reinterpret_cast<const f32x4*>(p.dO + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmDO));
-      in.cp = *reinterpret_cast<const f32x4*>(p.Cst + fr * 128 + slc4(pp, ch, P, p.cqm & kCqmC));
-      const u32x4* gp = reinterpret_cast<const u32x4*>(p.Gt + fr * 512 + slcg(pp, ch, P, p.cqm & kCqmG));
-      in.gt[0] = gp[0];
-      in.gt[1] = gp[1];
-    } else {
-      in.dO = in.cp = f32x4{0.f, 0.f, 0.f, 0.f};
-      in.gt[0] = in.gt[1] = u32x4{0u, 0u, 0u, 0u};
-    }
+    const bool v = pp < P;
+    const size_t fr = (size_t)s * M + (size_t)b * P;
+    const int ch = 32 * hrb + 4 * (ln >> 5) + 8 * g;
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc(p.dO + fr * 128, (uint32_t)(P * 128 * 4));
+    const __amdgpu_buffer_rsrc_t rc = make_rsrc(p.Cst + fr * 128, (uint32_t)(P * 128 * 4));
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc(p.Gt + fr * 512, (uint32_t)(P * 512 * 2));
+    in.dO = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          ro, v ? (uint32_t)(slc4(pp, ch, P, p.cqm & kCqmDO) * 4) : kOOB, 0, 0));
+    in.cp = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rc, v ? (uint32_t)(slc4(pp, ch, P, p.cqm & kCqmC) * 4) : kOOB, 0, 0));
+    const uint32_t go = v ? (uint32_t)(slcg(pp, ch, P, p.cqm & kCqmG) * 2) : kOOB;
+    in.gt[0] = __builtin_amdgcn_raw_buffer_load_b128(rg, go, 0, 0);
+    in.gt[1] = __builtin_amdgcn_raw_buffer_load_b128(rg, go, 16, 0);
     return in;
   };
 
