@@ -469,6 +469,81 @@ __device__ __forceinline__ void split_bf16(const float (&x)[8], bf16x8& hi, bf16
   }
 }
 
+// One K tile of the register-staged GEMMs from the LDS tiles Ac / Bc into the wave's accumulators
+// (gemm_kernel, gemm_kernel_deep): BK / 16 / WK k steps of 16 per wave, the fp32 paths split into bf16
+// parts (SPLIT3 / SPLIT6) or on the fp32 MFMA.
+template <class C, class TA, class TB, int MI, int MJ>
+__device__ __forceinline__ void gemm_mma_tile(const typename C::type* Ac, const typename C::type* Bc,
+                                              f32x16 (&acc)[MI][MJ], int wi, int wj, int wk, int r32, int h) {
+  using T = typename C::type;
+  constexpr int BK = C::BK, WK = C::WK, WTI = C::BI / C::WI, WTJ = C::BJ / C::WJ;
+#pragma unroll
+  for (int s2 = 0; s2 < BK / 16 / WK; ++s2) {
+    const int kofs = 16 * (s2 * WK + wk) + 8 * h;
+    if constexpr (is_f32<T>::value) {
+      float af[MI][8], bfr[MJ][8];
+#pragma unroll
+      for (int a = 0; a < MI; ++a) frag_f32<TA>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
+#pragma unroll
+      for (int b = 0; b < MJ; ++b) frag_f32<TB>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
+      if constexpr (split6_of<C>::value) {
+        // as SPLIT3 below, with a three-way split; smallest products first
+        bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
+#pragma unroll
+        for (int a = 0; a < MI; ++a)
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      } else if constexpr (split3_of<C>::value) {
+        // the 8 k of a lane's fp32 fragment are the 8 k of the bf16 operand layout
+        // (lane (r32, h): k 8h .. 8h+7 of the 16-k step)
+        bf16x8 ah[MI], al[MI], bh[MJ], bl[MJ];
+#pragma unroll
+        for (int a = 0; a < MI; ++a) split_bf16(af[a], ah[a], al[a]);
+#pragma unroll
+        for (int b = 0; b < MJ; ++b) split_bf16(bfr[b], bh[b], bl[b]);
+#pragma unroll
+        for (int a = 0; a < MI; ++a)
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+          for (int a = 0; a < MI; ++a)
+#pragma unroll
+            for (int b = 0; b < MJ; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
+      }
+    } else {
+      bf16x8 af[MI], bfr[MJ];
+#pragma unroll
+      for (int a = 0; a < MI; ++a) af[a] = frag_bf16<TA>(Ac, wi * WTI + a * 32 + r32, kofs);
+#pragma unroll
+      for (int b = 0; b < MJ; ++b) bfr[b] = frag_bf16<TB>(Bc, wj * WTJ + b * 32 + r32, kofs);
+#pragma unroll
+      for (int a = 0; a < MI; ++a)
+#pragma unroll
+        for (int b = 0; b < MJ; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  }
+}
+
 template <class C, class LA, class LB, class EP>
 __global__ void __launch_bounds__(C::NT)
 gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
@@ -526,71 +601,7 @@ gemm_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kc
       la.fetch(kb + (kt + 1) * BK, ke, ra);
       lb.fetch(kb + (kt + 1) * BK, ke, rb);
     }
-#pragma unroll
-    for (int s2 = 0; s2 < BK / 16 / WK; ++s2) {
-      const int kofs = 16 * (s2 * WK + wk) + 8 * h;
-      if constexpr (is_f32<T>::value) {
-        float af[MI][8], bfr[MJ][8];
-#pragma unroll
-        for (int a = 0; a < MI; ++a) frag_f32<TA>(Ac, wi * WTI + a * 32 + r32, kofs, af[a]);
-#pragma unroll
-        for (int b = 0; b < MJ; ++b) frag_f32<TB>(Bc, wj * WTJ + b * 32 + r32, kofs, bfr[b]);
-        if constexpr (split6_of<C>::value) {
-          // as SPLIT3 below, with a three-way split; smallest products first
-          bf16x8 ah[MI], am[MI], al[MI], bh[MJ], bm[MJ], bl[MJ];
-#pragma unroll
-          for (int a = 0; a < MI; ++a) split3_bf16(af[a], ah[a], am[a], al[a]);
-#pragma unroll
-          for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
-#pragma unroll
-          for (int a = 0; a < MI; ++a)
-#pragma unroll
-            for (int b = 0; b < MJ; ++b) {
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-            }
-        } else if constexpr (split3_of<C>::value) {
-          // the 8 k of a lane's fp32 fragment are the 8 k of the bf16 operand layout
-          // (lane (r32, h): k 8h .. 8h+7 of the 16-k step)
-          bf16x8 ah[MI], al[MI], bh[MJ], bl[MJ];
-#pragma unroll
-          for (int a = 0; a < MI; ++a) split_bf16(af[a], ah[a], al[a]);
-#pragma unroll
-          for (int b = 0; b < MJ; ++b) split_bf16(bfr[b], bh[b], bl[b]);
-#pragma unroll
-          for (int a = 0; a < MI; ++a)
-#pragma unroll
-            for (int b = 0; b < MJ; ++b) {
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-            for (int a = 0; a < MI; ++a)
-#pragma unroll
-              for (int b = 0; b < MJ; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][kk], bfr[b][kk], acc[a][b], 0, 0, 0);
-        }
-      } else {
-        bf16x8 af[MI], bfr[MJ];
-#pragma unroll
-        for (int a = 0; a < MI; ++a) af[a] = frag_bf16<TA>(Ac, wi * WTI + a * 32 + r32, kofs);
-#pragma unroll
-        for (int b = 0; b < MJ; ++b) bfr[b] = frag_bf16<TB>(Bc, wj * WTJ + b * 32 + r32, kofs);
-#pragma unroll
-        for (int a = 0; a < MI; ++a)
-#pragma unroll
-          for (int b = 0; b < MJ; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a], bfr[b], acc[a][b], 0, 0, 0);
-      }
-    }
+    gemm_mma_tile<C, TA, TB, MI, MJ>(Ac, Bc, acc, wi, wj, wk, r32, h);
     if (more) {
       la.commit(odd ? As0 : As1, ra);
       lb.commit(odd ? Bs0 : Bs1, rb);

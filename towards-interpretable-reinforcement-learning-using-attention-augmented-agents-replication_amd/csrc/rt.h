@@ -22,6 +22,7 @@
 #include "gemm.h"
 #include "loaders_b.h"
 #include "glds.h"
+#include "gemm_deep.h"
 #include "halo.h"
 #include "recur.h"
 #include "recur_bwd.h"
@@ -348,32 +349,57 @@ struct TailPrecision {
 template <class C> struct S3Of { using type = GemmCfgS3<C::BI, C::BJ, C::BK, C::WI, C::WJ, C::WK>; };
 template <class C> struct S6Of { using type = GemmCfgS6<C::BI, C::BJ, C::BK, C::WI, C::WJ, C::WK>; };
 
+// The deep-pipeline (gemm_deep.h) form of a tail loader: LdRows -> LdRowsN, LdRowsT -> LdRowsTN.
+template <template <typename, typename, int, int, int> class L> struct DeepLd;
+template <> struct DeepLd<LdRows> {
+  template <typename G, typename T, int R, int BK, int NT> using type = LdRowsN<G, T, R, BK, NT>;
+  static bool fits(const void*, int ld, int nrows) { return ld % 4 == 0 && (size_t)nrows * ld * 4 < (1u << 31); }
+};
+template <> struct DeepLd<LdRowsT> {
+  template <typename G, typename T, int R, int BK, int NT> using type = LdRowsTN<G, T, R, BK, NT>;
+  static bool fits(const void*, int ld, int nrows) { return ld % 4 == 0 && nrows % 4 == 0; }
+};
+constexpr int kTailStages = 8;
+#ifdef AAA_ABLATION
+constexpr bool kAblationBuild = true;
+#else
+constexpr bool kAblationBuild = false;
+#endif   // K tiles of global loads in flight per workgroup (gemm_kernel_deep)
+
 template <template <typename, typename, int, int, int> class LA_,
           template <typename, typename, int, int, int> class LB_, class PA, class PB, class EP>
 static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, int Nj, int K, int nsplit,
                             hipStream_t st) {
   const int mode = ab_int("AAA_HEAD_TILE", 0);
   const long tiles = (long)cdiv(Mi, 64) * cdiv(Nj, 64) * std::max(nsplit, 1);
-  auto splitk = [&](auto cfg0) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
-    if (g_tail6) {
-      using C = typename S6Of<decltype(cfg0)>::type;
-      using A = LA_<float, float, C::BI, C::BK, C::NT>;
-      using B = LB_<float, float, C::BJ, C::BK, C::NT>;
-      return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows},
-                                  typename B::Params{pb.src, pb.ld, pb.nrows}, ep, Mi, Nj, K, nsplit, st);
+  // ablation builds, AAA_TAIL_DEEP=1: kTailStages register stages of K tiles in flight (gemm_kernel_deep)
+#ifdef AAA_ABLATION   // measured no faster (profiles/r06/ab/tail_deep/): ablation builds only
+  const bool deep = ab_int("AAA_TAIL_DEEP", 0) && DeepLd<LA_>::fits(pa.src, pa.ld, pa.nrows) &&
+                    DeepLd<LB_>::fits(pb.src, pb.ld, pb.nrows) && (size_t)K * pa.ld * 4 < (1u << 31) &&
+                    (size_t)K * pb.ld * 4 < (1u << 31);
+#else
+  constexpr bool deep = false;
+#endif
+  auto run = [&](auto cfg) {
+    using C = decltype(cfg);
+    if constexpr (!kAblationBuild) {
+      (void)deep;
+    } else if (deep) {
+      using A = typename DeepLd<LA_>::template type<float, float, C::BI, C::BK, C::NT>;
+      using B = typename DeepLd<LB_>::template type<float, float, C::BJ, C::BK, C::NT>;
+      return launch_gemm_deep<C, A, B, EP, kTailStages>(typename A::Params{pa.src, pa.ld, pa.nrows},
+                                                        typename B::Params{pb.src, pb.ld, pb.nrows}, ep, Mi, Nj, K,
+                                                        nsplit, st);
     }
-    if (g_tail3) {
-      using C = typename S3Of<decltype(cfg0)>::type;
-      using A = LA_<float, float, C::BI, C::BK, C::NT>;
-      using B = LB_<float, float, C::BJ, C::BK, C::NT>;
-      return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows},
-                                  typename B::Params{pb.src, pb.ld, pb.nrows}, ep, Mi, Nj, K, nsplit, st);
-    }
-    using C = decltype(cfg0);
     using A = LA_<float, float, C::BI, C::BK, C::NT>;
     using B = LB_<float, float, C::BJ, C::BK, C::NT>;
     return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
                                 ep, Mi, Nj, K, nsplit, st);
+  };
+  auto splitk = [&](auto cfg0) {   // 32x64 tile, in-WG split-K over 2-4 waves (long K, few tiles)
+    if (g_tail6) return run(typename S6Of<decltype(cfg0)>::type{});
+    if (g_tail3) return run(typename S3Of<decltype(cfg0)>::type{});
+    return run(cfg0);
   };
   if (mode == 0 && tiles < 192) return splitk(CFK4{});
   if (mode == 1 || (mode == 0 && tiles >= 192)) return splitk(CF{});
