@@ -114,6 +114,7 @@ int pair_check();           // AAA_E_STRANDED if any are pending
 // the caller's stream by events; the caller's stream waits for it before the
 // call returns (fork/join inside each call).  Created lazily, once per device.
 hipStream_t aux_stream();   // nullptr unless AAA_OVERLAP=1 (measured slower on C2, round 1)
+hipStream_t side_stream();  // the backward HEAD phase's weight gradients (rt_core.hip); nullptr: AAA_SIDE=0
 // Record a pooled event on ``s`` (everything enqueued on s so far).
 hipError_t record_event(hipStream_t s, hipEvent_t* out);
 // ``to`` waits for everything enqueued on ``from`` so far.

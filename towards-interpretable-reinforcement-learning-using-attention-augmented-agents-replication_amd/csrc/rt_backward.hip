@@ -606,17 +606,33 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     } else {
     std::unique_ptr<TimerScope> tail(new TimerScope(AAA_TIMER_TAIL_BWD, st, 2.0 * F * (tail_fwd_flop(L) + 2.0 * 256 * L.ldy),
                                                     "heads + LSTMCell + answer MLP backward (fp32 GEMMs)"));
+    // The dgrad chain (heads -> LSTMCell -> answer MLP -> readout) on st; each layer's weight gradient
+    // on the side stream once the chain has produced its input gradient (few-tile GEMMs: the two
+    // streams fill CUs the other leaves idle); joined before the gradients are unpacked.
+    // Below ~2048 frames the GEMMs are too short for the overlap to pay for the second queue's dispatch
+    // cost on the rest of the step (C2, 640 frames: tail bwd -20 us but the step +10-15 us;
+    // profiles/r06/ab/side/): one stream there.
+    hipStream_t ss = F >= 2048 ? side_stream() : nullptr;
+    hipStream_t ws_ = ss ? ss : st;   // the weight gradients' stream
+    if (ss) HIPCHK(stream_order(st, ss));   // the zeroed accumulators, the cotangent concat
+    {  // heads wgrad (dY from the prologue)
+      LTf::Params pa{Wf(L.dY), L.ldy, L.ldy};
+      LTfj::Params pb{Wf(L.LH), 256, 256};
+      EpiStore<true> ep{Wf(L.gWhd), 256, L.ldy, 256};
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), ws_)));
+    }
     {  // heads dgrad fused with the zero-state LSTMCell backward
       LTf::Params pa{(const float*)(pk + L.k_Whd), 256, 256};
       LRfj::Params pb{Wf(L.dY), L.ldy, F};
       EpiLstmCellBwd ep{Wf(L.LG), Wf(L.LC), Wf(L.dLG), F};
       HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, F, L.ldy, 1, st)));
     }
-    {  // heads wgrad
-      LTf::Params pa{Wf(L.dY), L.ldy, L.ldy};
-      LTfj::Params pb{Wf(L.LH), 256, 256};
-      EpiStore<true> ep{Wf(L.gWhd), 256, L.ldy, 256};
-      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, L.ldy, 256, F, wgrad_splits(cdiv(L.ldy, 64) * 4, F, CF::BK), st)));
+    if (ss) HIPCHK(stream_order(st, ss));   // dLG
+    {  // LSTMCell weight_ih grad (weight_hh grad is exactly zero: h0 = 0, Q1)
+      LTf::Params pa{Wf(L.dLG), 1024, 1024};
+      LTfj::Params pb{Wf(L.AO), 256, 256};
+      EpiStore<true> ep{Wf(L.gWihp), 256, 1024, 256};
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), ws_)));
     }
     {  // LSTMCell input dgrad
       LTf::Params pa{(const float*)(pk + L.k_Wihp), 256, 256};
@@ -624,11 +640,12 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       EpiStoreT<float> ep{Wf(L.dAO), 256, 256, F, nullptr, 0};
       HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 256, F, 1024, 1, st)));
     }
-    {  // LSTMCell weight_ih grad (weight_hh grad is exactly zero: h0 = 0, Q1)
-      LTf::Params pa{Wf(L.dLG), 1024, 1024};
-      LTfj::Params pb{Wf(L.AO), 256, 256};
-      EpiStore<true> ep{Wf(L.gWihp), 256, 1024, 256};
-      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 1024, 256, F, wgrad_splits(16 * 4, F, CF::BK), st)));
+    if (ss) HIPCHK(stream_order(st, ss));   // dAO
+    {  // answer_processor.2 wgrad / bias
+      LTf::Params pa{Wf(L.dAO), 256, 256};
+      LTfj::Params pb{Wf(L.hid1), 512, 512};
+      EpiStore<true> ep{grads + L.poff[A2W], 512, 256, 512};
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), ws_)));
     }
     {  // answer_processor.2 dgrad fused with ReLU backward
       LTf::Params pa{prm + L.poff[A2W], 512, 512};
@@ -636,24 +653,19 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       EpiReluBwdT ep{Wf(L.dH1), Wf(L.hid1), 512, 512, 512, F};
       HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, 512, F, 256, 1, st)));
     }
-    {  // answer_processor.2 wgrad / bias
-      LTf::Params pa{Wf(L.dAO), 256, 256};
-      LTfj::Params pb{Wf(L.hid1), 512, 512};
-      EpiStore<true> ep{grads + L.poff[A2W], 512, 256, 512};
-      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 256, 512, F, wgrad_splits(4 * 8, F, CF::BK), st)));
+    if (ss) HIPCHK(stream_order(st, ss));   // dH1
+    {  // answer_processor.0 wgrad / bias
+      LTf::Params pa{Wf(L.dH1), 512, 512};
+      LTfj::Params pb{Wf(L.ans), L.ans_ld, L.ans_ld};
+      EpiStore<true> ep{Wf(L.gW1p), L.ans_ld, 512, L.ans_ld};
+      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 512, L.ans_ld, F,
+                                        wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), ws_)));
     }
     {  // answer_processor.0 dgrad (readout columns only)
       LTf::Params pa{(const float*)(pk + L.k_W1p), L.ans_ld, L.da};
       LRfj::Params pb{Wf(L.dH1), 512, F};
       EpiStoreT<float> ep{Wf(L.dAns), L.da, L.da, F, nullptr, 0};
       HIPCHK((head_gemm<LdRowsT, LdRows>(pa, pb, ep, L.da, F, 512, 1, st)));
-    }
-    {  // answer_processor.0 wgrad / bias
-      LTf::Params pa{Wf(L.dH1), 512, 512};
-      LTfj::Params pb{Wf(L.ans), L.ans_ld, L.ans_ld};
-      EpiStore<true> ep{Wf(L.gW1p), L.ans_ld, 512, L.ans_ld};
-      HIPCHK((head_gemm<LdRowsT, LdRowsT>(pa, pb, ep, 512, L.ans_ld, F,
-                                        wgrad_splits(8 * cdiv(L.ans_ld, 64), F, CF::BK), st)));
     }
     tail.reset();
     // attention readout / softmax / logits backward, then the query MLP
@@ -676,6 +688,7 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
                      prm + L.poff[Q4W], (const float*)(pk + L.k_q1), (const float*)(pk + L.k_q2), grads + L.poff[Q4W],
                      grads + L.poff[Q4B],
                      grads + L.poff[Q2W], grads + L.poff[Q2B], grads + L.poff[Q0B], st));
+    if (ss) HIPCHK(stream_order(ss, st));   // join: the weight gradients
     F32Unpack up;
     up.gW1p = Wf(L.gW1p); up.gWihp = Wf(L.gWihp); up.gblc = Wf(L.gblc); up.gWhd = Wf(L.gWhd); up.gbhd = Wf(L.gbhd);
     up.a0w = grads + L.poff[A0W]; up.wih = grads + L.poff[WIH]; up.bih = grads + L.poff[BIH];
@@ -696,6 +709,45 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
     const int rows = (hi - lo) * M;                       // pixels of these frames
     const int F1 = (hi - lo) * L.B;                       // frames
     const T* dz = Wt(L.dZ) + (size_t)lo * M * 512;
+    // conv2 / conv1 backward of these frames (needs dY2 only)
+    auto vision = [&](hipStream_t vs) -> int {
+      const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
+      T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
+      if (vbwd_on<T>(L, F1)) {   // one frame-resident launch (+ its partials' sum)
+        TimerScope tim(AAA_TIMER_VISION_BWD, vs, (double)F1 * vision_bwd_flop(L),
+                       "frame-resident conv2 wgrad + dgrad + conv1 wgrad [kernel: k_vision_bwd_frames]");
+        return vbwd_run<T>(L, pk, io->frames, lo * L.B, F1, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, dy1,
+                           Wf(L.gWp2), Wf(L.gWp1), grads + L.poff[C0B], vs);
+      }
+      TimerScope tim(AAA_TIMER_VISION_BWD, vs, (double)F1 * vision_bwd_flop(L), "conv2 wgrad + dgrad, conv1 wgrad");
+      const int rows1 = F1 * L.P1;
+      constexpr bool f32 = std::is_same<T, float>::value;   // fp32 with AAA_CONV2_DGRAD_RING=0: conv1 bias by a column sum
+      {  // conv2 wgrad
+        const int rc = conv2_wgrad<T>(L, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, F1, Wf(L.gWp2), vs);
+        if (rc) return rc;
+      }
+      {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
+        int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], vs);
+        if (!rc && L.xpc < L.F)   // Xp chunk buffer: rebuilt from the observation
+          rc = conv1_wgrad_frames<T>(L, dy1, (const char*)io->frames + (size_t)lo * L.B * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
+                                     F1, Wt(L.Xp), Wf(L.gWp1), vs);
+        else if (!rc)
+          rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), vs);
+        if (rc) return rc;
+        if (f32 && !ab_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], vs));
+      }
+      return AAA_OK;
+    };
+    // (the layered vision backward on the side stream beside the ConvLSTM weight gradient, ablation
+    // builds with AAA_VIS_SIDE=1: C2 232.0k -> 228.6-229.2k, C5 within noise -- the two contend for
+    // the CUs; profiles/r06/ab/side/)
+    hipStream_t vside = vision_here && dx_fused && !vbwd_on<T>(L, F1) && ab_int("AAA_VIS_SIDE", 0) ? side_stream()
+                                                                                                 : nullptr;
+    if (vside) {
+      HIPCHK(stream_order(s, vside));
+      const int rc = vision(vside);
+      if (rc) return rc;
+    }
     {
       const int rc = lstm_wgrad<T>(dz, Wt(L.XH) + (size_t)lo * M * 192, rows, L.h, L.w, Wf(L.gWpl), s, s != st);
       if (rc) return rc;
@@ -796,32 +848,8 @@ int backward_impl(const Layout& L, const aaa_io* io, int phases, hipStream_t st)
       }
     }
     if (!vision_here) return AAA_OK;
-    const T* dy2 = Wt(L.dY2) + (size_t)lo * M * 64;
-    T* dy1 = Wt(L.dY1) + (size_t)lo * L.B * L.P1 * 32;
-    if (vbwd_on<T>(L, F1)) {   // one frame-resident launch (+ its partials' sum)
-      TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L),
-                     "frame-resident conv2 wgrad + dgrad + conv1 wgrad [kernel: k_vision_bwd_frames]");
-      return vbwd_run<T>(L, pk, io->frames, lo * L.B, F1, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, dy1,
-                         Wf(L.gWp2), Wf(L.gWp1), grads + L.poff[C0B], s);
-    }
-    TimerScope tim(AAA_TIMER_VISION_BWD, s, (double)F1 * vision_bwd_flop(L), "conv2 wgrad + dgrad, conv1 wgrad");
-    const int rows1 = F1 * L.P1;
-    constexpr bool f32 = std::is_same<T, float>::value;   // fp32 with AAA_CONV2_DGRAD_RING=0: conv1 bias by a column sum
-    {  // conv2 wgrad
-      const int rc = conv2_wgrad<T>(L, dy2, Wt(L.Y1) + (size_t)lo * L.B * L.P1 * 32, F1, Wf(L.gWp2), s);
-      if (rc) return rc;
-    }
-    {  // conv2 dgrad (4 parity classes) -> dY1, then conv1 wgrad / bias
-      int rc = conv2_dgrad<T>(L, pk, dy2, dy1, F1, grads + L.poff[C0B], s);
-      if (!rc && L.xpc < L.F)   // Xp chunk buffer: rebuilt from the observation
-        rc = conv1_wgrad_frames<T>(L, dy1, (const char*)io->frames + (size_t)lo * L.B * L.H * L.W * 3 * (L.fu8 ? 1 : 4),
-                                   F1, Wt(L.Xp), Wf(L.gWp1), s);
-      else if (!rc)
-        rc = conv1_wgrad<T>(L, dy1, Wt(L.Xp) + (size_t)lo * L.B * (L.H + 2) * (L.W + 2) * 4, F1, Wf(L.gWp1), s);
-      if (rc) return rc;
-      if (f32 && !ab_int("AAA_CONV2_DGRAD_RING", 1)) HIPCHK(colsum(dy1, 32, rows1, 32, grads + L.poff[C0B], s));
-    }
-    return AAA_OK;
+    if (vside) return stream_order(vside, s) == hipSuccess ? AAA_OK : fail(AAA_E_LAUNCH, "side-stream join");
+    return vision(s);
   };
 
   if (phases & AAA_BWD_CORE) {

@@ -313,6 +313,30 @@ hipStream_t aux_stream() {
   return a.s;
 }
 
+// Side stream: the backward HEAD phase's weight gradients run on it beside the phase's dgrad chain
+// (each waits only for the chain product it reads; the chain waits for all of them before the grads
+// are unpacked), low priority so the chain's small GEMMs take CUs first.  AAA_SIDE=0: one stream.
+static hipStream_t g_side[64];
+hipStream_t side_stream() {
+  if (!env_int("AAA_SIDE", 1)) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_aux_mu);
+  if (!g_side[dev]) {
+    AuxStream& a = g_aux[dev];
+    if (!a.ev[0])   // the event pool stream_order draws from (created with the aux stream otherwise)
+      for (auto& e : a.ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&g_side[dev], hipStreamNonBlocking, lo) != hipSuccess) {
+      g_side[dev] = nullptr;
+      return nullptr;
+    }
+  }
+  return g_side[dev];
+}
+
 // Record a pooled event on ``s`` (everything enqueued on s so far).
 hipError_t record_event(hipStream_t s, hipEvent_t* out) {
   int dev = 0;
