@@ -709,10 +709,12 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
     __bf16* nxt = smem + (e ^ 1) * STG;
     const bool more = kt + 1 < nk;
     if constexpr (FD == 2) {   // tile kt+2 into register stage e (tile kt's, committed a step ago)
-      if (kt + 2 < nk) {
-        la.fetch(kb + (kt + 2) * BK, ke, ra[e]);
-        lb.fetch(kb + (kt + 2) * BK, ke, rb[e]);
-      }
+      // unconditional: a tile past the slice is fetched and never committed (the TB loaders read it in
+      // range or as zeros); guarded by kt + 2 < nk, the compiler waited for tile kt+1 at the top of the
+      // step instead of keeping it in flight to the commit (C2 wgrad 641-646 -> 632-647 us,
+      // profiles/r06/ab/s6l_prio/)
+      la.fetch(kb + (kt + 2) * BK, ke, ra[e]);
+      lb.fetch(kb + (kt + 2) * BK, ke, rb[e]);
     } else if (more) {
       la.fetch(kb + (kt + 1) * BK, ke, ra[0]);
       lb.fetch(kb + (kt + 1) * BK, ke, rb[0]);

@@ -947,7 +947,7 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
 // each barrier is a builtin the compiler sees, so it does not add waits for
 // the current set behind the reads of the next one.  ABL (diagnostic builds):
 // bit 0 = no in-loop DMA, bit 2 = no epilogue.
-template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0>
+template <class C, class LA, class LB, class EP, int NBUF, int ABL = 0, int PRIO = 1>
 __global__ void __launch_bounds__(C::NT)
 gemm_pipe_ra_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K, int kchunk, TileMap tm) {
   using T = typename C::type;
@@ -1041,6 +1041,9 @@ gemm_pipe_ra_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K
     T* const st = smem + ((kt + NBUF - 1) % NBUF) * STG;
     const int kn = kb + (kt + NBUF - 1) * BK;
     __builtin_amdgcn_sched_barrier(0);
+    // raised issue priority over the MFMA cluster (two waves per SIMD: the other wave's reads and DMA
+    // issue wait; C3 wgrad 1012-1014 -> 976-988 us, profiles/r06/ab/s6l_prio/)
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < S2; ++s2) {
 #pragma unroll
@@ -1057,6 +1060,7 @@ gemm_pipe_ra_kernel(typename LA::Params pa, typename LB::Params pb, EP ep, int K
     }
     __builtin_amdgcn_sched_barrier(0);
     if (pf) lb.issue(st + AEL, kn);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 
