@@ -284,6 +284,10 @@ k_attn_fwd(const TO* __restrict__ Hs, int old, const float* __restrict__ S, cons
   }
 }
 
+}  // namespace aaa
+#include "attn_mfma.h"
+namespace aaa {
+
 #ifdef AAA_STAMPS
 // Diagnostic builds only (tools/ubench/attn_stamps): per-workgroup phase stamps (s_memrealtime, 100 MHz).
 __device__ uint64_t aaa_attn_stamps[16384 * 8];
@@ -1161,6 +1165,20 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
 #else
   constexpr int pre_env = -1, sl_env = -1;
 #endif
+  // the readout product on the MFMA for bf16 O (attn_mfma.h); AAA_ATTN_MFMA=0: the VALU kernel below
+  static const int mfma_env = getenv("AAA_ATTN_MFMA") ? atoi(getenv("AAA_ATTN_MFMA")) : 1;
+  if (mfma_env && O.bf16 && (nq == 4 || nq == 8)) {
+    if (O.ld < 128 || O.ld % 8) return hipErrorInvalidValue;   // 16-B loads
+    const size_t sh = attn_mfma_lds(P, nq);
+    if (sh > 160 * 1024) return hipErrorInvalidValue;
+    auto kern = nq == 4 ? k_attn_fwd_mfma<4> : k_attn_fwd_mfma<8>;
+    if (sh > 64 * 1024)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sh);
+    hipLaunchKernelGGL(kern, dim3(F), dim3(256), sh, st, (const __bf16*)O.p, O.ld, S, Q, qs, SQ, pr, pa, P, Am, ans,
+                       ans_ld);
+    return hipGetLastError();
+  }
   const bool pre = pre_env >= 0 ? pre_env != 0 : P > 2 * kAttnSlices * 11;
   const int sl = O.bf16 ? kAttnSlicesBf : sl_env > 0 ? sl_env : kAttnSlices;
   const size_t sh = (size_t)(P * nq + nq * 72 + sl * nq * 184) * sizeof(float);
