@@ -424,7 +424,7 @@ static int forward_tail_stateful(const Layout& L, const aaa_io* io, hipStream_t 
     }
     // attention readout with this step's per-frame queries (basis logits in-kernel)
     {
-      TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)B * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), "k_attn_fwd, per-frame query (stateful core)");
+      TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)B * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), L.esz == 2 ? "k_attn_fwd_mfma, per-frame query (stateful core)" : "k_attn_fwd, per-frame query (stateful core)");
       HIPCHK(attn_fwd(readout_h(L, ws).frame(f0, P), io->basis, Qt, nullptr, io->prev_reward ? io->prev_reward + f0 : nullptr,
                       io->prev_action ? io->prev_action + f0 : nullptr, B, P, L.nq, Wf(L.Am) + f0 * P * L.nq,
                       Wf(L.ans) + f0 * L.ans_ld, L.ans_ld, st, qd));
@@ -475,7 +475,7 @@ static int forward_tail(const Layout& L, const aaa_io* io, hipStream_t st) {
     HIPCHK(query_sq(io->basis, Qc, P, L.nq, Wf(L.SQ), st));
   }
   {
-    TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), "k_attn_fwd, 1 WG per frame");
+    TimerScope tim(AAA_TIMER_ATTN_FWD, st, (double)F * attn_fwd_bytes(P, L.nq, L.ans_ld, L.esz), L.esz == 2 ? "k_attn_fwd_mfma (readout on the MFMA, map and basis in bf16 parts), 1 WG per frame" : "k_attn_fwd (VALU), 1 WG per frame");
     HIPCHK(attn_fwd(readout_h(L, ws), io->basis, Qc, Wf(L.SQ), io->prev_reward, io->prev_action, F, P, L.nq, Wf(L.Am),
                     Wf(L.ans), L.ans_ld, st));
   }
