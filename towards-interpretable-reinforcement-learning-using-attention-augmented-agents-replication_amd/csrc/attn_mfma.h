@@ -66,7 +66,8 @@ inline size_t attn_mfma_lds(int P, int nq) {
   return (size_t)attn_mfma_img(P, nq) + (size_t)3 * nq * (2 * attn_mfma_pp(P) + 16) + (size_t)nq * 72 * 4;
 }
 
-template <int NQ>
+// NTL_: the frame's O rows loaded non-temporal (nt: streamed past L2, keeping the basis resident there)
+template <int NQ, bool NTL_>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NQ == 8 ? 4 : 3)))
 k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q,
                 int qs, const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa, int P,
@@ -87,6 +88,7 @@ k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict_
   const __amdgpu_buffer_rsrc_t ro = make_rsrc(O, (uint32_t)((size_t)P * old * 2));
   const __amdgpu_buffer_rsrc_t rsb = make_rsrc(S, (uint32_t)(P * 256));
   const __amdgpu_buffer_rsrc_t rsq = make_rsrc(SQ ? SQ : S, SQ ? (uint32_t)(P * NQ * 4) : 0u);
+  auto oload = [&](uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, NTL_ ? 2 : 0); };
 
   // ---- loads in the order they are used: queries, keys and basis logits of positions tid, tid + 256,
   // then the first D chunks (the waits for the first ones are then counted, not drained)
@@ -99,7 +101,7 @@ k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict_
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int p = tid + 256 * i;
-    kr[i] = bload(ro, p < P ? (uint32_t)(p * old * 2) : kOOB);
+    kr[i] = oload(p < P ? (uint32_t)(p * old * 2) : kOOB);
     const uint32_t so = p < P ? (uint32_t)(p * NQ * 4) : kOOB;
 #pragma unroll
     for (int j = 0; j < NQ / 4; ++j) sq[i][j] = __builtin_bit_cast(f32x4, bload(rsq, so + 16 * j));
@@ -112,7 +114,7 @@ k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict_
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int i = tid + 256 * j, p = pb + (i >> 4);
-      o[j] = bload(ro, p < P ? (uint32_t)(p * old * 2 + 16 * (i & 15)) : kOOB);
+      o[j] = oload(p < P ? (uint32_t)(p * old * 2 + 16 * (i & 15)) : kOOB);
       s[j] = bload(rsb, p < P ? (uint32_t)(p * 256 + 16 * (i & 15)) : kOOB);
     }
   };

@@ -1171,7 +1171,9 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
     if (O.ld < 128 || O.ld % 8) return hipErrorInvalidValue;   // 16-B loads
     const size_t sh = attn_mfma_lds(P, nq);
     if (sh > 160 * 1024) return hipErrorInvalidValue;
-    auto kern = nq == 4 ? k_attn_fwd_mfma<4> : k_attn_fwd_mfma<8>;
+    static const int nt_env = getenv("AAA_ATTN_NT") ? atoi(getenv("AAA_ATTN_NT")) : 0;   // (A/B)
+    auto kern = nt_env ? (nq == 4 ? k_attn_fwd_mfma<4, true> : k_attn_fwd_mfma<8, true>)
+                       : (nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>);
     if (sh > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sh);
