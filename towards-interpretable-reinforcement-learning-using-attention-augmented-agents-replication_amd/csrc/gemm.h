@@ -434,6 +434,26 @@ struct GemmCfgS6L : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, 1> {
   static constexpr bool SPLIT3 = true, SPLIT6 = true, SPLIT6L = true;
   static constexpr int FD = FD_;   // K tiles of global loads in flight (register stages)
 };
+// B operand exact in bf16 (configs with BEXACT: conv1's operand when the frames are uint8 -- integers
+// 0..255 are bf16 values): its mid and lo parts are zero, so of the six split products only lo.hi,
+// mid.hi and hi.hi are issued (in the SPLIT6 order; the three skipped ones add exact zeros -- the same
+// sums) and B is converted, not split.
+template <class C, class = void> struct bexact_of : std::false_type {};
+template <class C> struct bexact_of<C, std::enable_if_t<C::BEXACT>> : std::true_type {};
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int WK_ = 1>
+struct GemmCfgS6BX : GemmCfgS6<BI_, BJ_, BK_, WI_, WJ_, WK_> {
+  static constexpr bool BEXACT = true;
+};
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int FD_ = 1>
+struct GemmCfgS6LBX : GemmCfgS6L<BI_, BJ_, BK_, WI_, WJ_, FD_> {
+  static constexpr bool BEXACT = true;
+};
+__device__ __forceinline__ bf16x8 to_bf16x8(const float (&x)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (__bf16)x[e];
+  return r;
+}
 __device__ __forceinline__ void split3_bf16(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -661,6 +681,7 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
   using TA = TileK<__bf16, BI, BK, LA::KC>;
   using TB = TileK<__bf16, BJ, BK, LB::KC>;
   constexpr int PA = TA::ELEMS, PB = TB::ELEMS, STG = 3 * (PA + PB);
+  constexpr bool BX = bexact_of<C>::value;   // B's hi part only (commit1), three products
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STG];
 
   int ti, tj, tz;
@@ -699,7 +720,8 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
     }
   }
   la.commit3(smem, PA, ra[0]);
-  lb.commit3(smem + 3 * PA, PB, rb[0]);
+  if constexpr (BX) lb.commit1(smem + 3 * PA, rb[0]);
+  else lb.commit3(smem + 3 * PA, PB, rb[0]);
   __syncthreads();
 
   // one K step; E = kt & 1 (compile-time, so the register stages stay in registers)
@@ -730,23 +752,26 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
 #pragma unroll
       for (int b = 0; b < MJ; ++b)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bfr[b][p] = frag_bf16<TB>(cur + 3 * PA + p * PB, wj * WTJ + b * 32 + r32, kofs);
+        for (int p = 0; p < (BX ? 1 : 3); ++p) bfr[b][p] = frag_bf16<TB>(cur + 3 * PA + p * PB, wj * WTJ + b * 32 + r32, kofs);
 #pragma unroll
       for (int a = 0; a < MI; ++a)
 #pragma unroll
         for (int b = 0; b < MJ; ++b) {   // smallest products first, as gemm_kernel's SPLIT6
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][2], bfr[b][0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][2], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][1], acc[a][b], 0, 0, 0);
+          if constexpr (!BX) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][2], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][1], acc[a][b], 0, 0, 0);
+          }
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][0], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][1], acc[a][b], 0, 0, 0);
+          if constexpr (!BX) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][1], acc[a][b], 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][0], acc[a][b], 0, 0, 0);
         }
     }
     if (more) {   // tile kt+1: register stage e ^ 1 (FD 2) or 0
       constexpr int rs1 = FD == 2 ? (e ^ 1) : 0;
       la.commit3(nxt, PA, ra[rs1]);
-      lb.commit3(nxt + 3 * PA, PB, rb[rs1]);
+      if constexpr (BX) lb.commit1(nxt + 3 * PA, rb[rs1]);
+      else lb.commit3(nxt + 3 * PA, PB, rb[rs1]);
     }
     __syncthreads();
   };

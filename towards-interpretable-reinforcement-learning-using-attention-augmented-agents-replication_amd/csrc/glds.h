@@ -823,6 +823,9 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
               bm[b] = frag_sw<BK>(Bb + BJ * BK, r, kofs);
               bl[b] = frag_sw<BK>(Bb + 2 * BJ * BK, r, kofs);
             }
+          } else if constexpr (bexact_of<C>::value) {   // B exact in bf16: converted, its parts zero
+#pragma unroll
+            for (int b = 0; b < MJ; ++b) bh[b] = to_bf16x8(bfr[b]);
           } else {
 #pragma unroll
             for (int b = 0; b < MJ; ++b) split3_bf16(bfr[b], bh[b], bm[b], bl[b]);
@@ -832,10 +835,13 @@ gemm_pipe_kernel(typename LA::Params pa, typename LB::Params pb, EP ep_, int K, 
 #pragma unroll
             for (int b = 0; b < MJ; ++b) {
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+              if constexpr (!bexact_of<C>::value) {
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bm[b], acc[a][b], 0, 0, 0);
+              }
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[a], bh[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
+              if constexpr (!bexact_of<C>::value)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bm[b], acc[a][b], 0, 0, 0);
               acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh[b], acc[a][b], 0, 0, 0);
             }
         } else {

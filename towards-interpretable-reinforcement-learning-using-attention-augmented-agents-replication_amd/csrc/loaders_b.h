@@ -281,6 +281,12 @@ struct LdIm2colTB {
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_split3(lds + off16(threadIdx.x + c * NT), plane, buf[c]);
   }
+  // the hi part only, for a source exact in bf16 (GemmCfgS6LBX)
+  __device__ __forceinline__ void commit1(__bf16* lds, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_chunk<G, __bf16>(lds + off16(threadIdx.x + c * NT), buf[c]);
+  }
 };
 
 }  // namespace aaa

@@ -222,7 +222,9 @@ static int conv1_wgrad(const Layout& L, const T* dy1, const T* xp, int frames, f
       HIPCHK((launch_gemm<CW, LA6, LB6>(pa6, pb6, ep6, 32, 256, rows1, std::max(1, std::min(ns, rows1 / 128)), s)));
       return AAA_OK;
     };
-    if (c1s == 1) return s6l(GemmCfgS6L<32, 256, 16, 1, 4, 2>{}, 512);
+    if (c1s == 1)   // uint8 frames: the RGBx operand exact in bf16 (GemmCfgS6LBX: three of the six products)
+      return L.fu8 && ab_int("AAA_CONV1_BEXACT", 1) ? s6l(GemmCfgS6LBX<32, 256, 16, 1, 4, 2>{}, 512)
+                                                     : s6l(GemmCfgS6L<32, 256, 16, 1, 4, 2>{}, 512);
 #ifdef AAA_ABLATION
     if (c1s == 2) return s6l(GemmCfgS6L<32, 256, 16, 1, 4, 2>{}, 256);
     if (c1s == 3) return s6l(GemmCfgS6L<32, 128, 16, 1, 2, 2>{}, 512);

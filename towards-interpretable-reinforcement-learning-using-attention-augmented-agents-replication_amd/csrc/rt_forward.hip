@@ -96,7 +96,9 @@ static int vision_fwd_chunk(const Layout& L, int F, const char* pk, const float*
       const int c1t = ab_int("AAA_CONV1_TILE", 0);
       int rc;
       if constexpr (std::is_same<T, float>::value) {   // fp32 accuracy on the bf16 MFMA (gemm.h SPLIT6)
-        if (f32_split6()) rc = conv1(GemmCfgS6<32, 128, BKc, 1, 4>{});
+        // uint8 frames: the RGBx operand is exact in bf16 (three of the six split products, GemmCfgS6BX)
+        if (f32_split6()) rc = L.fu8 && ab_int("AAA_CONV1_BEXACT", 1) ? conv1(GemmCfgS6BX<32, 128, BKc, 1, 4>{})
+                                                                      : conv1(GemmCfgS6<32, 128, BKc, 1, 4>{});
         else rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
       } else {
         rc = c1t == 1 ? conv1(GemmCfg<T, 32, 256, BKc, 1, 4>{}) : conv1(GemmCfg<T, 32, 128, BKc, 1, 4>{});
