@@ -288,4 +288,216 @@ k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict_
   }
 }
 
+// Attention readout backward with the dA pass on the MFMA, bf16 O (attention.py:336-348, 235-254
+// backward; the VALU kernel k_attn_bwd computes the same -- phases 2-4 below are its code).
+//   dA[p][q] = sum_c V[p][c] da[q][c],  V = [O[:, 8:128] | S]
+// as 16x16x32 bf16 MFMAs over 16-position blocks: M = positions, K = the channels of V' = [O[:, 0:128] |
+// S hi | S mid | S lo] (the A operand straight from the O and S rows: 8 consecutive channels of one
+// position per lane, S split on the fly), N = the rows n = s*NQ + q of Dp[n][k'], the answer gradient
+// da split into bf16 parts (zero for O's key channels 0..7; its S columns repeated under each S part,
+// so all nine S-part x da-part products are summed).  Exact to fp32 up to summation order.  Dp lives
+// in the dQ reduction's LDS (red, used only after the pass).  The key channels for dQ are taken from
+// the O fragments of channels 0..7.
+template <int NQ>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))   // two frames per CU
+k_attn_bwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q,
+                int qs, const float* __restrict__ Am, const float* __restrict__ dAns, int da_ld, int addq, int P,
+                float* __restrict__ dO, float* __restrict__ dQp, int cqm) {
+  constexpr int NT = 512, NW = NT / 64;
+  constexpr int G = 7;                                  // position groups of the dQ reduction (7*72 <= NT)
+  constexpr int NR = 3 * NQ, NTN = NQ == 8 ? 2 : 1;    // da-part rows, their 16-row tiles
+  constexpr int DS = 320 * 2 + 16;                      // Dp row bytes: 320 bf16 (K of V') + pad
+  static_assert(NR * DS <= G * NQ * 72 * 4, "Dp aliases the dQ reduction buffer");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* A = sm;                 // P*NQ
+  float* dA = A + P * NQ;        // P*NQ  (becomes dlogits)
+  float* da = dA + P * NQ;       // NQ*184
+  float* Qs = da + NQ * 184;     // NQ*72
+  float* ss = Qs + NQ * 72;      // NQ (padded to 8)
+  float* red = ss + 8;           // G*NQ*72; Dp during the dA pass
+  float* Kc = red + G * NQ * 72; // P*8  key channels O[:8] as fp32
+  unsigned char* const Dp = reinterpret_cast<unsigned char*>(red);
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const __bf16* O = Hs + (size_t)f * P * old;
+  const __amdgpu_buffer_rsrc_t ro = make_rsrc(O, (uint32_t)((size_t)P * old * 2));
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(S, (uint32_t)(P * 256));
+  // a position block's A-operand loads of this lane: O channels 32 kk + 8g .. +7 (kk < 4) and S channels
+  // 32 h + 8g .. +7 (h < 2, two 16-B pieces each) of position p0 + li (past the grid: zeros)
+  struct Blk { u32x4 o[4], s[4]; };
+  auto bfetch = [&](int p0, Blk& b) {
+    const int p = p0 + li;
+    const bool v = p < P;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) b.o[kk] = bload(ro, v ? (uint32_t)((p * old + 32 * kk + 8 * g) * 2) : kOOB);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        b.s[2 * h + e] = bload(rsb, v ? (uint32_t)((p * 64 + 32 * h + 8 * g + 4 * e) * 4) : kOOB);
+  };
+  const int nb = (P + 15) / 16;
+  Blk cur;
+  bfetch(16 * wave, cur);   // (a block past the grid loads zeros and is never used)
+  for (int i = tid; i < P * NQ; i += NT) A[i] = Am[(size_t)f * P * NQ + i];
+  for (int i = tid; i < NQ * 184; i += NT) da[i] = dAns[(size_t)f * da_ld + i];
+  for (int i = tid; i < NQ * 72; i += NT) Qs[i] = Q[(size_t)f * qs + i];
+  __syncthreads();
+  // Dp[n = s NQ + q][k'] = part s of: 0 (k' < 8), da[q][k' - 8] (k' < 128), da[q][120 + (k' - 128) % 64]
+  for (int i = tid; i < NR * 80; i += NT) {
+    const int n = i / 80, k = 4 * (i - n * 80), sp = n / NQ, q = n - sp * NQ;
+    bf16x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kk = k + e;
+      const float x = kk < 8 ? 0.f : da[q * 184 + (kk < 128 ? kk - 8 : 120 + ((kk - 128) & 63))];
+      __bf16 h, m, l;
+      am_split(x, h, m, l);
+      v[e] = sp == 0 ? h : sp == 1 ? m : l;
+    }
+    *reinterpret_cast<bf16x4*>(Dp + n * DS + 2 * k) = v;
+  }
+  __syncthreads();
+  // ---- phase 1: dA on the MFMA, wave w takes blocks w, w + 8, ...
+  {
+    const int n0 = li, n1 = 16 + li;
+    const unsigned char* db0 = Dp + min(n0, NR - 1) * DS + 16 * g;
+    const unsigned char* db1 = Dp + min(n1, NR - 1) * DS + 16 * g;
+    const bf16x8 zero8 = {};
+    for (int b = wave; b < nb; b += NW) {
+      Blk nxt;
+      if (b + NW < nb) bfetch(16 * (b + NW), nxt);
+      bf16x8 a[10];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) a[kk] = __builtin_bit_cast(bf16x8, cur.o[kk]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 x0 = __builtin_bit_cast(f32x4, cur.s[2 * h]), x1 = __builtin_bit_cast(f32x4, cur.s[2 * h + 1]);
+        bf16x8 hi, mi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 th, tm, tl;
+          am_split(e < 4 ? x0[e] : x1[e - 4], th, tm, tl);
+          hi[e] = th;
+          mi[e] = tm;
+          lo[e] = tl;
+        }
+        a[4 + h] = hi;
+        a[6 + h] = mi;
+        a[8 + h] = lo;
+      }
+      f32x4 acc[NTN];
+#pragma unroll
+      for (int n = 0; n < NTN; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 10; ++ks) {
+        bf16x8 w0 = *reinterpret_cast<const bf16x8*>(db0 + 64 * ks);
+        if (n0 >= NR) w0 = zero8;
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], w0, acc[0], 0, 0, 0);
+        if constexpr (NTN == 2) {
+          bf16x8 w1 = *reinterpret_cast<const bf16x8*>(db1 + 64 * ks);
+          if (n1 >= NR) w1 = zero8;
+          acc[NTN - 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], w1, acc[NTN - 1], 0, 0, 0);
+        }
+      }
+      // lane (g, li) holds D[position p0 + 4g + r][n = li (+16)]: the parts of q are n = q, NQ + q, 2 NQ + q
+      const int p0 = 16 * b;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v0 = acc[0][r];
+        float v;
+        if constexpr (NQ == 4) v = v0 + __shfl_down(v0, 4, 64) + __shfl_down(v0, 8, 64);
+        else v = v0 + __shfl_down(v0, 8, 64) + acc[NTN - 1][r];
+        const int p = p0 + 4 * g + r;
+        if (li < NQ && p < P) dA[p * NQ + li] = v;
+      }
+      if (g == 0 && p0 + li < P) {   // the key channels O[p][0..7] for dQ
+        const u32x4 k = cur.o[0];
+        *reinterpret_cast<f32x4*>(Kc + (p0 + li) * 8) = bf4_f32(u32x2{k.x, k.y});
+        *reinterpret_cast<f32x4*>(Kc + (p0 + li) * 8 + 4) = bf4_f32(u32x2{k.z, k.w});
+      }
+      cur = nxt;
+    }
+  }
+  __syncthreads();
+  // ---- phases 2-4 as k_attn_bwd
+  // softmax backward: dlogit = A (dA - sum_p A dA)
+  for (int q = wave; q < NQ; q += NW) {
+    float s = 0.f;
+    for (int p = lane; p < P; p += 64) s += A[p * NQ + q] * dA[p * NQ + q];
+    s = wave_sum(s);
+    if (lane == 0) ss[q] = s;
+  }
+  __syncthreads();
+  for (int i = tid; i < P * NQ; i += NT) {
+    const int q = i - (i / NQ) * NQ;
+    dA[i] = A[i] * (dA[i] - ss[q]);
+  }
+  __syncthreads();
+  // dO[p][c4..c4+3] = sum_q w[p][q] coef[q][0..3]: key channels (c4 < 8) w = dlogit, coef = Q[q][c4..];
+  // the rest w = A, coef = da[q][c4-8..]
+  float* dOf = dO + (size_t)f * P * 128;
+  auto dO_pos = [&](int p, const f32x4 (&coef)[NQ], const float* W) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NQ / 4; ++j) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(W + p * NQ + 4 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc += w[i] * coef[4 * j + i];
+    }
+    return acc;
+  };
+  if (cqm) {   // quad-major: a wave per channel quad, lanes along the positions (1-KB stores)
+    for (int qd = wave; qd < 32; qd += NW) {
+      const int c4 = qd * 4;
+      f32x4 coef[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        coef[q] = *reinterpret_cast<const f32x4*>(c4 < 8 ? Qs + q * 72 + c4 : da + q * 184 + c4 - 8);
+      const float* W = c4 < 8 ? dA : A;
+      for (int p = lane; p < P; p += 64)
+        *reinterpret_cast<f32x4*>(dOf + ((size_t)qd * P + p) * 4) = dO_pos(p, coef, W);
+    }
+  } else {     // row-major: lanes along a row's 32 quads, 16 positions per pass (512-B stores)
+    const int qd = lane & 31, c4 = qd * 4;
+    f32x4 coef[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const f32x4 cq = *reinterpret_cast<const f32x4*>(Qs + q * 72 + min(c4, 4));
+      const f32x4 cd = *reinterpret_cast<const f32x4*>(da + q * 184 + max(c4 - 8, 0));
+      coef[q] = c4 < 8 ? cq : cd;
+    }
+    for (int p = 2 * wave + (lane >> 5); p < P; p += 2 * NW) {
+      const f32x4 a = dO_pos(p, coef, A), d = dO_pos(p, coef, dA);
+      *reinterpret_cast<f32x4*>(dOf + (size_t)p * 128 + c4) = c4 < 8 ? d : a;
+    }
+  }
+  // dQ[q][c] = sum_p dlogit[p][q] K[p][c], K = [O[:8] (Kc) | S]: G position groups, partials through LDS
+  if (tid < G * 72) {
+    const int gg = tid / 72, c = tid - gg * 72;
+    float acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = 0.f;
+    const float* ks = S + max(c - 8, 0);
+    const float* kc = Kc + min(c, 7);
+#pragma unroll 8
+    for (int p = gg; p < P; p += G) {
+      const float kS = ks[p * 64], kO = kc[p * 8];
+      const float k = c < 8 ? kO : kS;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) acc[q] += dA[p * NQ + q] * k;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) red[(gg * NQ + q) * 72 + c] = acc[q];
+  }
+  __syncthreads();
+  for (int i = tid; i < NQ * 72; i += NT) {
+    float acc = 0.f;
+#pragma unroll 4
+    for (int gg = 0; gg < G; ++gg) acc += red[gg * NQ * 72 + i];
+    if (addq) acc += dAns[(size_t)f * da_ld + NQ * 184 + i];   // the answer row's copy of Q (stateful core)
+    dQp[(size_t)f * NQ * 72 + i] = acc;
+  }
+}
+
 }  // namespace aaa

@@ -1246,6 +1246,13 @@ hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, con
 #endif
   const int ppl = ppl_env ? ppl_env : P > 256 ? 2 : 1;
   if (ppl != 1 && ppl != 2) return hipErrorInvalidValue;
+  // bf16 O: the dA pass on the MFMA (attn_mfma.h); AAA_ATTN_BWD_MFMA=0: the VALU kernel
+  static const int bm_env = getenv("AAA_ATTN_BWD_MFMA") ? atoi(getenv("AAA_ATTN_BWD_MFMA")) : 1;
+  if (O.bf16 && bm_env) {
+    const __bf16* o = (const __bf16*)O.p;
+    nq == 4 ? launch(k_attn_bwd_mfma<4>, o) : launch(k_attn_bwd_mfma<8>, o);
+    return hipGetLastError();
+  }
   if (O.bf16) {
     const __bf16* o = (const __bf16*)O.p;
     if (ppl == 2) nq == 4 ? launch(k_attn_bwd<4, __bf16, 2>, o) : launch(k_attn_bwd<8, __bf16, 2>, o);
