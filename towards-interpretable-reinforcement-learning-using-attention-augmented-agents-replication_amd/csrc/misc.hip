@@ -1246,9 +1246,11 @@ hipError_t attn_bwd(OSrc O, const float* S, const float* Q, const float* Am, con
 #endif
   const int ppl = ppl_env ? ppl_env : P > 256 ? 2 : 1;
   if (ppl != 1 && ppl != 2) return hipErrorInvalidValue;
-  // bf16 O: the dA pass on the MFMA (attn_mfma.h); AAA_ATTN_BWD_MFMA=0: the VALU kernel
+  // bf16 O on large grids: the dA pass on the MFMA (attn_mfma.h; C5, P = 441: 320 -> 290 us; at 84x84,
+  // P = 121, the VALU pass is faster: 126 vs 139 us, profiles/r06/ab/attn_bwd_mfma/).  AAA_ATTN_BWD_MFMA=0:
+  // the VALU kernel everywhere, 2: the MFMA pass everywhere
   static const int bm_env = getenv("AAA_ATTN_BWD_MFMA") ? atoi(getenv("AAA_ATTN_BWD_MFMA")) : 1;
-  if (O.bf16 && bm_env) {
+  if (O.bf16 && (bm_env == 2 || (bm_env == 1 && P > 256))) {
     const __bf16* o = (const __bf16*)O.p;
     nq == 4 ? launch(k_attn_bwd_mfma<4>, o) : launch(k_attn_bwd_mfma<8>, o);
     return hipGetLastError();
