@@ -1171,9 +1171,13 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
     if (O.ld < 128 || O.ld % 8) return hipErrorInvalidValue;   // 16-B loads
     const size_t sh = attn_mfma_lds(P, nq);
     if (sh > 160 * 1024) return hipErrorInvalidValue;
-    static const int nt_env = getenv("AAA_ATTN_NT") ? atoi(getenv("AAA_ATTN_NT")) : 0;   // (A/B)
+#ifdef AAA_ABLATION   // O loaded non-temporal (A/B: the backward then reads those rows slower, profiles/r06/ab/attn_nt/)
+    static const int nt_env = getenv("AAA_ATTN_NT") ? atoi(getenv("AAA_ATTN_NT")) : 0;
     auto kern = nt_env ? (nq == 4 ? k_attn_fwd_mfma<4, true> : k_attn_fwd_mfma<8, true>)
                        : (nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>);
+#else
+    auto kern = nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>;
+#endif
     if (sh > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sh);
