@@ -67,8 +67,9 @@ inline size_t attn_mfma_lds(int P, int nq) {
 }
 
 // NTL_: the frame's O rows loaded non-temporal (nt: streamed past L2, keeping the basis resident there)
-template <int NQ, bool NTL_>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NQ == 8 ? 4 : 3)))
+// SQP_: the basis half of the logits comes precomputed (SQ, a constant query); else computed here (per-frame query)
+template <int NQ, bool NTL_, bool SQP_ = true>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NQ == 8 ? 4 : 5)))
 k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict__ S, const float* __restrict__ Q,
                 int qs, const float* __restrict__ SQ, const float* __restrict__ pr, const float* __restrict__ pa, int P,
                 float* __restrict__ Am, float* __restrict__ ans, int ans_ld) {
@@ -151,7 +152,7 @@ k_attn_fwd_mfma(const __bf16* __restrict__ Hs, int old, const float* __restrict_
       acc[q] = ka[0] * qq[0] + ka[1] * qq[1] + ka[2] * qq[2] + ka[3] * qq[3] + kb[0] * qq[4] + kb[1] * qq[5] +
                kb[2] * qq[6] + kb[3] * qq[7];
     }
-    if (SQ) {
+    if constexpr (SQP_) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) acc[q] += sqp[q / 4][q % 4];
     } else {   // per-frame query: the basis half here

@@ -1173,11 +1173,12 @@ hipError_t attn_fwd(OSrc O, const float* S, const float* Q, const float* SQ, con
     if (sh > 160 * 1024) return hipErrorInvalidValue;
 #ifdef AAA_ABLATION   // O loaded non-temporal (A/B: the backward then reads those rows slower, profiles/r06/ab/attn_nt/)
     static const int nt_env = getenv("AAA_ATTN_NT") ? atoi(getenv("AAA_ATTN_NT")) : 0;
-    auto kern = nt_env ? (nq == 4 ? k_attn_fwd_mfma<4, true> : k_attn_fwd_mfma<8, true>)
-                       : (nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>);
 #else
-    auto kern = nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>;
+    constexpr int nt_env = 0;
 #endif
+    auto kern = !SQ ? (nq == 4 ? k_attn_fwd_mfma<4, false, false> : k_attn_fwd_mfma<8, false, false>)
+                : nt_env ? (nq == 4 ? k_attn_fwd_mfma<4, true> : k_attn_fwd_mfma<8, true>)
+                         : (nq == 4 ? k_attn_fwd_mfma<4, false> : k_attn_fwd_mfma<8, false>);
     if (sh > 64 * 1024)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)sh);
