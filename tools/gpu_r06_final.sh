@@ -2,7 +2,7 @@
 # Round 6 end-of-round measurements at HEAD: smoke(), the full -m gpu suite, the default bench line (C2 + drop-in +
 # episode + CPU baseline), the C3 / C4 / C5 lines, and a kernel trace of the default C2 line at the bench's own
 # steps checked against its event timings (tools/trace_vs_events.py).
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/r06final; mkdir -p $O; cd $R; export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${FINAL_DIR:-r06final}; mkdir -p $O; cd $R; export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests > $O/tests.log 2>&1; rc=$?
