@@ -434,6 +434,27 @@ struct GemmCfgS6L : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, 1> {
   static constexpr bool SPLIT3 = true, SPLIT6 = true, SPLIT6L = true;
   static constexpr int FD = FD_;   // K tiles of global loads in flight (register stages)
 };
+// The bf16 path's tail precision (SPLIT3: hi + lo parts, three products) split at commit the same
+// way (gemm_kernel_s6l with two part tiles per operand): bit-identical to gemm_kernel's SPLIT3 path.
+template <int BI_, int BJ_, int BK_, int WI_, int WJ_, int FD_ = 2>
+struct GemmCfgS3L : GemmCfg<float, BI_, BJ_, BK_, WI_, WJ_, 1> {
+  static constexpr bool SPLIT3 = true, SPLIT6L = true, TWO_PARTS = true;
+  static constexpr int FD = FD_;
+};
+template <class C, class = void> struct two_parts_of : std::false_type {};
+template <class C> struct two_parts_of<C, std::enable_if_t<C::TWO_PARTS>> : std::true_type {};
+// 4 fp32 of a staged chunk -> hi, lo bf16 parts (split_bf16), 8 B each, ``plane`` elements apart
+__device__ __forceinline__ void lds_store_split2(__bf16* dst, int plane, const u32x4& raw) {
+  const f32x4 f = __builtin_bit_cast(f32x4, raw);
+  bf16x4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = (__bf16)f[e];
+    lo[e] = (__bf16)(f[e] - (float)hi[e]);
+  }
+  *reinterpret_cast<bf16x4*>(dst) = hi;
+  *reinterpret_cast<bf16x4*>(dst + plane) = lo;
+}
 // B operand exact in bf16 (configs with BEXACT: conv1's operand when the frames are uint8 -- integers
 // 0..255 are bf16 values): its mid and lo parts are zero, so of the six split products only lo.hi,
 // mid.hi and hi.hi are issued (in the SPLIT6 order; the three skipped ones add exact zeros -- the same
@@ -680,8 +701,11 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
   static_assert(C::WK == 1 && MI >= 1 && MJ >= 1 && BK % 16 == 0, "tile shape");
   using TA = TileK<__bf16, BI, BK, LA::KC>;
   using TB = TileK<__bf16, BJ, BK, LB::KC>;
-  constexpr int PA = TA::ELEMS, PB = TB::ELEMS, STG = 3 * (PA + PB);
+  constexpr bool TWO = two_parts_of<C>::value;   // SPLIT3 (hi, lo) instead of SPLIT6 (hi, mid, lo)
+  constexpr int NPT = TWO ? 2 : 3;               // part tiles per operand
+  constexpr int PA = TA::ELEMS, PB = TB::ELEMS, STG = NPT * (PA + PB);
   constexpr bool BX = bexact_of<C>::value;   // B's hi part only (commit1), three products
+  static_assert(!(TWO && BX), "exact B: three-part configs only");
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STG];
 
   int ti, tj, tz;
@@ -693,6 +717,15 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
 
   LA la(pa, i0);
   LB lb(pb, j0);
+  auto commit_a = [&](__bf16* dst, const typename LA::Regs& r) {
+    if constexpr (TWO) la.commit2(dst, PA, r);
+    else la.commit3(dst, PA, r);
+  };
+  auto commit_b = [&](__bf16* dst, const typename LB::Regs& r) {
+    if constexpr (BX) lb.commit1(dst, r);
+    else if constexpr (TWO) lb.commit2(dst, PB, r);
+    else lb.commit3(dst, PB, r);
+  };
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wi = wave / WJ, wj = wave - (wave / WJ) * WJ;
   const int r32 = lane & 31, h = lane >> 5;
@@ -719,9 +752,8 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
       lb.fetch(kb + BK, ke, rb[1]);
     }
   }
-  la.commit3(smem, PA, ra[0]);
-  if constexpr (BX) lb.commit1(smem + 3 * PA, rb[0]);
-  else lb.commit3(smem + 3 * PA, PB, rb[0]);
+  commit_a(smem, ra[0]);
+  commit_b(smem + NPT * PA, rb[0]);
   __syncthreads();
 
   // one K step; E = kt & 1 (compile-time, so the register stages stay in registers)
@@ -748,11 +780,22 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
 #pragma unroll
       for (int a = 0; a < MI; ++a)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) af[a][p] = frag_bf16<TA>(cur + p * PA, wi * WTI + a * 32 + r32, kofs);
+        for (int p = 0; p < NPT; ++p) af[a][p] = frag_bf16<TA>(cur + p * PA, wi * WTI + a * 32 + r32, kofs);
 #pragma unroll
       for (int b = 0; b < MJ; ++b)
 #pragma unroll
-        for (int p = 0; p < (BX ? 1 : 3); ++p) bfr[b][p] = frag_bf16<TB>(cur + 3 * PA + p * PB, wj * WTJ + b * 32 + r32, kofs);
+        for (int p = 0; p < (BX ? 1 : NPT); ++p)
+          bfr[b][p] = frag_bf16<TB>(cur + NPT * PA + p * PB, wj * WTJ + b * 32 + r32, kofs);
+      if constexpr (TWO) {   // as gemm_kernel's SPLIT3: lo.hi, hi.lo, hi.hi
+#pragma unroll
+        for (int a = 0; a < MI; ++a)
+#pragma unroll
+          for (int b = 0; b < MJ; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][1], bfr[b][0], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][1], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[a][0], bfr[b][0], acc[a][b], 0, 0, 0);
+          }
+      } else
 #pragma unroll
       for (int a = 0; a < MI; ++a)
 #pragma unroll
@@ -769,9 +812,8 @@ gemm_kernel_s6l(typename LA::Params pa, typename LB::Params pb, EP ep, int K, in
     }
     if (more) {   // tile kt+1: register stage e ^ 1 (FD 2) or 0
       constexpr int rs1 = FD == 2 ? (e ^ 1) : 0;
-      la.commit3(nxt, PA, ra[rs1]);
-      if constexpr (BX) lb.commit1(nxt + 3 * PA, rb[rs1]);
-      else lb.commit3(nxt + 3 * PA, PB, rb[rs1]);
+      commit_a(nxt, ra[rs1]);
+      commit_b(nxt + NPT * PA, rb[rs1]);
     }
     __syncthreads();
   };

@@ -55,6 +55,17 @@ struct LdRowsN {
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, true>::off(lr[c], kc[c]), buf[c]);
   }
+  // split-at-commit part tiles (gemm_kernel_s6l): bf16 tiles of the same shape, ``plane`` elements apart
+  __device__ __forceinline__ void commit3(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split3(lds + Tile<__bf16, R, BK, true>::off(lr[c], kc[c]), plane, buf[c]);
+  }
+  __device__ __forceinline__ void commit2(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split2(lds + Tile<__bf16, R, BK, true>::off(lr[c], kc[c]), plane, buf[c]);
+  }
 };
 
 // Transposed rows (LdRowsT's layout), element (row, k) at src[k*ld + row]; nrows % VG == 0 (the host
@@ -96,6 +107,16 @@ struct LdRowsTN {
 #pragma unroll
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_chunk<G, T>(lds + Tile<T, R, BK, false>::off(lc[c], kr[c]), buf[c]);
+  }
+  __device__ __forceinline__ void commit3(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split3(lds + Tile<__bf16, R, BK, false>::off(lc[c], kr[c]), plane, buf[c]);
+  }
+  __device__ __forceinline__ void commit2(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split2(lds + Tile<__bf16, R, BK, false>::off(lc[c], kr[c]), plane, buf[c]);
   }
 };
 

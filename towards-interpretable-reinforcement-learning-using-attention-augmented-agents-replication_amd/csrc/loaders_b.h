@@ -117,6 +117,11 @@ struct LdRowsTB {
     for (int c = 0; c < PER; ++c)
       if (NCH % NT == 0 || act[c]) lds_store_split3(lds + off16(threadIdx.x + c * NT), plane, buf[c]);
   }
+  __device__ __forceinline__ void commit2(__bf16* lds, int plane, const Regs& buf) const {
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (NCH % NT == 0 || act[c]) lds_store_split2(lds + off16(threadIdx.x + c * NT), plane, buf[c]);
+  }
 };
 
 // Per-(pixel row m, chunk column kc) constants of the implicit-GEMM gather:

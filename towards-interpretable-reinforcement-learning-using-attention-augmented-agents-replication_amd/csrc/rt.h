@@ -403,6 +403,17 @@ static hipError_t head_gemm(const PA& pa, const PB& pb, const EP& ep, int Mi, in
     return run(cfg0);
   };
   if (mode == 0 && tiles < 192) return splitk(CFK4{});
+  // bf16 path, 64x64 tiles: the operands split once at their LDS commit (hi, lo part tiles, gemm_kernel_s6l),
+  // not per wave per fragment read -- the same products in the same order (AAA_TAIL_S3L=1, ablation builds: A/B)
+  if (mode == 0 && g_tail3 && ab_int("AAA_TAIL_S3L", 0) && DeepLd<LA_>::fits(pa.src, pa.ld, pa.nrows) &&
+      DeepLd<LB_>::fits(pb.src, pb.ld, pb.nrows) && (size_t)K * pa.ld * 4 < (1u << 31) &&
+      (size_t)K * pb.ld * 4 < (1u << 31)) {
+    using C = GemmCfgS3L<64, 64, 32, 2, 2, 2>;
+    using A = typename DeepLd<LA_>::template type<float, float, C::BI, C::BK, C::NT>;
+    using B = typename DeepLd<LB_>::template type<float, float, C::BJ, C::BK, C::NT>;
+    return launch_gemm<C, A, B>(typename A::Params{pa.src, pa.ld, pa.nrows}, typename B::Params{pb.src, pb.ld, pb.nrows},
+                                ep, Mi, Nj, K, nsplit, st);
+  }
   if (mode == 1 || (mode == 0 && tiles >= 192)) return splitk(CF{});
 #ifdef AAA_ABLATION   // the measured-slower tail tiles (AAA_HEAD_TILE 2-5)
   if (mode == 3) return splitk(CFK{});
